@@ -1,0 +1,281 @@
+/*
+ * surreal_mi.h — C ABI of the MI355X-native SURREAL centralized-learner hot path.
+ *
+ * One shared library (libsurreal_mi.so, gfx950 code objects) exposes plain
+ * `extern "C"` entry points.  Every entry point:
+ *   - takes caller-owned DEVICE pointers (HBM) plus explicit sizes/strides;
+ *   - takes the hipStream_t to enqueue on as `void* stream` (NULL = default);
+ *   - never allocates, never synchronises (safe inside hipGraph capture);
+ *   - returns 0 on success, a negative SMI_E* code on argument errors, or
+ *     -(hipError_t) if the launch failed; smi_last_error() holds a message.
+ *
+ * Each function names the reference interface it replaces (file:line in
+ * tanwanirahul/surreal).  Host-side mirrors of the reference Python classes
+ * live in surreal_amd/ (learner.py, model.py, replay.py) and call these.
+ *
+ * Parameter-buffer layout ("flat MLP layout", used by every MLP argument):
+ *   W1[H1][IN] b1[H1] W2[H2][H1] b2[H2] W3[OUT][H2] b3[OUT] (+ log_var[OUT] for
+ *   PPO actors).  Row-major, fp32, i.e. torch nn.Linear (out, in) weights laid
+ *   end to end — see smi_mlp_param_count().
+ */
+#ifndef SURREAL_MI_H
+#define SURREAL_MI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- errors */
+#define SMI_OK            0
+#define SMI_E_ARG        -1   /* bad size / null pointer / unsupported dims */
+#define SMI_E_NOFIT      -2   /* problem does not fit the requested kernel variant */
+#define SMI_E_LAUNCH     -3   /* hip launch error (see smi_last_error) */
+
+int         smi_version(void);
+const char* smi_last_error(void);
+
+/* Device scratch for the multi-workgroup reductions (ZFilter column partials,
+ * Adam norm partials).  The caller allocates smi_workspace_bytes() of device
+ * memory once and registers it; launches that need it are stream-ordered. */
+int64_t smi_workspace_bytes(void);
+int     smi_set_workspace(void* dev_ptr, int64_t bytes);
+
+/* --------------------------------------------------------------- layouts */
+/* Number of floats in a flat MLP buffer (in -> h1 -> h2 -> out [+ log_var]). */
+int64_t smi_mlp_param_count(int in_dim, int h1, int h2, int out_dim, int with_log_var);
+
+/* Dynamic LDS bytes the fused small-batch PPO kernel needs; more than 163840
+ * (160 KiB, one CU) means it does not fit and the modular path must be used. */
+int64_t smi_ppo_fused_lds_bytes(int rows, int obs_dim, int h1, int h2, int act_dim,
+                                int critic_h1, int critic_h2);
+
+/* ----------------------------------------------------------- ZFilter ops */
+/* Replaces ZFilter.forward (surreal/model/z_filter.py:59-79):
+ *   out = clamp((x - sum/count) / max(sqrt(sumsq/count - mean^2), eps), -5, 5)
+ * x, out: [rows][dim] (may alias). */
+int smi_zfilter_apply(const float* x, float* out, int64_t rows, int dim,
+                      const float* running_sum, const float* running_sumsq,
+                      const float* count, float eps, void* stream);
+
+/* Replaces ZFilter.z_update (surreal/model/z_filter.py:44-57):
+ *   running_sum += sum_r x[r], running_sumsq += sum_r x[r]^2, count += rows.
+ * Rows are read with an explicit row stride (floats) so obs[:,0,:] can be passed
+ * without a copy. */
+int smi_zfilter_update(const float* x, int64_t rows, int dim, int64_t row_stride,
+                       float* running_sum, float* running_sumsq, float* count,
+                       void* stream);
+
+/* Column sums / sums of squares only (no buffer update): out_sum[dim],
+ * out_sumsq[dim] — used by the data-parallel learner before its all-reduce. */
+int smi_zfilter_colstats(const float* x, int64_t rows, int dim, int64_t row_stride,
+                         float* out_sum, float* out_sumsq, void* stream);
+
+/* Replaces RewardFilter.forward / RewardFilter.update
+ * (surreal/model/reward_filter.py:18-56) as used by _preprocess_batch_ppo
+ * (ppo.py:452-456): rewards *= reward_scale, then by `mode` bits
+ *   1 = forward (whiten with the stats from before this call),
+ *   2 = update  (count += n; running_sum += sum; running_sumsq = sum of squares —
+ *                the reference's `=` instead of `+=` at reward_filter.py:42).
+ * mode 0 only scales.  In place on rewards[n]. */
+int smi_reward_filter(float* rewards, int64_t n, float reward_scale, int mode,
+                      float* running_sum, float* running_sumsq, float* count,
+                      float eps, void* stream);
+
+/* ---------------------------------------------------------- DiagGauss ops */
+/* Replaces DiagGauss.loglikelihood / likelihood / kl / entropy
+ * (surreal/model/ppo_net.py:29-72).  prob rows are [mean(A) | std(A)].
+ * Each output is [rows]; pass NULL for outputs you do not need.
+ *   loglik[r] = -0.5*sum(((a-mu)/sd)^2) - 0.5*log(2pi)*A - sum(log sd)
+ *   lik[r]    = max(exp(loglik[r]), 1e-5)
+ *   kl[r]     = KL(prob0[r] || prob1[r])
+ *   ent[r]    = 0.5*sum(log sd) + 0.5*log(2 pi e)*A            (of prob0) */
+int smi_diag_gauss(const float* actions, const float* prob0, const float* prob1,
+                   int64_t rows, int act_dim,
+                   float* loglik, float* lik, float* kl, float* entropy, void* stream);
+
+/* ------------------------------------------------------------ MLP forward */
+/* Replaces PPOModel.forward_actor / forward_critic for the low-dim MLP model
+ * (surreal/model/ppo_net.py:253-315, builders.py:86-175):
+ *   x -> [ZFilter] -> Linear-ReLU-Linear-ReLU-Linear [-Tanh]
+ * act: 0 none (critic), 2 tanh (actor mean).  If with_log_var, out has 2*OUT
+ * columns: [tanh(...) | exp(log_var)] exactly like PPO_ActorNetwork.forward.
+ * zf_* may be NULL when use_zf == 0.  x rows are strided (row_stride floats). */
+int smi_mlp_forward(const float* params, int in_dim, int h1, int h2, int out_dim,
+                    int out_act, int with_log_var,
+                    const float* x, int64_t rows, int64_t row_stride,
+                    int use_zf, const float* zf_sum, const float* zf_sumsq,
+                    const float* zf_count, float zf_eps,
+                    float* out, void* stream);
+
+/* ------------------------------------------------------- PPO: GAE/returns */
+/* Replaces PPOLearner._gae_and_return, non-RNN branch
+ * (surreal/learner/ppo.py:355-387,408-418): the critic forward over
+ * cat(obs, obs_next) (B*(T+1) rows, ZFilter fused into the first layer),
+ * done-masking values[:,1:] *= 1-dones, then the windowed sums
+ *   ret[b] = sum_t g[t]*r[b,t] + Vm[b,T]*gamma_T
+ *   adv[b] = sum_t (td[b,t]*g[t])*l[t],  td = r + gamma*Vm[:,1:] - Vm[:,:-1]
+ * g/l are torch.pow(float32) tables (length T) computed by the host exactly as
+ * the reference does (ppo.py:372-374); gamma_T = float(gamma**T).
+ * Outputs: values[B][T+1] (masked; may be NULL), adv_raw[B] (NOT normalised),
+ * ret[B].  obs: [B][T][D] obs_next: [B][1][D] rewards/dones: [B][T]. */
+int smi_ppo_critic_gae(const float* critic_params, int obs_dim, int h1, int h2,
+                       int use_zf, const float* zf_sum, const float* zf_sumsq,
+                       const float* zf_count, float zf_eps,
+                       const float* obs, const float* obs_next,
+                       const float* rewards, const float* dones, int B, int T,
+                       const float* gamma_tab, const float* lam_tab,
+                       float gamma, float gamma_T,
+                       float* values, float* adv_raw, float* ret, void* stream);
+
+/* Replaces the windowed GAE of the RNN branch (ppo.py:389-406) — and, with
+ * horizon == T, the non-RNN sums — given already computed critic values
+ * values[B][T+1] (masked in place here: values[:,1:] *= 1-dones):
+ *   E = T - horizon + 1 windows per segment, s in [0,E):
+ *   ret[b,s] = sum_{k<H} g[k]*r[b,s+k] + Vm[b,s+H]*gamma_H
+ *   adv[b,s] = sum_{k<H} (td[b,s+k]*g[k])*l[k]
+ * LDS-staged, coalesced streaming kernel.  adv_partials receives per-workgroup
+ * (sum, sumsq) doubles; *n_partials is set on return (host-side value). */
+int smi_gae_windows(float* values, const float* rewards, const float* dones,
+                    int64_t B, int T, int horizon,
+                    const float* gamma_tab, const float* lam_tab,
+                    float gamma, float gamma_H,
+                    float* adv, float* ret, double* adv_partials,
+                    int* n_partials, void* stream);
+int smi_gae_windows_max_partials(int64_t B, int T);
+
+/* (sum, sum of squares, count) in fp64 of x[n] -> out[3]; if partials != NULL
+ * and n_partials > 0 the (sum, sumsq) pairs are reduced instead of x (count = n).
+ * Deterministic (fixed order).  Feeds the advantage normaliser (ppo.py:413-416). */
+int smi_moments(const float* x, int64_t n, const double* partials, int n_partials,
+                double* out3, void* stream);
+
+/* ------------------------------------------------- PPO: fused small batch */
+/* The whole PPO optimisation of one learn() call for a non-RNN low-dim model
+ * when the batch fits one CU (rows <= 256 and params fit LDS):
+ * PPOLearner._optimize (surreal/learner/ppo.py:487-586) minus GAE/z_update:
+ *   advantage normalisation (ppo.py:413-416), ref_pol (ppo.py:539), up to
+ *   epoch_policy actor updates with the KL early stop (ppo.py:541-557; clip
+ *   ppo.py:194-248 or adapt ppo.py:250-309, clip_grad_norm_, Adam), and
+ *   epoch_baseline critic updates (ppo.py:311-353,561-562), plus the
+ *   statistics of ppo.py:568-576.
+ * Workgroup 0 runs the policy loop, workgroup 1 the value loop (independent
+ * parameter sets in the reference).  Hyper-parameters that the host may change
+ * between calls (clip_epsilon, beta, learning rates) are read from `hyper`
+ * (device memory), so the call can be captured once in a hipGraph.
+ * See struct smi_ppo_args for every field. */
+typedef struct smi_ppo_args {
+  /* dims */
+  int B;              /* policy rows (segments)                         */
+  int obs_dim, h1, h2, act_dim;
+  int critic_h1, critic_h2;
+  int epoch_policy, epoch_baseline;
+  int mode;           /* 0 = clip, 1 = adapt                             */
+  int norm_adv;
+  int clip_actor_grad, clip_critic_grad;
+  int use_zf;
+  /* inputs: row r of each is base + r*stride (floats) */
+  const float* obs;      int64_t obs_stride;      /* obs[:,0,:]          */
+  const float* actions;  int64_t act_stride;      /* actions[:,0,:]      */
+  const float* behave;   int64_t beh_stride;      /* pds[:,0,:] (2A)     */
+  const float* adv_raw;                           /* [B]                 */
+  const double* adv_moments;  /* NULL: normalise over these B rows; else
+                                 [3] = global (sum, sum of squares, count)
+                                 of the raw advantages (data parallel) */
+  const float* ret;                               /* [B]                 */
+  /* ZFilter buffers of the model and of ref_target_model */
+  const float* zf_sum;  const float* zf_sumsq;  const float* zf_count;
+  const float* rzf_sum; const float* rzf_sumsq; const float* rzf_count;
+  float zf_eps;
+  /* parameters (flat MLP layout), Adam state, step counters */
+  float* actor;  const float* ref_actor;  float* critic;
+  float* actor_m; float* actor_v; float* critic_m; float* critic_v;
+  int* actor_step; int* critic_step;
+  /* device hyper-parameters: see SMI_HYP_* */
+  const float* hyper;
+  /* constants */
+  double kl_target;           /* python float semantics in comparisons */
+  float kl_cutoff_coeff;
+  float actor_max_norm, critic_max_norm;
+  float actor_wd, critic_wd;
+  float beta1, beta2, adam_eps;
+  /* outputs */
+  float* stats;                /* [SMI_ST_COUNT]                       */
+  float* kl_record; int* kl_count; int kl_capacity;
+} smi_ppo_args;
+
+/* device hyper-parameter slots (float) */
+#define SMI_HYP_CLIP_EPS   0
+#define SMI_HYP_BETA       1
+#define SMI_HYP_LR_ACTOR   2
+#define SMI_HYP_LR_CRITIC  3
+#define SMI_HYPX_CLIP_LO   4   /* float(1 - clip_epsilon) (torch.clamp bound) */
+#define SMI_HYPX_CLIP_HI   5   /* float(1 + clip_epsilon)                      */
+#define SMI_HYP_COUNT      6
+
+/* statistics slots written by the PPO kernels (float) */
+#define SMI_ST_SURR_LOSS        0   /* _surr_loss                          */
+#define SMI_ST_CLIP_SURR_LOSS   1   /* _clip_surr_loss (clip mode)         */
+#define SMI_ST_KL_LOSS_ADAPT    2   /* _kl_loss_adapt (adapt mode)         */
+#define SMI_ST_ENTROPY          3   /* _entropy                            */
+#define SMI_ST_POL_KL           4   /* _pol_kl (after the last update)     */
+#define SMI_ST_GRAD_NORM_ACTOR  5   /* grad_norm_actor                     */
+#define SMI_ST_VAL_LOSS         6   /* _val_loss                           */
+#define SMI_ST_VAL_EXPL_VAR     7   /* _val_explained_var                  */
+#define SMI_ST_GRAD_NORM_CRITIC 8   /* grad_norm_critic                    */
+#define SMI_ST_AVG_RETURN       9   /* _avg_return_targ                    */
+#define SMI_ST_AVG_LOG_SIG     10   /* _avg_log_sig                        */
+#define SMI_ST_AVG_BEHAVE_LIK  11   /* _avg_behave_likelihood              */
+#define SMI_ST_AVG_IS_WEIGHT   12   /* _avg_is_weight                      */
+#define SMI_ST_REF_BEHAVE_DIFF 13   /* _ref_behave_diff                    */
+#define SMI_ST_EPOCHS_RUN      14   /* policy updates applied (float)      */
+#define SMI_ST_POL_KL_ADAPT    15   /* kl used by the adapt loss           */
+#define SMI_ST_COUNT           16
+
+int smi_ppo_update_fused(const smi_ppo_args* args, void* stream);
+
+/* ---------------------------------------------------------- Adam / clip */
+/* Replaces torch.nn.utils.clip_grad_norm_ + torch.optim.Adam.step
+ * (as called at ppo.py:243-247,348-352) on one flat parameter buffer:
+ *   norm = ||grad||; coef = min(1, max_norm/(norm+1e-6)) (if max_norm > 0);
+ *   g = coef*grad (+ wd*p); m = lerp(m, g, 1-b1); v = b2*v + (1-b2) g^2;
+ *   p -= (lr/(1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+ * `*step` (device int) is incremented; lr read from lr_ptr (device).
+ * If skip_flag != NULL and *skip_flag != 0 the update is skipped entirely.
+ * norm_out (device, may be NULL) receives the pre-clip norm. */
+int smi_adam_clip(float* params, const float* grad, float* m, float* v, int64_t n,
+                  int* step, const float* lr_ptr, float beta1, float beta2,
+                  float eps, float weight_decay, float max_norm,
+                  const int* skip_flag, float* norm_out, void* stream);
+
+/* ------------------------------------------------------ DDPG n-step target */
+/* Replaces the target of DDPGLearner._optimize (surreal/learner/ddpg.py:279-283):
+ *   y = r + gamma_n * q_next * (1 - done); with twin critics y = min(y, y2). */
+int smi_ddpg_target(const float* rewards, const float* dones, const float* q_next,
+                    const float* q_next2, int64_t n, float gamma_n, float* y,
+                    void* stream);
+
+/* ----------------------------------------- CPython-exact uniform sampling */
+/* Replaces UniformReplay.sample's index draw
+ * (surreal/replay/uniform_replay.py:43-47):
+ *   [random.randint(0, n-1) for _ in range(batch)]
+ * bit-exact with CPython's MT19937 (random.seed(int) init_by_array seeding,
+ * _randbelow = getrandbits(k) with rejection).  The 624-word state lives in
+ * device memory: state[0..623] words, state[624] = position.
+ * smi_mt_seed runs on the HOST (it fills a host buffer of 625 uint32). */
+int smi_mt_seed(uint64_t seed, uint32_t* host_state625);
+int smi_mt_randint_host(uint32_t* host_state625, int64_t n, int64_t batch,
+                        int64_t* out);
+/* n must be in [1, 2^32 - 1]. */
+int smi_mt_randint(uint32_t* dev_state625, int64_t n, int64_t batch,
+                   int64_t* out_indices, void* stream);
+
+/* Replay gather: out[i][:] = table[idx[i]][:] for `cols` floats per row. */
+int smi_gather_rows(const float* table, int64_t cols, const int64_t* idx,
+                    int64_t batch, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SURREAL_MI_H */

@@ -1,0 +1,153 @@
+"""ctypes binding of libsurreal_mi.so (the C ABI of include/surreal_mi.h).
+
+The product path has no CPU fallback: if the library is missing or no GPU is
+visible, calls raise.  torch is imported first so the process holds torch's
+HIP runtime before the library binds to it (same SONAME, one runtime).
+"""
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libsurreal_mi.so')
+
+c_int, c_i64, c_f32, c_f64, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
+P = ctypes.c_void_p
+
+# device hyper-parameter / statistics slots (include/surreal_mi.h)
+HYP_CLIP_EPS, HYP_BETA, HYP_LR_ACTOR, HYP_LR_CRITIC, HYP_CLIP_LO, HYP_CLIP_HI, HYP_COUNT = range(7)
+ST_NAMES = ['_surr_loss', '_clip_surr_loss', '_kl_loss_adapt', '_entropy', '_pol_kl',
+            'grad_norm_actor', '_val_loss', '_val_explained_var', 'grad_norm_critic',
+            '_avg_return_targ', '_avg_log_sig', '_avg_behave_likelihood', '_avg_is_weight',
+            '_ref_behave_diff', 'epochs_run', '_pol_kl_adapt']
+ST_COUNT = len(ST_NAMES)
+ST = {n: i for i, n in enumerate(ST_NAMES)}
+
+
+class PPOArgs(ctypes.Structure):
+    """struct smi_ppo_args (include/surreal_mi.h)."""
+    _fields_ = [
+        ('B', c_int), ('obs_dim', c_int), ('h1', c_int), ('h2', c_int), ('act_dim', c_int),
+        ('critic_h1', c_int), ('critic_h2', c_int),
+        ('epoch_policy', c_int), ('epoch_baseline', c_int),
+        ('mode', c_int), ('norm_adv', c_int),
+        ('clip_actor_grad', c_int), ('clip_critic_grad', c_int), ('use_zf', c_int),
+        ('obs', P), ('obs_stride', c_i64),
+        ('actions', P), ('act_stride', c_i64),
+        ('behave', P), ('beh_stride', c_i64),
+        ('adv_raw', P), ('adv_moments', P), ('ret', P),
+        ('zf_sum', P), ('zf_sumsq', P), ('zf_count', P),
+        ('rzf_sum', P), ('rzf_sumsq', P), ('rzf_count', P),
+        ('zf_eps', c_f32),
+        ('actor', P), ('ref_actor', P), ('critic', P),
+        ('actor_m', P), ('actor_v', P), ('critic_m', P), ('critic_v', P),
+        ('actor_step', P), ('critic_step', P),
+        ('hyper', P),
+        ('kl_target', c_f64), ('kl_cutoff_coeff', c_f32),
+        ('actor_max_norm', c_f32), ('critic_max_norm', c_f32),
+        ('actor_wd', c_f32), ('critic_wd', c_f32),
+        ('beta1', c_f32), ('beta2', c_f32), ('adam_eps', c_f32),
+        ('stats', P),
+        ('kl_record', P), ('kl_count', P), ('kl_capacity', c_int),
+    ]
+
+
+_SIGS = {
+    'smi_version': (c_int, []),
+    'smi_last_error': (ctypes.c_char_p, []),
+    'smi_workspace_bytes': (c_i64, []),
+    'smi_set_workspace': (c_int, [P, c_i64]),
+    'smi_mlp_param_count': (c_i64, [c_int, c_int, c_int, c_int, c_int]),
+    'smi_ppo_fused_lds_bytes': (c_i64, [c_int] * 7),
+    'smi_zfilter_apply': (c_int, [P, P, c_i64, c_int, P, P, P, c_f32, P]),
+    'smi_zfilter_update': (c_int, [P, c_i64, c_int, c_i64, P, P, P, P]),
+    'smi_zfilter_colstats': (c_int, [P, c_i64, c_int, c_i64, P, P, P]),
+    'smi_reward_filter': (c_int, [P, c_i64, c_f32, c_int, P, P, P, c_f32, P]),
+    'smi_diag_gauss': (c_int, [P, P, P, c_i64, c_int, P, P, P, P, P]),
+    'smi_mlp_forward': (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_i64, c_i64,
+                                c_int, P, P, P, c_f32, P, P]),
+    'smi_ppo_critic_gae': (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, c_f32, P, P, P, P,
+                                   c_int, c_int, P, P, c_f32, c_f32, P, P, P, P]),
+    'smi_gae_windows': (c_int, [P, P, P, c_i64, c_int, c_int, P, P, c_f32, c_f32, P, P, P,
+                                P, P]),
+    'smi_gae_windows_max_partials': (c_int, [c_i64, c_int]),
+    'smi_moments': (c_int, [P, c_i64, P, c_int, P, P]),
+    'smi_ppo_update_fused': (c_int, [ctypes.POINTER(PPOArgs), P]),
+    'smi_adam_clip': (c_int, [P, P, P, P, c_i64, P, P, c_f32, c_f32, c_f32, c_f32, c_f32, P,
+                              P, P]),
+    'smi_ddpg_target': (c_int, [P, P, P, P, c_i64, c_f32, P, P]),
+    'smi_mt_seed': (c_int, [ctypes.c_uint64, P]),
+    'smi_mt_randint_host': (c_int, [P, c_i64, c_i64, P]),
+    'smi_mt_randint': (c_int, [P, c_i64, c_i64, P, P]),
+    'smi_gather_rows': (c_int, [P, c_i64, P, c_i64, P, P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load the library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError('libsurreal_mi.so not built: run `python -c "import __graft_entry__ as '
+                               'g; g.build()"` (no CPU fallback exists)')
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc, name):
+    if rc != 0:
+        msg = lib().smi_last_error().decode(errors='replace')
+        raise RuntimeError(f'{name} failed (rc={rc}): {msg}')
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    check(rc, name)
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a CUDA(HIP) tensor, or None."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError('surreal_amd kernels take device (HIP) tensors; got a CPU tensor '
+                           '(there is no CPU fallback)')
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_workspaces = {}
+
+
+def ensure_workspace(device):
+    """Allocate and register the reduction workspace once per device."""
+    dev = torch.device(device)
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _workspaces:
+        nbytes = lib().smi_workspace_bytes()
+        ws = torch.zeros(nbytes // 4, dtype=torch.float32, device=dev)
+        _workspaces[key] = ws
+        check(lib().smi_set_workspace(ctypes.c_void_p(ws.data_ptr()), nbytes), 'smi_set_workspace')
+    return _workspaces[key]
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError('surreal_amd requires an AMD GPU (HIP); none is visible and there is '
+                           'no CPU fallback')

@@ -1,0 +1,59 @@
+"""Builds libsurreal_mi.so (gfx950) in-tree from surreal_amd/csrc/*.hip.
+
+Objects are compiled with hipcc for --offload-arch=gfx950 and linked against
+the HIP runtime that ships inside torch (same SONAME libamdhip64.so.7), with a
+RUNPATH to it, so a process that imports torch ends up with ONE HIP runtime
+whichever library is loaded first.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+ROOT = os.path.dirname(HERE)
+BUILD = os.path.join(ROOT, 'build', 'obj')
+LIB = os.path.join(HERE, 'libsurreal_mi.so')
+SOURCES = ['ppo_kernels.hip', 'ops_kernels.hip', 'sampler_kernels.hip', 'capi.hip']
+HEADERS = ['smi_device.hpp', 'smi_internal.hpp']
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = 'gfx950'
+CXXFLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-mcode-object-version=5',
+            '-Wall', '-Wno-unused-function']
+
+
+def torch_lib_dir():
+    import torch
+    return os.path.join(os.path.dirname(torch.__file__), 'lib')
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else -1.0
+
+
+def build(verbose=False, force=False):
+    os.makedirs(BUILD, exist_ok=True)
+    deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'surreal_mi.h')]
+    dep_t = max(_mtime(d) for d in deps)
+    objs = []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        op = os.path.join(BUILD, src.replace('.hip', '.o'))
+        objs.append(op)
+        if force or _mtime(op) < max(_mtime(sp), dep_t):
+            cmd = [HIPCC] + CXXFLAGS + ['-c', sp, '-o', op]
+            if verbose:
+                print(' '.join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+    if force or _mtime(LIB) < max(_mtime(o) for o in objs):
+        tl = torch_lib_dir()
+        cmd = ['g++', '-shared', '-o', LIB] + objs + [
+            f'-L{tl}', '-l:libamdhip64.so', f'-Wl,-rpath,{tl}', '-Wl,--no-undefined', '-lstdc++']
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == '__main__':
+    build(verbose=True, force='--force' in sys.argv)

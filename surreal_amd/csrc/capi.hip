@@ -1,0 +1,228 @@
+// capi.hip — the extern "C" boundary declared in include/surreal_mi.h.
+// Validates arguments, forwards to the launchers, and keeps the thread-local
+// error message for smi_last_error().
+#include <stdio.h>
+#include <string.h>
+#include "smi_device.hpp"
+#include "smi_internal.hpp"
+
+namespace smi {
+
+static thread_local char g_err[512] = "";
+
+int set_error(int code, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return -(int)e;
+  }
+  return SMI_OK;
+}
+
+// caller-registered device workspace (smi_set_workspace)
+static void* g_ws = nullptr;
+static int64_t g_ws_bytes = 0;
+float* workspace_f32(int64_t nfloats) {
+  if (!g_ws || nfloats * 4 > g_ws_bytes) return nullptr;
+  return static_cast<float*>(g_ws);
+}
+
+// declared in the other translation units
+int launch_zfilter_apply(const float*, float*, int64_t, int, const float*, const float*,
+                         const float*, float, hipStream_t);
+int launch_colstats(const float*, int64_t, int, int64_t, int, float*, float*, float*,
+                    hipStream_t);
+int launch_reward_filter(float*, int64_t, float, int, float*, float*, float*, float,
+                         hipStream_t);
+int launch_diag_gauss(const float*, const float*, const float*, int64_t, int, float*, float*,
+                      float*, float*, hipStream_t);
+int launch_mlp_forward(const float*, int, int, int, int, int, int, const float*, int64_t,
+                       int64_t, int, const float*, const float*, const float*, float, float*,
+                       hipStream_t);
+int launch_moments(const float*, int64_t, const double*, int, double*, hipStream_t);
+int launch_adam_clip(float*, const float*, float*, float*, int64_t, int*, const float*, float,
+                     float, float, float, float, const int*, float*, hipStream_t);
+int launch_ddpg_target(const float*, const float*, const float*, const float*, int64_t, float,
+                       float*, hipStream_t);
+void mt_seed_host(uint64_t, uint32_t*);
+int mt_randint_host(uint32_t*, int64_t, int64_t, int64_t*);
+int launch_mt_randint(uint32_t*, int64_t, int64_t, int64_t*, hipStream_t);
+int launch_gather_rows(const float*, int64_t, const int64_t*, int64_t, float*, hipStream_t);
+
+}  // namespace smi
+
+using namespace smi;
+
+#define SMI_STREAM(s) (static_cast<hipStream_t>(s))
+#define REQUIRE(cond, msg) \
+  do { if (!(cond)) return set_error(SMI_E_ARG, msg); } while (0)
+
+extern "C" {
+
+int smi_version(void) { return 1; }
+const char* smi_last_error(void) { return g_err; }
+
+/* Registers the device scratch used by the multi-workgroup reductions
+ * (colstats partials, Adam norm partials).  Not part of the reference API. */
+int smi_set_workspace(void* dev_ptr, int64_t bytes) {
+  g_ws = dev_ptr;
+  g_ws_bytes = bytes;
+  return SMI_OK;
+}
+int64_t smi_workspace_bytes(void) { return (int64_t)4 << 20; }
+
+int64_t smi_mlp_param_count(int in_dim, int h1, int h2, int out_dim, int with_log_var) {
+  return mlp_layout(in_dim, h1, h2, out_dim, with_log_var).fcount;
+}
+
+int64_t smi_ppo_fused_lds_bytes(int rows, int obs_dim, int h1, int h2, int act_dim,
+                                int critic_h1, int critic_h2) {
+  return fused_lds_bytes(rows, obs_dim, h1, h2, act_dim, critic_h1, critic_h2);
+}
+
+int smi_zfilter_apply(const float* x, float* out, int64_t rows, int dim, const float* rs,
+                      const float* rsq, const float* cnt, float eps, void* stream) {
+  REQUIRE(x && out && rs && rsq && cnt && rows >= 0 && dim > 0, "zfilter_apply: bad args");
+  return launch_zfilter_apply(x, out, rows, dim, rs, rsq, cnt, eps, SMI_STREAM(stream));
+}
+
+int smi_zfilter_update(const float* x, int64_t rows, int dim, int64_t row_stride, float* rs,
+                       float* rsq, float* cnt, void* stream) {
+  REQUIRE(x && rs && rsq && cnt && rows >= 0 && dim > 0 && row_stride >= dim,
+          "zfilter_update: bad args");
+  return launch_colstats(x, rows, dim, row_stride, 1, rs, rsq, cnt, SMI_STREAM(stream));
+}
+
+int smi_zfilter_colstats(const float* x, int64_t rows, int dim, int64_t row_stride,
+                         float* out_sum, float* out_sumsq, void* stream) {
+  REQUIRE(x && out_sum && out_sumsq && rows >= 0 && dim > 0 && row_stride >= dim,
+          "zfilter_colstats: bad args");
+  return launch_colstats(x, rows, dim, row_stride, 0, out_sum, out_sumsq, nullptr,
+                         SMI_STREAM(stream));
+}
+
+int smi_reward_filter(float* rewards, int64_t n, float reward_scale, int mode, float* rs,
+                      float* rsq, float* cnt, float eps, void* stream) {
+  REQUIRE(rewards && n >= 0 && mode >= 0 && mode <= 3, "reward_filter: bad args");
+  REQUIRE(mode == 0 || (rs && rsq && cnt), "reward_filter: filter buffers required");
+  return launch_reward_filter(rewards, n, reward_scale, mode, rs, rsq, cnt, eps,
+                              SMI_STREAM(stream));
+}
+
+int smi_diag_gauss(const float* actions, const float* prob0, const float* prob1, int64_t rows,
+                   int act_dim, float* loglik, float* lik, float* kl, float* entropy,
+                   void* stream) {
+  REQUIRE(prob0 && rows >= 0 && act_dim > 0, "diag_gauss: bad args");
+  REQUIRE(!(loglik || lik) || actions, "diag_gauss: actions required for loglik");
+  REQUIRE(!kl || prob1, "diag_gauss: prob1 required for kl");
+  if (rows == 0) return SMI_OK;
+  return launch_diag_gauss(actions, prob0, prob1, rows, act_dim, loglik, lik, kl, entropy,
+                           SMI_STREAM(stream));
+}
+
+int smi_mlp_forward(const float* params, int in_dim, int h1, int h2, int out_dim, int out_act,
+                    int with_log_var, const float* x, int64_t rows, int64_t row_stride,
+                    int use_zf, const float* zs, const float* zsq, const float* zc, float zeps,
+                    float* out, void* stream) {
+  REQUIRE(params && x && out && in_dim > 0 && h1 > 0 && h2 > 0 && out_dim > 0 && rows >= 0,
+          "mlp_forward: bad args");
+  REQUIRE(row_stride >= in_dim, "mlp_forward: row_stride < in_dim");
+  REQUIRE(out_act == ACT_NONE || out_act == ACT_TANH, "mlp_forward: out_act must be 0 or 2");
+  REQUIRE(!use_zf || (zs && zsq && zc), "mlp_forward: zfilter buffers required");
+  return launch_mlp_forward(params, in_dim, h1, h2, out_dim, out_act, with_log_var, x, rows,
+                            row_stride, use_zf, zs, zsq, zc, zeps, out, SMI_STREAM(stream));
+}
+
+int smi_ppo_critic_gae(const float* critic_params, int obs_dim, int h1, int h2, int use_zf,
+                       const float* zs, const float* zsq, const float* zc, float zeps,
+                       const float* obs, const float* obs_next, const float* rewards,
+                       const float* dones, int B, int T, const float* gtab, const float* ltab,
+                       float gamma, float gamma_T, float* values, float* adv_raw, float* ret,
+                       void* stream) {
+  REQUIRE(critic_params && obs && obs_next && rewards && dones && gtab && ltab && adv_raw && ret,
+          "ppo_critic_gae: null pointer");
+  REQUIRE(B >= 1 && T >= 1 && obs_dim >= 1 && h1 >= 1 && h2 >= 1, "ppo_critic_gae: bad dims");
+  REQUIRE(!use_zf || (zs && zsq && zc), "ppo_critic_gae: zfilter buffers required");
+  return launch_critic_gae(critic_params, obs_dim, h1, h2, use_zf, zs, zsq, zc, zeps, obs,
+                           obs_next, rewards, dones, B, T, gtab, ltab, gamma, gamma_T, values,
+                           adv_raw, ret, SMI_STREAM(stream));
+}
+
+int smi_gae_windows(float* values, const float* rewards, const float* dones, int64_t B, int T,
+                    int horizon, const float* gtab, const float* ltab, float gamma,
+                    float gamma_H, float* adv, float* ret, double* partials, int* n_partials,
+                    void* stream) {
+  REQUIRE(values && rewards && dones && gtab && ltab && adv && ret, "gae_windows: null pointer");
+  REQUIRE(B >= 0 && T >= 1, "gae_windows: bad dims");
+  if (B == 0) { if (n_partials) *n_partials = 0; return SMI_OK; }
+  return launch_gae_windows(values, rewards, dones, B, T, horizon, gtab, ltab, gamma, gamma_H,
+                            adv, ret, partials, n_partials, SMI_STREAM(stream));
+}
+
+int smi_gae_windows_max_partials(int64_t B, int T) { return gae_windows_max_partials(B, T); }
+
+int smi_moments(const float* x, int64_t n, const double* partials, int n_partials, double* out3,
+                void* stream) {
+  REQUIRE(out3 && (x || (partials && n_partials > 0)), "moments: bad args");
+  return launch_moments(x, n, partials, n_partials, out3, SMI_STREAM(stream));
+}
+
+int smi_ppo_update_fused(const smi_ppo_args* a, void* stream) {
+  REQUIRE(a, "ppo_update_fused: null args");
+  REQUIRE(a->obs && a->actions && a->behave && a->adv_raw && a->ret && a->actor &&
+              a->ref_actor && a->critic && a->actor_m && a->actor_v && a->critic_m &&
+              a->critic_v && a->actor_step && a->critic_step && a->hyper && a->stats,
+          "ppo_update_fused: null pointer");
+  REQUIRE(!a->use_zf || (a->zf_sum && a->zf_sumsq && a->zf_count && a->rzf_sum &&
+                         a->rzf_sumsq && a->rzf_count),
+          "ppo_update_fused: zfilter buffers required");
+  REQUIRE(a->mode == 0 || a->mode == 1, "ppo_update_fused: mode must be 0 (clip) or 1 (adapt)");
+  REQUIRE(a->epoch_policy >= 0 && a->epoch_baseline >= 0, "ppo_update_fused: bad epochs");
+  return launch_ppo_fused(a, SMI_STREAM(stream));
+}
+
+int smi_adam_clip(float* params, const float* grad, float* m, float* v, int64_t n, int* step,
+                  const float* lr_ptr, float beta1, float beta2, float eps, float weight_decay,
+                  float max_norm, const int* skip_flag, float* norm_out, void* stream) {
+  REQUIRE(params && grad && m && v && step && lr_ptr && n > 0, "adam_clip: bad args");
+  return launch_adam_clip(params, grad, m, v, n, step, lr_ptr, beta1, beta2, eps, weight_decay,
+                          max_norm, skip_flag, norm_out, SMI_STREAM(stream));
+}
+
+int smi_ddpg_target(const float* rewards, const float* dones, const float* q_next,
+                    const float* q_next2, int64_t n, float gamma_n, float* y, void* stream) {
+  REQUIRE(rewards && dones && q_next && y && n >= 0, "ddpg_target: bad args");
+  if (n == 0) return SMI_OK;
+  return launch_ddpg_target(rewards, dones, q_next, q_next2, n, gamma_n, y, SMI_STREAM(stream));
+}
+
+int smi_mt_seed(uint64_t seed, uint32_t* host_state625) {
+  REQUIRE(host_state625, "mt_seed: null state");
+  mt_seed_host(seed, host_state625);
+  return SMI_OK;
+}
+
+int smi_mt_randint_host(uint32_t* host_state625, int64_t n, int64_t batch, int64_t* out) {
+  REQUIRE(host_state625 && out && n >= 1 && n <= 0xffffffffLL && batch >= 0,
+          "mt_randint_host: bad args");
+  return mt_randint_host(host_state625, n, batch, out);
+}
+
+int smi_mt_randint(uint32_t* dev_state625, int64_t n, int64_t batch, int64_t* out_indices,
+                   void* stream) {
+  REQUIRE(dev_state625 && out_indices && batch >= 0, "mt_randint: bad args");
+  return launch_mt_randint(dev_state625, n, batch, out_indices, SMI_STREAM(stream));
+}
+
+int smi_gather_rows(const float* table, int64_t cols, const int64_t* idx, int64_t batch,
+                    float* out, void* stream) {
+  REQUIRE(table && idx && out && cols > 0 && batch >= 0, "gather_rows: bad args");
+  return launch_gather_rows(table, cols, idx, batch, out, SMI_STREAM(stream));
+}
+
+}  // extern "C"

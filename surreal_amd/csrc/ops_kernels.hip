@@ -1,0 +1,448 @@
+// ops_kernels.hip — elementwise / reduction kernels of the learner hot path and
+// the standalone model ops behind the PPOModel / ZFilter / DiagGauss mirrors.
+//
+//   zfilter_apply / zfilter_colstats / zfilter_update   z_filter.py:44-79
+//   reward_filter                                        reward_filter.py:18-56
+//   diag_gauss                                           ppo_net.py:29-72
+//   mlp_forward                                          ppo_net.py:253-315
+//   moments                                              ppo.py:402-405,413-416
+//   adam_clip                                            ppo.py:243-247 (torch Adam)
+//   ddpg_target                                          ddpg.py:279-283
+#include "smi_device.hpp"
+#include "smi_internal.hpp"
+
+namespace smi {
+
+// ------------------------------------------------------------- ZFilter apply
+__global__ void __launch_bounds__(kWG)
+zfilter_apply_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t n, int dim,
+                     const float* sum, const float* sumsq, const float* count, float eps) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* zm = sm;
+  float* zs = sm + round4(dim);
+  zfilter_colstats(sum, sumsq, count, eps, dim, zm, zs);
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
+    const int c = (int)(i % dim);
+    float v = (x[i] - zm[c]) / zs[c];
+    out[i] = fminf(fmaxf(v, -5.f), 5.f);
+  }
+}
+
+// ------------------------------------------------ ZFilter column statistics
+// Column sums and sums of squares over `rows` strided rows.  Each workgroup
+// owns a column slab of width <= 64 and a row range; partial sums go to
+// `part` [gridDim.y][2][dim], reduced in a fixed order by the finisher.
+__global__ void __launch_bounds__(kWG)
+colstats_partial_kernel(const float* __restrict__ x, int64_t rows, int dim, int64_t stride,
+                        float* __restrict__ part) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;            // 4 row lanes
+  __shared__ float s1[kNW][64], s2[kNW][64];
+  float a1 = 0.f, a2 = 0.f;
+  if (c < dim) {
+    for (int64_t r = (int64_t)blockIdx.y * kNW + rl; r < rows; r += (int64_t)gridDim.y * kNW) {
+      const float v = x[r * stride + c];
+      a1 += v;
+      a2 += v * v;
+    }
+  }
+  s1[rl][threadIdx.x & 63] = a1;
+  s2[rl][threadIdx.x & 63] = a2;
+  __syncthreads();
+  if (rl == 0 && c < dim) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int w = 0; w < kNW; ++w) { t1 += s1[w][threadIdx.x]; t2 += s2[w][threadIdx.x]; }
+    part[((int64_t)blockIdx.y * 2) * dim + c] = t1;
+    part[((int64_t)blockIdx.y * 2 + 1) * dim + c] = t2;
+  }
+}
+
+// finisher: mode 0 -> write sums; mode 1 -> add into running buffers and count
+__global__ void __launch_bounds__(kWG)
+colstats_finish_kernel(const float* __restrict__ part, int nparts, int dim, int64_t rows,
+                       int mode, float* out_sum, float* out_sumsq, float* count) {
+  for (int c = threadIdx.x + blockIdx.x * kWG; c < dim; c += gridDim.x * kWG) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int p = 0; p < nparts; ++p) {
+      t1 += part[((int64_t)p * 2) * dim + c];
+      t2 += part[((int64_t)p * 2 + 1) * dim + c];
+    }
+    if (mode == 0) {
+      out_sum[c] = t1;
+      out_sumsq[c] = t2;
+    } else {
+      out_sum[c] += t1;      // running_sum += torch.sum(x, 0)   (z_filter.py:54)
+      out_sumsq[c] += t2;    // running_sumsq += torch.sum(x*x, 0) (z_filter.py:55)
+    }
+  }
+  if (mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) count[0] += (float)rows;  // :56
+}
+
+// Single-pass variant for small inputs: one workgroup, no partial buffer.
+__global__ void __launch_bounds__(kWG)
+colstats_small_kernel(const float* __restrict__ x, int64_t rows, int dim, int64_t stride,
+                      int mode, float* out_sum, float* out_sumsq, float* count) {
+  __shared__ float s1[kNW][64], s2[kNW][64];
+  const int rl = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  for (int c0 = 0; c0 < dim; c0 += 64) {
+    const int c = c0 + cl;
+    float a1 = 0.f, a2 = 0.f;
+    if (c < dim)
+      for (int64_t r = rl; r < rows; r += kNW) {
+        const float v = x[r * stride + c];
+        a1 += v;
+        a2 += v * v;
+      }
+    s1[rl][cl] = a1; s2[rl][cl] = a2;
+    __syncthreads();
+    if (rl == 0 && c < dim) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int w = 0; w < kNW; ++w) { t1 += s1[w][cl]; t2 += s2[w][cl]; }
+      if (mode == 0) { out_sum[c] = t1; out_sumsq[c] = t2; }
+      else { out_sum[c] += t1; out_sumsq[c] += t2; }
+    }
+    __syncthreads();
+  }
+  if (mode == 1 && threadIdx.x == 0) count[0] += (float)rows;
+}
+
+// ------------------------------------------------------------- RewardFilter
+// rewards *= reward_scale (ppo.py:452); then, by mode bits,
+//   1: forward  — clamp((r - mean)/max(sqrt(sumsq/count - mean^2), eps), +-5)
+//      with the running stats from BEFORE this call's update (reward_filter.py:44-56)
+//   2: update   — count += n, running_sum += sum(r), running_sumsq = sum(r*r)
+//      (the reference's '=' instead of '+=' at reward_filter.py:42 is kept)
+__global__ void __launch_bounds__(kWG)
+reward_filter_kernel(float* __restrict__ r, int64_t n, float scale, int mode,
+                     float* rsum, float* rsumsq, float* rcount, float eps) {
+  __shared__ double scr[kNW];
+  float mean = 0.f, sd = 1.f;
+  if (mode & 1) {
+    const float cnt = rcount[0];
+    mean = rsum[0] / cnt;
+    const float v = rsumsq[0] / cnt - mean * mean;
+    sd = sqrtf(v);
+    sd = sd < eps ? eps : sd;
+  }
+  double a1 = 0.0, a2 = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += kWG) {
+    const float x = r[i] * scale;
+    a1 += (double)x;
+    a2 += (double)(x * x);
+    if (mode & 1) {
+      const float y = (x - mean) / sd;
+      r[i] = fminf(fmaxf(y, -5.f), 5.f);
+    } else {
+      r[i] = x;
+    }
+  }
+  if (mode & 2) {
+    const double t1 = block_sum_d(a1, scr);
+    const double t2 = block_sum_d(a2, scr);
+    if (threadIdx.x == 0) {
+      rcount[0] = rcount[0] + (float)n;
+      rsum[0] = rsum[0] + (float)t1;
+      rsumsq[0] = (float)t2;
+    }
+  }
+}
+
+// ------------------------------------------------------------ DiagGauss ops
+__global__ void __launch_bounds__(kWG)
+diag_gauss_kernel(const float* __restrict__ a, const float* __restrict__ p0,
+                  const float* __restrict__ p1, int64_t rows, int A, float c_ll, float c_ent,
+                  float* loglik, float* lik, float* kl, float* ent) {
+  for (int64_t r = (int64_t)blockIdx.x * kWG + threadIdx.x; r < rows; r += (int64_t)gridDim.x * kWG) {
+    const float* q0 = p0 + r * 2 * A;
+    if (loglik || lik) {
+      float s = 0.f, l = 0.f;
+      for (int j = 0; j < A; ++j) {
+        const float u = (a[r * A + j] - q0[j]) / q0[A + j];
+        s += u * u;
+        l += logf(q0[A + j]);
+      }
+      const float ll = (-0.5f * s - c_ll) - l;
+      if (loglik) loglik[r] = ll;
+      if (lik) lik[r] = fmaxf(expf(ll), 1e-5f);
+    }
+    if (kl && p1) {
+      const float* q1 = p1 + r * 2 * A;
+      float s1 = 0.f, s2 = 0.f;
+      for (int j = 0; j < A; ++j) {
+        s1 += logf(q1[A + j] / q0[A + j]);
+        const float d = q0[j] - q1[j];
+        s2 += (q0[A + j] * q0[A + j] + d * d) / (2.f * (q1[A + j] * q1[A + j]));
+      }
+      kl[r] = (s1 + s2) - 0.5f * (float)A;
+    }
+    if (ent) {
+      float l = 0.f;
+      for (int j = 0; j < A; ++j) l += logf(q0[A + j]);
+      ent[r] = 0.5f * l + c_ent;
+    }
+  }
+}
+
+// -------------------------------------------------------------- MLP forward
+struct MlpFwdArgs {
+  const float* params; int in, h1, h2, out, act, lv;
+  const float* x; int64_t rows, stride;
+  int use_zf; const float *zsum, *zsumsq, *zcount; float zeps;
+  float* y; int params_in_lds;
+};
+
+__global__ void __launch_bounds__(kWG)
+mlp_forward_kernel(MlpFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const MlpLayout L = mlp_layout(a.in, a.h1, a.h2, a.out, a.lv);
+  const int ldX = pad_ld(a.in), ldH1 = pad_ld(a.h1), ldH2 = pad_ld(a.h2), ldO = pad_small(a.out);
+  float* zm = sm;
+  float* zs = zm + round4(a.in);
+  float* X0 = zs + round4(a.in);
+  float* H1 = X0 + kRT * ldX;
+  float* H2 = H1 + kRT * ldH1;
+  float* OUT = H2 + kRT * ldH2;
+  float* P = OUT + kRT * ldO;
+  if (a.use_zf) zfilter_colstats(a.zsum, a.zsumsq, a.zcount, a.zeps, a.in, zm, zs);
+  MlpView V;
+  if (a.params_in_lds) { mlp_load_lds(L, a.params, P); V = view_padded(L, P); }
+  else V = view_flat(L, a.params);
+  for (int e = threadIdx.x; e < kRT * (ldH1 + ldH2 + ldO); e += kWG) H1[e] = 0.f;
+  __syncthreads();
+  const int ntiles = (int)((a.rows + kRT - 1) / kRT);
+  const int ocols = a.lv ? 2 * a.out : a.out;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t r0 = (int64_t)tile * kRT;
+    const int nr = (int)min((int64_t)kRT, a.rows - r0);
+    load_obs_tile(a.x + r0 * a.stride, a.stride, nr, a.in, a.use_zf ? zm : nullptr, zs, X0, ldX);
+    __syncthreads();
+    dense_fwd<ACT_RELU>(X0, ldX, V.W1, V.ld1, V.b1, a.in, a.h1, H1, ldH1);
+    __syncthreads();
+    dense_fwd<ACT_RELU>(H1, ldH1, V.W2, V.ld2, V.b2, a.h1, a.h2, H2, ldH2);
+    __syncthreads();
+    if (a.act == ACT_TANH) dense_fwd<ACT_TANH>(H2, ldH2, V.W3, V.ld3, V.b3, a.h2, a.out, OUT, ldO);
+    else dense_fwd<ACT_NONE>(H2, ldH2, V.W3, V.ld3, V.b3, a.h2, a.out, OUT, ldO);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nr * ocols; e += kWG) {
+      const int r = e / ocols, j = e - r * ocols;
+      const float v = j < a.out ? OUT[r * ldO + j] : expf(V.lv[j - a.out]);
+      a.y[(r0 + r) * ocols + j] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// -------------------------------------------------------------- moments
+__global__ void __launch_bounds__(kWG)
+moments_kernel(const float* __restrict__ x, int64_t n, const double* partials, int np,
+               double* out) {
+  __shared__ double scr[kNW];
+  double a1 = 0.0, a2 = 0.0;
+  if (partials && np > 0) {
+    for (int i = threadIdx.x; i < np; i += kWG) { a1 += partials[2 * i]; a2 += partials[2 * i + 1]; }
+  } else {
+    for (int64_t i = threadIdx.x; i < n; i += kWG) {
+      const double v = (double)x[i];
+      a1 += v;
+      a2 += v * v;
+    }
+  }
+  const double t1 = block_sum_d(a1, scr);
+  const double t2 = block_sum_d(a2, scr);
+  if (threadIdx.x == 0) { out[0] = t1; out[1] = t2; out[2] = (double)n; }
+}
+
+// ------------------------------------------------------------ Adam + clip
+// Two kernels: partial sums of squares per workgroup, then the update (every
+// workgroup recomputes the global norm from the partials in the same order, so
+// the coefficient is identical everywhere without a grid barrier).
+__global__ void __launch_bounds__(kWG)
+sumsq_partial_kernel(const float* __restrict__ g, int64_t n, double* part) {
+  __shared__ double scr[kNW];
+  double a = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
+    const double v = (double)g[i];
+    a += v * v;
+  }
+  a = block_sum_d(a, scr);
+  if (threadIdx.x == 0) part[blockIdx.x] = a;
+}
+
+__global__ void __launch_bounds__(kWG)
+adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+            float* __restrict__ v, int64_t n, int* step, const float* lr_ptr, float beta1,
+            float beta2, float eps, float wd, float max_norm, const double* part, int np,
+            const int* skip, float* norm_out) {
+  if (skip && skip[0] != 0) return;
+  __shared__ float s_coef;
+  __shared__ int s_t;
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < np; ++i) s += part[i];
+    const float norm = (float)sqrt(s);
+    float coef = 1.f;
+    if (max_norm > 0.f) {
+      const float cc = max_norm / (norm + 1e-6f);
+      coef = cc < 1.f ? cc : 1.f;
+    }
+    s_coef = coef;
+    s_t = step[0] + 1;
+    if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+  }
+  __syncthreads();
+  const int t = s_t;
+  const float coef = s_coef;
+  const double bc1 = 1.0 - pow((double)beta1, (double)t);
+  const double bc2 = 1.0 - pow((double)beta2, (double)t);
+  const float lr = lr_ptr[0];
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  const float w1 = (float)(1.0 - (double)beta1);
+  const float w2 = (float)(1.0 - (double)beta2);
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
+    float gi = g[i] * coef;
+    float pi = p[i];
+    if (wd != 0.f) gi = gi + wd * pi;
+    float mi = m[i], vi = v[i];
+    mi = mi + w1 * (gi - mi);
+    vi = vi * beta2 + (w2 * gi) * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi + (-step_size) * (mi / denom);
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+// step counter increment after every workgroup of adam_kernel has read it
+__global__ void step_inc_kernel(int* step, const int* skip) {
+  if (skip && skip[0] != 0) return;
+  step[0] += 1;
+}
+
+// ------------------------------------------------------------- DDPG target
+__global__ void __launch_bounds__(kWG)
+ddpg_target_kernel(const float* __restrict__ r, const float* __restrict__ d,
+                   const float* __restrict__ q, const float* __restrict__ q2, int64_t n,
+                   float gn, float* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
+    const float nd = 1.f - d[i];
+    float v = r[i] + (gn * q[i]) * nd;     // r + gamma^n * Q' * (1 - done)
+    if (q2) {
+      const float v2 = r[i] + (gn * q2[i]) * nd;
+      v = fminf(v, v2);                       // torch.min(y, y2)
+    }
+    y[i] = v;
+  }
+}
+
+static int grid_for(int64_t n, int cap = 2048) {
+  int64_t g = (n + kWG - 1) / kWG;
+  if (g < 1) g = 1;
+  return (int)(g < cap ? g : cap);
+}
+
+// ============================================================ launchers
+int launch_zfilter_apply(const float* x, float* out, int64_t rows, int dim, const float* s,
+                         const float* sq, const float* cnt, float eps, hipStream_t st) {
+  const int64_t n = rows * dim;
+  if (n == 0) return SMI_OK;
+  hipLaunchKernelGGL(zfilter_apply_kernel, dim3(grid_for(n)), dim3(kWG),
+                     (size_t)(2 * round4(dim) * 4), st, x, out, n, dim, s, sq, cnt, eps);
+  return check_launch("zfilter_apply_kernel");
+}
+
+// scratch for colstats partials: caller-provided workspace is avoided by
+// bounding the partial count; the partial buffer lives in a static device
+// allocation made once at library load (see capi.cpp: smi_workspace()).
+float* workspace_f32(int64_t nfloats);
+
+int launch_colstats(const float* x, int64_t rows, int dim, int64_t stride, int mode,
+                    float* osum, float* osq, float* cnt, hipStream_t st) {
+  if (rows * (int64_t)dim <= (int64_t)1 << 16) {
+    hipLaunchKernelGGL(colstats_small_kernel, dim3(1), dim3(kWG), 0, st, x, rows, dim, stride,
+                       mode, osum, osq, cnt);
+    return check_launch("colstats_small_kernel");
+  }
+  const int gx = (dim + 63) / 64;
+  int gy = (int)((rows + 1023) / 1024);
+  if (gy > 512) gy = 512;
+  float* part = workspace_f32((int64_t)gy * 2 * dim);
+  if (!part) return set_error(SMI_E_ARG, "colstats: workspace unavailable");
+  hipLaunchKernelGGL(colstats_partial_kernel, dim3(gx, gy), dim3(kWG), 0, st, x, rows, dim,
+                     stride, part);
+  int rc = check_launch("colstats_partial_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(colstats_finish_kernel, dim3((dim + kWG - 1) / kWG), dim3(kWG), 0, st,
+                     part, gy, dim, rows, mode, osum, osq, cnt);
+  return check_launch("colstats_finish_kernel");
+}
+
+int launch_reward_filter(float* r, int64_t n, float scale, int use, float* s, float* sq,
+                         float* c, float eps, hipStream_t st) {
+  hipLaunchKernelGGL(reward_filter_kernel, dim3(1), dim3(kWG), 0, st, r, n, scale, use, s, sq,
+                     c, eps);
+  return check_launch("reward_filter_kernel");
+}
+
+int launch_diag_gauss(const float* a, const float* p0, const float* p1, int64_t rows, int A,
+                      float* ll, float* lik, float* kl, float* ent, hipStream_t st) {
+  const float c_ll = (float)(0.5 * log(2.0 * 3.141592653589793) * (double)A);
+  const float c_ent = (float)(0.5 * log(2.0 * 3.141592653589793 * 2.718281828459045) * (double)A);
+  hipLaunchKernelGGL(diag_gauss_kernel, dim3(grid_for(rows)), dim3(kWG), 0, st, a, p0, p1, rows,
+                     A, c_ll, c_ent, ll, lik, kl, ent);
+  return check_launch("diag_gauss_kernel");
+}
+
+int launch_mlp_forward(const float* params, int in, int h1, int h2, int out, int act, int lv,
+                       const float* x, int64_t rows, int64_t stride, int use_zf,
+                       const float* zs, const float* zsq, const float* zc, float zeps,
+                       float* y, hipStream_t st) {
+  MlpFwdArgs a;
+  a.params = params; a.in = in; a.h1 = h1; a.h2 = h2; a.out = out; a.act = act; a.lv = lv;
+  a.x = x; a.rows = rows; a.stride = stride; a.use_zf = use_zf; a.zsum = zs; a.zsumsq = zsq;
+  a.zcount = zc; a.zeps = zeps; a.y = y;
+  const MlpLayout L = mlp_layout(in, h1, h2, out, lv);
+  const int64_t base = 2 * round4(in) +
+                       (int64_t)kRT * (pad_ld(in) + pad_ld(h1) + pad_ld(h2) + pad_small(out));
+  a.params_in_lds = ((base + L.pcount) * 4 <= 64 * 1024) ? 1 : 0;
+  const int64_t lds = (base + (a.params_in_lds ? L.pcount : 0)) * 4;
+  if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "mlp_forward: LDS does not fit");
+  const int64_t ntiles = (rows + kRT - 1) / kRT;
+  if (ntiles == 0) return SMI_OK;
+  const int grid = (int)(ntiles < 1024 ? ntiles : 1024);
+  hipLaunchKernelGGL(mlp_forward_kernel, dim3(grid), dim3(kWG), (size_t)lds, st, a);
+  return check_launch("mlp_forward_kernel");
+}
+
+int launch_moments(const float* x, int64_t n, const double* part, int np, double* out,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(kWG), 0, st, x, n, part, np, out);
+  return check_launch("moments_kernel");
+}
+
+int launch_adam_clip(float* p, const float* g, float* m, float* v, int64_t n, int* step,
+                     const float* lr, float b1, float b2, float eps, float wd, float max_norm,
+                     const int* skip, float* norm_out, hipStream_t st) {
+  const int grid = grid_for(n, 512);
+  double* part = reinterpret_cast<double*>(workspace_f32(2 * 512));
+  if (!part) return set_error(SMI_E_ARG, "adam: workspace unavailable");
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kWG), 0, st, g, n, part);
+  int rc = check_launch("sumsq_partial_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kWG), 0, st, p, g, m, v, n, step, lr, b1, b2,
+                     eps, wd, max_norm, part, grid, skip, norm_out);
+  rc = check_launch("adam_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step, skip);
+  return check_launch("step_inc_kernel");
+}
+
+int launch_ddpg_target(const float* r, const float* d, const float* q, const float* q2,
+                       int64_t n, float gn, float* y, hipStream_t st) {
+  hipLaunchKernelGGL(ddpg_target_kernel, dim3(grid_for(n)), dim3(kWG), 0, st, r, d, q, q2, n, gn,
+                     y);
+  return check_launch("ddpg_target_kernel");
+}
+
+}  // namespace smi

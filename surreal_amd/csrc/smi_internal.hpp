@@ -1,0 +1,28 @@
+// smi_internal.hpp — host-side plumbing shared by the .hip translation units:
+// error state for smi_last_error() and launch checking.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/surreal_mi.h"
+
+namespace smi {
+
+int set_error(int code, const char* msg);
+int check_launch(const char* what);
+
+int64_t fused_lds_bytes(int B, int D, int H1, int H2, int A, int cH1, int cH2);
+
+int launch_critic_gae(const float* critic_params, int D, int H1, int H2, int use_zf,
+                      const float* zf_sum, const float* zf_sumsq, const float* zf_count,
+                      float zf_eps, const float* obs, const float* obs_next,
+                      const float* rewards, const float* dones, int B, int T,
+                      const float* gtab, const float* ltab, float gamma, float gamma_T,
+                      float* values, float* adv, float* ret, hipStream_t stream);
+int gae_windows_max_partials(int64_t B, int T);
+int launch_gae_windows(float* values, const float* rewards, const float* dones, int64_t B,
+                       int T, int H, const float* gtab, const float* ltab, float gamma,
+                       float gamma_H, float* adv, float* ret, double* partials,
+                       int* n_partials, hipStream_t stream);
+int launch_ppo_fused(const smi_ppo_args* args, hipStream_t stream);
+
+}  // namespace smi

@@ -1,0 +1,414 @@
+"""PPOLearner / DDPGLearner mirrors (surreal/learner/ppo.py, ddpg.py) whose
+learn() runs as a short sequence of HIP launches on one stream:
+
+  PPO learn()  (ppo.py:588-613)
+    1. smi_reward_filter     reward_scale [+ RewardFilter]        ppo.py:452-456
+    2. smi_ppo_critic_gae    critic fwd over B(T+1) rows + GAE     ppo.py:355-418
+    3. smi_ppo_update_fused  ref_pol, <=epoch_policy actor updates
+                             with KL early stop, epoch_baseline
+                             critic updates, statistics            ppo.py:487-576
+    4. smi_zfilter_update    z_update(obs_iter)                     ppo.py:578-582
+No host synchronisation happens inside learn(): statistics, the KL record and
+the Adam step counters stay on the device until something asks for them
+(last_stats(), _post_publish()).  The data-dependent branches of the reference
+(KL early stop ppo.py:556, adapt penalty ppo.py:275) are evaluated on device.
+
+Construction needs no tensorplex/loggerplex/ZMQ: metrics go to an injectable
+`metrics` callable and parameters to an injectable `publisher` callable.
+"""
+import math
+import time
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .aggregator import MultistepAggregatorWithInfo, SSARAggregator, stage
+from .config import Config, ConfigError
+from .model import DiagGauss, PPOModel, RewardFilter
+
+
+def _as_config(c):
+    return c if isinstance(c, Config) else Config(c or {})
+
+
+class LinearWithMinLR(object):
+    """Learning-rate schedule named by the reference config
+    (ppo_configs.py:43-46).  torchx's implementation is not available; this is
+    the build's statement of it: every `update_freq` scheduler steps the rate
+    decays linearly from the initial value towards `min_lr` over `num_updates`
+    steps, never below `min_lr`.  With the default min_lr == lr it is constant."""
+
+    def __init__(self, lr, num_updates, update_freq=1, min_lr=0.0):
+        self.base_lr = float(lr)
+        self.num_updates = max(1, int(num_updates))
+        self.update_freq = max(1, int(update_freq))
+        self.min_lr = float(min_lr)
+        self.steps = 0
+
+    def step(self):
+        self.steps += 1
+
+    def get_lr(self):
+        k = (self.steps // self.update_freq) * self.update_freq
+        frac = min(1.0, k / self.num_updates)
+        return [max(self.min_lr, self.base_lr - (self.base_lr - self.min_lr) * frac)]
+
+    def state_dict(self):
+        return {'steps': self.steps}
+
+    def load_state_dict(self, d):
+        self.steps = int(d['steps'])
+
+
+class PPOLearner(object):
+    """ppo.py:12-682 on MI355X.  Same constructor, learn/module_dict/
+    publish_parameter/checkpoint_attributes/preprocess/_prefetcher_preprocess."""
+
+    def __init__(self, learner_config, env_config, session_config=None, metrics=None,
+                 publisher=None, device=None, seed=0):
+        L.require_gpu()
+        self.learner_config = lc = _as_config(learner_config)
+        self.env_config = ec = _as_config(env_config)
+        self.session_config = _as_config(session_config)
+        self.metrics = metrics
+        self.publisher = publisher
+        self.device = torch.device(device) if device is not None else \
+            torch.device('cuda', torch.cuda.current_device())
+        L.ensure_workspace(self.device)
+
+        self.current_iteration = 0
+        self.global_step = 0
+        algo = lc.algo
+        self.gamma = algo.gamma
+        self.lam = algo.advantage.lam
+        self.n_step = algo.n_step
+        self.use_z_filter = algo.use_z_filter
+        self.use_r_filter = algo.use_r_filter
+        self.norm_adv = algo.advantage.norm_adv
+        self.batch_size = lc.replay.batch_size
+        self.action_dim = ec.action_spec['dim'][0]
+        self.obs_spec = ec.obs_spec
+        self.init_log_sig = algo.consts.init_log_sig
+        self.ppo_mode = algo.ppo_mode
+        self.if_rnn_policy = algo.rnn.if_rnn_policy
+        self.horizon = algo.rnn.horizon
+        self.lr_actor = algo.network.lr_actor
+        self.lr_critic = algo.network.lr_critic
+        self.epoch_policy = algo.consts.epoch_policy
+        self.epoch_baseline = algo.consts.epoch_baseline
+        self.kl_target = algo.consts.kl_target
+        self.adjust_threshold = algo.consts.adjust_threshold
+        self.reward_scale = algo.advantage.reward_scale
+        self.kl_cutoff_coeff = algo.adapt_consts.kl_cutoff_coeff
+        self.beta_init = algo.adapt_consts.beta_init
+        self.beta_range = algo.adapt_consts.beta_range
+        self.clip_range = algo.clip_consts.clip_range
+        self.clip_epsilon_init = algo.clip_consts.clip_epsilon_init
+        if self.ppo_mode == 'adapt':
+            self.beta = self.beta_init
+            self.eta = self.kl_cutoff_coeff
+            self.beta_upper, self.beta_lower = self.beta_range[1], self.beta_range[0]
+            self.beta_adjust_threshold = self.adjust_threshold
+            self.clip_epsilon = self.clip_epsilon_init
+        elif self.ppo_mode == 'clip':
+            self.clip_epsilon = self.clip_epsilon_init
+            self.clip_adjust_threshold = self.adjust_threshold
+            self.clip_upper, self.clip_lower = self.clip_range[1], self.clip_range[0]
+            self.beta = self.beta_init
+        else:
+            raise ConfigError('ppo_mode must be clip or adapt')
+        if self.if_rnn_policy:
+            raise NotImplementedError('surreal_amd: RNN (LSTM) PPO policy is SURVEY §8(f) rank 1; '
+                                      'set algo.rnn.if_rnn_policy=False')
+        if ec.get('pixel_input', False):
+            raise NotImplementedError('surreal_amd: pixel inputs are SURVEY §8(f) rank 1')
+
+        anneal = algo.network.anneal
+        num_updates = int(anneal.frames_to_anneal / lc.parameter_publish.exp_interval)
+        self.exp_counter = 0
+        self.kl_record = []
+
+        gen = torch.Generator().manual_seed(seed)
+        mk = lambda: PPOModel(self.obs_spec, self.action_dim, lc.model, True, self.init_log_sig,  # noqa: E731
+                              self.use_z_filter, False, algo.rnn, self.device, gen)
+        self.model = mk()
+        self.ref_target_model = mk()
+        self.ref_target_model.update_target_params(self.model)
+
+        net = algo.network
+        self.clip_actor_gradient = net.clip_actor_gradient
+        self.actor_gradient_clip_value = net.actor_gradient_norm_clip
+        self.clip_critic_gradient = net.clip_critic_gradient
+        self.critic_gradient_clip_value = net.critic_gradient_norm_clip
+        self.actor_regularization = net.actor_regularization
+        self.critic_regularization = net.critic_regularization
+        # Adam state (torch.optim.Adam defaults: betas (0.9, 0.999), eps 1e-8)
+        dev = self.device
+        self.adam_betas, self.adam_eps = (0.9, 0.999), 1e-8
+        self.actor_m = torch.zeros_like(self.model.actor.flat)
+        self.actor_v = torch.zeros_like(self.model.actor.flat)
+        self.critic_m = torch.zeros_like(self.model.critic.flat)
+        self.critic_v = torch.zeros_like(self.model.critic.flat)
+        self.actor_step = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.critic_step = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.actor_lr_scheduler = LinearWithMinLR(self.lr_actor, num_updates,
+                                                  anneal.lr_update_frequency, anneal.min_lr)
+        self.critic_lr_scheduler = LinearWithMinLR(self.lr_critic, num_updates,
+                                                   anneal.lr_update_frequency, anneal.min_lr)
+        self.hyper = torch.zeros(L.HYP_COUNT, dtype=torch.float32, device=dev)
+        self._write_hyper()
+
+        self.aggregator = MultistepAggregatorWithInfo(self.obs_spec, ec.action_spec)
+        self.pd = DiagGauss(self.action_dim)
+        self.cells = None
+        if self.use_r_filter:
+            self.reward_filter = RewardFilter(device=dev)
+
+        # device-resident learn() state
+        self.stats_buf = torch.zeros(L.ST_COUNT, dtype=torch.float32, device=dev)
+        self.kl_capacity = 1 << 16
+        self.kl_record_buf = torch.zeros(self.kl_capacity, dtype=torch.float32, device=dev)
+        self.kl_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        idx = torch.tensor(range(self.n_step), dtype=torch.float32)
+        self.gamma_tab = torch.pow(self.gamma, idx).to(dev)        # ppo.py:372-374
+        self.lam_tab = torch.pow(self.lam, idx).to(dev)
+        self._bufs = {}
+        self._pinned = {}
+        self._args = L.PPOArgs()
+        # optional per-kernel HIP event timing: {kernel name: [(start, end), ...]}
+        self.kernel_events = None
+
+    def _ev(self, name):
+        """Context for recording a (start, end) event pair around one launch."""
+        learner = self
+
+        class _Ctx(object):
+            def __enter__(self):
+                if learner.kernel_events is not None:
+                    self.s = torch.cuda.Event(enable_timing=True)
+                    self.e = torch.cuda.Event(enable_timing=True)
+                    self.s.record()
+                return self
+
+            def __exit__(self, *exc):
+                if learner.kernel_events is not None:
+                    self.e.record()
+                    learner.kernel_events.setdefault(name, []).append((self.s, self.e))
+                return False
+        return _Ctx()
+
+    # ------------------------------------------------------------ helpers
+    def _write_hyper(self):
+        h = np.zeros(L.HYP_COUNT, dtype=np.float32)
+        h[L.HYP_CLIP_EPS] = self.clip_epsilon
+        h[L.HYP_BETA] = self.beta
+        h[L.HYP_LR_ACTOR] = self.actor_lr_scheduler.get_lr()[0] if hasattr(self, 'actor_lr_scheduler') else self.lr_actor
+        h[L.HYP_LR_CRITIC] = self.critic_lr_scheduler.get_lr()[0] if hasattr(self, 'critic_lr_scheduler') else self.lr_critic
+        h[L.HYP_CLIP_LO] = np.float32(1 - self.clip_epsilon)     # torch.clamp scalar bounds
+        h[L.HYP_CLIP_HI] = np.float32(1 + self.clip_epsilon)
+        self.hyper.copy_(torch.from_numpy(h))
+
+    def _buf(self, name, shape, dtype=torch.float32):
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape):
+            t = torch.zeros(shape, dtype=dtype, device=self.device)
+            self._bufs[name] = t
+        return t
+
+    def _low_dim(self, obs):
+        if isinstance(obs, torch.Tensor):
+            return obs
+        parts = [obs['low_dim'][k] for k in obs['low_dim']]
+        return parts[0] if len(parts) == 1 else torch.cat(parts, -1)
+
+    # ------------------------------------------------------- reference API
+    def _preprocess_batch_ppo(self, batch):                 # ppo.py:420-484
+        if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
+            batch = stage(batch, self.device, self._pinned)
+        else:
+            batch = dict(batch)
+        rewards = batch['rewards'].to(torch.float32).contiguous().clone()   # filtered in place
+        if self.use_r_filter:
+            self.reward_filter.scale_forward_update_(rewards, self.reward_scale)
+        elif self.reward_scale != 1.0:
+            L.call('smi_reward_filter', L.ptr(rewards), rewards.numel(), float(self.reward_scale),
+                   0, None, None, None, 0.0, L.stream(self.device))
+        batch['rewards'] = rewards
+        return Config(batch) if not isinstance(batch, Config) else batch
+
+    def _optimize(self, obs, actions, rewards, obs_next, persistent_infos, onetime_infos, dones):
+        """ppo.py:487-586 (non-RNN low-dim model)."""
+        x = self._low_dim(obs).contiguous()
+        xn = self._low_dim(obs_next).contiguous()
+        B, T, D = x.shape
+        if B != self.batch_size or T != self.n_step:
+            raise ValueError(f'batch shape (B={B}, T={T}) != config (batch_size={self.batch_size}, '
+                             f'n_step={self.n_step})')
+        A = self.action_dim
+        pds = persistent_infos[-1].contiguous()
+        actions = actions.contiguous()
+        dones = dones.contiguous()
+        st = L.stream(self.device)
+        m, rm = self.model, self.ref_target_model
+        zf = m.z_filter if self.use_z_filter else None
+        rzf = rm.z_filter if self.use_z_filter else None
+        c_h1, c_h2 = self.learner_config.model.critic_fc_hidden_sizes
+        a_h1, a_h2 = self.learner_config.model.actor_fc_hidden_sizes
+        values = self._buf('values', (B, T + 1))
+        adv_raw = self._buf('adv_raw', (B,))
+        ret = self._buf('ret', (B,))
+        zp = (lambda t: L.ptr(t) if zf is not None else None)
+        # --- GAE over the critic (ppo.py:355-418)
+        with self._ev('critic_gae_kernel'):
+            L.call('smi_ppo_critic_gae', L.ptr(m.critic.flat), D, c_h1, c_h2, 1 if zf else 0,
+                   zp(zf.running_sum if zf else None), zp(zf.running_sumsq if zf else None),
+                   zp(zf.count if zf else None), float(zf.eps if zf else 1e-5),
+                   L.ptr(x), L.ptr(xn), L.ptr(rewards), L.ptr(dones), B, T,
+                   L.ptr(self.gamma_tab), L.ptr(self.lam_tab), float(self.gamma),
+                   float(self.gamma ** self.n_step), L.ptr(values), L.ptr(adv_raw), L.ptr(ret), st)
+        # --- epochs (ppo.py:505-576)
+        lds = L.lib().smi_ppo_fused_lds_bytes(B, D, a_h1, a_h2, A, c_h1, c_h2)
+        if B > 256 or lds > 160 * 1024:
+            raise NotImplementedError('batch/model too large for the fused single-CU path; the '
+                                      'multi-CU epoch path is not built yet')
+        a = self._args
+        a.B, a.obs_dim, a.h1, a.h2, a.act_dim = B, D, a_h1, a_h2, A
+        a.critic_h1, a.critic_h2 = c_h1, c_h2
+        a.epoch_policy, a.epoch_baseline = self.epoch_policy, self.epoch_baseline
+        a.mode = 0 if self.ppo_mode == 'clip' else 1
+        a.norm_adv = 1 if self.norm_adv else 0
+        a.clip_actor_grad = 1 if self.clip_actor_gradient else 0
+        a.clip_critic_grad = 1 if self.clip_critic_gradient else 0
+        a.use_zf = 1 if zf is not None else 0
+        a.obs, a.obs_stride = x.data_ptr(), T * D                     # obs[:, 0, :]
+        a.actions, a.act_stride = actions.data_ptr(), T * A           # actions[:, 0, :]
+        a.behave, a.beh_stride = pds.data_ptr(), T * 2 * A            # pds[:, 0, :]
+        a.adv_raw, a.adv_moments, a.ret = adv_raw.data_ptr(), None, ret.data_ptr()
+        if zf is not None:
+            a.zf_sum, a.zf_sumsq, a.zf_count = (zf.running_sum.data_ptr(),
+                                                zf.running_sumsq.data_ptr(), zf.count.data_ptr())
+            a.rzf_sum, a.rzf_sumsq, a.rzf_count = (rzf.running_sum.data_ptr(),
+                                                   rzf.running_sumsq.data_ptr(), rzf.count.data_ptr())
+            a.zf_eps = zf.eps
+        else:
+            a.zf_sum = a.zf_sumsq = a.zf_count = a.rzf_sum = a.rzf_sumsq = a.rzf_count = None
+            a.zf_eps = 1e-5
+        a.actor, a.ref_actor, a.critic = (m.actor.flat.data_ptr(), rm.actor.flat.data_ptr(),
+                                          m.critic.flat.data_ptr())
+        a.actor_m, a.actor_v = self.actor_m.data_ptr(), self.actor_v.data_ptr()
+        a.critic_m, a.critic_v = self.critic_m.data_ptr(), self.critic_v.data_ptr()
+        a.actor_step, a.critic_step = self.actor_step.data_ptr(), self.critic_step.data_ptr()
+        a.hyper = self.hyper.data_ptr()
+        a.kl_target = float(self.kl_target)
+        a.kl_cutoff_coeff = float(self.kl_cutoff_coeff)
+        a.actor_max_norm = float(self.actor_gradient_clip_value)
+        a.critic_max_norm = float(self.critic_gradient_clip_value)
+        a.actor_wd, a.critic_wd = float(self.actor_regularization), float(self.critic_regularization)
+        a.beta1, a.beta2, a.adam_eps = self.adam_betas[0], self.adam_betas[1], self.adam_eps
+        a.stats = self.stats_buf.data_ptr()
+        a.kl_record, a.kl_count, a.kl_capacity = (self.kl_record_buf.data_ptr(),
+                                                  self.kl_count.data_ptr(), self.kl_capacity)
+        with self._ev('ppo_fused_kernel'):
+            L.check(L.lib().smi_ppo_update_fused(a, st), 'smi_ppo_update_fused')
+        # --- z_update(obs_iter) after the updates (ppo.py:578-582)
+        if zf is not None:
+            with self._ev('colstats_small_kernel'):
+                L.call('smi_zfilter_update', L.ptr(x), B, D, T * D, L.ptr(zf.running_sum),
+                       L.ptr(zf.running_sumsq), L.ptr(zf.count), st)
+        self._last_ret = ret
+
+    def learn(self, batch):                                   # ppo.py:588-613
+        self.current_iteration += 1
+        batch = self._preprocess_batch_ppo(batch)
+        self._optimize(batch['obs'], batch['actions'], batch['rewards'], batch['obs_next'],
+                       batch['persistent_infos'], batch['onetime_infos'], batch['dones'])
+        if self.metrics is not None:
+            self.metrics(self.last_stats(), self.global_step)
+        self.exp_counter += self.batch_size
+        self.global_step += 1
+
+    def last_stats(self):
+        """Statistics dict of the last learn() (ppo.py:219-224,278-284,328-331,555,571-582).
+        Synchronises with the device."""
+        v = self.stats_buf.cpu().numpy()
+        s = {}
+        if self.ppo_mode == 'clip':
+            for k in ('_surr_loss', '_clip_surr_loss', '_entropy'):
+                s[k] = float(v[L.ST[k]])
+            s['_clip_epsilon'] = self.clip_epsilon
+        else:
+            for k in ('_kl_loss_adapt', '_surr_loss', '_entropy'):
+                s[k] = float(v[L.ST[k]])
+            s['_beta'] = self.beta
+        s['_pol_kl'] = float(v[L.ST['_pol_kl']])
+        if self.clip_actor_gradient:
+            s['grad_norm_actor'] = float(v[L.ST['grad_norm_actor']])
+        for k in ('_val_loss', '_val_explained_var', '_avg_return_targ', '_avg_log_sig',
+                  '_avg_behave_likelihood', '_avg_is_weight', '_ref_behave_diff'):
+            s[k] = float(v[L.ST[k]])
+        if self.clip_critic_gradient:
+            s['grad_norm_critic'] = float(v[L.ST['grad_norm_critic']])
+        s['_lr'] = self.actor_lr_scheduler.get_lr()[0]
+        s['epochs_run'] = int(v[L.ST['epochs_run']])
+        if self.use_z_filter:
+            zf = self.model.z_filter
+            s['obs_running_mean'] = float(np.mean(zf.running_mean()))
+            s['obs_running_square'] = float(np.mean(zf.running_square()))
+            s['obs_running_std'] = float(np.mean(zf.running_std()))
+        if self.use_r_filter:
+            s['reward_mean'] = self.reward_filter.reward_mean()
+        return s
+
+    def module_dict(self):
+        return {'ppo': self.model}
+
+    def publish_parameter(self, iteration, message=''):       # ppo.py:623-635
+        if self.exp_counter >= self.learner_config.parameter_publish.exp_interval:
+            if self.publisher is not None:
+                self.publisher(iteration, message, self.module_dict())
+            self._post_publish()
+
+    def _post_publish(self):                                  # ppo.py:637-666
+        n = int(self.kl_count.item())
+        rec = self.kl_record_buf[:min(n, self.kl_capacity)].cpu().numpy().astype(np.float64)
+        self.kl_record = list(rec)
+        final_kl = np.mean(self.kl_record)
+        consts = self.learner_config.algo
+        if self.ppo_mode == 'clip':
+            if final_kl > self.kl_target * self.clip_adjust_threshold[1]:
+                if self.clip_lower < self.clip_epsilon:
+                    self.clip_epsilon = self.clip_epsilon / consts.clip_consts.scale_constant
+            elif final_kl < self.kl_target * self.clip_adjust_threshold[0]:
+                if self.clip_upper > self.clip_epsilon:
+                    self.clip_epsilon = self.clip_epsilon * consts.clip_consts.scale_constant
+        else:
+            if final_kl > self.kl_target * self.beta_adjust_threshold[1]:
+                if self.beta_upper > self.beta:
+                    self.beta = self.beta * consts.adapt_consts.scale_constant
+            elif final_kl < self.kl_target * self.beta_adjust_threshold[0]:
+                if self.beta_lower < self.beta:
+                    self.beta = self.beta / consts.adapt_consts.scale_constant
+        self.ref_target_model.update_target_params(self.model)
+        self.kl_record = []
+        self.kl_count.zero_()
+        self.exp_counter = 0
+        self.actor_lr_scheduler.step()
+        self.critic_lr_scheduler.step()
+        self._write_hyper()
+
+    def checkpoint_attributes(self):                          # ppo.py:668-678
+        return ['model', 'ref_target_model', 'actor_lr_scheduler', 'critic_lr_scheduler',
+                'current_iteration']
+
+    def preprocess(self, batch):                              # learner/base.py:321-330
+        return batch
+
+    def _prefetcher_preprocess(self, batch):                  # ppo.py:680-682
+        return self.aggregator.aggregate(batch)
+
+    # extra (not in the reference API): optimizer state for tests/checkpoints
+    def optimizer_state(self):
+        return {'actor_m': self.actor_m, 'actor_v': self.actor_v, 'actor_step': self.actor_step,
+                'critic_m': self.critic_m, 'critic_v': self.critic_v,
+                'critic_step': self.critic_step}

@@ -1,0 +1,69 @@
+"""Shared test helpers: configs and oracle <-> product weight transfer."""
+import copy
+
+import numpy as np
+import torch
+
+from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, Config, gym_env_config
+
+
+def ppo_config(B=64, T=50, mode='clip', use_z_filter=True, hidden=(64, 64), lam=0.95,
+               gamma=0.99, epochs=(10, 10), norm_adv=True, use_r_filter=False, reward_scale=1.0,
+               kl_target=0.02, lr=(3e-4, 3e-4), wd=(0.0, 0.0)):
+    lc = copy.deepcopy(PPO_DEFAULT_LEARNER_CONFIG)
+    lc.model.actor_fc_hidden_sizes = list(hidden)
+    lc.model.critic_fc_hidden_sizes = list(hidden)
+    lc.algo.use_z_filter = use_z_filter
+    lc.algo.use_r_filter = use_r_filter
+    lc.algo.gamma = gamma
+    lc.algo.n_step = T
+    lc.algo.ppo_mode = mode
+    lc.algo.advantage.lam = lam
+    lc.algo.advantage.norm_adv = norm_adv
+    lc.algo.advantage.reward_scale = reward_scale
+    lc.algo.rnn.if_rnn_policy = False
+    lc.algo.consts.epoch_policy = epochs[0]
+    lc.algo.consts.epoch_baseline = epochs[1]
+    lc.algo.consts.kl_target = kl_target
+    lc.algo.network.lr_actor = lr[0]
+    lc.algo.network.lr_critic = lr[1]
+    lc.algo.network.anneal.min_lr = min(lr)
+    lc.algo.network.actor_regularization = wd[0]
+    lc.algo.network.critic_regularization = wd[1]
+    lc.replay.batch_size = B
+    return lc
+
+
+def env_config(D=17, A=6):
+    return gym_env_config(D, A)
+
+
+def copy_weights_to_oracle(learner, ref):
+    """product (device flat buffers) -> oracle (CPU torch modules)."""
+    ref.model.actor.load_flat(learner.model.actor.flat.detach().cpu())
+    ref.model.critic.load_flat(learner.model.critic.flat.detach().cpu())
+    ref.ref_target_model.actor.load_flat(learner.ref_target_model.actor.flat.detach().cpu())
+    ref.ref_target_model.critic.load_flat(learner.ref_target_model.critic.flat.detach().cpu())
+    if learner.use_z_filter:
+        for a, b in ((learner.model.z_filter, ref.model.z_filter),
+                     (learner.ref_target_model.z_filter, ref.ref_target_model.z_filter)):
+            b.running_sum.copy_(a.running_sum.cpu())
+            b.running_sumsq.copy_(a.running_sumsq.cpu())
+            b.count.copy_(a.count.cpu())
+
+
+def oracle_batch(batch):
+    """Synthetic batch (surreal_amd.synthetic layout) -> oracle learn() dict."""
+    key = list(batch['obs']['low_dim'])[0]
+    return {'obs': batch['obs']['low_dim'][key], 'obs_next': batch['obs_next']['low_dim'][key],
+            'actions': batch['actions'], 'rewards': batch['rewards'], 'dones': batch['dones'],
+            'pds': batch['persistent_infos'][-1], 'onetime': batch['onetime_infos']}
+
+
+def max_rel_err(x, ref, floor=None):
+    """max |x - ref| / (|ref| + floor), floor defaults to 1e-3 * max|ref|."""
+    x = np.asarray(x, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    if floor is None:
+        floor = 1e-3 * max(1e-30, float(np.max(np.abs(ref))) if ref.size else 1.0)
+    return float(np.max(np.abs(x - ref) / (np.abs(ref) + floor))) if ref.size else 0.0

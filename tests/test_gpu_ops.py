@@ -1,0 +1,313 @@
+"""GPU parity of the individual HIP kernels (C ABI) against the CPU oracle and
+the committed golden fixtures.  Tolerances: fp32 kernels 1e-5 relative (with a
+floor of 1e-3 x the largest reference magnitude for values that cancel to ~0);
+integer/index work bit-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ppo_ref as R
+from oracle import sampler_ref as SR
+from surreal_amd import _lib as L
+from surreal_amd.model import DiagGauss, RewardFilter, ZFilter
+from tests.helpers import max_rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+RTOL = 1e-5
+
+
+def st():
+    return L.stream()
+
+
+def setup_module(m):
+    L.ensure_workspace(DEV)
+
+
+def _mlp(d_in, h1, h2, d_out, tanh, seed):
+    torch.manual_seed(seed)
+    m = R.MLP3(d_in, h1, h2, d_out, tanh)
+    return m
+
+
+@pytest.mark.parametrize('rows,d_in,h1,h2,d_out,tanh,lv,use_zf', [
+    (300, 17, 64, 64, 6, True, True, True),
+    (64, 17, 64, 64, 1, False, False, False),
+    (5, 42, 300, 200, 8, True, True, True),      # params exceed the LDS budget -> global path
+    (1, 3, 16, 16, 2, True, False, False),
+    (129, 11, 48, 32, 1, False, False, True),
+])
+def test_mlp_forward(rows, d_in, h1, h2, d_out, tanh, lv, use_zf):
+    m = _mlp(d_in, h1, h2, d_out, tanh, rows)
+    x = torch.randn(rows, d_in) * 2.0
+    flat = m.flat()
+    logv = torch.randn(d_out) * 0.3
+    if lv:
+        flat = torch.cat([flat, logv])
+    zf = R.ZFilterRef(d_in)
+    if use_zf:
+        zf.z_update(torch.randn(50, d_in) * 3 + 1)
+    xin = zf(x) if use_zf else x
+    ref = m(xin)
+    if lv:
+        ref = torch.cat([ref, torch.exp(logv).expand(rows, d_out)], 1)
+    fd, xd = flat.to(DEV), x.to(DEV)
+    out = torch.empty(rows, 2 * d_out if lv else d_out, device=DEV)
+    zs, zq, zc = (zf.running_sum.to(DEV), zf.running_sumsq.to(DEV), zf.count.to(DEV))
+    L.call('smi_mlp_forward', L.ptr(fd), d_in, h1, h2, d_out, 2 if tanh else 0, int(lv), L.ptr(xd),
+           rows, d_in, int(use_zf), L.ptr(zs), L.ptr(zq), L.ptr(zc), 1e-5, L.ptr(out), st())
+    assert max_rel_err(out.cpu(), ref.detach()) < RTOL
+
+
+def test_mlp_forward_strided_rows():
+    # obs[:, 0, :] of a (B, T, D) batch is read in place with row stride T*D
+    B, T, D = 37, 9, 17
+    m = _mlp(D, 64, 64, 1, False, 3)
+    obs = torch.randn(B, T, D)
+    ref = m(obs[:, 0, :])
+    od, fd = obs.to(DEV), m.flat().to(DEV)
+    out = torch.empty(B, 1, device=DEV)
+    L.call('smi_mlp_forward', L.ptr(fd), D, 64, 64, 1, 0, 0, L.ptr(od), B, T * D, 0, None, None,
+           None, 1e-5, L.ptr(out), st())
+    assert max_rel_err(out.cpu(), ref.detach()) < RTOL
+
+
+def test_zfilter_ops_and_known_answer():
+    k = json.load(open(os.path.join(GOLD, 'known_answers.json')))['zfilter']
+    zf = ZFilter({'low_dim': {'x': (3,)}}, device=DEV)
+    x = torch.full((k['B'], 3), k['c'], device=DEV)
+    zf.z_update(x)
+    mean = zf.running_mean()
+    assert np.allclose(mean, k['mean'], rtol=1e-6)
+    assert abs(float(zf.count.item()) - k['count']) <= 1e-6 * k['count']
+    # apply + update vs oracle over several rounds, strided input
+    ref = R.ZFilterRef(17)
+    dz = ZFilter({'low_dim': {'x': (17,)}}, device=DEV)
+    g = torch.Generator().manual_seed(1)
+    for rnd in range(3):
+        big = torch.randn(40, 5, 17, generator=g) * (1 + rnd) + rnd
+        xs = big[:, 0, :]
+        ref.z_update(xs)
+        dz.z_update(big.to(DEV)[:, 0, :])
+        y = torch.randn(23, 17, generator=g) * 4
+        assert max_rel_err(dz(y.to(DEV)).cpu(), ref(y)) < RTOL
+    assert max_rel_err(dz.running_sum.cpu(), ref.running_sum) < RTOL
+    assert max_rel_err(dz.running_sumsq.cpu(), ref.running_sumsq) < RTOL
+    assert float(dz.count.item()) == float(ref.count.item())
+
+
+def test_zfilter_update_large_partials():
+    # multi-workgroup partial path (rows*dim > 65536), fixed-order reduction
+    rows, D = 70000, 42
+    x = torch.randn(rows, D, dtype=torch.float64)
+    zf = ZFilter({'low_dim': {'x': (D,)}}, device=DEV)
+    zf.z_update(x.float().to(DEV))
+    s = x.float().double().sum(0)
+    assert max_rel_err(zf.running_sum.cpu(), s, floor=1e-3 * float(s.abs().max())) < 1e-4
+    assert float(zf.count.item()) == pytest.approx(rows + 1e-5)
+
+
+def test_diag_gauss_vs_oracle_and_kats():
+    A, N = 6, 257
+    g = torch.Generator().manual_seed(2)
+    p0 = torch.cat([torch.rand(N, A, generator=g) - 0.5, 0.2 + torch.rand(N, A, generator=g)], 1)
+    p1 = torch.cat([torch.rand(N, A, generator=g) - 0.5, 0.2 + torch.rand(N, A, generator=g)], 1)
+    a = torch.rand(N, A, generator=g) * 2 - 1
+    ref = R.DiagGaussRef(A)
+    pd = DiagGauss(A)
+    ad, p0d, p1d = a.to(DEV), p0.to(DEV), p1.to(DEV)
+    assert max_rel_err(pd.loglikelihood(ad, p0d).cpu(), ref.loglikelihood(a, p0)) < RTOL
+    assert max_rel_err(pd.likelihood(ad, p0d).cpu(), ref.likelihood(a, p0)) < RTOL
+    assert max_rel_err(pd.kl(p0d, p1d).cpu(), ref.kl(p0, p1)) < RTOL
+    assert max_rel_err(pd.entropy(p0d).cpu(), ref.entropy(p0)) < RTOL
+    k = json.load(open(os.path.join(GOLD, 'known_answers.json')))['diag_gauss']
+    mu, sd = torch.tensor(k['mu']).float(), torch.tensor(k['sd']).float()
+    p = torch.cat([mu, sd]).view(1, -1).to(DEV)
+    pd5 = DiagGauss(k['A'])
+    assert abs(pd5.loglikelihood(mu.view(1, -1).to(DEV), p).item() - k['loglik_at_mean']) < 1e-5
+    assert abs(pd5.entropy(p).item() - k['entropy']) < 1e-5
+    assert abs(pd5.kl(p, p).item()) < 1e-6
+    q = torch.cat([mu + k['shift'], sd]).view(1, -1).to(DEV)
+    assert abs(pd5.kl(p, q).item() - k['kl_shift']) < 1e-5 * max(1, k['kl_shift'])
+
+
+def test_reward_filter_keeps_reference_bug():
+    ref = R.RewardFilterRef()
+    rf = RewardFilter(device=DEV)
+    g = torch.Generator().manual_seed(3)
+    for _ in range(3):
+        r = torch.randn(8, 10, generator=g) * 2 + 0.5
+        exp = ref.forward(r * 0.5)
+        ref.update(r * 0.5)
+        rd = r.to(DEV).clone()
+        rf.scale_forward_update_(rd, 0.5)
+        assert max_rel_err(rd.cpu(), exp) < RTOL
+        assert abs(rf.running_sumsq.item() - ref.running_sumsq.item()) <= 1e-5 * abs(ref.running_sumsq.item())
+        assert abs(rf.running_sum.item() - ref.running_sum.item()) <= 1e-5 * (abs(ref.running_sum.item()) + 1)
+
+
+def _gae_windows_gpu(values, rewards, dones, gamma, lam, T, H):
+    idx = torch.tensor(range(T), dtype=torch.float32)
+    gt, lt = torch.pow(gamma, idx), torch.pow(lam, idx)
+    B = values.shape[0]
+    E = T - H + 1
+    vd, rd, dd = values.to(DEV).contiguous(), rewards.to(DEV).contiguous(), dones.to(DEV).contiguous()
+    adv = torch.empty(B, E, device=DEV)
+    ret = torch.empty(B, E, device=DEV)
+    part = torch.zeros(2 * 2048, dtype=torch.float64, device=DEV)
+    import ctypes
+    n = ctypes.c_int(0)
+    L.call('smi_gae_windows', L.ptr(vd), L.ptr(rd), L.ptr(dd), B, T, H, L.ptr(gt.to(DEV)),
+           L.ptr(lt.to(DEV)), float(gamma), float(gamma ** H), L.ptr(adv), L.ptr(ret), L.ptr(part),
+           ctypes.byref(n), st())
+    return adv.cpu(), ret.cpu(), vd.cpu(), part[:2 * n.value].cpu().view(-1, 2)
+
+
+def test_gae_known_answers():
+    for case in json.load(open(os.path.join(GOLD, 'known_answers.json')))['gae']:
+        T = case['T']
+        v = torch.tensor(case['values']).float()
+        r = torch.tensor(case['rewards']).float()
+        d = torch.tensor(case['dones']).float()
+        adv, ret, _, _ = _gae_windows_gpu(v, r, d, case['gamma'], case['lam'], T, T)
+        assert np.allclose(adv[:, 0].numpy(), case['adv'], rtol=1e-5, atol=1e-5), case['name']
+        assert np.allclose(ret[:, 0].numpy(), case['ret'], rtol=1e-5, atol=1e-5), case['name']
+
+
+@pytest.mark.parametrize('B,T,H', [(64, 50, 50), (33, 25, 5), (1, 7, 1), (200, 25, 25), (5, 1, 1)])
+def test_gae_windows_vs_oracle(B, T, H):
+    g = torch.Generator().manual_seed(B + T)
+    v = torch.randn(B, T + 1, generator=g)
+    r = torch.randn(B, T, generator=g)
+    d = (torch.rand(B, T, generator=g) < 0.1).float()
+    gamma, lam = 0.99, 0.95
+    rnn = H != T
+    radv, rret = R.gae_and_return(v.clone(), r, d, gamma, lam, T, H, rnn, norm_adv=False)
+    adv, ret, vm, part = _gae_windows_gpu(v, r, d, gamma, lam, T, H)
+    radv, rret = radv.reshape(B, -1), rret.reshape(B, -1)
+    assert max_rel_err(adv, radv) < RTOL
+    assert max_rel_err(ret, rret) < RTOL
+    vref = v.clone(); vref[:, 1:] *= 1 - d
+    assert torch.equal(vm, vref)
+    s = part.sum(0)
+    assert abs(float(s[0]) - float(adv.double().sum())) <= 1e-9 * (1 + float(adv.double().abs().sum()))
+
+
+def test_gae_windows_full_size_property():
+    # BASELINE C3-scale stream (1024 actors x 64 batches) checked on sampled segments
+    B, T, H = 65536, 25, 5
+    g = torch.Generator().manual_seed(9)
+    v = torch.randn(B, T + 1, generator=g)
+    r = torch.randn(B, T, generator=g)
+    d = (torch.rand(B, T, generator=g) < 0.02).float()
+    adv, ret, _, _ = _gae_windows_gpu(v, r, d, 0.99, 1.0, T, H)
+    idx = torch.randint(0, B, (512,), generator=g)
+    radv, rret = R.gae_and_return(v[idx].clone(), r[idx], d[idx], 0.99, 1.0, T, H, True, False)
+    assert max_rel_err(adv[idx], radv) < RTOL
+    assert max_rel_err(ret[idx], rret) < RTOL
+
+
+def test_moments():
+    x = torch.randn(10001, dtype=torch.float64) * 3 + 1
+    out = torch.zeros(3, dtype=torch.float64, device=DEV)
+    xd = x.float().to(DEV)
+    L.call('smi_moments', L.ptr(xd), xd.numel(), None, 0, L.ptr(out), st())
+    xf = x.float().double()
+    o = out.cpu()
+    assert abs(o[0] - xf.sum()) < 1e-9 * xf.abs().sum()
+    assert abs(o[1] - (xf * xf).sum()) < 1e-9 * (xf * xf).sum()
+    assert o[2] == 10001
+
+
+@pytest.mark.parametrize('wd,max_norm', [(0.0, 10.0), (1e-3, 0.5), (0.0, 0.0)])
+def test_adam_clip_vs_torch(wd, max_norm):
+    n = 5000
+    g = torch.Generator().manual_seed(5)
+    p_ref = torch.nn.Parameter(torch.randn(n, generator=g))
+    opt = torch.optim.Adam([p_ref], lr=3e-4, weight_decay=wd)
+    pd = p_ref.detach().clone().to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    lr = torch.tensor([3e-4], device=DEV)
+    norm = torch.zeros(1, device=DEV)
+    for it in range(4):
+        grad = torch.randn(n, generator=g) * (0.01 if it % 2 else 3.0)
+        p_ref.grad = grad.clone()
+        ref_norm = None
+        if max_norm > 0:
+            ref_norm = float(torch.nn.utils.clip_grad_norm_([p_ref], max_norm))
+        opt.step()
+        gd = grad.to(DEV)
+        L.call('smi_adam_clip', L.ptr(pd), L.ptr(gd), L.ptr(m), L.ptr(v), n, L.ptr(step), L.ptr(lr),
+               0.9, 0.999, 1e-8, wd, max_norm, None, L.ptr(norm), st())
+        if ref_norm is not None:
+            assert abs(norm.item() - ref_norm) <= 1e-5 * ref_norm
+        assert max_rel_err(pd.cpu(), p_ref.detach()) < RTOL
+    assert step.item() == 4
+    # skip flag leaves everything untouched
+    skip = torch.ones(1, dtype=torch.int32, device=DEV)
+    before = pd.clone()
+    L.call('smi_adam_clip', L.ptr(pd), L.ptr(gd), L.ptr(m), L.ptr(v), n, L.ptr(step), L.ptr(lr),
+           0.9, 0.999, 1e-8, wd, max_norm, L.ptr(skip), None, st())
+    assert torch.equal(pd, before) and step.item() == 4
+
+
+def test_adam_known_answer():
+    k = json.load(open(os.path.join(GOLD, 'known_answers.json')))['adam']
+    p = torch.tensor(k['p0']).float().to(DEV)
+    gr = torch.tensor(k['g']).float().to(DEV)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    lr = torch.tensor([k['lr']], device=DEV)
+    L.call('smi_adam_clip', L.ptr(p), L.ptr(gr), L.ptr(m), L.ptr(v), 4, L.ptr(step), L.ptr(lr), 0.9,
+           0.999, k['eps'], 0.0, 0.0, None, None, st())
+    assert np.allclose(p.cpu().numpy(), k['p1'], rtol=1e-6, atol=1e-7)
+
+
+def test_ddpg_target():
+    n = 1000
+    g = torch.Generator().manual_seed(6)
+    r, q, q2 = (torch.randn(n, generator=g) for _ in range(3))
+    d = (torch.rand(n, generator=g) < 0.1).float()
+    gn = 0.99 ** 3
+    y = torch.empty(n, device=DEV)
+    L.call('smi_ddpg_target', L.ptr(r.to(DEV)), L.ptr(d.to(DEV)), L.ptr(q.to(DEV)), None, n, gn,
+           L.ptr(y), st())
+    ref = r + gn * q * (1.0 - d)
+    assert max_rel_err(y.cpu(), ref) < RTOL
+    L.call('smi_ddpg_target', L.ptr(r.to(DEV)), L.ptr(d.to(DEV)), L.ptr(q.to(DEV)), L.ptr(q2.to(DEV)),
+           n, gn, L.ptr(y), st())
+    ref2 = torch.min(ref, r + gn * q2 * (1.0 - d))
+    assert max_rel_err(y.cpu(), ref2) < RTOL
+
+
+def test_sampler_bit_exact_vs_cpython_golden():
+    from surreal_amd.replay import CPythonRandom
+    gold = json.load(open(os.path.join(GOLD, 'sampler_streams.json')))
+    for c in gold['cases']:
+        rng = CPythonRandom(c['seed'], DEV)
+        # split the 700 draws across calls of different sizes: state carries over
+        parts = [rng.randint_device(c['n'], k).cpu().numpy() for k in (1, 511, 188)]
+        got = np.concatenate(parts)
+        assert got.tolist() == c['draws'], (c['seed'], c['n'])
+        host = CPythonRandom(c['seed']).randint_host(c['n'], 700)
+        assert host.tolist() == c['draws']
+
+
+def test_gather_rows():
+    table = torch.randn(1000, 37, device=DEV)
+    idx = torch.randint(0, 1000, (512,), device=DEV)
+    out = torch.empty(512, 37, device=DEV)
+    L.call('smi_gather_rows', L.ptr(table), 37, L.ptr(idx), 512, L.ptr(out), st())
+    assert torch.equal(out, table[idx])
+    t4 = torch.randn(100, 40, device=DEV)
+    o4 = torch.empty(512, 40, device=DEV)
+    idx4 = torch.randint(0, 100, (512,), device=DEV)
+    L.call('smi_gather_rows', L.ptr(t4), 40, L.ptr(idx4), 512, L.ptr(o4), st())
+    assert torch.equal(o4, t4[idx4])
