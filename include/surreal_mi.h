@@ -203,6 +203,10 @@ typedef struct smi_ppo_args {
   /* outputs */
   float* stats;                /* [SMI_ST_COUNT]                       */
   float* kl_record; int* kl_count; int kl_capacity;
+  /* data-parallel epochs (smi_ppo_epoch_grad / smi_ppo_epoch_apply) */
+  int64_t B_global;            /* rows over all ranks (0: = B)         */
+  float* xbuf;                 /* exchange buffer, smi_ppo_xbuf_floats */
+  int* dp_state;               /* [4] zeroed by the caller per learn()  */
 } smi_ppo_args;
 
 /* device hyper-parameter slots (float) */
@@ -234,6 +238,32 @@ typedef struct smi_ppo_args {
 #define SMI_ST_COUNT           16
 
 int smi_ppo_update_fused(const smi_ppo_args* args, void* stream);
+
+/* Data-parallel form of the same epochs (one process per GPU, the batch
+ * sharded on the segment axis).  Phase e in [0, max(E+1, Ev))
+ * of one learn() is
+ *     smi_ppo_epoch_grad(args, e)  -> this rank's share of the gradients and
+ *                                     statistic sums in args->xbuf
+ *     all-reduce(SUM) of xbuf (smi_ppo_xbuf_floats floats) across ranks
+ *     smi_ppo_epoch_apply(args, e) -> KL early stop / adapt coefficient from
+ *                                     the global KL, clip_grad_norm_ + Adam on
+ *                                     the summed gradients, statistics
+ * Per-row gradient weights use 1/B_global, so the all-reduced sum is the
+ * gradient of the reference's mean over the global batch.  args->adv_moments
+ * must hold the all-reduced (sum, sumsq, count) of the raw advantages.
+ * The early-stop decision is data dependent but identical on every rank, and
+ * later phases become no-ops on device: the host issues the same sequence on
+ * every rank with no synchronisation. */
+int64_t smi_ppo_xbuf_floats(int obs_dim, int h1, int h2, int act_dim, int critic_h1,
+                            int critic_h2, int mode);
+int smi_ppo_epoch_grad(const smi_ppo_args* args, int epoch, void* stream);
+int smi_ppo_epoch_apply(const smi_ppo_args* args, int epoch, void* stream);
+
+/* running_sum += sum_in, running_sumsq += sumsq_in, count += rows — the
+ * data-parallel z_update after the column statistics were all-reduced. */
+int smi_zfilter_accumulate(const float* sum_in, const float* sumsq_in, int dim, float rows,
+                           float* running_sum, float* running_sumsq, float* count,
+                           void* stream);
 
 /* ---------------------------------------------------------- Adam / clip */
 /* Replaces torch.nn.utils.clip_grad_norm_ + torch.optim.Adam.step

@@ -50,6 +50,7 @@ class PPOArgs(ctypes.Structure):
         ('beta1', c_f32), ('beta2', c_f32), ('adam_eps', c_f32),
         ('stats', P),
         ('kl_record', P), ('kl_count', P), ('kl_capacity', c_int),
+        ('B_global', c_i64), ('xbuf', P), ('dp_state', P),
     ]
 
 
@@ -74,6 +75,10 @@ _SIGS = {
     'smi_gae_windows_max_partials': (c_int, [c_i64, c_int]),
     'smi_moments': (c_int, [P, c_i64, P, c_int, P, P]),
     'smi_ppo_update_fused': (c_int, [ctypes.POINTER(PPOArgs), P]),
+    'smi_ppo_xbuf_floats': (c_i64, [c_int] * 7),
+    'smi_ppo_epoch_grad': (c_int, [ctypes.POINTER(PPOArgs), c_int, P]),
+    'smi_ppo_epoch_apply': (c_int, [ctypes.POINTER(PPOArgs), c_int, P]),
+    'smi_zfilter_accumulate': (c_int, [P, P, c_int, c_f32, P, P, P, P]),
     'smi_adam_clip': (c_int, [P, P, P, P, c_i64, P, P, c_f32, c_f32, c_f32, c_f32, c_f32, P,
                               P, P]),
     'smi_ddpg_target': (c_int, [P, P, P, P, c_i64, c_f32, P, P]),

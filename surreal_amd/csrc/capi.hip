@@ -53,6 +53,8 @@ void mt_seed_host(uint64_t, uint32_t*);
 int mt_randint_host(uint32_t*, int64_t, int64_t, int64_t*);
 int launch_mt_randint(uint32_t*, int64_t, int64_t, int64_t*, hipStream_t);
 int launch_gather_rows(const float*, int64_t, const int64_t*, int64_t, float*, hipStream_t);
+int launch_zfilter_accumulate(const float*, const float*, int, float, float*, float*, float*,
+                              hipStream_t);
 
 }  // namespace smi
 
@@ -172,18 +174,51 @@ int smi_moments(const float* x, int64_t n, const double* partials, int n_partial
   return launch_moments(x, n, partials, n_partials, out3, SMI_STREAM(stream));
 }
 
+static int check_ppo_args(const smi_ppo_args* a);
+
 int smi_ppo_update_fused(const smi_ppo_args* a, void* stream) {
-  REQUIRE(a, "ppo_update_fused: null args");
+  const int rc = check_ppo_args(a);
+  if (rc) return rc;
+  return launch_ppo_fused(a, SMI_STREAM(stream));
+}
+
+int64_t smi_ppo_xbuf_floats(int obs_dim, int h1, int h2, int act_dim, int critic_h1,
+                            int critic_h2, int mode) {
+  return ppo_xbuf_floats(obs_dim, h1, h2, act_dim, critic_h1, critic_h2, mode);
+}
+
+static int check_ppo_args(const smi_ppo_args* a) {
+  REQUIRE(a, "ppo epochs: null args");
   REQUIRE(a->obs && a->actions && a->behave && a->adv_raw && a->ret && a->actor &&
               a->ref_actor && a->critic && a->actor_m && a->actor_v && a->critic_m &&
               a->critic_v && a->actor_step && a->critic_step && a->hyper && a->stats,
-          "ppo_update_fused: null pointer");
+          "ppo epochs: null pointer");
   REQUIRE(!a->use_zf || (a->zf_sum && a->zf_sumsq && a->zf_count && a->rzf_sum &&
                          a->rzf_sumsq && a->rzf_count),
-          "ppo_update_fused: zfilter buffers required");
-  REQUIRE(a->mode == 0 || a->mode == 1, "ppo_update_fused: mode must be 0 (clip) or 1 (adapt)");
-  REQUIRE(a->epoch_policy >= 0 && a->epoch_baseline >= 0, "ppo_update_fused: bad epochs");
-  return launch_ppo_fused(a, SMI_STREAM(stream));
+          "ppo epochs: zfilter buffers required");
+  REQUIRE(a->mode == 0 || a->mode == 1, "ppo epochs: mode must be 0 (clip) or 1 (adapt)");
+  REQUIRE(a->epoch_policy >= 0 && a->epoch_baseline >= 0, "ppo epochs: bad epochs");
+  return SMI_OK;
+}
+
+int smi_ppo_epoch_grad(const smi_ppo_args* a, int epoch, void* stream) {
+  const int rc = check_ppo_args(a);
+  if (rc) return rc;
+  REQUIRE(epoch >= 0, "ppo_epoch_grad: epoch < 0");
+  return launch_ppo_epoch_grad(a, epoch, SMI_STREAM(stream));
+}
+
+int smi_ppo_epoch_apply(const smi_ppo_args* a, int epoch, void* stream) {
+  const int rc = check_ppo_args(a);
+  if (rc) return rc;
+  REQUIRE(epoch >= 0, "ppo_epoch_apply: epoch < 0");
+  return launch_ppo_epoch_apply(a, epoch, SMI_STREAM(stream));
+}
+
+int smi_zfilter_accumulate(const float* sum_in, const float* sumsq_in, int dim, float rows,
+                           float* rs, float* rsq, float* cnt, void* stream) {
+  REQUIRE(sum_in && sumsq_in && rs && rsq && cnt && dim > 0, "zfilter_accumulate: bad args");
+  return launch_zfilter_accumulate(sum_in, sumsq_in, dim, rows, rs, rsq, cnt, SMI_STREAM(stream));
 }
 
 int smi_adam_clip(float* params, const float* grad, float* m, float* v, int64_t n, int* step,

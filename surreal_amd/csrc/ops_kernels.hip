@@ -411,6 +411,7 @@ int launch_mlp_forward(const float* params, int in, int h1, int h2, int out, int
   const int64_t ntiles = (rows + kRT - 1) / kRT;
   if (ntiles == 0) return SMI_OK;
   const int grid = (int)(ntiles < 1024 ? ntiles : 1024);
+  allow_lds(mlp_forward_kernel, (size_t)lds);
   hipLaunchKernelGGL(mlp_forward_kernel, dim3(grid), dim3(kWG), (size_t)lds, st, a);
   return check_launch("mlp_forward_kernel");
 }
@@ -436,6 +437,24 @@ int launch_adam_clip(float* p, const float* g, float* m, float* v, int64_t n, in
   if (rc) return rc;
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step, skip);
   return check_launch("step_inc_kernel");
+}
+
+// data-parallel z_update: add all-reduced column sums into the running buffers
+__global__ void __launch_bounds__(kWG)
+zfilter_accumulate_kernel(const float* __restrict__ s, const float* __restrict__ s2, int dim,
+                          float rows, float* rs, float* rsq, float* cnt) {
+  for (int c = threadIdx.x; c < dim; c += kWG) {
+    rs[c] += s[c];
+    rsq[c] += s2[c];
+  }
+  if (threadIdx.x == 0) cnt[0] += rows;
+}
+
+int launch_zfilter_accumulate(const float* s, const float* s2, int dim, float rows, float* rs,
+                              float* rsq, float* cnt, hipStream_t st) {
+  hipLaunchKernelGGL(zfilter_accumulate_kernel, dim3(1), dim3(kWG), 0, st, s, s2, dim, rows, rs,
+                     rsq, cnt);
+  return check_launch("zfilter_accumulate_kernel");
 }
 
 int launch_ddpg_target(const float* r, const float* d, const float* q, const float* q2,

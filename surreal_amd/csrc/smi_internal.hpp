@@ -10,6 +10,15 @@ namespace smi {
 int set_error(int code, const char* msg);
 int check_launch(const char* what);
 
+// Opt a kernel in to > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
+// Host-only attribute call: no allocation, no stream work (graph-capture safe).
+template <typename K>
+inline void allow_lds(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 int64_t fused_lds_bytes(int B, int D, int H1, int H2, int A, int cH1, int cH2);
 
 int launch_critic_gae(const float* critic_params, int D, int H1, int H2, int use_zf,
@@ -24,5 +33,8 @@ int launch_gae_windows(float* values, const float* rewards, const float* dones, 
                        float gamma_H, float* adv, float* ret, double* partials,
                        int* n_partials, hipStream_t stream);
 int launch_ppo_fused(const smi_ppo_args* args, hipStream_t stream);
+int64_t ppo_xbuf_floats(int D, int H1, int H2, int A, int cH1, int cH2, int mode);
+int launch_ppo_epoch_grad(const smi_ppo_args* args, int epoch, hipStream_t stream);
+int launch_ppo_epoch_apply(const smi_ppo_args* args, int epoch, hipStream_t stream);
 
 }  // namespace smi

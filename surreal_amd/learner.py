@@ -61,13 +61,36 @@ class LinearWithMinLR(object):
         self.steps = int(d['steps'])
 
 
+class TorchDistAllReduce(object):
+    """Data-parallel group over torch.distributed (backend 'nccl' = RCCL over
+    xGMI on MI355X; 'gloo' for CPU tests).  all_reduce is enqueued stream-
+    ordered with the learner's kernels; no host synchronisation."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self._dist = dist
+        self.group = group
+        self.world_size = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def allreduce_(self, t):
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group)
+        return t
+
+
 class PPOLearner(object):
     """ppo.py:12-682 on MI355X.  Same constructor, learn/module_dict/
     publish_parameter/checkpoint_attributes/preprocess/_prefetcher_preprocess."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
-                 publisher=None, device=None, seed=0):
+                 publisher=None, device=None, seed=0, dp=None):
+        """dp: None (one GPU) or a data-parallel group exposing `world_size` and
+        `allreduce_(tensor)` (in-place SUM, stream-ordered), e.g.
+        TorchDistAllReduce() over RCCL.  Each rank passes its own shard of
+        `replay.batch_size` segments; the update equals the reference's on the
+        concatenated global batch."""
         L.require_gpu()
+        self.dp = dp
         self.learner_config = lc = _as_config(learner_config)
         self.env_config = ec = _as_config(env_config)
         self.session_config = _as_config(session_config)
@@ -123,6 +146,9 @@ class PPOLearner(object):
                                       'set algo.rnn.if_rnn_policy=False')
         if ec.get('pixel_input', False):
             raise NotImplementedError('surreal_amd: pixel inputs are SURVEY §8(f) rank 1')
+        if dp is not None and self.use_r_filter:
+            raise NotImplementedError('surreal_amd: RewardFilter under data parallelism needs a '
+                                      'global reward all-reduce (not built yet)')
 
         anneal = algo.network.anneal
         num_updates = int(anneal.frames_to_anneal / lc.parameter_publish.exp_interval)
@@ -270,9 +296,12 @@ class PPOLearner(object):
         # --- epochs (ppo.py:505-576)
         lds = L.lib().smi_ppo_fused_lds_bytes(B, D, a_h1, a_h2, A, c_h1, c_h2)
         if B > 256 or lds > 160 * 1024:
-            raise NotImplementedError('batch/model too large for the fused single-CU path; the '
-                                      'multi-CU epoch path is not built yet')
+            raise NotImplementedError('batch/model too large for the single-CU epoch kernels; '
+                                      'the multi-CU epoch path is not built yet')
         a = self._args
+        dp = self.dp
+        a.B_global = B * (dp.world_size if dp is not None else 1)
+        a.xbuf = a.dp_state = None
         a.B, a.obs_dim, a.h1, a.h2, a.act_dim = B, D, a_h1, a_h2, A
         a.critic_h1, a.critic_h2 = c_h1, c_h2
         a.epoch_policy, a.epoch_baseline = self.epoch_policy, self.epoch_baseline
@@ -309,24 +338,56 @@ class PPOLearner(object):
         a.stats = self.stats_buf.data_ptr()
         a.kl_record, a.kl_count, a.kl_capacity = (self.kl_record_buf.data_ptr(),
                                                   self.kl_count.data_ptr(), self.kl_capacity)
-        with self._ev('ppo_fused_kernel'):
-            L.check(L.lib().smi_ppo_update_fused(a, st), 'smi_ppo_update_fused')
-        # --- z_update(obs_iter) after the updates (ppo.py:578-582)
-        if zf is not None:
-            with self._ev('colstats_small_kernel'):
-                L.call('smi_zfilter_update', L.ptr(x), B, D, T * D, L.ptr(zf.running_sum),
-                       L.ptr(zf.running_sumsq), L.ptr(zf.count), st)
         self._last_ret = ret
+        if dp is None:
+            with self._ev('ppo_fused_kernel'):
+                L.check(L.lib().smi_ppo_update_fused(a, st), 'smi_ppo_update_fused')
+            # --- z_update(obs_iter) after the updates (ppo.py:578-582)
+            if zf is not None:
+                with self._ev('colstats_small_kernel'):
+                    L.call('smi_zfilter_update', L.ptr(x), B, D, T * D, L.ptr(zf.running_sum),
+                           L.ptr(zf.running_sumsq), L.ptr(zf.count), st)
+            return
+        # ---- data parallel: global advantage moments, then
+        # max(E+1, Ev) phases of [rank-local gradients -> all-reduce -> apply]
+        mom = self._buf('adv_moments', (3,), torch.float64)
+        L.call('smi_moments', L.ptr(adv_raw), B, None, 0, L.ptr(mom), st)
+        yield mom
+        a.adv_moments = mom.data_ptr()
+        nx = L.lib().smi_ppo_xbuf_floats(D, a_h1, a_h2, A, c_h1, c_h2, a.mode)
+        xbuf = self._buf('xbuf', (nx,))
+        dp_state = self._buf('dp_state', (4,), torch.int32)
+        dp_state.zero_()
+        a.xbuf, a.dp_state = xbuf.data_ptr(), dp_state.data_ptr()
+        for e in range(max(self.epoch_policy + 1, self.epoch_baseline)):
+            with self._ev('ppo_epoch_grad_kernel'):
+                L.check(L.lib().smi_ppo_epoch_grad(a, e, st), 'smi_ppo_epoch_grad')
+            yield xbuf
+            with self._ev('ppo_epoch_apply_kernel'):
+                L.check(L.lib().smi_ppo_epoch_apply(a, e, st), 'smi_ppo_epoch_apply')
+        if zf is not None:                                    # global z_update
+            zbuf = self._buf('zbuf', (2, D))
+            L.call('smi_zfilter_colstats', L.ptr(x), B, D, T * D, L.ptr(zbuf[0]), L.ptr(zbuf[1]), st)
+            yield zbuf
+            L.call('smi_zfilter_accumulate', L.ptr(zbuf[0]), L.ptr(zbuf[1]), D, float(a.B_global),
+                   L.ptr(zf.running_sum), L.ptr(zf.running_sumsq), L.ptr(zf.count), st)
 
-    def learn(self, batch):                                   # ppo.py:588-613
+    def _learn_phases(self, batch):
+        """learn() as a generator of the buffers a data-parallel learner must
+        all-reduce (SUM) between its launches; yields nothing when dp is None."""
         self.current_iteration += 1
         batch = self._preprocess_batch_ppo(batch)
-        self._optimize(batch['obs'], batch['actions'], batch['rewards'], batch['obs_next'],
-                       batch['persistent_infos'], batch['onetime_infos'], batch['dones'])
+        yield from self._optimize(batch['obs'], batch['actions'], batch['rewards'],
+                                  batch['obs_next'], batch['persistent_infos'],
+                                  batch['onetime_infos'], batch['dones'])
         if self.metrics is not None:
             self.metrics(self.last_stats(), self.global_step)
-        self.exp_counter += self.batch_size
+        self.exp_counter += self.batch_size * (self.dp.world_size if self.dp is not None else 1)
         self.global_step += 1
+
+    def learn(self, batch):                                   # ppo.py:588-613
+        for buf in self._learn_phases(batch):
+            self.dp.allreduce_(buf)
 
     def last_stats(self):
         """Statistics dict of the last learn() (ppo.py:219-224,278-284,328-331,555,571-582).

@@ -27,7 +27,7 @@ RTOL = 1e-5
 def _compare_params(name, got, ref, lr, updates, report):
     got = np.asarray(got, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
-    floor = 1e-3 * np.max(np.abs(ref))
+    floor = 1e-2 * np.max(np.abs(ref))
     rel = np.abs(got - ref) / (np.abs(ref) + floor)
     bad = rel > RTOL
     flips = np.abs(got - ref)[bad]
