@@ -276,8 +276,52 @@ int smi_zfilter_accumulate(const float* sum_in, const float* sumsq_in, int dim, 
  * norm_out (device, may be NULL) receives the pre-clip norm. */
 int smi_adam_clip(float* params, const float* grad, float* m, float* v, int64_t n,
                   int* step, const float* lr_ptr, float beta1, float beta2,
-                  float eps, float weight_decay, float max_norm,
+                  float eps, float weight_decay, float max_norm, float clip_value,
                   const int* skip_flag, float* norm_out, void* stream);
+/* clip_value > 0 first clamps every gradient entry to [-clip_value, clip_value]
+ * (nnx.Module.clip_grad_value as called at ddpg.py:309,332; torchx is not
+ * available — the build states it as torch.nn.utils.clip_grad_value_). */
+
+/* ------------------------------------------------ dense layers (MFMA GEMM) */
+/* The Linear layers of builders.py:35-84 (DDPG ActorNetworkX / CriticNetworkX)
+ * and any head too large for the single-CU kernels, as LDS-tiled fp32 MFMA
+ * GEMMs over row-major operands with explicit leading dimensions (so a layer
+ * can write into a column block of a wider concat buffer):
+ *   forward:          y[r][o] = act(b[o] + sum_i x[r][i] w[o][i])   act 0/1/2
+ *   backward_input:   dx[r][i] = [relu_mask[r][i] > 0] * sum_o dy[r][o] w[o][i]
+ *   backward_weight:  dw[o][i] (+)= sum_r dy[r][o] x[r][i];  db[o] (+)= sum_r dy[r][o]
+ * w is [out][ldw] row-major (torch nn.Linear when ldw == in); a column block of a
+ * wider weight (the action block of CriticNetworkX's concat layer) is addressed
+ * by offsetting w and keeping ldw.  Deterministic (no atomics). */
+int smi_linear_forward(const float* x, int64_t ldx, int rows, int in_dim, const float* w,
+                       int64_t ldw, const float* b, int out_dim, int act, float* y, int64_t ldy,
+                       void* stream);
+int smi_linear_backward_input(const float* dy, int64_t ldg, int rows, int out_dim,
+                              const float* w, int64_t ldw, int in_dim, const float* relu_mask,
+                              int64_t ldm, float* dx, int64_t lddx, void* stream);
+int smi_linear_backward_weight(const float* dy, int64_t ldg, int rows, int out_dim,
+                               const float* x, int64_t ldx, int in_dim, float* dw, int64_t lddw,
+                               float* db, int accumulate, void* stream);
+
+/* ------------------------------------------------------- DDPG loss pieces */
+/* critic loss nn.MSELoss()(Q, y) (ddpg.py:306): loss = mean((Q-y)^2), dQ = 2(Q-y)/n */
+int smi_mse_grad(const float* q, int64_t q_stride, const float* y, int64_t n, float* dq,
+                 float* loss, void* stream);
+/* actor loss -Q(s, mu(s)).mean() (ddpg.py:325-329): loss, dQ = -1/n */
+int smi_neg_mean_grad(const float* q, int64_t q_stride, int64_t n, float* dq, float* loss,
+                      void* stream);
+/* dz = dy * (1 - y^2) for y = tanh(z) */
+int smi_tanh_backward(const float* dy, int64_t ldg, const float* y, int64_t ldy, int64_t rows,
+                      int cols, float* dz, int64_t ldz, void* stream);
+/* dst[r][0:cols] = src[r][0:cols] (strided) — the action block of torch.cat((h, a), 1) */
+int smi_copy_cols(const float* src, int64_t lds, int64_t rows, int cols, float* dst,
+                  int64_t ldd, void* stream);
+/* target <- tau*src + (1-tau)*target (soft target update, ddpg.py:409-417) */
+int smi_soft_update(float* target, const float* src, int64_t n, float tau, void* stream);
+/* action_norm, rewards, Q_target, Q_policy means of ddpg.py:335-345 -> stats4 */
+int smi_ddpg_stats(const float* actions, int64_t lda, int act_dim, const float* rewards,
+                   int64_t rs, const float* y, const float* q, int64_t qs, int64_t n,
+                   float* stats4, void* stream);
 
 /* ------------------------------------------------------ DDPG n-step target */
 /* Replaces the target of DDPGLearner._optimize (surreal/learner/ddpg.py:279-283):

@@ -1,0 +1,127 @@
+"""ORACLE (test infrastructure only — see oracle/__init__.py).
+
+fp32 CPU restatement of the DDPG learner step (low-dim observations, no
+layernorm — the reference default, ddpg_configs.py:21):
+  ActorNetworkX / CriticNetworkX   surreal/model/model_builders/builders.py:35-84
+  DDPGModel.forward                surreal/model/ddpg_net.py:86-93
+  DDPGLearner._optimize            surreal/learner/ddpg.py:244-352
+  DDPGLearner._target_update       surreal/learner/ddpg.py:403-428
+torchx's nnx.Module.clip_grad_value / soft_update / hard_update are not
+available; they are stated here as torch.nn.utils.clip_grad_value_,
+target <- tau*src + (1-tau)*target and a parameter copy.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+
+class ActorX(nn.Module):
+    """Linear-ReLU-Linear-ReLU-Linear-Tanh (builders.py:35-56)."""
+
+    def __init__(self, d_in, d_act, hidden):
+        super().__init__()
+        self.l1 = nn.Linear(d_in, hidden[0])
+        self.l2 = nn.Linear(hidden[0], hidden[1])
+        self.l3 = nn.Linear(hidden[1], d_act)
+
+    def forward(self, x):
+        return torch.tanh(self.l3(torch.relu(self.l2(torch.relu(self.l1(x))))))
+
+    def params(self):
+        return [self.l1.weight, self.l1.bias, self.l2.weight, self.l2.bias, self.l3.weight, self.l3.bias]
+
+
+class CriticX(nn.Module):
+    """obs -> Linear-ReLU ; cat(h, a) -> Linear-ReLU-Linear (builders.py:58-84)."""
+
+    def __init__(self, d_in, d_act, hidden):
+        super().__init__()
+        self.lo = nn.Linear(d_in, hidden[0])
+        self.lc = nn.Linear(hidden[0] + d_act, hidden[1])
+        self.lq = nn.Linear(hidden[1], 1)
+
+    def forward(self, obs, act):
+        h = torch.relu(self.lo(obs))
+        return self.lq(torch.relu(self.lc(torch.cat((h, act), 1))))
+
+    def params(self):
+        return [self.lo.weight, self.lo.bias, self.lc.weight, self.lc.bias, self.lq.weight, self.lq.bias]
+
+
+def flat_of(params):
+    return torch.cat([p.detach().reshape(-1) for p in params])
+
+
+def load_flat(params, f):
+    o = 0
+    with torch.no_grad():
+        for p in params:
+            n = p.numel()
+            p.copy_(torch.as_tensor(f[o:o + n]).reshape(p.shape))
+            o += n
+
+
+class DDPGLearnerRef:
+    def __init__(self, lc, obs_dim, act_dim, seed=0):
+        torch.manual_seed(seed)
+        net = lc['algo']['network']
+        self.gamma = lc['algo']['gamma']
+        self.n_step = lc['algo']['n_step']
+        self.batch_size = lc['replay']['batch_size']
+        ah, ch = lc['model']['actor_fc_hidden_sizes'], lc['model']['critic_fc_hidden_sizes']
+        self.actor, self.critic = ActorX(obs_dim, act_dim, ah), CriticX(obs_dim, act_dim, ch)
+        self.actor_t, self.critic_t = ActorX(obs_dim, act_dim, ah), CriticX(obs_dim, act_dim, ch)
+        self.hard_update()
+        self.clip_actor = net['clip_actor_gradient']
+        self.actor_clip_value = net['actor_gradient_value_clip']
+        self.clip_critic = net['clip_critic_gradient']
+        self.critic_clip_value = net['critic_gradient_value_clip']
+        self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=net['lr_critic'],
+                                             weight_decay=net['critic_regularization'])
+        self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=net['lr_actor'],
+                                            weight_decay=net['actor_regularization'])
+        tu = net['target_update']
+        self.target_update_type = tu['type']
+        self.tau = tu.get('tau', 1e-3)
+        self.interval = tu.get('interval', 500)
+        self.counter = 0
+
+    def hard_update(self):
+        self.actor_t.load_state_dict(self.actor.state_dict())
+        self.critic_t.load_state_dict(self.critic.state_dict())
+
+    def optimize(self, obs, actions, rewards, obs_next, done):          # ddpg.py:244-352
+        assert actions.max().item() <= 1.0 and actions.min().item() >= -1.0
+        with torch.no_grad():
+            a_t = self.actor_t(obs_next)
+            q_t = self.critic_t(obs_next, a_t)
+            y = rewards + pow(self.gamma, self.n_step) * q_t * (1.0 - done)
+        q = self.critic(obs, actions)
+        self.critic.zero_grad()
+        critic_loss = nn.MSELoss()(q, y)
+        critic_loss.backward()
+        if self.clip_critic:
+            nn.utils.clip_grad_value_(self.critic.parameters(), self.critic_clip_value)
+        self.critic_optim.step()
+        self.actor.zero_grad()
+        actor_loss = -self.critic(obs, self.actor(obs)).mean()
+        actor_loss.backward()
+        if self.clip_actor:
+            nn.utils.clip_grad_value_(self.actor.parameters(), self.actor_clip_value)
+        self.actor_optim.step()
+        stats = {'actor_loss': actor_loss.item(), 'critic_loss': critic_loss.item(),
+                 'action_norm': actions.norm(2, 1).mean().item(), 'rewards': rewards.mean().item(),
+                 'Q_target': y.mean().item(), 'Q_policy': q.mean().item()}
+        self.target_update()
+        return stats
+
+    def target_update(self):                                            # ddpg.py:403-428
+        if self.target_update_type == 'soft':
+            with torch.no_grad():
+                for t, s in zip(list(self.actor_t.parameters()) + list(self.critic_t.parameters()),
+                                list(self.actor.parameters()) + list(self.critic.parameters())):
+                    t.copy_(self.tau * s + (1 - self.tau) * t)
+        else:
+            self.counter += 1
+            if self.counter % self.interval == 0:
+                self.hard_update()

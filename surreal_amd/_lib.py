@@ -79,8 +79,19 @@ _SIGS = {
     'smi_ppo_epoch_grad': (c_int, [ctypes.POINTER(PPOArgs), c_int, P]),
     'smi_ppo_epoch_apply': (c_int, [ctypes.POINTER(PPOArgs), c_int, P]),
     'smi_zfilter_accumulate': (c_int, [P, P, c_int, c_f32, P, P, P, P]),
-    'smi_adam_clip': (c_int, [P, P, P, P, c_i64, P, P, c_f32, c_f32, c_f32, c_f32, c_f32, P,
-                              P, P]),
+    'smi_adam_clip': (c_int, [P, P, P, P, c_i64, P, P, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32,
+                              P, P, P]),
+    'smi_linear_forward': (c_int, [P, c_i64, c_int, c_int, P, c_i64, P, c_int, c_int, P, c_i64, P]),
+    'smi_linear_backward_input': (c_int, [P, c_i64, c_int, c_int, P, c_i64, c_int, P, c_i64, P,
+                                          c_i64, P]),
+    'smi_linear_backward_weight': (c_int, [P, c_i64, c_int, c_int, P, c_i64, c_int, P, c_i64, P,
+                                           c_int, P]),
+    'smi_mse_grad': (c_int, [P, c_i64, P, c_i64, P, P, P]),
+    'smi_neg_mean_grad': (c_int, [P, c_i64, c_i64, P, P, P]),
+    'smi_tanh_backward': (c_int, [P, c_i64, P, c_i64, c_i64, c_int, P, c_i64, P]),
+    'smi_copy_cols': (c_int, [P, c_i64, c_i64, c_int, P, c_i64, P]),
+    'smi_soft_update': (c_int, [P, P, c_i64, c_f32, P]),
+    'smi_ddpg_stats': (c_int, [P, c_i64, c_int, P, c_i64, P, P, c_i64, c_i64, P, P]),
     'smi_ddpg_target': (c_int, [P, P, P, P, c_i64, c_f32, P, P]),
     'smi_mt_seed': (c_int, [ctypes.c_uint64, P]),
     'smi_mt_randint_host': (c_int, [P, c_i64, c_i64, P]),

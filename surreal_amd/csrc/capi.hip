@@ -46,7 +46,21 @@ int launch_mlp_forward(const float*, int, int, int, int, int, int, const float*,
                        hipStream_t);
 int launch_moments(const float*, int64_t, const double*, int, double*, hipStream_t);
 int launch_adam_clip(float*, const float*, float*, float*, int64_t, int*, const float*, float,
-                     float, float, float, float, const int*, float*, hipStream_t);
+                     float, float, float, float, float, const int*, float*, hipStream_t);
+int launch_linear_fwd(const float*, int64_t, int, int, const float*, int64_t, const float*, int,
+                      int, float*, int64_t, hipStream_t);
+int launch_linear_bwd_dx(const float*, int64_t, int, int, const float*, int64_t, int,
+                         const float*, int64_t, float*, int64_t, hipStream_t);
+int launch_linear_bwd_dw(const float*, int64_t, int, int, const float*, int64_t, int, float*,
+                         int64_t, float*, int, hipStream_t);
+int launch_mse_grad(const float*, int64_t, const float*, int64_t, float*, float*, hipStream_t);
+int launch_neg_mean_grad(const float*, int64_t, int64_t, float*, float*, hipStream_t);
+int launch_tanh_backward(const float*, int64_t, const float*, int64_t, int64_t, int, float*,
+                         int64_t, hipStream_t);
+int launch_copy_cols(const float*, int64_t, int64_t, int, float*, int64_t, hipStream_t);
+int launch_soft_update(float*, const float*, int64_t, float, hipStream_t);
+int launch_ddpg_stats(const float*, int64_t, int, const float*, int64_t, const float*,
+                      const float*, int64_t, int64_t, float*, hipStream_t);
 int launch_ddpg_target(const float*, const float*, const float*, const float*, int64_t, float,
                        float*, hipStream_t);
 void mt_seed_host(uint64_t, uint32_t*);
@@ -223,10 +237,79 @@ int smi_zfilter_accumulate(const float* sum_in, const float* sumsq_in, int dim, 
 
 int smi_adam_clip(float* params, const float* grad, float* m, float* v, int64_t n, int* step,
                   const float* lr_ptr, float beta1, float beta2, float eps, float weight_decay,
-                  float max_norm, const int* skip_flag, float* norm_out, void* stream) {
+                  float max_norm, float clip_value, const int* skip_flag, float* norm_out,
+                  void* stream) {
   REQUIRE(params && grad && m && v && step && lr_ptr && n > 0, "adam_clip: bad args");
   return launch_adam_clip(params, grad, m, v, n, step, lr_ptr, beta1, beta2, eps, weight_decay,
-                          max_norm, skip_flag, norm_out, SMI_STREAM(stream));
+                          max_norm, clip_value, skip_flag, norm_out, SMI_STREAM(stream));
+}
+
+int smi_linear_forward(const float* x, int64_t ldx, int rows, int in_dim, const float* w,
+                       int64_t ldw, const float* b, int out_dim, int act, float* y, int64_t ldy,
+                       void* stream) {
+  REQUIRE(x && w && y && rows >= 0 && in_dim > 0 && out_dim > 0, "linear_forward: bad args");
+  REQUIRE(ldx >= in_dim && ldy >= out_dim && ldw >= in_dim, "linear_forward: leading dims too small");
+  REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_TANH, "linear_forward: act 0/1/2");
+  return launch_linear_fwd(x, ldx, rows, in_dim, w, ldw, b, out_dim, act, y, ldy,
+                           SMI_STREAM(stream));
+}
+
+int smi_linear_backward_input(const float* dy, int64_t ldg, int rows, int out_dim, const float* w,
+                              int64_t ldw, int in_dim, const float* relu_mask, int64_t ldm,
+                              float* dx, int64_t lddx, void* stream) {
+  REQUIRE(dy && w && dx && rows >= 0 && in_dim > 0 && out_dim > 0 && ldw >= in_dim,
+          "linear_backward_input: bad args");
+  return launch_linear_bwd_dx(dy, ldg, rows, out_dim, w, ldw, in_dim, relu_mask, ldm, dx, lddx,
+                              SMI_STREAM(stream));
+}
+
+int smi_linear_backward_weight(const float* dy, int64_t ldg, int rows, int out_dim, const float* x,
+                               int64_t ldx, int in_dim, float* dw, int64_t lddw, float* db,
+                               int accumulate, void* stream) {
+  REQUIRE(dy && x && dw && rows >= 0 && in_dim > 0 && out_dim > 0 && lddw >= in_dim,
+          "linear_backward_weight: bad args");
+  return launch_linear_bwd_dw(dy, ldg, rows, out_dim, x, ldx, in_dim, dw, lddw, db, accumulate,
+                              SMI_STREAM(stream));
+}
+
+int smi_mse_grad(const float* q, int64_t q_stride, const float* y, int64_t n, float* dq,
+                 float* loss, void* stream) {
+  REQUIRE(q && y && dq && n > 0, "mse_grad: bad args");
+  return launch_mse_grad(q, q_stride, y, n, dq, loss, SMI_STREAM(stream));
+}
+
+int smi_neg_mean_grad(const float* q, int64_t q_stride, int64_t n, float* dq, float* loss,
+                      void* stream) {
+  REQUIRE(q && dq && n > 0, "neg_mean_grad: bad args");
+  return launch_neg_mean_grad(q, q_stride, n, dq, loss, SMI_STREAM(stream));
+}
+
+int smi_tanh_backward(const float* dy, int64_t ldg, const float* y, int64_t ldy, int64_t rows,
+                      int cols, float* dz, int64_t ldz, void* stream) {
+  REQUIRE(dy && y && dz && rows >= 0 && cols > 0, "tanh_backward: bad args");
+  if (rows == 0) return SMI_OK;
+  return launch_tanh_backward(dy, ldg, y, ldy, rows, cols, dz, ldz, SMI_STREAM(stream));
+}
+
+int smi_copy_cols(const float* src, int64_t lds, int64_t rows, int cols, float* dst, int64_t ldd,
+                  void* stream) {
+  REQUIRE(src && dst && rows >= 0 && cols > 0, "copy_cols: bad args");
+  if (rows == 0) return SMI_OK;
+  return launch_copy_cols(src, lds, rows, cols, dst, ldd, SMI_STREAM(stream));
+}
+
+int smi_soft_update(float* target, const float* src, int64_t n, float tau, void* stream) {
+  REQUIRE(target && src && n >= 0, "soft_update: bad args");
+  if (n == 0) return SMI_OK;
+  return launch_soft_update(target, src, n, tau, SMI_STREAM(stream));
+}
+
+int smi_ddpg_stats(const float* actions, int64_t lda, int act_dim, const float* rewards,
+                   int64_t rs, const float* y, const float* q, int64_t qs, int64_t n,
+                   float* stats4, void* stream) {
+  REQUIRE(actions && rewards && y && q && stats4 && n > 0 && act_dim > 0, "ddpg_stats: bad args");
+  return launch_ddpg_stats(actions, lda, act_dim, rewards, rs, y, q, qs, n, stats4,
+                           SMI_STREAM(stream));
 }
 
 int smi_ddpg_target(const float* rewards, const float* dones, const float* q_next,

@@ -258,11 +258,13 @@ moments_kernel(const float* __restrict__ x, int64_t n, const double* partials, i
 // workgroup recomputes the global norm from the partials in the same order, so
 // the coefficient is identical everywhere without a grid barrier).
 __global__ void __launch_bounds__(kWG)
-sumsq_partial_kernel(const float* __restrict__ g, int64_t n, double* part) {
+sumsq_partial_kernel(const float* __restrict__ g, int64_t n, float clip_value, double* part) {
   __shared__ double scr[kNW];
   double a = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
-    const double v = (double)g[i];
+    float gi = g[i];
+    if (clip_value > 0.f) gi = fminf(fmaxf(gi, -clip_value), clip_value);
+    const double v = (double)gi;
     a += v * v;
   }
   a = block_sum_d(a, scr);
@@ -272,8 +274,8 @@ sumsq_partial_kernel(const float* __restrict__ g, int64_t n, double* part) {
 __global__ void __launch_bounds__(kWG)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, int64_t n, int* step, const float* lr_ptr, float beta1,
-            float beta2, float eps, float wd, float max_norm, const double* part, int np,
-            const int* skip, float* norm_out) {
+            float beta2, float eps, float wd, float max_norm, float clip_value, const double* part,
+            int np, const int* skip, float* norm_out) {
   if (skip && skip[0] != 0) return;
   __shared__ float s_coef;
   __shared__ int s_t;
@@ -301,7 +303,9 @@ adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restric
   const float w1 = (float)(1.0 - (double)beta1);
   const float w2 = (float)(1.0 - (double)beta2);
   for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
-    float gi = g[i] * coef;
+    float gi = g[i];
+    if (clip_value > 0.f) gi = fminf(fmaxf(gi, -clip_value), clip_value);   // clip_grad_value_
+    gi = gi * coef;
     float pi = p[i];
     if (wd != 0.f) gi = gi + wd * pi;
     float mi = m[i], vi = v[i];
@@ -424,15 +428,15 @@ int launch_moments(const float* x, int64_t n, const double* part, int np, double
 
 int launch_adam_clip(float* p, const float* g, float* m, float* v, int64_t n, int* step,
                      const float* lr, float b1, float b2, float eps, float wd, float max_norm,
-                     const int* skip, float* norm_out, hipStream_t st) {
+                     float clip_value, const int* skip, float* norm_out, hipStream_t st) {
   const int grid = grid_for(n, 512);
   double* part = reinterpret_cast<double*>(workspace_f32(2 * 512));
   if (!part) return set_error(SMI_E_ARG, "adam: workspace unavailable");
-  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kWG), 0, st, g, n, part);
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kWG), 0, st, g, n, clip_value, part);
   int rc = check_launch("sumsq_partial_kernel");
   if (rc) return rc;
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kWG), 0, st, p, g, m, v, n, step, lr, b1, b2,
-                     eps, wd, max_norm, part, grid, skip, norm_out);
+                     eps, wd, max_norm, clip_value, part, grid, skip, norm_out);
   rc = check_launch("adam_kernel");
   if (rc) return rc;
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step, skip);

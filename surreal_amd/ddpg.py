@@ -1,0 +1,386 @@
+"""DDPGModel / DDPGLearner mirrors (surreal/model/ddpg_net.py,
+surreal/learner/ddpg.py) on the MFMA GEMM layers of linear_kernels.hip.
+
+One DDPG learn() (ddpg.py:244-352, batch 512, actor 17-300-200-6, critic
+17-400 | +6 -300-1) is ~45 launches on one stream and no host sync:
+target actor + target critic forward, n-step target, critic forward, MSE
+gradient, critic backward, Adam; actor forward, critic forward with the
+updated critic, -mean(Q) gradient, backward through the critic's action block
+and the actor, Adam; target update; statistics.  Layernorm (off by default,
+ddpg_configs.py:21) and pixel inputs are not built.
+
+Parameter layouts (flat, torch (out, in) order):
+  actor : W1[h1][D] b1 W2[h2][h1] b2 W3[A][h2] b3
+  critic: Wo[c1][D] bo Wc[c2][c1+A] bc Wq[1][c2] bq
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from .config import Config, ConfigError
+from .model import _LinearView
+
+RELU, TANH, NONE = 1, 2, 0
+
+
+class _FlatNet(nn.Module):
+    def __init__(self, shapes, device, generator=None):
+        super().__init__()
+        n = sum(o * i + o for (i, o) in shapes)
+        flat = torch.zeros(n, dtype=torch.float32, device=device)
+        self.__dict__['flat'] = flat
+        self.layers = []
+        off = 0
+        for (i, o) in shapes:
+            lin = _LinearView(flat, off, i, o)
+            lin.reset_parameters(generator)
+            off = lin.end
+            self.layers.append(lin)
+
+    def wb(self, k):
+        lin = self.layers[k]
+        return lin.weight, lin.bias
+
+
+class ActorNetworkX(_FlatNet):
+    """builders.py:35-56 (use_layernorm=False)."""
+
+    def __init__(self, D_in, D_act, hidden_sizes=(300, 200), device=None, generator=None):
+        shapes = [(D_in, hidden_sizes[0]), (hidden_sizes[0], hidden_sizes[1]), (hidden_sizes[1], D_act)]
+        super().__init__(shapes, device, generator)
+        self.model = nn.Sequential(self.layers[0], nn.ReLU(), self.layers[1], nn.ReLU(),
+                                   self.layers[2], nn.Tanh())
+        self.dims = (D_in, hidden_sizes[0], hidden_sizes[1], D_act)
+
+
+class CriticNetworkX(_FlatNet):
+    """builders.py:58-84 (use_layernorm=False)."""
+
+    def __init__(self, D_in, D_act, hidden_sizes=(400, 300), device=None, generator=None):
+        c1, c2 = hidden_sizes
+        shapes = [(D_in, c1), (c1 + D_act, c2), (c2, 1)]
+        super().__init__(shapes, device, generator)
+        self.model_obs = nn.Sequential(self.layers[0], nn.ReLU())
+        self.model_concat = nn.Sequential(self.layers[1], nn.ReLU(), self.layers[2])
+        self.dims = (D_in, c1, c2, D_act)
+
+
+class DDPGModel(nn.Module):
+    """ddpg_net.py:9-95 for low-dimensional observations."""
+
+    def __init__(self, obs_spec, action_dim, use_layernorm, actor_fc_hidden_sizes,
+                 critic_fc_hidden_sizes, conv_out_channels=None, conv_kernel_sizes=None,
+                 conv_strides=None, conv_hidden_dim=None, critic_only=False, device=None,
+                 generator=None):
+        super().__init__()
+        L.require_gpu()
+        if 'pixel' in obs_spec:
+            raise NotImplementedError('surreal_amd: DDPG pixel inputs are SURVEY §8(f) rank 1')
+        if use_layernorm:
+            raise NotImplementedError('surreal_amd: DDPG layernorm is not built')
+        self.device = torch.device(device) if device is not None else torch.device('cuda')
+        self.action_dim = action_dim
+        self.input_dim = int(obs_spec['low_dim']['flat_inputs'][0])
+        self.actor = None if critic_only else ActorNetworkX(
+            self.input_dim, action_dim, actor_fc_hidden_sizes, self.device, generator)
+        self.critic = CriticNetworkX(self.input_dim, action_dim, critic_fc_hidden_sizes,
+                                     self.device, generator)
+
+    def get_actor_parameters(self):
+        return self.actor.parameters()
+
+    def get_critic_parameters(self):
+        return self.critic.parameters()
+
+    def forward_perception(self, obs):
+        if isinstance(obs, torch.Tensor):
+            return obs
+        return obs['low_dim']['flat_inputs']
+
+    def forward_actor(self, obs):
+        net = _Net(self)
+        return net.actor_fwd(obs.contiguous(), obs.shape[0], store=None)
+
+    def forward_critic(self, obs, action):
+        net = _Net(self)
+        return net.critic_fwd(self.critic, obs.contiguous(), action.contiguous(), obs.shape[0], None)
+
+    def forward(self, obs_in, calculate_value=True, action=None):
+        x = self.forward_perception(obs_in)
+        if action is None:
+            action = self.forward_actor(x)
+        value = self.forward_critic(x, action) if calculate_value else None
+        return action, value
+
+
+def _p(t):
+    return L.ptr(t)
+
+
+class _Net(object):
+    """Launch helpers over a DDPGModel's flat buffers."""
+
+    def __init__(self, model, bufs=None):
+        self.m = model
+        self.st = L.stream(model.device)
+        self.bufs = bufs if bufs is not None else {}
+
+    def buf(self, name, shape):
+        t = self.bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape):
+            t = torch.zeros(shape, dtype=torch.float32, device=self.m.device)
+            self.bufs[name] = t
+        return t
+
+    def lin(self, x, ldx, rows, k, w, ldw, b, n, act, y, ldy):
+        L.call('smi_linear_forward', _p(x), ldx, rows, k, _p(w), ldw, _p(b), n, act, _p(y), ldy,
+               self.st)
+
+    def actor_fwd(self, obs, rows, store='a', actor=None):
+        actor = actor if actor is not None else self.m.actor
+        D, h1, h2, A = actor.dims
+        pre = store or 'tmp'
+        H1 = self.buf(pre + '_h1', (rows, h1))
+        H2 = self.buf(pre + '_h2', (rows, h2))
+        out = self.buf(pre + '_act', (rows, A))
+        (w1, b1), (w2, b2), (w3, b3) = actor.wb(0), actor.wb(1), actor.wb(2)
+        self.lin(obs, obs.stride(0), rows, D, w1, D, b1, h1, RELU, H1, h1)
+        self.lin(H1, h1, rows, h1, w2, h1, b2, h2, RELU, H2, h2)
+        self.lin(H2, h2, rows, h2, w3, h2, b3, A, TANH, out, A)
+        return out if store else out.clone()
+
+    def critic_fwd(self, critic, obs, act, rows, store):
+        D, c1, c2, A = critic.dims
+        pre = store or 'ctmp'
+        CAT = self.buf(pre + '_cat', (rows, c1 + A))
+        H2 = self.buf(pre + '_h2', (rows, c2))
+        Q = self.buf(pre + '_q', (rows, 1))
+        (wo, bo), (wc, bc), (wq, bq) = critic.wb(0), critic.wb(1), critic.wb(2)
+        self.lin(obs, obs.stride(0), rows, D, wo, D, bo, c1, RELU, CAT, c1 + A)
+        L.call('smi_copy_cols', _p(act), act.stride(0), rows, A, _p(CAT[:, c1:]), c1 + A, self.st)
+        self.lin(CAT, c1 + A, rows, c1 + A, wc, c1 + A, bc, c2, RELU, H2, c2)
+        self.lin(H2, c2, rows, c2, wq, c2, bq, 1, NONE, Q, 1)
+        return Q if store else Q.clone()
+
+
+class DDPGLearner(object):
+    """ddpg.py:12-440 on MI355X (low-dim, no layernorm)."""
+
+    def __init__(self, learner_config, env_config, session_config=None, metrics=None,
+                 device=None, seed=0):
+        L.require_gpu()
+        self.learner_config = lc = learner_config if isinstance(learner_config, Config) else Config(learner_config)
+        self.env_config = ec = env_config if isinstance(env_config, Config) else Config(env_config)
+        self.session_config = session_config
+        self.metrics = metrics
+        self.device = torch.device(device) if device is not None else \
+            torch.device('cuda', torch.cuda.current_device())
+        L.ensure_workspace(self.device)
+        self.current_iteration = 0
+        self.batch_size = lc.replay.batch_size
+        self.discount_factor = lc.algo.gamma
+        self.n_step = lc.algo.n_step
+        self.is_pixel_input = ec.get('pixel_input', False)
+        self.use_layernorm = lc.model.use_layernorm
+        net = lc.algo.network
+        self.use_double_critic = net.use_double_critic
+        self.use_action_regularization = net.use_action_regularization
+        if self.use_double_critic or self.use_action_regularization:
+            raise NotImplementedError('surreal_amd: TD3 options (double critic / target noise) '
+                                      'are not built yet')
+        tu = net.target_update
+        self.target_update_type = tu.type
+        if tu.type == 'soft':
+            self.target_update_tau = tu.tau
+        elif tu.type == 'hard':
+            self.target_update_counter = 0
+            self.target_update_interval = tu.interval
+        else:
+            raise ConfigError('Unsupported ddpg update type: {}'.format(tu.type))
+        self.clip_actor_gradient = net.clip_actor_gradient
+        self.actor_gradient_clip_value = net.actor_gradient_value_clip
+        self.clip_critic_gradient = net.clip_critic_gradient
+        self.critic_gradient_clip_value = net.critic_gradient_value_clip
+        self.action_dim = ec.action_spec['dim'][0]
+        gen = torch.Generator().manual_seed(seed)
+        mk = lambda: DDPGModel(ec.obs_spec, self.action_dim, self.use_layernorm,  # noqa: E731
+                               lc.model.actor_fc_hidden_sizes, lc.model.critic_fc_hidden_sizes,
+                               device=self.device, generator=gen)
+        self.model = mk()
+        self.model_target = mk()
+        self._hard_update()
+        dev = self.device
+        self.opt = {}
+        for name, flat, lr, wd in (('critic', self.model.critic.flat, net.lr_critic, net.critic_regularization),
+                                   ('actor', self.model.actor.flat, net.lr_actor, net.actor_regularization)):
+            self.opt[name] = {'m': torch.zeros_like(flat), 'v': torch.zeros_like(flat),
+                              'step': torch.zeros(1, dtype=torch.int32, device=dev),
+                              'lr': torch.tensor([lr], dtype=torch.float32, device=dev),
+                              'wd': float(wd), 'g': torch.zeros_like(flat)}
+        self.stats_buf = torch.zeros(8, dtype=torch.float32, device=dev)
+        self._bufs = {}
+        self.kernel_events = None
+
+    # ------------------------------------------------------------ helpers
+    def _hard_update(self):
+        with torch.no_grad():
+            self.model_target.actor.flat.copy_(self.model.actor.flat)
+            self.model_target.critic.flat.copy_(self.model.critic.flat)
+
+    def _adam(self, name, flat, clip_value, st):
+        o = self.opt[name]
+        L.call('smi_adam_clip', _p(flat), _p(o['g']), _p(o['m']), _p(o['v']), flat.numel(),
+               _p(o['step']), _p(o['lr']), 0.9, 0.999, 1e-8, o['wd'], 0.0, float(clip_value),
+               None, None, st)
+
+    def preprocess(self, batch):                                         # ddpg.py:186-242
+        out = {}
+        for k in ('obs', 'obs_next'):
+            v = batch[k]
+            if isinstance(v, dict):
+                if 'pixel' in v:
+                    raise NotImplementedError('surreal_amd: pixel inputs')
+                v = v['low_dim']['flat_inputs']
+            out[k] = torch.as_tensor(v, dtype=torch.float32).to(self.device, non_blocking=True)
+        for k in ('actions', 'rewards', 'dones'):
+            out[k] = torch.as_tensor(batch[k], dtype=torch.float32).to(self.device, non_blocking=True)
+        return Config(out)
+
+    # --------------------------------------------------------- _optimize
+    def _optimize(self, obs, actions, rewards, obs_next, done):          # ddpg.py:244-352
+        B = obs.shape[0]
+        st = L.stream(self.device)
+        net = _Net(self.model, self._bufs)
+        tnet = _Net(self.model_target, self._bufs)
+        D, h1, h2, A = self.model.actor.dims
+        _, c1, c2, _ = self.model.critic.dims
+        rs = rewards.stride(0) if rewards.dim() == 2 else 1
+        # target: y = r + gamma^n * Q'(s', mu'(s')) * (1 - d)           (ddpg.py:266-284)
+        a_t = tnet.actor_fwd(obs_next, B, store='ta')
+        q_t = tnet.critic_fwd(self.model_target.critic, obs_next, a_t, B, store='tc')
+        y = net.buf('y', (B, 1))
+        r1 = rewards if rewards.is_contiguous() else rewards.contiguous()
+        d1 = done if done.is_contiguous() else done.contiguous()
+        L.call('smi_ddpg_target', _p(r1), _p(d1), _p(q_t), None, B,
+               float(pow(self.discount_factor, self.n_step)), _p(y), st)
+        # critic update (ddpg.py:287-310)
+        crit = self.model.critic
+        q = net.critic_fwd(crit, obs, actions, B, store='c')
+        dq = net.buf('dq', (B, 1))
+        L.call('smi_mse_grad', _p(q), 1, _p(y), B, _p(dq), _p(self.stats_buf[1:2]), st)
+        g = self.opt['critic']['g']
+        self._critic_backward(net, crit, obs, B, dq, 'c', g, st, need_obs_grad=True)
+        self._adam('critic', crit.flat,
+                   self.critic_gradient_clip_value if self.clip_critic_gradient else 0.0, st)
+        # actor update with the updated critic (ddpg.py:323-333)
+        act = self.model.actor
+        a = net.actor_fwd(obs, B, store='a')
+        q2 = net.critic_fwd(crit, obs, a, B, store='c2')
+        dq2 = net.buf('dq2', (B, 1))
+        L.call('smi_neg_mean_grad', _p(q2), 1, B, _p(dq2), _p(self.stats_buf[0:1]), st)
+        dA = self._critic_backward(net, crit, obs, B, dq2, 'c2', None, st, need_obs_grad=False)
+        self._actor_backward(net, act, obs, B, dA, self.opt['actor']['g'], st)
+        self._adam('actor', act.flat,
+                   self.actor_gradient_clip_value if self.clip_actor_gradient else 0.0, st)
+        # statistics (ddpg.py:335-345)
+        L.call('smi_ddpg_stats', _p(actions), actions.stride(0), A, _p(rewards), rs, _p(y), _p(q), 1,
+               B, _p(self.stats_buf[2:6]), st)
+        self._target_update()
+
+    def _critic_backward(self, net, crit, obs, B, dq, pre, g, st, need_obs_grad):
+        """Backward through CriticNetworkX.  With g: weight grads into g (flat).
+        Always returns d loss / d action (B, A) when g is None."""
+        D, c1, c2, A = crit.dims
+        CAT = net.bufs[pre + '_cat']
+        H2 = net.bufs[pre + '_h2']
+        (wo, bo), (wc, bc), (wq, bq) = crit.wb(0), crit.wb(1), crit.wb(2)
+        dH2 = net.buf('dH2', (B, c2))
+        L.call('smi_linear_backward_input', _p(dq), 1, B, 1, _p(wq), c2, c2, _p(H2), c2, _p(dH2),
+               c2, st)
+        if g is not None:
+            off_bo = c1 * D
+            off_wc = off_bo + c1
+            off_bc = off_wc + c2 * (c1 + A)
+            off_wq = off_bc + c2
+            off_bq = off_wq + c2
+            L.call('smi_linear_backward_weight', _p(dq), 1, B, 1, _p(H2), c2, c2, _p(g[off_wq:]), c2,
+                   _p(g[off_bq:]), 0, st)
+            L.call('smi_linear_backward_weight', _p(dH2), c2, B, c2, _p(CAT), c1 + A, c1 + A,
+                   _p(g[off_wc:]), c1 + A, _p(g[off_bc:]), 0, st)
+            dH1 = net.buf('dH1c', (B, c1))
+            L.call('smi_linear_backward_input', _p(dH2), c2, B, c2, _p(wc), c1 + A, c1, _p(CAT),
+                   c1 + A, _p(dH1), c1, st)
+            L.call('smi_linear_backward_weight', _p(dH1), c1, B, c1, _p(obs), obs.stride(0), D,
+                   _p(g[0:]), D, _p(g[off_bo:]), 0, st)
+            return None
+        dA = net.buf('dA', (B, A))
+        L.call('smi_linear_backward_input', _p(dH2), c2, B, c2, _p(wc[:, c1:]), c1 + A, A, None, 0,
+               _p(dA), A, st)
+        return dA
+
+    def _actor_backward(self, net, act, obs, B, dA, g, st):
+        D, h1, h2, A = act.dims
+        H1, H2, out = net.bufs['a_h1'], net.bufs['a_h2'], net.bufs['a_act']
+        (w1, b1), (w2, b2), (w3, b3) = act.wb(0), act.wb(1), act.wb(2)
+        dZ = net.buf('dZ3', (B, A))
+        L.call('smi_tanh_backward', _p(dA), A, _p(out), A, B, A, _p(dZ), A, st)
+        off_b1 = h1 * D
+        off_w2 = off_b1 + h1
+        off_b2 = off_w2 + h2 * h1
+        off_w3 = off_b2 + h2
+        off_b3 = off_w3 + A * h2
+        L.call('smi_linear_backward_weight', _p(dZ), A, B, A, _p(H2), h2, h2, _p(g[off_w3:]), h2,
+               _p(g[off_b3:]), 0, st)
+        dH2 = net.buf('dH2a', (B, h2))
+        L.call('smi_linear_backward_input', _p(dZ), A, B, A, _p(w3), h2, h2, _p(H2), h2, _p(dH2), h2, st)
+        L.call('smi_linear_backward_weight', _p(dH2), h2, B, h2, _p(H1), h1, h1, _p(g[off_w2:]), h1,
+               _p(g[off_b2:]), 0, st)
+        dH1 = net.buf('dH1a', (B, h1))
+        L.call('smi_linear_backward_input', _p(dH2), h2, B, h2, _p(w2), h1, h1, _p(H1), h1, _p(dH1),
+               h1, st)
+        L.call('smi_linear_backward_weight', _p(dH1), h1, B, h1, _p(obs), obs.stride(0), D, _p(g[0:]),
+               D, _p(g[off_b1:]), 0, st)
+
+    def _target_update(self):                                            # ddpg.py:403-428
+        st = L.stream(self.device)
+        if self.target_update_type == 'soft':
+            for t, s in ((self.model_target.actor.flat, self.model.actor.flat),
+                         (self.model_target.critic.flat, self.model.critic.flat)):
+                L.call('smi_soft_update', _p(t), _p(s), t.numel(), float(self.target_update_tau), st)
+        else:
+            self.target_update_counter += 1
+            if self.target_update_counter % self.target_update_interval == 0:
+                self._hard_update()
+
+    # ------------------------------------------------------- reference API
+    def learn(self, batch):                                              # ddpg.py:354-376
+        self.current_iteration += 1
+        if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
+            batch = self.preprocess(batch)
+        obs = batch['obs']
+        obs = obs['low_dim']['flat_inputs'] if isinstance(obs, dict) else obs
+        obs_next = batch['obs_next']
+        obs_next = obs_next['low_dim']['flat_inputs'] if isinstance(obs_next, dict) else obs_next
+        self._optimize(obs, batch['actions'], batch['rewards'], obs_next, batch['dones'])
+        if self.metrics is not None:
+            self.metrics(self.last_stats(), self.current_iteration)
+
+    def last_stats(self):
+        v = self.stats_buf.cpu().numpy()
+        return {'actor_loss': float(v[0]), 'critic_loss': float(v[1]), 'action_norm': float(v[2]),
+                'rewards': float(v[3]), 'Q_target': float(v[4]), 'Q_policy': float(v[5])}
+
+    def module_dict(self):
+        return {'ddpg': self.model}
+
+    def checkpoint_attributes(self):
+        return ['current_iteration', 'model', 'model_target']
+
+    def _prefetcher_preprocess(self, batch):
+        from .aggregator import FrameStackPreprocessor, SSARAggregator
+        if not self.env_config.get('frame_stack_concatenate_on_env', True):
+            batch = FrameStackPreprocessor(self.env_config.frame_stacks).preprocess_list(batch)
+        return SSARAggregator(self.env_config.obs_spec, self.env_config.action_spec).aggregate(batch)

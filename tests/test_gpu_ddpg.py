@@ -1,0 +1,108 @@
+"""DDPG learner step (ddpg.py:244-428) on the MFMA GEMM layers vs the CPU
+oracle, plus the uniform replay (CPython-exact indices) feeding it.  Tolerance
+as test_gpu_ppo.py (1e-5 relative, scale floor, Adam sign-flip budget)."""
+import copy
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ddpg_ref as R
+from surreal_amd import _lib as L
+from surreal_amd import synthetic
+from surreal_amd.config import DDPG_DEFAULT_LEARNER_CONFIG, gym_env_config
+from surreal_amd.ddpg import DDPGLearner
+from tests.helpers import max_rel_err
+from tests.test_gpu_ppo import _compare_params
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(B=512, target='hard', clip_critic=False):
+    lc = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
+    lc.replay.batch_size = B
+    lc.algo.network.clip_critic_gradient = clip_critic
+    if target == 'soft':
+        lc.algo.network.target_update = {'type': 'soft', 'tau': 1e-3}
+    else:
+        lc.algo.network.target_update = {'type': 'hard', 'interval': 2}
+    return lc
+
+
+def _sync_weights(learner, ref):
+    R.load_flat(ref.actor.params(), learner.model.actor.flat.cpu())
+    R.load_flat(ref.critic.params(), learner.model.critic.flat.cpu())
+    ref.hard_update()
+
+
+@pytest.mark.parametrize('rows,k,n', [(512, 17, 300), (70, 406, 300), (512, 300, 1), (3, 5, 7)])
+def test_linear_ops_vs_torch(rows, k, n):
+    g = torch.Generator().manual_seed(rows + k)
+    x = torch.randn(rows, k, generator=g)
+    lin = torch.nn.Linear(k, n)
+    y_ref = torch.relu(lin(x))
+    dy = torch.randn(rows, n, generator=g)
+    xd, wd, bd = x.cuda(), lin.weight.detach().cuda().contiguous(), lin.bias.detach().cuda()
+    y = torch.empty(rows, n, device='cuda')
+    st = L.stream()
+    L.call('smi_linear_forward', L.ptr(xd), k, rows, k, L.ptr(wd), k, L.ptr(bd), n, 1, L.ptr(y), n, st)
+    assert max_rel_err(y.cpu(), y_ref.detach()) < 1e-5
+    dyd = dy.cuda()
+    dx = torch.empty(rows, k, device='cuda')
+    L.call('smi_linear_backward_input', L.ptr(dyd), n, rows, n, L.ptr(wd), k, k, L.ptr(xd), k,
+           L.ptr(dx), k, st)
+    dx_ref = (dy @ lin.weight.detach()) * (x > 0)
+    assert max_rel_err(dx.cpu(), dx_ref) < 1e-5
+    dw = torch.empty(n, k, device='cuda')
+    db = torch.empty(n, device='cuda')
+    L.call('smi_linear_backward_weight', L.ptr(dyd), n, rows, n, L.ptr(xd), k, k, L.ptr(dw), k,
+           L.ptr(db), 0, st)
+    assert max_rel_err(dw.cpu(), dy.t() @ x) < 1e-5
+    assert max_rel_err(db.cpu(), dy.sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize('target,clip_critic', [('hard', False), ('soft', True)])
+def test_ddpg_learn_matches_oracle(target, clip_critic):
+    B, D, A = 512, 17, 6
+    lc = _cfg(B, target, clip_critic)
+    learner = DDPGLearner(lc, gym_env_config(D, A), seed=2)
+    ref = R.DDPGLearnerRef(lc, D, A)
+    _sync_weights(learner, ref)
+    report = {}
+    for it in range(3):
+        b = synthetic.ddpg_batch(B, D, A, seed=it)
+        rs = ref.optimize(b['obs'], b['actions'], b['rewards'], b['obs_next'], b['dones'])
+        learner.learn({k: v.cuda() for k, v in b.items()})
+        s = learner.last_stats()
+        for k in rs:
+            assert abs(s[k] - rs[k]) <= 1e-4 * abs(rs[k]) + 1e-5, (it, k, s[k], rs[k])
+        _compare_params(f'critic{it}', learner.model.critic.flat.cpu(), R.flat_of(ref.critic.params()),
+                        1e-3, it + 1, report)
+        _compare_params(f'actor{it}', learner.model.actor.flat.cpu(), R.flat_of(ref.actor.params()),
+                        1e-4, it + 1, report)
+        _compare_params(f'tcritic{it}', learner.model_target.critic.flat.cpu(),
+                        R.flat_of(ref.critic_t.params()), 1e-3, it + 1, report)
+    print('ddpg parity report:', report)
+
+
+def test_replay_sample_feeds_learner_with_cpython_indices():
+    from surreal_amd.replay import UniformReplay
+    D, A, B = 17, 6, 512
+    lc = _cfg(B)
+    lc.replay.memory_size = 5000
+    lc.replay.sampling_start_size = 100
+    ec = gym_env_config(D, A)
+    rep = UniformReplay(lc, ec, seed=1234)
+    rows = np.random.RandomState(0).randn(3000, rep.width).astype(np.float32)
+    rows[:, D:D + A] = np.tanh(rows[:, D:D + A])
+    rep.insert_rows(rows)
+    assert rep.start_sample_condition()
+    idx, got = rep.sample(B)
+    random.seed(1234)
+    exp = [random.randint(0, 3000 - 1) for _ in range(B)]
+    assert idx.cpu().tolist() == exp
+    assert torch.equal(got.cpu(), torch.from_numpy(rows[exp]))
+    learner = DDPGLearner(lc, ec, seed=0)
+    learner.learn(rep.split(got))
+    assert np.isfinite(list(learner.last_stats().values())).all()

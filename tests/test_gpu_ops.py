@@ -245,7 +245,7 @@ def test_adam_clip_vs_torch(wd, max_norm):
         opt.step()
         gd = grad.to(DEV)
         L.call('smi_adam_clip', L.ptr(pd), L.ptr(gd), L.ptr(m), L.ptr(v), n, L.ptr(step), L.ptr(lr),
-               0.9, 0.999, 1e-8, wd, max_norm, None, L.ptr(norm), st())
+               0.9, 0.999, 1e-8, wd, max_norm, 0.0, None, L.ptr(norm), st())
         if ref_norm is not None:
             assert abs(norm.item() - ref_norm) <= 1e-5 * ref_norm
         assert max_rel_err(pd.cpu(), p_ref.detach()) < RTOL
@@ -254,7 +254,7 @@ def test_adam_clip_vs_torch(wd, max_norm):
     skip = torch.ones(1, dtype=torch.int32, device=DEV)
     before = pd.clone()
     L.call('smi_adam_clip', L.ptr(pd), L.ptr(gd), L.ptr(m), L.ptr(v), n, L.ptr(step), L.ptr(lr),
-           0.9, 0.999, 1e-8, wd, max_norm, L.ptr(skip), None, st())
+           0.9, 0.999, 1e-8, wd, max_norm, 0.0, L.ptr(skip), None, st())
     assert torch.equal(pd, before) and step.item() == 4
 
 
@@ -266,7 +266,7 @@ def test_adam_known_answer():
     step = torch.zeros(1, dtype=torch.int32, device=DEV)
     lr = torch.tensor([k['lr']], device=DEV)
     L.call('smi_adam_clip', L.ptr(p), L.ptr(gr), L.ptr(m), L.ptr(v), 4, L.ptr(step), L.ptr(lr), 0.9,
-           0.999, k['eps'], 0.0, 0.0, None, None, st())
+           0.999, k['eps'], 0.0, 0.0, 0.0, None, None, st())
     assert np.allclose(p.cpu().numpy(), k['p1'], rtol=1e-6, atol=1e-7)
 
 
