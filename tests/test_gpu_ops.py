@@ -162,8 +162,9 @@ def _gae_windows_gpu(values, rewards, dones, gamma, lam, T, H):
     part = torch.zeros(2 * 2048, dtype=torch.float64, device=DEV)
     import ctypes
     n = ctypes.c_int(0)
-    L.call('smi_gae_windows', L.ptr(vd), L.ptr(rd), L.ptr(dd), B, T, H, L.ptr(gt.to(DEV)),
-           L.ptr(lt.to(DEV)), float(gamma), float(gamma ** H), L.ptr(adv), L.ptr(ret), L.ptr(part),
+    gtd, ltd = gt.to(DEV), lt.to(DEV)       # keep the device tables alive across the call
+    L.call('smi_gae_windows', L.ptr(vd), L.ptr(rd), L.ptr(dd), B, T, H, L.ptr(gtd),
+           L.ptr(ltd), float(gamma), float(gamma ** H), L.ptr(adv), L.ptr(ret), L.ptr(part),
            ctypes.byref(n), st())
     return adv.cpu(), ret.cpu(), vd.cpu(), part[:2 * n.value].cpu().view(-1, 2)
 
@@ -277,12 +278,11 @@ def test_ddpg_target():
     d = (torch.rand(n, generator=g) < 0.1).float()
     gn = 0.99 ** 3
     y = torch.empty(n, device=DEV)
-    L.call('smi_ddpg_target', L.ptr(r.to(DEV)), L.ptr(d.to(DEV)), L.ptr(q.to(DEV)), None, n, gn,
-           L.ptr(y), st())
+    rd, dd, qd, q2d = r.to(DEV), d.to(DEV), q.to(DEV), q2.to(DEV)
+    L.call('smi_ddpg_target', L.ptr(rd), L.ptr(dd), L.ptr(qd), None, n, gn, L.ptr(y), st())
     ref = r + gn * q * (1.0 - d)
     assert max_rel_err(y.cpu(), ref) < RTOL
-    L.call('smi_ddpg_target', L.ptr(r.to(DEV)), L.ptr(d.to(DEV)), L.ptr(q.to(DEV)), L.ptr(q2.to(DEV)),
-           n, gn, L.ptr(y), st())
+    L.call('smi_ddpg_target', L.ptr(rd), L.ptr(dd), L.ptr(qd), L.ptr(q2d), n, gn, L.ptr(y), st())
     ref2 = torch.min(ref, r + gn * q2 * (1.0 - d))
     assert max_rel_err(y.cpu(), ref2) < RTOL
 
