@@ -51,6 +51,11 @@ int64_t smi_mlp_param_count(int in_dim, int h1, int h2, int out_dim, int with_lo
 int64_t smi_ppo_fused_lds_bytes(int rows, int obs_dim, int h1, int h2, int act_dim,
                                 int critic_h1, int critic_h2);
 
+/* Largest per-network parameter count smi_ppo_update_fused accepts (its Adam
+ * moments are register-resident); larger networks use the epoch phases
+ * (smi_ppo_epoch_grad / smi_ppo_epoch_apply) even on a single GPU. */
+int64_t smi_ppo_fused_max_params(void);
+
 /* ----------------------------------------------------------- ZFilter ops */
 /* Replaces ZFilter.forward (surreal/model/z_filter.py:59-79):
  *   out = clamp((x - sum/count) / max(sqrt(sumsq/count - mean^2), eps), -5, 5)

@@ -10,7 +10,9 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libsurreal_mi.so')
+# SMI_LIB_VARIANT=prof selects the developer phase-timer build (build.py VARIANTS)
+_VARIANT = os.environ.get('SMI_LIB_VARIANT')
+LIB_PATH = os.path.join(HERE, 'libsurreal_mi.so' if not _VARIANT else f'libsurreal_mi_{_VARIANT}.so')
 
 c_int, c_i64, c_f32, c_f64, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 P = ctypes.c_void_p
@@ -61,6 +63,7 @@ _SIGS = {
     'smi_set_workspace': (c_int, [P, c_i64]),
     'smi_mlp_param_count': (c_i64, [c_int, c_int, c_int, c_int, c_int]),
     'smi_ppo_fused_lds_bytes': (c_i64, [c_int] * 7),
+    'smi_ppo_fused_max_params': (c_i64, []),
     'smi_zfilter_apply': (c_int, [P, P, c_i64, c_int, P, P, P, c_f32, P]),
     'smi_zfilter_update': (c_int, [P, c_i64, c_int, c_i64, P, P, P, P]),
     'smi_zfilter_colstats': (c_int, [P, c_i64, c_int, c_i64, P, P, P]),

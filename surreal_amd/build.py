@@ -32,29 +32,42 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else -1.0
 
 
-def build(verbose=False, force=False):
-    os.makedirs(BUILD, exist_ok=True)
+# Developer variants: 'prof' adds the epoch-kernel phase timer (-DSMI_PROF,
+# tools/fused_breakdown.py --phases); 'noinl' keeps the dense helpers out of line.  The product library is variant None.
+VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
+            'noinl_prof': ['-DSMI_DENSE_NOINLINE', '-DSMI_PROF']}
+
+
+def lib_path(variant=None):
+    return LIB if variant is None else LIB.replace('.so', f'_{variant}.so')
+
+
+def build(verbose=False, force=False, variant=None):
+    build_dir = BUILD if variant is None else f'{BUILD}_{variant}'
+    lib = lib_path(variant)
+    os.makedirs(build_dir, exist_ok=True)
     deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'surreal_mi.h')]
     dep_t = max(_mtime(d) for d in deps)
     objs = []
     for src in SOURCES:
         sp = os.path.join(CSRC, src)
-        op = os.path.join(BUILD, src.replace('.hip', '.o'))
+        op = os.path.join(build_dir, src.replace('.hip', '.o'))
         objs.append(op)
         if force or _mtime(op) < max(_mtime(sp), dep_t):
-            cmd = [HIPCC] + CXXFLAGS + ['-c', sp, '-o', op]
+            cmd = [HIPCC] + CXXFLAGS + VARIANTS[variant] + ['-c', sp, '-o', op]
             if verbose:
                 print(' '.join(cmd), flush=True)
             subprocess.run(cmd, check=True)
-    if force or _mtime(LIB) < max(_mtime(o) for o in objs):
+    if force or _mtime(lib) < max(_mtime(o) for o in objs):
         tl = torch_lib_dir()
-        cmd = ['g++', '-shared', '-o', LIB] + objs + [
+        cmd = ['g++', '-shared', '-o', lib] + objs + [
             f'-L{tl}', '-l:libamdhip64.so', f'-Wl,-rpath,{tl}', '-Wl,--no-undefined', '-lstdc++']
         if verbose:
             print(' '.join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 if __name__ == '__main__':
-    build(verbose=True, force='--force' in sys.argv)
+    var = next((a.split('=', 1)[1] for a in sys.argv if a.startswith('--variant=')), None)
+    build(verbose=True, force='--force' in sys.argv, variant=var)

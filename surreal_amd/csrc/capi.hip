@@ -101,6 +101,8 @@ int64_t smi_ppo_fused_lds_bytes(int rows, int obs_dim, int h1, int h2, int act_d
   return fused_lds_bytes(rows, obs_dim, h1, h2, act_dim, critic_h1, critic_h2);
 }
 
+int64_t smi_ppo_fused_max_params(void) { return ppo_fused_max_params(); }
+
 int smi_zfilter_apply(const float* x, float* out, int64_t rows, int dim, const float* rs,
                       const float* rsq, const float* cnt, float eps, void* stream) {
   REQUIRE(x && out && rs && rsq && cnt && rows >= 0 && dim > 0, "zfilter_apply: bad args");

@@ -18,6 +18,34 @@
 
 namespace smi {
 
+#ifndef SMI_FWG
+#define SMI_FWG 256
+#endif
+#ifndef SMI_ADAM_PER
+#define SMI_ADAM_PER 24
+#endif
+constexpr int kFWG = SMI_FWG;          // threads of the epoch workgroups (4 waves, 1 per SIMD)
+constexpr int kAdamPer = SMI_ADAM_PER; // parameters per thread held in registers
+
+// Developer phase timer (tools/fused_breakdown.py --phases): built only with
+// -DSMI_PROF; accumulates wall-clock ticks (100 MHz) per phase and workgroup.
+#ifdef SMI_PROF
+__device__ unsigned long long g_phase_ticks[2][32];
+#define PROF_START() c.prof_t = wall_clock64()
+#define PROF(id)                                                          \
+  do {                                                                    \
+    __syncthreads();                                                      \
+    if (threadIdx.x == 0) {                                               \
+      const unsigned long long n_ = wall_clock64();                       \
+      g_phase_ticks[blockIdx.x & 1][id] += n_ - c.prof_t;                 \
+      c.prof_t = n_;                                                      \
+    }                                                                     \
+  } while (0)
+#else
+#define PROF_START() (void)0
+#define PROF(id) (void)0
+#endif
+
 // ---------------------------------------------------------------- layout
 struct FusedLayout {
   MlpLayout A, C;
@@ -157,6 +185,7 @@ struct FusedCtx {
   float invB;       // 1 / rows of the (global) batch
   float *P, *G, *refmu, *mu, *act, *beh, *adv, *bpl, *zm, *zs, *rzm, *rzs;
   float *sig, *logsig, *refsig, *reflogsig, *gsig, *gsr;
+  unsigned long long prof_t;   // SMI_PROF builds only
 };
 
 __device__ inline void ctx_init(FusedCtx& c, const smi_ppo_args& args, float* sm) {
@@ -181,21 +210,27 @@ __device__ inline void ctx_init(FusedCtx& c, const smi_ppo_args& args, float* sm
 }
 
 // actor forward of one 64-row tile into the policy buffers
-__device__ void policy_fwd_tile(const FusedCtx& c, const MlpView& V, int tile,
+// Every epoch-loop helper is force-inlined: an out-of-line call passes the
+// context structs through scratch and saves/restores registers around it.
+#ifndef SMI_INL
+#define SMI_INL __device__ __attribute__((always_inline))
+#endif
+
+SMI_INL void policy_fwd_tile(const FusedCtx& c, const MlpView& V, int tile,
                                 const float* zm, const float* zs) {
   const smi_ppo_args& a = *c.a;
   const FusedLayout& F = c.F;
   float* sm = c.sm;
   const int r0 = tile * kRT;
   const int nr = min(kRT, a.B - r0);
-  load_obs_tile(a.obs + (int64_t)r0 * a.obs_stride, a.obs_stride, nr, a.obs_dim,
+  load_obs_tile<kFWG>(a.obs + (int64_t)r0 * a.obs_stride, a.obs_stride, nr, a.obs_dim,
                 a.use_zf ? zm : nullptr, zs, sm + F.pX0, F.ldX);
   __syncthreads();
-  dense_fwd<ACT_RELU>(sm + F.pX0, F.ldX, V.W1, V.ld1, V.b1, a.obs_dim, a.h1, sm + F.pH1, F.ldH1);
+  dense_fwd<ACT_RELU, kFWG>(sm + F.pX0, F.ldX, V.W1, V.ld1, V.b1, a.obs_dim, a.h1, sm + F.pH1, F.ldH1);
   __syncthreads();
-  dense_fwd<ACT_RELU>(sm + F.pH1, F.ldH1, V.W2, V.ld2, V.b2, a.h1, a.h2, sm + F.pH2, F.ldH);
+  dense_fwd<ACT_RELU, kFWG>(sm + F.pH1, F.ldH1, V.W2, V.ld2, V.b2, a.h1, a.h2, sm + F.pH2, F.ldH);
   __syncthreads();
-  dense_fwd<ACT_TANH>(sm + F.pH2, F.ldH, V.W3, V.ld3, V.b3, a.h2, a.act_dim, sm + F.pOUT, F.ldO);
+  dense_fwd<ACT_TANH, kFWG>(sm + F.pH2, F.ldH, V.W3, V.ld3, V.b3, a.h2, a.act_dim, sm + F.pOUT, F.ldO);
   __syncthreads();
 }
 
@@ -203,17 +238,17 @@ __device__ void policy_fwd_tile(const FusedCtx& c, const MlpView& V, int tile,
 // stats, per-row actions / behaviour policy / normalised advantages /
 // behaviour likelihoods, the reference policy ref_pol (ppo.py:539), and the
 // model actor in LDS with zeroed gradients.
-__device__ void policy_prologue(FusedCtx& c) {
+SMI_INL void policy_prologue(FusedCtx& c) {
   const smi_ppo_args& a = *c.a;
   const FusedLayout& F = c.F;
   float* sm = c.sm;
   const int A = a.act_dim, B = a.B;
-  for (int e = F.pX0 + threadIdx.x; e < F.pRefMu; e += kWG) sm[e] = 0.f;
+  for (int e = F.pX0 + threadIdx.x; e < F.pRefMu; e += kFWG) sm[e] = 0.f;
   if (a.use_zf) {
-    zfilter_colstats(a.zf_sum, a.zf_sumsq, a.zf_count, a.zf_eps, a.obs_dim, c.zm, c.zs);
-    zfilter_colstats(a.rzf_sum, a.rzf_sumsq, a.rzf_count, a.zf_eps, a.obs_dim, c.rzm, c.rzs);
+    zfilter_colstats<kFWG>(a.zf_sum, a.zf_sumsq, a.zf_count, a.zf_eps, a.obs_dim, c.zm, c.zs);
+    zfilter_colstats<kFWG>(a.rzf_sum, a.rzf_sumsq, a.rzf_count, a.zf_eps, a.obs_dim, c.rzm, c.rzs);
   }
-  for (int e = threadIdx.x; e < F.Bp * A; e += kWG) {
+  for (int e = threadIdx.x; e < F.Bp * A; e += kFWG) {
     const int r = e / A, j = e - r * A;
     const bool v = r < B;
     c.act[e] = v ? a.actions[(int64_t)r * a.act_stride + j] : 0.f;
@@ -227,30 +262,30 @@ __device__ void policy_prologue(FusedCtx& c) {
       s1 = a.adv_moments[0]; s2 = a.adv_moments[1]; n = a.adv_moments[2];
     } else {
       double l1 = 0.0;
-      for (int r = threadIdx.x; r < B; r += kWG) l1 += (double)a.adv_raw[r];
-      s1 = block_sum_d(l1, c.scr);
+      for (int r = threadIdx.x; r < B; r += kFWG) l1 += (double)a.adv_raw[r];
+      s1 = block_sum_d<kFWG>(l1, c.scr);
       n = (double)B;
       const double mean = s1 / n;
       double l2 = 0.0;
-      for (int r = threadIdx.x; r < B; r += kWG) {
+      for (int r = threadIdx.x; r < B; r += kFWG) {
         const double d = (double)a.adv_raw[r] - mean;
         l2 += d * d;
       }
-      s2 = block_sum_d(l2, c.scr) + n * mean * mean;
+      s2 = block_sum_d<kFWG>(l2, c.scr) + n * mean * mean;
     }
     const double mean_d = s1 / n;
     const double var_d = (s2 - n * mean_d * mean_d) / (n - 1.0);
     const float mean_f = (float)mean_d;
     const float std_f = (float)sqrt(var_d > 0.0 ? var_d : 0.0);
     const float denom = std_f > 1e-4f ? std_f : 1e-4f;
-    for (int r = threadIdx.x; r < F.Bp; r += kWG) {
+    for (int r = threadIdx.x; r < F.Bp; r += kFWG) {
       float v = 0.f;
       if (r < B) v = a.norm_adv ? (a.adv_raw[r] - mean_f) / denom : a.adv_raw[r];
       c.adv[r] = v;
     }
   }
   __syncthreads();
-  for (int r = threadIdx.x; r < F.Bp; r += kWG) {
+  for (int r = threadIdx.x; r < F.Bp; r += kFWG) {
     float v = 1.f;
     if (r < B) {
       const float* p = c.beh + r * 2 * A;
@@ -259,24 +294,24 @@ __device__ void policy_prologue(FusedCtx& c) {
     c.bpl[r] = v;
   }
   // reference policy with ref_target_model (its own ZFilter)
-  mlp_load_lds(F.A, a.ref_actor, c.P);
+  mlp_load_lds<kFWG>(F.A, a.ref_actor, c.P);
   {
     const MlpView V = view_padded(F.A, c.P);
-    for (int j = threadIdx.x; j < A; j += kWG) {
+    for (int j = threadIdx.x; j < A; j += kFWG) {
       c.refsig[j] = expf(V.lv[j]);
       c.reflogsig[j] = logf(c.refsig[j]);
     }
     for (int tile = 0; tile < F.ntiles; ++tile) {
       policy_fwd_tile(c, V, tile, c.rzm, c.rzs);
-      for (int e = threadIdx.x; e < kRT * A; e += kWG) {
+      for (int e = threadIdx.x; e < kRT * A; e += kFWG) {
         const int r = e / A, j = e - r * A;
         c.refmu[(tile * kRT + r) * A + j] = sm[F.pOUT + r * F.ldO + j];
       }
       __syncthreads();
     }
   }
-  mlp_load_lds(F.A, a.actor, c.P);
-  for (int i = threadIdx.x; i < F.A.pcount; i += kWG) c.G[i] = 0.f;
+  mlp_load_lds<kFWG>(F.A, a.actor, c.P);
+  for (int i = threadIdx.x; i < F.A.pcount; i += kFWG) c.G[i] = 0.f;
   __syncthreads();
 }
 
@@ -284,11 +319,11 @@ __device__ void policy_prologue(FusedCtx& c) {
 // means) in LDS and returns the block sums of KL(ref || curr) (ppo.py:553-554)
 // and of the final-statistics terms (ppo.py:568-575).
 struct PolicySums { float kl, isw, bl, rbd, ret; };
-__device__ PolicySums policy_forward_all(FusedCtx& c, const MlpView& V) {
+SMI_INL PolicySums policy_forward_all(FusedCtx& c, const MlpView& V) {
   const smi_ppo_args& a = *c.a;
   const FusedLayout& F = c.F;
   const int A = a.act_dim, B = a.B;
-  for (int j = threadIdx.x; j < A; j += kWG) {
+  for (int j = threadIdx.x; j < A; j += kFWG) {
     c.sig[j] = expf(V.lv[j]);                  // builders.py:127
     c.logsig[j] = logf(c.sig[j]);
   }
@@ -296,12 +331,13 @@ __device__ PolicySums policy_forward_all(FusedCtx& c, const MlpView& V) {
   float klp = 0.f, iswp = 0.f, blp = 0.f, rbdp = 0.f, retp = 0.f;
   for (int tile = 0; tile < F.ntiles; ++tile) {
     policy_fwd_tile(c, V, tile, c.zm, c.zs);
-    for (int e = threadIdx.x; e < kRT * A; e += kWG) {
+    PROF(8);
+    for (int e = threadIdx.x; e < kRT * A; e += kFWG) {
       const int r = e / A, j = e - r * A;
       c.mu[(tile * kRT + r) * A + j] = c.sm[F.pOUT + r * F.ldO + j];
     }
     __syncthreads();
-    for (int r = threadIdx.x; r < kRT; r += kWG) {
+    for (int r = threadIdx.x; r < kRT; r += kFWG) {
       const int gr = tile * kRT + r;
       if (gr < B) {
         const float* m = c.mu + gr * A;
@@ -316,12 +352,13 @@ __device__ PolicySums policy_forward_all(FusedCtx& c, const MlpView& V) {
       }
     }
   }
+  PROF(9);
   PolicySums s;
-  s.kl = block_sum_f(klp, c.scr);
-  s.isw = block_sum_f(iswp, c.scr);
-  s.bl = block_sum_f(blp, c.scr);
-  s.rbd = block_sum_f(rbdp, c.scr);
-  s.ret = block_sum_f(retp, c.scr);
+  s.kl = block_sum_f<kFWG>(klp, c.scr);
+  s.isw = block_sum_f<kFWG>(iswp, c.scr);
+  s.bl = block_sum_f<kFWG>(blp, c.scr);
+  s.rbd = block_sum_f<kFWG>(rbdp, c.scr);
+  s.ret = block_sum_f<kFWG>(retp, c.scr);
   return s;
 }
 
@@ -331,7 +368,7 @@ __device__ PolicySums policy_forward_all(FusedCtx& c, const MlpView& V) {
 //              surrogate term, weight invB per row
 //   gkl    = d loss / d KL_i of the adapt penalty term (0 = none)
 // When recompute is false the tile's activations must still be in LDS.
-__device__ void policy_loss_bwd_tile(FusedCtx& c, const MlpView& V, int tile, bool recompute,
+SMI_INL void policy_loss_bwd_tile(FusedCtx& c, const MlpView& V, int tile, bool recompute,
                                      float surr_w, float gkl, float clip_lo, float clip_hi,
                                      float* p_surr, float* p_clip) {
   const smi_ppo_args& a = *c.a;
@@ -340,7 +377,7 @@ __device__ void policy_loss_bwd_tile(FusedCtx& c, const MlpView& V, int tile, bo
   const int A = a.act_dim, B = a.B;
   if (recompute) policy_fwd_tile(c, V, tile, c.zm, c.zs);
   float* dOut = sm + F.pDG2;
-  for (int r = threadIdx.x; r < kRT; r += kWG) {
+  for (int r = threadIdx.x; r < kRT; r += kFWG) {
     const int gr = tile * kRT + r;
     float* dz = dOut + r * F.ldO;
     if (gr >= B) {
@@ -391,7 +428,8 @@ __device__ void policy_loss_bwd_tile(FusedCtx& c, const MlpView& V, int tile, bo
     for (int j = A; j < F.ldO; ++j) dz[j] = 0.f;
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < A; j += kWG) {
+  PROF(10);
+  for (int j = threadIdx.x; j < A; j += kFWG) {
     float s = 0.f;
     for (int r = 0; r < kRT; ++r) s += c.gsr[r * A + j];
     c.gsig[j] += s;
@@ -401,58 +439,96 @@ __device__ void policy_loss_bwd_tile(FusedCtx& c, const MlpView& V, int tile, bo
   float* DG1 = sm + F.pDG1;
   const MlpLayout& L = F.A;
   float* G = c.G;
-  dense_bwd_dw(dOut, F.ldO, H2, F.ldH, a.h2, A, G + L.pW3, L.ld3, G + L.pb3);
-  dense_bwd_dx<ACT_RELU>(dOut, F.ldO, V.W3, V.ld3, a.h2, A, H2, F.ldH, DG1, F.ldDG);
+  PROF(11);
+  dense_bwd_dw<kFWG>(dOut, F.ldO, H2, F.ldH, a.h2, A, G + L.pW3, L.ld3, G + L.pb3);
+  dense_bwd_dx<ACT_RELU, kFWG>(dOut, F.ldO, V.W3, V.ld3, a.h2, A, H2, F.ldH, DG1, F.ldDG);
   __syncthreads();
-  dense_bwd_dw(DG1, F.ldDG, H1, F.ldH1, a.h1, a.h2, G + L.pW2, L.ld2, G + L.pb2);
-  dense_bwd_dx<ACT_RELU>(DG1, F.ldDG, V.W2, V.ld2, a.h1, a.h2, H1, F.ldH1, H2, F.ldH);
+  dense_bwd_dw<kFWG>(DG1, F.ldDG, H1, F.ldH1, a.h1, a.h2, G + L.pW2, L.ld2, G + L.pb2);
+  dense_bwd_dx<ACT_RELU, kFWG>(DG1, F.ldDG, V.W2, V.ld2, a.h1, a.h2, H1, F.ldH1, H2, F.ldH);
   __syncthreads();
-  dense_bwd_dw(H2, F.ldH, X0, F.ldX, a.obs_dim, a.h1, G + L.pW1, L.ld1, G + L.pb1);
+  dense_bwd_dw<kFWG>(H2, F.ldH, X0, F.ldX, a.obs_dim, a.h1, G + L.pW1, L.ld1, G + L.pb1);
   __syncthreads();
+  PROF(12);
 }
 
 // log_var gradient: std = exp(log_var) * ones -> sum over rows of g_std * std
 __device__ inline void policy_finish_logvar_grad(FusedCtx& c) {
-  for (int j = threadIdx.x; j < c.a->act_dim; j += kWG) c.G[c.F.A.plv + j] = c.gsig[j] * c.sig[j];
+  for (int j = threadIdx.x; j < c.a->act_dim; j += kFWG) c.G[c.F.A.plv + j] = c.gsig[j] * c.sig[j];
   __syncthreads();
 }
 
 // Adam on a padded LDS parameter image (torch.optim.Adam single-tensor path):
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
 //   p.addcdiv_(m, v.sqrt()/sqrt(1-b2^t) + eps, value=-lr/(1-b1^t))
-__device__ void adam_lds(const MlpLayout& L, float* P, const float* G, float* m, float* v,
-                         int t, float lr, float beta1, float beta2, float eps, float wd,
-                         float coef) {
-  __syncthreads();
-  const double bc1 = 1.0 - pow((double)beta1, (double)t);
-  const double bc2 = 1.0 - pow((double)beta2, (double)t);
-  const float step_size = (float)((double)lr / bc1);
-  const float bc2_sqrt = (float)sqrt(bc2);
-  const float w1 = (float)(1.0 - (double)beta1);
-  const float w2 = (float)(1.0 - (double)beta2);
-  for (int i = threadIdx.x; i < L.fcount; i += kWG) {
-    const int pi = mlp_flat_to_pad(L, i);
-    float g = G[pi] * coef;
-    float p = P[pi];
-    if (wd != 0.f) g = g + wd * p;
-    float mi = m[i], vi = v[i];
-    mi = mi + w1 * (g - mi);
-    vi = vi * beta2 + (w2 * g) * g;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p = p + (-step_size) * (mi / denom);
-    m[i] = mi; v[i] = vi; P[pi] = p;
-  }
-  __syncthreads();
-}
+// The Adam moments of the parameters a thread owns (flat index
+// threadIdx.x + u*kFWG) stay in registers for the whole epoch loop, with the
+// LDS index of each parameter precomputed: no global traffic and no index
+// arithmetic per update.  Loaded once per launch, stored once at the end.
+struct AdamRegs {
+  float m[kAdamPer], v[kAdamPer];
+  int pi[kAdamPer];
 
-__device__ float grad_norm_lds(const MlpLayout& L, const float* G, double* scr) {
-  double s = 0.0;
-  for (int i = threadIdx.x; i < L.fcount; i += kWG) {
-    const float g = G[mlp_flat_to_pad(L, i)];
-    s += (double)g * (double)g;
+  SMI_INL void load(const MlpLayout& L, const float* __restrict__ gm,
+                       const float* __restrict__ gv) {
+#pragma unroll
+    for (int u = 0; u < kAdamPer; ++u) {
+      const int i = threadIdx.x + u * kFWG;
+      const bool ok = i < L.fcount;
+      m[u] = ok ? gm[i] : 0.f;
+      v[u] = ok ? gv[i] : 0.f;
+      pi[u] = ok ? mlp_flat_to_pad(L, i) : 0;
+    }
   }
-  return (float)sqrt(block_sum_d(s, scr));
-}
+  SMI_INL void store(const MlpLayout& L, float* __restrict__ gm, float* __restrict__ gv) const {
+#pragma unroll
+    for (int u = 0; u < kAdamPer; ++u) {
+      const int i = threadIdx.x + u * kFWG;
+      if (i < L.fcount) { gm[i] = m[u]; gv[i] = v[u]; }
+    }
+  }
+  // global L2 norm of the gradient image (fp64 accumulation)
+  SMI_INL float grad_norm(const MlpLayout& L, const float* G, double* scr) const {
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < kAdamPer; ++u) {
+      const int i = threadIdx.x + u * kFWG;
+      if (i < L.fcount) {
+        const float g = G[pi[u]];
+        s += (double)g * (double)g;
+      }
+    }
+    return (float)sqrt(block_sum_d<kFWG>(s, scr));
+  }
+  // torch.optim.Adam single-tensor path on the padded LDS image P:
+  //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+  //   p.addcdiv_(m, v.sqrt()/sqrt(1-b2^t) + eps, value=-lr/(1-b1^t))
+  SMI_INL void step(const MlpLayout& L, float* P, const float* G, int t, float lr,
+                       float beta1, float beta2, float eps, float wd, float coef) {
+    __syncthreads();
+    const double bc1 = 1.0 - pow((double)beta1, (double)t);
+    const double bc2 = 1.0 - pow((double)beta2, (double)t);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    const float w1 = (float)(1.0 - (double)beta1);
+    const float w2 = (float)(1.0 - (double)beta2);
+#pragma unroll
+    for (int u = 0; u < kAdamPer; ++u) {
+      const int i = threadIdx.x + u * kFWG;
+      if (i < L.fcount) {
+        float g = G[pi[u]] * coef;
+        float p = P[pi[u]];
+        if (wd != 0.f) g = g + wd * p;
+        float mi = m[u], vi = v[u];
+        mi = mi + w1 * (g - mi);
+        vi = vi * beta2 + (w2 * g) * g;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        P[pi[u]] = p + (-step_size) * (mi / denom);
+        m[u] = mi; v[u] = vi;
+      }
+    }
+    __syncthreads();
+  }
+};
 
 __device__ inline float clip_coef(float norm, float max_norm) {
   const float cc = max_norm / (norm + 1e-6f);       // clip_grad_norm_
@@ -470,7 +546,7 @@ __device__ inline bool adapt_penalty_on(float kl, double kl_target) {
 }
 
 // ============================================================ fused kernel
-__device__ void policy_wg(FusedCtx& c) {
+SMI_INL void policy_wg(FusedCtx& c) {
   const smi_ppo_args& a = *c.a;
   const FusedLayout& F = c.F;
   const int A = a.act_dim;
@@ -478,16 +554,21 @@ __device__ void policy_wg(FusedCtx& c) {
   const float clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   const float beta = a.hyper[SMI_HYP_BETA];
   const float lr = a.hyper[SMI_HYP_LR_ACTOR];
+  PROF_START();
   policy_prologue(c);
+  PROF(0);
   const MlpView V = view_padded(F.A, c.P);
   float st_surr = 0.f, st_clip = 0.f, st_kladapt = 0.f, st_ent = 0.f, st_gnorm = 0.f;
   float st_klad = 0.f, pol_kl = 0.f;
   int epochs_run = 0;
   int astep = a.actor_step[0];
+  AdamRegs opt;
+  opt.load(F.A, a.actor_m, a.actor_v);
   PolicySums fin;
   const int E = a.epoch_policy;
   for (int e = 0; e <= E; ++e) {
     fin = policy_forward_all(c, V);
+    PROF(1);
     const float kl = fin.kl * c.invB;
     if (e > 0) {
       pol_kl = kl;                                            // ppo.py:553-555
@@ -501,13 +582,14 @@ __device__ void policy_wg(FusedCtx& c) {
         coef = beta + a.kl_cutoff_coeff * 2.f * (kl - (float)(2.0 * a.kl_target));
       gkl = coef * c.invB;
     }
-    for (int j = threadIdx.x; j < A; j += kWG) c.gsig[j] = 0.f;
+    for (int j = threadIdx.x; j < A; j += kFWG) c.gsig[j] = 0.f;
     float p_surr = 0.f, p_clip = 0.f;
     for (int tile = 0; tile < F.ntiles; ++tile)
       policy_loss_bwd_tile(c, V, tile, F.ntiles > 1, 1.f, gkl, clip_lo, clip_hi, &p_surr, &p_clip);
     policy_finish_logvar_grad(c);
-    const float tot_surr = block_sum_f(p_surr, c.scr);
-    const float tot_clip = block_sum_f(p_clip, c.scr);
+    PROF(2);
+    const float tot_surr = block_sum_f<kFWG>(p_surr, c.scr);
+    const float tot_clip = block_sum_f<kFWG>(p_clip, c.scr);
     if (a.mode == 0) {
       st_surr = tot_surr * c.invB;
       st_clip = tot_clip * c.invB;
@@ -523,20 +605,24 @@ __device__ void policy_wg(FusedCtx& c) {
       st_klad = kl;
     }
     st_ent = entropy_of(c);
-    const float norm = grad_norm_lds(F.A, c.G, c.scr);          // clip_grad_norm_ (ppo.py:243)
+    PROF(3);
+    const float norm = opt.grad_norm(F.A, c.G, c.scr);          // clip_grad_norm_ (ppo.py:243)
     float coef = 1.f;
     if (a.clip_actor_grad) {
       coef = clip_coef(norm, a.actor_max_norm);
       st_gnorm = norm;
     }
+    PROF(4);
     ++astep;
-    adam_lds(F.A, c.P, c.G, a.actor_m, a.actor_v, astep, lr, a.beta1, a.beta2, a.adam_eps,
-             a.actor_wd, coef);                                   // ppo.py:247
-    for (int i = threadIdx.x; i < F.A.pcount; i += kWG) c.G[i] = 0.f;
+    opt.step(F.A, c.P, c.G, astep, lr, a.beta1, a.beta2, a.adam_eps, a.actor_wd, coef);  // :247
+    for (int i = threadIdx.x; i < F.A.pcount; i += kFWG) c.G[i] = 0.f;
     ++epochs_run;
     __syncthreads();
+    PROF(5);
   }
-  mlp_store_flat(F.A, c.P, a.actor);
+  mlp_store_flat<kFWG>(F.A, c.P, a.actor);
+  opt.store(F.A, a.actor_m, a.actor_v);
+  PROF(6);
   if (threadIdx.x == 0) {
     float lvs = 0.f;
     for (int j = 0; j < A; ++j) lvs += V.lv[j];
@@ -566,7 +652,7 @@ __device__ void policy_wg(FusedCtx& c) {
 // value workgroup: one critic epoch's forward + loss + backward into G over all
 // tiles (ppo.py:311-331), returning the double sums used by the statistics
 struct ValueSums { double se, d, d2, r, r2; };
-__device__ ValueSums value_grad_epoch(const smi_ppo_args& a, const FusedLayout& F, float* sm,
+SMI_INL ValueSums value_grad_epoch(const smi_ppo_args& a, const FusedLayout& F, float* sm,
                                       const MlpView& V, float invB) {
   const MlpLayout& L = F.C;
   double* scr = reinterpret_cast<double*>(sm + F.vScr);
@@ -579,17 +665,17 @@ __device__ ValueSums value_grad_epoch(const smi_ppo_args& a, const FusedLayout& 
   const int B = a.B;
   for (int tile = 0; tile < F.ntiles; ++tile) {
     const int r0 = tile * kRT, nr = min(kRT, B - r0);
-    load_obs_tile(a.obs + (int64_t)r0 * a.obs_stride, a.obs_stride, nr, a.obs_dim,
+    load_obs_tile<kFWG>(a.obs + (int64_t)r0 * a.obs_stride, a.obs_stride, nr, a.obs_dim,
                   a.use_zf ? zm : nullptr, zs, X0, F.ldX);
     __syncthreads();
-    dense_fwd<ACT_RELU>(X0, F.ldX, V.W1, V.ld1, V.b1, a.obs_dim, a.critic_h1, H1, ldH1);
+    dense_fwd<ACT_RELU, kFWG>(X0, F.ldX, V.W1, V.ld1, V.b1, a.obs_dim, a.critic_h1, H1, ldH1);
     __syncthreads();
-    dense_fwd<ACT_RELU>(H1, ldH1, V.W2, V.ld2, V.b2, a.critic_h1, a.critic_h2, H2, ldH);
+    dense_fwd<ACT_RELU, kFWG>(H1, ldH1, V.W2, V.ld2, V.b2, a.critic_h1, a.critic_h2, H2, ldH);
     __syncthreads();
-    dense_fwd<ACT_NONE>(H2, ldH, V.W3, V.ld3, V.b3, a.critic_h2, 1, OUT, ldO);
+    dense_fwd<ACT_NONE, kFWG>(H2, ldH, V.W3, V.ld3, V.b3, a.critic_h2, 1, OUT, ldO);
     __syncthreads();
     // d/dV mean((V - R)^2) = 2 (V - R) / B   (ppo.py:326)
-    for (int r = threadIdx.x; r < kRT; r += kWG) {
+    for (int r = threadIdx.x; r < kRT; r += kFWG) {
       const int gr = r0 + r;
       float g = 0.f;
       if (gr < B) {
@@ -601,17 +687,17 @@ __device__ ValueSums value_grad_epoch(const smi_ppo_args& a, const FusedLayout& 
       for (int j = 1; j < ldO; ++j) DG2[r * ldO + j] = 0.f;
     }
     __syncthreads();
-    dense_bwd_dw(DG2, ldO, H2, ldH, a.critic_h2, 1, G + L.pW3, L.ld3, G + L.pb3);
-    dense_bwd_dx<ACT_RELU>(DG2, ldO, V.W3, V.ld3, a.critic_h2, 1, H2, ldH, DG1, ldH);
+    dense_bwd_dw<kFWG>(DG2, ldO, H2, ldH, a.critic_h2, 1, G + L.pW3, L.ld3, G + L.pb3);
+    dense_bwd_dx<ACT_RELU, kFWG>(DG2, ldO, V.W3, V.ld3, a.critic_h2, 1, H2, ldH, DG1, ldH);
     __syncthreads();
-    dense_bwd_dw(DG1, ldH, H1, ldH1, a.critic_h1, a.critic_h2, G + L.pW2, L.ld2, G + L.pb2);
-    dense_bwd_dx<ACT_RELU>(DG1, ldH, V.W2, V.ld2, a.critic_h1, a.critic_h2, H1, ldH1, H2, ldH);
+    dense_bwd_dw<kFWG>(DG1, ldH, H1, ldH1, a.critic_h1, a.critic_h2, G + L.pW2, L.ld2, G + L.pb2);
+    dense_bwd_dx<ACT_RELU, kFWG>(DG1, ldH, V.W2, V.ld2, a.critic_h1, a.critic_h2, H1, ldH1, H2, ldH);
     __syncthreads();
-    dense_bwd_dw(H2, ldH, X0, F.ldX, a.obs_dim, a.critic_h1, G + L.pW1, L.ld1, G + L.pb1);
+    dense_bwd_dw<kFWG>(H2, ldH, X0, F.ldX, a.obs_dim, a.critic_h1, G + L.pW1, L.ld1, G + L.pb1);
     __syncthreads();
   }
   double l_se = 0.0, l_d = 0.0, l_d2 = 0.0, l_r = 0.0, l_r2 = 0.0;
-  for (int r = threadIdx.x; r < B; r += kWG) {
+  for (int r = threadIdx.x; r < B; r += kFWG) {
     const float e = Vv[r] - ret[r];
     const double d = (double)ret[r] - (double)Vv[r];
     l_se += (double)(e * e);
@@ -619,11 +705,11 @@ __device__ ValueSums value_grad_epoch(const smi_ppo_args& a, const FusedLayout& 
     l_r += (double)ret[r]; l_r2 += (double)ret[r] * (double)ret[r];
   }
   ValueSums s;
-  s.se = block_sum_d(l_se, scr);
-  s.d = block_sum_d(l_d, scr);
-  s.d2 = block_sum_d(l_d2, scr);
-  s.r = block_sum_d(l_r, scr);
-  s.r2 = block_sum_d(l_r2, scr);
+  s.se = block_sum_d<kFWG>(l_se, scr);
+  s.d = block_sum_d<kFWG>(l_d, scr);
+  s.d2 = block_sum_d<kFWG>(l_d2, scr);
+  s.r = block_sum_d<kFWG>(l_r, scr);
+  s.r2 = block_sum_d<kFWG>(l_r2, scr);
   return s;
 }
 
@@ -632,17 +718,17 @@ __device__ inline float unbiased_var(double s, double s2, double n) {
   return (float)((s2 - n * mean * mean) / (n - 1.0));
 }
 
-__device__ void value_prologue(const smi_ppo_args& a, const FusedLayout& F, float* sm) {
-  for (int e = F.vX0 + threadIdx.x; e < F.vRet; e += kWG) sm[e] = 0.f;
+SMI_INL void value_prologue(const smi_ppo_args& a, const FusedLayout& F, float* sm) {
+  for (int e = F.vX0 + threadIdx.x; e < F.vRet; e += kFWG) sm[e] = 0.f;
   if (a.use_zf)
-    zfilter_colstats(a.zf_sum, a.zf_sumsq, a.zf_count, a.zf_eps, a.obs_dim, sm + F.vZm, sm + F.vZs);
-  for (int r = threadIdx.x; r < F.Bp; r += kWG) sm[F.vRet + r] = r < a.B ? a.ret[r] : 0.f;
-  mlp_load_lds(F.C, a.critic, sm + F.vP);
-  for (int i = threadIdx.x; i < F.C.pcount; i += kWG) sm[F.vG + i] = 0.f;
+    zfilter_colstats<kFWG>(a.zf_sum, a.zf_sumsq, a.zf_count, a.zf_eps, a.obs_dim, sm + F.vZm, sm + F.vZs);
+  for (int r = threadIdx.x; r < F.Bp; r += kFWG) sm[F.vRet + r] = r < a.B ? a.ret[r] : 0.f;
+  mlp_load_lds<kFWG>(F.C, a.critic, sm + F.vP);
+  for (int i = threadIdx.x; i < F.C.pcount; i += kFWG) sm[F.vG + i] = 0.f;
   __syncthreads();
 }
 
-__device__ void value_wg(FusedCtx& c) {
+SMI_INL void value_wg(FusedCtx& c) {
   const smi_ppo_args& a = *c.a;
   const FusedLayout& F = c.F;
   float* sm = c.sm;
@@ -651,28 +737,36 @@ __device__ void value_wg(FusedCtx& c) {
   float* P = sm + F.vP;
   float* G = sm + F.vG;
   const float lr = a.hyper[SMI_HYP_LR_CRITIC];
+  PROF_START();
   value_prologue(a, F, sm);
+  PROF(0);
   const MlpView V = view_padded(L, P);
   float st_loss = 0.f, st_ev = 0.f, st_gnorm = 0.f;
   int cstep = a.critic_step[0];
+  AdamRegs opt;
+  opt.load(L, a.critic_m, a.critic_v);
   const double n = (double)a.B;
   for (int e = 0; e < a.epoch_baseline; ++e) {
     const ValueSums s = value_grad_epoch(a, F, sm, V, c.invB);
+    PROF(2);
     st_loss = (float)(s.se / n);
     st_ev = 1.f - unbiased_var(s.d, s.d2, n) / unbiased_var(s.r, s.r2, n);   // ppo.py:325
-    const float norm = grad_norm_lds(L, G, scr);
+    const float norm = opt.grad_norm(L, G, scr);
+    PROF(4);
     float coef = 1.f;
     if (a.clip_critic_grad) {
       coef = clip_coef(norm, a.critic_max_norm);
       st_gnorm = norm;
     }
     ++cstep;
-    adam_lds(L, P, G, a.critic_m, a.critic_v, cstep, lr, a.beta1, a.beta2, a.adam_eps,
-             a.critic_wd, coef);
-    for (int i = threadIdx.x; i < L.pcount; i += kWG) G[i] = 0.f;
+    opt.step(L, P, G, cstep, lr, a.beta1, a.beta2, a.adam_eps, a.critic_wd, coef);
+    for (int i = threadIdx.x; i < L.pcount; i += kFWG) G[i] = 0.f;
     __syncthreads();
+    PROF(5);
   }
-  mlp_store_flat(L, P, a.critic);
+  mlp_store_flat<kFWG>(L, P, a.critic);
+  opt.store(L, a.critic_m, a.critic_v);
+  PROF(6);
   if (threadIdx.x == 0) {
     a.stats[SMI_ST_VAL_LOSS] = st_loss;
     a.stats[SMI_ST_VAL_EXPL_VAR] = st_ev;
@@ -681,7 +775,7 @@ __device__ void value_wg(FusedCtx& c) {
   }
 }
 
-__global__ void __launch_bounds__(kWG)
+__global__ void __launch_bounds__(kFWG)
 ppo_fused_kernel(smi_ppo_args args) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   FusedCtx c;
@@ -692,7 +786,7 @@ ppo_fused_kernel(smi_ppo_args args) {
 
 // ================================================== data-parallel phases
 // dp_state: [0] policy stopped, [1] policy updates applied
-__global__ void __launch_bounds__(kWG)
+__global__ void __launch_bounds__(kFWG)
 ppo_epoch_grad_kernel(smi_ppo_args args, int e) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   FusedCtx c;
@@ -704,7 +798,7 @@ ppo_epoch_grad_kernel(smi_ppo_args args, int e) {
   if (blockIdx.x == 0) {
     if (a.dp_state[0] != 0 || e > a.epoch_policy) {
       // stopped: contribute zeros so the all-reduced sums stay defined
-      for (int i = threadIdx.x; i < X.offC; i += kWG) a.xbuf[i] = 0.f;
+      for (int i = threadIdx.x; i < X.offC; i += kFWG) a.xbuf[i] = 0.f;
       if (threadIdx.x == 0)
         for (int k = XS_KL; k <= XS_CLIP; ++k) xs[k] = 0.f;
       return;
@@ -718,35 +812,35 @@ ppo_epoch_grad_kernel(smi_ppo_args args, int e) {
     if (e < a.epoch_policy) {
       // surrogate gradient (the adapt KL term goes to its own slot: its weight
       // depends on the GLOBAL KL, known only after the all-reduce)
-      for (int j = threadIdx.x; j < a.act_dim; j += kWG) c.gsig[j] = 0.f;
+      for (int j = threadIdx.x; j < a.act_dim; j += kFWG) c.gsig[j] = 0.f;
       for (int tile = 0; tile < F.ntiles; ++tile)
         policy_loss_bwd_tile(c, V, tile, F.ntiles > 1, 1.f, 0.f, clip_lo, clip_hi, &p_surr, &p_clip);
       policy_finish_logvar_grad(c);
-      for (int i = threadIdx.x; i < F.A.fcount; i += kWG)
+      for (int i = threadIdx.x; i < F.A.fcount; i += kFWG)
         a.xbuf[X.offA + i] = c.G[mlp_flat_to_pad(F.A, i)];
       if (a.mode == 1) {
         __syncthreads();
-        for (int i = threadIdx.x; i < F.A.pcount; i += kWG) c.G[i] = 0.f;
-        for (int j = threadIdx.x; j < a.act_dim; j += kWG) c.gsig[j] = 0.f;
+        for (int i = threadIdx.x; i < F.A.pcount; i += kFWG) c.G[i] = 0.f;
+        for (int j = threadIdx.x; j < a.act_dim; j += kFWG) c.gsig[j] = 0.f;
         float d0 = 0.f, d1 = 0.f;
         for (int tile = 0; tile < F.ntiles; ++tile)
           policy_loss_bwd_tile(c, V, tile, true, 0.f, c.invB, clip_lo, clip_hi, &d0, &d1);
         policy_finish_logvar_grad(c);
-        for (int i = threadIdx.x; i < F.A.fcount; i += kWG)
+        for (int i = threadIdx.x; i < F.A.fcount; i += kFWG)
           a.xbuf[X.offK + i] = c.G[mlp_flat_to_pad(F.A, i)];
       }
     } else {
-      for (int i = threadIdx.x; i < X.offC; i += kWG) a.xbuf[i] = 0.f;
+      for (int i = threadIdx.x; i < X.offC; i += kFWG) a.xbuf[i] = 0.f;
     }
-    const float t_surr = block_sum_f(p_surr, c.scr);
-    const float t_clip = block_sum_f(p_clip, c.scr);
+    const float t_surr = block_sum_f<kFWG>(p_surr, c.scr);
+    const float t_clip = block_sum_f<kFWG>(p_clip, c.scr);
     if (threadIdx.x == 0) {
       xs[XS_KL] = s.kl; xs[XS_ISW] = s.isw; xs[XS_BL] = s.bl; xs[XS_RBD] = s.rbd;
       xs[XS_RET] = s.ret; xs[XS_SURR] = t_surr; xs[XS_CLIP] = t_clip;
     }
   } else {
     if (e >= a.epoch_baseline) {
-      for (int i = threadIdx.x; i < X.nc; i += kWG) a.xbuf[X.offC + i] = 0.f;
+      for (int i = threadIdx.x; i < X.nc; i += kFWG) a.xbuf[X.offC + i] = 0.f;
       if (threadIdx.x == 0)
         for (int k = XS_VSE; k <= XS_VR2; ++k) xs[k] = 0.f;
       return;
@@ -754,7 +848,7 @@ ppo_epoch_grad_kernel(smi_ppo_args args, int e) {
     value_prologue(a, F, sm);
     const MlpView V = view_padded(F.C, sm + F.vP);
     const ValueSums s = value_grad_epoch(a, F, sm, V, c.invB);
-    for (int i = threadIdx.x; i < F.C.fcount; i += kWG)
+    for (int i = threadIdx.x; i < F.C.fcount; i += kFWG)
       a.xbuf[X.offC + i] = sm[F.vG + mlp_flat_to_pad(F.C, i)];
     if (threadIdx.x == 0) {
       xs[XS_VSE] = (float)s.se; xs[XS_VD] = (float)s.d; xs[XS_VD2] = (float)s.d2;
@@ -793,7 +887,7 @@ __device__ float sumsq_global(const float* ga, const float* gk, float kc, int n,
     const float g = gk ? ga[i] + kc * gk[i] : ga[i];
     s += (double)g * (double)g;
   }
-  return (float)sqrt(block_sum_d(s, scr));
+  return (float)sqrt(block_sum_d<kWG>(s, scr));
 }
 
 __global__ void __launch_bounds__(kWG)
@@ -922,10 +1016,16 @@ int launch_ppo_fused(const smi_ppo_args* args, hipStream_t stream) {
   if (rc) return rc;
   if (args->B < 2 && !args->adv_moments)
     return set_error(SMI_E_ARG, "ppo_fused: B >= 2 needed for the unbiased advantage std");
+  const MlpLayout LA = mlp_layout(args->obs_dim, args->h1, args->h2, args->act_dim, 1);
+  const MlpLayout LC = mlp_layout(args->obs_dim, args->critic_h1, args->critic_h2, 1, 0);
+  if (LA.fcount > kFWG * kAdamPer || LC.fcount > kFWG * kAdamPer)
+    return set_error(SMI_E_NOFIT, "ppo_fused: network larger than smi_ppo_fused_max_params()");
   allow_lds(ppo_fused_kernel, (size_t)lds);
-  hipLaunchKernelGGL(ppo_fused_kernel, dim3(2), dim3(kWG), (size_t)lds, stream, *args);
+  hipLaunchKernelGGL(ppo_fused_kernel, dim3(2), dim3(kFWG), (size_t)lds, stream, *args);
   return check_launch("ppo_fused_kernel");
 }
+
+int64_t ppo_fused_max_params() { return (int64_t)kFWG * kAdamPer; }
 
 int64_t ppo_xbuf_floats(int D, int H1, int H2, int A, int cH1, int cH2, int mode) {
   return x_layout(D, H1, H2, A, cH1, cH2, mode).total;
@@ -938,7 +1038,7 @@ int launch_ppo_epoch_grad(const smi_ppo_args* args, int epoch, hipStream_t strea
   if (!args->xbuf || !args->dp_state || !args->adv_moments)
     return set_error(SMI_E_ARG, "ppo_epoch_grad: xbuf, dp_state and adv_moments are required");
   allow_lds(ppo_epoch_grad_kernel, (size_t)lds);
-  hipLaunchKernelGGL(ppo_epoch_grad_kernel, dim3(2), dim3(kWG), (size_t)lds, stream, *args, epoch);
+  hipLaunchKernelGGL(ppo_epoch_grad_kernel, dim3(2), dim3(kFWG), (size_t)lds, stream, *args, epoch);
   return check_launch("ppo_epoch_grad_kernel");
 }
 
@@ -950,3 +1050,13 @@ int launch_ppo_epoch_apply(const smi_ppo_args* args, int epoch, hipStream_t stre
 }
 
 }  // namespace smi
+
+#ifdef SMI_PROF
+// Developer hook (SMI_PROF builds only): copy out and clear the phase ticks.
+extern "C" int smi_phase_ticks(unsigned long long* out /* [64] */) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(smi::g_phase_ticks), sizeof(smi::g_phase_ticks)) != hipSuccess)
+    return SMI_E_LAUNCH;
+  static const unsigned long long zero[64] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(smi::g_phase_ticks), zero, sizeof(zero)) == hipSuccess ? SMI_OK : SMI_E_LAUNCH;
+}
+#endif

@@ -1,22 +1,29 @@
 // smi_device.hpp — CDNA4 (gfx950) device building blocks for the SURREAL learner
 // hot path: LDS-resident 64-row tiles, fp32 MFMA (v_mfma_f32_16x16x4_f32) dense
 // layers with fused bias/activation epilogues and their backward passes, and
-// wave/block reductions.  All functions assume a 256-thread workgroup (4 waves).
+// wave/block reductions.  Every helper is templated on the workgroup size NT
+// (a multiple of 64); the fused epoch kernels run 512 threads (8 waves = 2 per
+// SIMD), the streaming kernels 256.
 //
 // MFMA operand maps (16x16x4 f32, cdna_hip_programming.md §3):
 //   A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15],
 //   D[row = (lane>>4)*4 + reg][col = lane&15].
 // The f32 MFMA is an exact k-ordered fmaf chain, so these layers are fp32
 // exact up to summation order (parity bar: 1e-5 relative vs the CPU oracle).
+//
+// Latency: at learner sizes every dense layer is a chain of dependent
+// LDS-read -> MFMA steps, so the k-loops load 8 k-steps of both operands into
+// registers before issuing the 8 MFMAs (one LDS round trip per 8 MFMAs).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace smi {
 
-constexpr int kWG = 256;          // threads per workgroup
-constexpr int kNW = kWG / 64;     // waves per workgroup
+constexpr int kWG = 256;          // default threads per workgroup
+constexpr int kNW = kWG / 64;     // waves of a default workgroup
 constexpr int kRT = 64;           // rows per tile
+constexpr int kMaxW = 16;         // max waves per workgroup (scratch sizing)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -42,6 +49,10 @@ __device__ __forceinline__ float act_f(float x) {
   else return x;
 }
 
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -53,8 +64,9 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-// Block-wide sums; `scratch` is >= kNW doubles of LDS.  Every thread gets the
-// result.  Order is fixed (deterministic).
+// Block-wide sum; `scratch` is >= NT/64 doubles of LDS.  Every thread gets the
+// result.  Fixed order (deterministic).
+template <int NT = kWG>
 __device__ __forceinline__ double block_sum_d(double v, double* scratch) {
   v = wave_sum_d(v);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -63,30 +75,39 @@ __device__ __forceinline__ double block_sum_d(double v, double* scratch) {
   __syncthreads();
   double s = 0.0;
 #pragma unroll
-  for (int w = 0; w < kNW; ++w) s += scratch[w];
+  for (int w = 0; w < NT / 64; ++w) s += scratch[w];
   __syncthreads();
   return s;
 }
+template <int NT = kWG>
 __device__ __forceinline__ float block_sum_f(float v, double* scratch) {
-  return (float)block_sum_d((double)v, scratch);
+  return (float)block_sum_d<NT>((double)v, scratch);
 }
 
 // --------------------------------------------------------------- dense layers
+// SMI_DENSE_NOINLINE (developer variant) emits each dense helper once instead of
+// inlining it at every call site: smaller code, at the price of call overhead.
+#ifdef SMI_DENSE_NOINLINE
+#define SMI_DENSE __device__ __attribute__((noinline))
+#else
+#define SMI_DENSE __device__
+#endif
 // Forward: Y[r][n] = act(b[n] + sum_k X[r][k] * W[n][k]),  r in [0,64), n in [0,N)
 //   X: LDS [64][ldx], columns [K, round4(K)) must be zero (finite).
 //   W: [N][ldw] row-major (k contiguous) in LDS or global; b: [N].
 //   Y: LDS [64][ldy]; only columns < N are written.
-// Tiles (16 rows x 16 outputs) are dealt round-robin to the 4 waves.
-template <int ACT>
-__device__ void dense_fwd(const float* __restrict__ X, int ldx,
+// 16x16 output tiles are dealt round-robin to the NT/64 waves.
+template <int ACT, int NT = kWG>
+SMI_DENSE void dense_fwd(const float* __restrict__ X, int ldx,
                           const float* __restrict__ W, int ldw,
                           const float* __restrict__ b, int K, int N,
                           float* __restrict__ Y, int ldy) {
+  constexpr int NW = NT / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
   const int CT = (N + 15) >> 4;
   const int K4 = round4(K);
-  for (int t = wave; t < 4 * CT; t += kNW) {
+  for (int t = wave; t < 4 * CT; t += NW) {
     const int rb = t & 3, ct = t >> 2;
     const int n = ct * 16 + li;
     const bool nv = n < N;
@@ -94,10 +115,21 @@ __device__ void dense_fwd(const float* __restrict__ X, int ldx,
     const float* wp = W + (nv ? n : 0) * ldw + lk;
     const float bn = nv ? b[n] : 0.f;
     f32x4 acc = {bn, bn, bn, bn};
-    for (int k0 = 0; k0 < K4; k0 += 4) {
+    int k0 = 0;
+    for (; k0 + 32 <= K4; k0 += 32) {
+      float a[8], w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = xp[k0 + 4 * u];
+        w[u] = (nv && (k0 + 4 * u + lk) < K) ? wp[k0 + 4 * u] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = mfma4(a[u], w[u], acc);
+    }
+    for (; k0 < K4; k0 += 4) {
       const float a = xp[k0];
       const float w = (nv && (k0 + lk) < K) ? wp[k0] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w, acc, 0, 0, 0);
+      acc = mfma4(a, w, acc);
     }
     if (nv) {
 #pragma unroll
@@ -110,25 +142,38 @@ __device__ void dense_fwd(const float* __restrict__ X, int ldx,
 // Backward to the layer input: dX[r][k] = mask(Xact[r][k]) * sum_n G[r][n] W[n][k]
 //   PREV_ACT = activation that produced X (ACT_RELU: mask Xact > 0; ACT_NONE: none)
 //   G: LDS [64][ldg], columns [N, round4(N)) finite.  dX must not alias G.
-template <int PREV_ACT>
-__device__ void dense_bwd_dx(const float* __restrict__ G, int ldg,
+template <int PREV_ACT, int NT = kWG>
+SMI_DENSE void dense_bwd_dx(const float* __restrict__ G, int ldg,
                              const float* __restrict__ W, int ldw, int K, int N,
                              const float* __restrict__ Xact, int ldx,
                              float* __restrict__ dX, int lddx) {
+  constexpr int NW = NT / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
   const int CT = (K + 15) >> 4;
   const int N4 = round4(N);
-  for (int t = wave; t < 4 * CT; t += kNW) {
+  for (int t = wave; t < 4 * CT; t += NW) {
     const int rb = t & 3, ct = t >> 2;
     const int k = ct * 16 + li;
     const bool kv = k < K;
     const float* gp = G + (rb * 16 + li) * ldg + lk;
+    const float* wp = W + lk * ldw + (kv ? k : 0);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int n0 = 0; n0 < N4; n0 += 4) {
+    int n0 = 0;
+    for (; n0 + 32 <= N4; n0 += 32) {
+      float a[8], w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = gp[n0 + 4 * u];
+        w[u] = (kv && (n0 + 4 * u + lk) < N) ? wp[(n0 + 4 * u) * ldw] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = mfma4(a[u], w[u], acc);
+    }
+    for (; n0 < N4; n0 += 4) {
       const float a = gp[n0];
-      const float w = (kv && (n0 + lk) < N) ? W[(n0 + lk) * ldw + k] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w, acc, 0, 0, 0);
+      const float w = (kv && (n0 + lk) < N) ? wp[n0 * ldw] : 0.f;
+      acc = mfma4(a, w, acc);
     }
     if (kv) {
 #pragma unroll
@@ -145,25 +190,32 @@ __device__ void dense_bwd_dx(const float* __restrict__ G, int ldg,
 // Weight/bias gradients, accumulated: gW[n][k] += sum_r G[r][n] X[r][k],
 // gb[n] += sum_r G[r][n], over the 64 rows of the tile (rows that are not
 // valid must carry G == 0 and finite X).
-__device__ void dense_bwd_dw(const float* __restrict__ G, int ldg,
+template <int NT = kWG>
+SMI_DENSE void dense_bwd_dw(const float* __restrict__ G, int ldg,
                              const float* __restrict__ X, int ldx, int K, int N,
                              float* __restrict__ gW, int ldgw,
                              float* __restrict__ gb) {
+  constexpr int NW = NT / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const int NT = (N + 15) >> 4, KT = (K + 15) >> 4;
-  for (int t = wave; t < NT * KT; t += kNW) {
+  const int NTL = (N + 15) >> 4, KT = (K + 15) >> 4;
+  for (int t = wave; t < NTL * KT; t += NW) {
     const int nt = t / KT, kt = t - nt * KT;
     const int na = nt * 16 + li;   // A-operand row (output n)
     const int kb = kt * 16 + li;   // B-operand col (input k)
     const bool nav = na < N, kbv = kb < K;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int r0 = 0; r0 < kRT; r0 += 4) {
-      const int r = r0 + lk;
-      const float a = nav ? G[r * ldg + na] : 0.f;
-      const float bx = kbv ? X[r * ldx + kb] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bx, acc, 0, 0, 0);
+#pragma unroll
+    for (int h = 0; h < kRT / 32; ++h) {
+      float a[8], x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = h * 32 + 4 * u + lk;
+        a[u] = nav ? G[r * ldg + na] : 0.f;
+        x[u] = kbv ? X[r * ldx + kb] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = mfma4(a[u], x[u], acc);
     }
     if (kbv) {
 #pragma unroll
@@ -173,8 +225,9 @@ __device__ void dense_bwd_dw(const float* __restrict__ G, int ldg,
       }
     }
   }
-  for (int n = threadIdx.x; n < N; n += kWG) {
+  for (int n = threadIdx.x; n < N; n += NT) {
     float s = 0.f;
+#pragma unroll 8
     for (int r = 0; r < kRT; ++r) s += G[r * ldg + n];
     gb[n] += s;
   }
@@ -247,27 +300,43 @@ __device__ inline MlpView view_flat(const MlpLayout& L, const float* F) {
   return v;
 }
 
-// Load a flat MLP buffer into LDS (padded); the padding is zeroed.
+// Load a flat MLP buffer into LDS (padded); the padding is zeroed.  The global
+// loads of a thread are issued 8 at a time before their LDS stores.
+template <int NT = kWG>
 __device__ inline void mlp_load_lds(const MlpLayout& L, const float* __restrict__ flat,
                                     float* __restrict__ P) {
-  for (int i = threadIdx.x; i < L.pcount; i += kWG) P[i] = 0.f;
+  for (int i = threadIdx.x; i < L.pcount; i += NT) P[i] = 0.f;
   __syncthreads();
-  for (int i = threadIdx.x; i < L.fcount; i += kWG) P[mlp_flat_to_pad(L, i)] = flat[i];
+  for (int base = 0; base < L.fcount; base += 8 * NT) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * NT + threadIdx.x;
+      v[u] = i < L.fcount ? flat[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * NT + threadIdx.x;
+      if (i < L.fcount) P[mlp_flat_to_pad(L, i)] = v[u];
+    }
+  }
   __syncthreads();
 }
+template <int NT = kWG>
 __device__ inline void mlp_store_flat(const MlpLayout& L, const float* __restrict__ P,
                                       float* __restrict__ flat) {
-  for (int i = threadIdx.x; i < L.fcount; i += kWG) flat[i] = P[mlp_flat_to_pad(L, i)];
+  for (int i = threadIdx.x; i < L.fcount; i += NT) flat[i] = P[mlp_flat_to_pad(L, i)];
 }
 
 // Load a 64-row observation tile into LDS X[64][ldx] (row r = tile row), with
 // the ZFilter of z_filter.py:59-79 applied when zmean != nullptr.  Rows >= nrows
 // and columns >= dim are zero.
+template <int NT = kWG>
 __device__ inline void load_obs_tile(const float* __restrict__ src, int64_t row_stride,
                                      int nrows, int dim, const float* zmean,
                                      const float* zstd, float* __restrict__ X, int ldx) {
   const int total = kRT * ldx;
-  for (int e = threadIdx.x; e < total; e += kWG) {
+  for (int e = threadIdx.x; e < total; e += NT) {
     const int r = e / ldx, c = e - r * ldx;
     float v = 0.f;
     if (r < nrows && c < dim) {
@@ -283,11 +352,12 @@ __device__ inline void load_obs_tile(const float* __restrict__ src, int64_t row_
 
 // ZFilter running mean / std per column (z_filter.py:69-72):
 //   mean = sum / count; std = max(sqrt(sumsq/count - mean^2), eps)
+template <int NT = kWG>
 __device__ inline void zfilter_colstats(const float* sum, const float* sumsq,
                                         const float* count, float eps, int dim,
                                         float* zmean, float* zstd) {
   const float cnt = count[0];
-  for (int c = threadIdx.x; c < dim; c += kWG) {
+  for (int c = threadIdx.x; c < dim; c += NT) {
     const float mean = sum[c] / cnt;
     const float sq = sumsq[c] / cnt;
     const float var = sq - mean * mean;

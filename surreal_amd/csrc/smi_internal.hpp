@@ -33,6 +33,7 @@ int launch_gae_windows(float* values, const float* rewards, const float* dones, 
                        float gamma_H, float* adv, float* ret, double* partials,
                        int* n_partials, hipStream_t stream);
 int launch_ppo_fused(const smi_ppo_args* args, hipStream_t stream);
+int64_t ppo_fused_max_params();
 int64_t ppo_xbuf_floats(int D, int H1, int H2, int A, int cH1, int cH2, int mode);
 int launch_ppo_epoch_grad(const smi_ppo_args* args, int epoch, hipStream_t stream);
 int launch_ppo_epoch_apply(const smi_ppo_args* args, int epoch, hipStream_t stream);

@@ -339,7 +339,10 @@ class PPOLearner(object):
         a.kl_record, a.kl_count, a.kl_capacity = (self.kl_record_buf.data_ptr(),
                                                   self.kl_count.data_ptr(), self.kl_capacity)
         self._last_ret = ret
-        if dp is None:
+        maxp = L.lib().smi_ppo_fused_max_params()
+        fused = dp is None and max(L.lib().smi_mlp_param_count(D, a_h1, a_h2, A, 1),
+                                   L.lib().smi_mlp_param_count(D, c_h1, c_h2, 1, 0)) <= maxp
+        if fused:
             with self._ev('ppo_fused_kernel'):
                 L.check(L.lib().smi_ppo_update_fused(a, st), 'smi_ppo_update_fused')
             # --- z_update(obs_iter) after the updates (ppo.py:578-582)
@@ -348,8 +351,9 @@ class PPOLearner(object):
                     L.call('smi_zfilter_update', L.ptr(x), B, D, T * D, L.ptr(zf.running_sum),
                            L.ptr(zf.running_sumsq), L.ptr(zf.count), st)
             return
-        # ---- data parallel: global advantage moments, then
-        # max(E+1, Ev) phases of [rank-local gradients -> all-reduce -> apply]
+        # ---- data parallel, or one GPU with networks too large
+        # for the fused kernel: global advantage moments, then max(E+1, Ev)
+        # phases of [rank-local gradients -> all-reduce (dp only) -> apply]
         mom = self._buf('adv_moments', (3,), torch.float64)
         L.call('smi_moments', L.ptr(adv_raw), B, None, 0, L.ptr(mom), st)
         yield mom
@@ -387,7 +391,8 @@ class PPOLearner(object):
 
     def learn(self, batch):                                   # ppo.py:588-613
         for buf in self._learn_phases(batch):
-            self.dp.allreduce_(buf)
+            if self.dp is not None:                           # single GPU: phases, no exchange
+                self.dp.allreduce_(buf)
 
     def last_stats(self):
         """Statistics dict of the last learn() (ppo.py:219-224,278-284,328-331,555,571-582).

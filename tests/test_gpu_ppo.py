@@ -38,10 +38,10 @@ def _compare_params(name, got, ref, lr, updates, report):
 
 
 def _run(mode, use_zf, B, T, iters=2, lr=(3e-4, 3e-4), use_r_filter=False, reward_scale=1.0,
-         epochs=(10, 10), seed=0, kl_target=0.02):
+         epochs=(10, 10), seed=0, kl_target=0.02, hidden=(64, 64)):
     D, A = 17, 6
     lc = ppo_config(B=B, T=T, mode=mode, use_z_filter=use_zf, lr=lr, use_r_filter=use_r_filter,
-                    reward_scale=reward_scale, epochs=epochs, kl_target=kl_target)
+                    reward_scale=reward_scale, epochs=epochs, kl_target=kl_target, hidden=hidden)
     learner = PPOLearner(lc, env_config(D, A), seed=seed + 11)
     ref = R.PPOLearnerRef(lc, D, A)
     copy_weights_to_oracle(learner, ref)
@@ -94,6 +94,15 @@ def test_c2_halfcheetah_parity(mode):
 ])
 def test_edge_shapes(mode, use_zf, B, T):
     _run(mode, use_zf, B, T, iters=1)
+
+
+@pytest.mark.parametrize('mode', ['clip', 'adapt'])
+def test_wide_networks_use_epoch_phases(mode):
+    # 64x80 hidden: more parameters than the fused kernel holds in registers,
+    # so one GPU runs the data-parallel phase kernels without an exchange
+    from surreal_amd import _lib as L
+    assert L.lib().smi_mlp_param_count(17, 64, 80, 6, 1) > L.lib().smi_ppo_fused_max_params()
+    _run(mode, True, 64, 10, iters=2, hidden=(64, 80))
 
 
 def test_early_stop_and_adapt_penalty():
