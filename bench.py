@@ -4,8 +4,12 @@ A step = one PPOLearner.learn() over one synthetic batch already resident in
 HBM: reward scaling, critic forward over B*(T+1) rows + windowed GAE, the fused
 policy/value epoch loop (ref_pol, <=10 actor updates with KL early stop, 10
 critic updates), z_update.  Workload at N=1 = BASELINE config 2 (HalfCheetah
-dims obs 17 / act 6, 64x64 MLP, 64 segments x 50 steps).  With --gpus N each
-rank runs its own learner on its own 64-segment batch (weak scaling).
+dims obs 17 / act 6, 64x64 MLP, 64 segments x 50 steps).  With --gpus N the
+learner is data parallel: each rank holds a 64-segment shard of
+one global N*64-segment batch and the ranks all-reduce advantage moments, the
+per-epoch gradient/statistic exchange buffer and the ZFilter column sums over
+RCCL (torch.distributed 'nccl') — weak scaling, every rank applies the update
+of the global batch.
 
 Prints ONE JSON line on rank 0 with the metric, a roofline object for the
 dominant kernel (HIP events on the learner's stream, inside the timed region)
@@ -100,11 +104,12 @@ def main():
     dev = torch.device('cuda', torch.cuda.current_device())
 
     from surreal_amd import synthetic
-    from surreal_amd.learner import PPOLearner
+    from surreal_amd.learner import PPOLearner, TorchDistAllReduce
     lc, ec = c2_config()
     B, T = lc.replay.batch_size, lc.algo.n_step
     D, A = 17, 6
-    learner = PPOLearner(lc, ec, seed=rank + 1, device=dev)
+    dp = TorchDistAllReduce() if dist is not None else None
+    learner = PPOLearner(lc, ec, seed=1, device=dev, dp=dp)
     pool = [synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=rank * 1000 + i), dev)
             for i in range(8)]
 
@@ -144,6 +149,8 @@ def main():
         # ref fwd + (epochs_run + 1) fwd + epochs_run bwd (policy)  +  E_v (fwd + bwd) (value)
         'ppo_fused_kernel': B * (af * (epochs_run + 2) + ab * epochs_run) + B * E_v * (cf + cb),
         'critic_gae_kernel': B * (T + 1) * cf,
+        # data parallel: one grad launch per phase (policy fwd/bwd and/or value fwd/bwd)
+        'ppo_epoch_grad_kernel': B * (af + ab + cf + cb),
     }
     if dominant in flops:
         ach = flops[dominant] / (kdur[dominant] * 1e-3) / 1e12
@@ -168,7 +175,7 @@ def main():
         'config': {'workload': 'C2: synthetic PPO learner batch, HalfCheetah dims (obs 17, act 6), '
                                '64x64 MLP, 64 segments x n_step 50 per GPU, adapt mode, z-filter, '
                                '10/10 epochs', 'segments_per_gpu': B, 'n_step': T,
-                   'env_steps_per_learn_per_gpu': B * T, 'parallelism': f'replicas{world}' if world > 1 else 'single',
+                   'env_steps_per_learn_per_gpu': B * T, 'global_segments': world * B, 'parallelism': f'dp{world}' if world > 1 else 'single',
                    'epochs_run_last': epochs_run},
         'roofline': roof,
         'kernels_avg_ms': {k: round(v, 5) for k, v in kdur.items()},

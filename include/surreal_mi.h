@@ -136,13 +136,16 @@ int smi_ppo_critic_gae(const float* critic_params, int obs_dim, int h1, int h2,
 
 /* Replaces the windowed GAE of the RNN branch (ppo.py:389-406) — and, with
  * horizon == T, the non-RNN sums — given already computed critic values
- * values[B][T+1] (masked in place here: values[:,1:] *= 1-dones):
+ * values[B][T+1].  The done mask values[:,1:] *= 1-dones (ppo.py:387) is
+ * applied on the fly; values_masked (may be NULL, may alias values) receives
+ * the masked values when the caller wants them:
  *   E = T - horizon + 1 windows per segment, s in [0,E):
  *   ret[b,s] = sum_{k<H} g[k]*r[b,s+k] + Vm[b,s+H]*gamma_H
  *   adv[b,s] = sum_{k<H} (td[b,s+k]*g[k])*l[k]
- * LDS-staged, coalesced streaming kernel.  adv_partials receives per-workgroup
+ * HBM-bound streaming kernel: 16-byte coalesced loads staged through LDS.  adv_partials receives per-workgroup
  * (sum, sumsq) doubles; *n_partials is set on return (host-side value). */
-int smi_gae_windows(float* values, const float* rewards, const float* dones,
+int smi_gae_windows(const float* values, float* values_masked,
+                    const float* rewards, const float* dones,
                     int64_t B, int T, int horizon,
                     const float* gamma_tab, const float* lam_tab,
                     float gamma, float gamma_H,

@@ -73,7 +73,7 @@ _SIGS = {
                                 c_int, P, P, P, c_f32, P, P]),
     'smi_ppo_critic_gae': (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, c_f32, P, P, P, P,
                                    c_int, c_int, P, P, c_f32, c_f32, P, P, P, P]),
-    'smi_gae_windows': (c_int, [P, P, P, c_i64, c_int, c_int, P, P, c_f32, c_f32, P, P, P,
+    'smi_gae_windows': (c_int, [P, P, P, P, c_i64, c_int, c_int, P, P, c_f32, c_f32, P, P, P,
                                 P, P]),
     'smi_gae_windows_max_partials': (c_int, [c_i64, c_int]),
     'smi_moments': (c_int, [P, c_i64, P, c_int, P, P]),

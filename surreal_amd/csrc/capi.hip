@@ -171,14 +171,15 @@ int smi_ppo_critic_gae(const float* critic_params, int obs_dim, int h1, int h2, 
                            adv_raw, ret, SMI_STREAM(stream));
 }
 
-int smi_gae_windows(float* values, const float* rewards, const float* dones, int64_t B, int T,
+int smi_gae_windows(const float* values, float* values_masked, const float* rewards,
+                    const float* dones, int64_t B, int T,
                     int horizon, const float* gtab, const float* ltab, float gamma,
                     float gamma_H, float* adv, float* ret, double* partials, int* n_partials,
                     void* stream) {
   REQUIRE(values && rewards && dones && gtab && ltab && adv && ret, "gae_windows: null pointer");
   REQUIRE(B >= 0 && T >= 1, "gae_windows: bad dims");
   if (B == 0) { if (n_partials) *n_partials = 0; return SMI_OK; }
-  return launch_gae_windows(values, rewards, dones, B, T, horizon, gtab, ltab, gamma, gamma_H,
+  return launch_gae_windows(values, values_masked, rewards, dones, B, T, horizon, gtab, ltab, gamma, gamma_H,
                             adv, ret, partials, n_partials, SMI_STREAM(stream));
 }
 

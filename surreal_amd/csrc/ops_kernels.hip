@@ -14,6 +14,8 @@
 namespace smi {
 
 // ------------------------------------------------------------- ZFilter apply
+// HBM-bound (8 B per element).  16-byte loads/stores; the column of each of a
+// float4's four elements is tracked incrementally (no per-element modulo).
 __global__ void __launch_bounds__(kWG)
 zfilter_apply_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t n, int dim,
                      const float* sum, const float* sumsq, const float* count, float eps) {
@@ -22,61 +24,102 @@ zfilter_apply_kernel(const float* __restrict__ x, float* __restrict__ out, int64
   float* zs = sm + round4(dim);
   zfilter_colstats(sum, sumsq, count, eps, dim, zm, zs);
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
+  const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  const int64_t n4 = vec ? (n >> 2) : 0;
+  const int64_t stride = (int64_t)gridDim.x * kWG;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  float4* o4 = reinterpret_cast<float4*>(out);
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n4; i += stride) {
+    const float4 v = x4[i];
+    int c = (int)((i << 2) % dim);
+    float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float y = (r[j] - zm[c]) / zs[c];
+      r[j] = fminf(fmaxf(y, -5.f), 5.f);
+      c = (c + 1 == dim) ? 0 : c + 1;
+    }
+    o4[i] = float4{r[0], r[1], r[2], r[3]};
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += stride) {
     const int c = (int)(i % dim);
-    float v = (x[i] - zm[c]) / zs[c];
-    out[i] = fminf(fmaxf(v, -5.f), 5.f);
+    const float y = (x[i] - zm[c]) / zs[c];
+    out[i] = fminf(fmaxf(y, -5.f), 5.f);
   }
 }
 
 // ------------------------------------------------ ZFilter column statistics
-// Column sums and sums of squares over `rows` strided rows.  Each workgroup
-// owns a column slab of width <= 64 and a row range; partial sums go to
-// `part` [gridDim.y][2][dim], reduced in a fixed order by the finisher.
+// Column sums and sums of squares over `rows` strided rows (HBM-bound, 4 B per
+// element).  A workgroup covers CB = min(dim, 256) columns with RP = 256/CB row
+// lanes, so for contiguous rows (stride == dim) one wave-instruction reads 256
+// consecutive bytes; 8 independent loads per thread are kept in flight.
+// Partial sums go to `part` [gridDim.y][2][dim], reduced in a fixed order by
+// the finisher (deterministic).
 __global__ void __launch_bounds__(kWG)
 colstats_partial_kernel(const float* __restrict__ x, int64_t rows, int dim, int64_t stride,
                         float* __restrict__ part) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rl = threadIdx.x >> 6;            // 4 row lanes
-  __shared__ float s1[kNW][64], s2[kNW][64];
+  __shared__ float s1[kWG], s2[kWG];
+  const int CB = dim < kWG ? dim : kWG;
+  const int RP = kWG / CB;
+  const int t = threadIdx.x;
+  const int rl = t / CB, cl = t - rl * CB;
+  const int c = blockIdx.x * CB + cl;
+  const bool active = rl < RP && c < dim;
   float a1 = 0.f, a2 = 0.f;
-  if (c < dim) {
-    for (int64_t r = (int64_t)blockIdx.y * kNW + rl; r < rows; r += (int64_t)gridDim.y * kNW) {
+  if (active) {
+    // this workgroup's contiguous row range (a wave walks consecutive memory)
+    const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
+    const int64_t r_lo = (int64_t)blockIdx.y * per;
+    const int64_t r_hi = min(rows, r_lo + per);
+    int64_t r = r_lo + rl;
+    for (; r + 7 * RP < r_hi; r += 8 * RP) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = x[(r + u * RP) * stride + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { a1 += v[u]; a2 += v[u] * v[u]; }
+    }
+    for (; r < r_hi; r += RP) {
       const float v = x[r * stride + c];
       a1 += v;
       a2 += v * v;
     }
   }
-  s1[rl][threadIdx.x & 63] = a1;
-  s2[rl][threadIdx.x & 63] = a2;
+  s1[t] = a1;
+  s2[t] = a2;
   __syncthreads();
   if (rl == 0 && c < dim) {
     float t1 = 0.f, t2 = 0.f;
-    for (int w = 0; w < kNW; ++w) { t1 += s1[w][threadIdx.x]; t2 += s2[w][threadIdx.x]; }
+    for (int w = 0; w < RP; ++w) { t1 += s1[w * CB + cl]; t2 += s2[w * CB + cl]; }
     part[((int64_t)blockIdx.y * 2) * dim + c] = t1;
     part[((int64_t)blockIdx.y * 2 + 1) * dim + c] = t2;
   }
 }
 
-// finisher: mode 0 -> write sums; mode 1 -> add into running buffers and count
+// finisher: one workgroup per column reduces the partials (fixed order);
+// mode 0 -> write sums; mode 1 -> add into running buffers and count
 __global__ void __launch_bounds__(kWG)
 colstats_finish_kernel(const float* __restrict__ part, int nparts, int dim, int64_t rows,
                        int mode, float* out_sum, float* out_sumsq, float* count) {
-  for (int c = threadIdx.x + blockIdx.x * kWG; c < dim; c += gridDim.x * kWG) {
-    float t1 = 0.f, t2 = 0.f;
-    for (int p = 0; p < nparts; ++p) {
-      t1 += part[((int64_t)p * 2) * dim + c];
-      t2 += part[((int64_t)p * 2 + 1) * dim + c];
-    }
+  __shared__ double scr[kNW];
+  const int c = blockIdx.x;
+  float t1 = 0.f, t2 = 0.f;
+  for (int p = threadIdx.x; p < nparts; p += kWG) {
+    t1 += part[((int64_t)p * 2) * dim + c];
+    t2 += part[((int64_t)p * 2 + 1) * dim + c];
+  }
+  const float s1 = block_sum_f(t1, scr);
+  const float s2 = block_sum_f(t2, scr);
+  if (threadIdx.x == 0) {
     if (mode == 0) {
-      out_sum[c] = t1;
-      out_sumsq[c] = t2;
+      out_sum[c] = s1;
+      out_sumsq[c] = s2;
     } else {
-      out_sum[c] += t1;      // running_sum += torch.sum(x, 0)   (z_filter.py:54)
-      out_sumsq[c] += t2;    // running_sumsq += torch.sum(x*x, 0) (z_filter.py:55)
+      out_sum[c] += s1;      // running_sum += torch.sum(x, 0)   (z_filter.py:54)
+      out_sumsq[c] += s2;    // running_sumsq += torch.sum(x*x, 0) (z_filter.py:55)
+      if (c == 0) count[0] += (float)rows;                          // :56
     }
   }
-  if (mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) count[0] += (float)rows;  // :56
 }
 
 // Single-pass variant for small inputs: one workgroup, no partial buffer.
@@ -149,38 +192,80 @@ reward_filter_kernel(float* __restrict__ r, int64_t n, float scale, int mode,
 }
 
 // ------------------------------------------------------------ DiagGauss ops
+// HBM-bound: a tile of DG_R rows of actions (A floats), prob0 and prob1 (2A
+// floats each) is staged through LDS with 16-byte coalesced loads (the tile is
+// contiguous in each array), then one thread per row forms the sums from LDS
+// with odd row strides (bank-conflict free); outputs are written coalesced.
+constexpr int DG_R = kWG;
+
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, int64_t r0, int nrows,
+                                           int w, float* __restrict__ dst, int ldd) {
+  const int n = nrows * w;
+  const float* g = src + r0 * w;
+  if (((reinterpret_cast<uintptr_t>(g)) & 15) == 0 && (w & 3) == 0) {
+    const int w4 = w >> 2;
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (int e = threadIdx.x; e < (n >> 2); e += kWG) {
+      const float4 v = g4[e];
+      const int r = e / w4, c = (e - r * w4) << 2;
+      float* d = dst + r * ldd + c;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+  } else {
+    for (int e = threadIdx.x; e < n; e += kWG) {
+      const int r = e / w, c = e - r * w;
+      dst[r * ldd + c] = g[e];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kWG)
 diag_gauss_kernel(const float* __restrict__ a, const float* __restrict__ p0,
                   const float* __restrict__ p1, int64_t rows, int A, float c_ll, float c_ent,
                   float* loglik, float* lik, float* kl, float* ent) {
-  for (int64_t r = (int64_t)blockIdx.x * kWG + threadIdx.x; r < rows; r += (int64_t)gridDim.x * kWG) {
-    const float* q0 = p0 + r * 2 * A;
-    if (loglik || lik) {
-      float s = 0.f, l = 0.f;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lda = A | 1, ldp = (2 * A) | 1;
+  const bool need_a = loglik || lik;
+  const bool need_p1 = kl && p1;
+  float* sa = sm;
+  float* s0 = sa + DG_R * lda;
+  float* s1 = s0 + DG_R * ldp;
+  const int64_t ntiles = (rows + DG_R - 1) / DG_R;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t r0 = tile * DG_R;
+    const int nr = (int)min((int64_t)DG_R, rows - r0);
+    __syncthreads();
+    if (need_a) stage_rows(a, r0, nr, A, sa, lda);
+    stage_rows(p0, r0, nr, 2 * A, s0, ldp);
+    if (need_p1) stage_rows(p1, r0, nr, 2 * A, s1, ldp);
+    __syncthreads();
+    const int r = threadIdx.x;
+    if (r >= nr) continue;
+    const float* q0 = s0 + r * ldp;
+    float lsum = 0.f;
+    for (int j = 0; j < A; ++j) lsum += logf(q0[A + j]);
+    if (need_a) {
+      const float* ar = sa + r * lda;
+      float sq = 0.f;
       for (int j = 0; j < A; ++j) {
-        const float u = (a[r * A + j] - q0[j]) / q0[A + j];
-        s += u * u;
-        l += logf(q0[A + j]);
+        const float u = (ar[j] - q0[j]) / q0[A + j];
+        sq += u * u;
       }
-      const float ll = (-0.5f * s - c_ll) - l;
-      if (loglik) loglik[r] = ll;
-      if (lik) lik[r] = fmaxf(expf(ll), 1e-5f);
+      const float ll = (-0.5f * sq - c_ll) - lsum;
+      if (loglik) loglik[r0 + r] = ll;
+      if (lik) lik[r0 + r] = fmaxf(expf(ll), 1e-5f);
     }
-    if (kl && p1) {
-      const float* q1 = p1 + r * 2 * A;
-      float s1 = 0.f, s2 = 0.f;
+    if (need_p1) {
+      const float* q1 = s1 + r * ldp;
+      float k1 = 0.f, k2 = 0.f;
       for (int j = 0; j < A; ++j) {
-        s1 += logf(q1[A + j] / q0[A + j]);
+        k1 += logf(q1[A + j] / q0[A + j]);
         const float d = q0[j] - q1[j];
-        s2 += (q0[A + j] * q0[A + j] + d * d) / (2.f * (q1[A + j] * q1[A + j]));
+        k2 += (q0[A + j] * q0[A + j] + d * d) / (2.f * (q1[A + j] * q1[A + j]));
       }
-      kl[r] = (s1 + s2) - 0.5f * (float)A;
+      kl[r0 + r] = (k1 + k2) - 0.5f * (float)A;
     }
-    if (ent) {
-      float l = 0.f;
-      for (int j = 0; j < A; ++j) l += logf(q0[A + j]);
-      ent[r] = 0.5f * l + c_ent;
-    }
+    if (ent) ent[r0 + r] = 0.5f * lsum + c_ent;
   }
 }
 
@@ -234,6 +319,40 @@ mlp_forward_kernel(MlpFwdArgs a) {
 }
 
 // -------------------------------------------------------------- moments
+// (sum, sumsq) of x in fp64: grid-stride partials with 16-byte loads, then a
+// one-workgroup fixed-order finish (deterministic); or, given partials, only
+// the finish.
+__global__ void __launch_bounds__(kWG)
+moments_partial_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ part) {
+  __shared__ double scr[kNW];
+  double a1 = 0.0, a2 = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * kWG;
+  const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const int64_t n4 = vec ? (n >> 2) : 0;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const float4 u = x4[i], w = x4[i + stride];
+    const float e[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const double d = (double)e[j]; a1 += d; a2 += d * d; }
+  }
+  for (; i < n4; i += stride) {
+    const float4 u = x4[i];
+    const float e[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { const double d = (double)e[j]; a1 += d; a2 += d * d; }
+  }
+  for (int64_t k = (n4 << 2) + (int64_t)blockIdx.x * kWG + threadIdx.x; k < n; k += stride) {
+    const double d = (double)x[k];
+    a1 += d;
+    a2 += d * d;
+  }
+  const double t1 = block_sum_d(a1, scr);
+  const double t2 = block_sum_d(a2, scr);
+  if (threadIdx.x == 0) { part[2 * blockIdx.x] = t1; part[2 * blockIdx.x + 1] = t2; }
+}
+
 __global__ void __launch_bounds__(kWG)
 moments_kernel(const float* __restrict__ x, int64_t n, const double* partials, int np,
                double* out) {
@@ -253,24 +372,51 @@ moments_kernel(const float* __restrict__ x, int64_t n, const double* partials, i
   if (threadIdx.x == 0) { out[0] = t1; out[1] = t2; out[2] = (double)n; }
 }
 
-// ------------------------------------------------------------ Adam + clip
-// Two kernels: partial sums of squares per workgroup, then the update (every
-// workgroup recomputes the global norm from the partials in the same order, so
-// the coefficient is identical everywhere without a grid barrier).
+// ||g||^2 partials in fp64 (clip_grad_norm_'s norm), 16-byte loads.
 __global__ void __launch_bounds__(kWG)
 sumsq_partial_kernel(const float* __restrict__ g, int64_t n, float clip_value, double* part) {
   __shared__ double scr[kNW];
   double a = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
+  const int64_t stride = (int64_t)gridDim.x * kWG;
+  const bool vec = (reinterpret_cast<uintptr_t>(g) & 15) == 0;
+  const int64_t n4 = vec ? (n >> 2) : 0;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n4; i += stride) {
+    const float4 u = g4[i];
+    const float e[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gi = e[j];
+      if (clip_value > 0.f) gi = fminf(fmaxf(gi, -clip_value), clip_value);
+      a += (double)gi * (double)gi;
+    }
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += stride) {
     float gi = g[i];
     if (clip_value > 0.f) gi = fminf(fmaxf(gi, -clip_value), clip_value);
-    const double v = (double)gi;
-    a += v * v;
+    a += (double)gi * (double)gi;
   }
   a = block_sum_d(a, scr);
   if (threadIdx.x == 0) part[blockIdx.x] = a;
 }
 
+struct AdamCoef {
+  float coef, wd, w1, beta2, w2, eps, step_size, bc2_sqrt, clip_value;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamCoef& k) {
+  if (k.clip_value > 0.f) g = fminf(fmaxf(g, -k.clip_value), k.clip_value);   // clip_grad_value_
+  g = g * k.coef;
+  if (k.wd != 0.f) g = g + k.wd * p;
+  m = m + k.w1 * (g - m);                      // m.lerp_(g, 1 - beta1)
+  v = v * k.beta2 + (k.w2 * g) * g;            // v.mul_(b2).addcmul_(g, g, 1 - b2)
+  const float denom = sqrtf(v) / k.bc2_sqrt + k.eps;
+  p = p + (-k.step_size) * (m / denom);
+}
+
+// torch.optim.Adam (single-tensor path) on a flat buffer, after the optional
+// clip_grad_norm_ coefficient.  HBM-bound: 28 B per parameter, 16-byte loads
+// and stores of p, g, m, v.
 __global__ void __launch_bounds__(kWG)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, int64_t n, int* step, const float* lr_ptr, float beta1,
@@ -279,9 +425,12 @@ adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restric
   if (skip && skip[0] != 0) return;
   __shared__ float s_coef;
   __shared__ int s_t;
+  __shared__ double s_red[kNW];
+  double s = 0.0;
+  if (part)
+    for (int i = threadIdx.x; i < np; i += kWG) s += part[i];
+  s = block_sum_d(s, s_red);
   if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int i = 0; i < np; ++i) s += part[i];
     const float norm = (float)sqrt(s);
     float coef = 1.f;
     if (max_norm > 0.f) {
@@ -294,31 +443,38 @@ adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restric
   }
   __syncthreads();
   const int t = s_t;
-  const float coef = s_coef;
   const double bc1 = 1.0 - pow((double)beta1, (double)t);
   const double bc2 = 1.0 - pow((double)beta2, (double)t);
-  const float lr = lr_ptr[0];
-  const float step_size = (float)((double)lr / bc1);
-  const float bc2_sqrt = (float)sqrt(bc2);
-  const float w1 = (float)(1.0 - (double)beta1);
-  const float w2 = (float)(1.0 - (double)beta2);
-  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
-    float gi = g[i];
-    if (clip_value > 0.f) gi = fminf(fmaxf(gi, -clip_value), clip_value);   // clip_grad_value_
-    gi = gi * coef;
-    float pi = p[i];
-    if (wd != 0.f) gi = gi + wd * pi;
-    float mi = m[i], vi = v[i];
-    mi = mi + w1 * (gi - mi);
-    vi = vi * beta2 + (w2 * gi) * gi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = pi + (-step_size) * (mi / denom);
-    m[i] = mi;
-    v[i] = vi;
+  AdamCoef k;
+  k.coef = s_coef; k.wd = wd; k.beta2 = beta2; k.eps = eps; k.clip_value = clip_value;
+  k.step_size = (float)((double)lr_ptr[0] / bc1);
+  k.bc2_sqrt = (float)sqrt(bc2);
+  k.w1 = (float)(1.0 - (double)beta1);
+  k.w2 = (float)(1.0 - (double)beta2);
+  const int64_t stride = (int64_t)gridDim.x * kWG;
+  const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                     reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+  const int64_t n4 = vec ? (n >> 2) : 0;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n4; i += stride) {
+    float4 pp = p4[i], mm = m4[i], vv = v4[i];
+    const float4 gg = g4[i];
+    adam_elem(pp.x, gg.x, mm.x, vv.x, k);
+    adam_elem(pp.y, gg.y, mm.y, vv.y, k);
+    adam_elem(pp.z, gg.z, mm.z, vv.z, k);
+    adam_elem(pp.w, gg.w, mm.w, vv.w, k);
+    p4[i] = pp; m4[i] = mm; v4[i] = vv;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += stride) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    adam_elem(pi, g[i], mi, vi, k);
+    p[i] = pi; m[i] = mi; v[i] = vi;
   }
 }
 
-// step counter increment after every workgroup of adam_kernel has read it
 __global__ void step_inc_kernel(int* step, const int* skip) {
   if (skip && skip[0] != 0) return;
   step[0] += 1;
@@ -351,7 +507,7 @@ int launch_zfilter_apply(const float* x, float* out, int64_t rows, int dim, cons
                          const float* sq, const float* cnt, float eps, hipStream_t st) {
   const int64_t n = rows * dim;
   if (n == 0) return SMI_OK;
-  hipLaunchKernelGGL(zfilter_apply_kernel, dim3(grid_for(n)), dim3(kWG),
+  hipLaunchKernelGGL(zfilter_apply_kernel, dim3(grid_for((n + 3) / 4)), dim3(kWG),
                      (size_t)(2 * round4(dim) * 4), st, x, out, n, dim, s, sq, cnt, eps);
   return check_launch("zfilter_apply_kernel");
 }
@@ -368,16 +524,19 @@ int launch_colstats(const float* x, int64_t rows, int dim, int64_t stride, int m
                        mode, osum, osq, cnt);
     return check_launch("colstats_small_kernel");
   }
-  const int gx = (dim + 63) / 64;
-  int gy = (int)((rows + 1023) / 1024);
-  if (gy > 512) gy = 512;
+  const int CB = dim < kWG ? dim : kWG;
+  const int RP = kWG / CB;
+  const int gx = (dim + CB - 1) / CB;
+  int gy = (int)((rows + 8 * RP - 1) / (8 * RP));
+  const int gy_cap = (2048 + gx - 1) / gx;
+  if (gy > gy_cap) gy = gy_cap;
+  if (gy < 1) gy = 1;
   float* part = workspace_f32((int64_t)gy * 2 * dim);
-  if (!part) return set_error(SMI_E_ARG, "colstats: workspace unavailable");
   hipLaunchKernelGGL(colstats_partial_kernel, dim3(gx, gy), dim3(kWG), 0, st, x, rows, dim,
                      stride, part);
   int rc = check_launch("colstats_partial_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(colstats_finish_kernel, dim3((dim + kWG - 1) / kWG), dim3(kWG), 0, st,
+  hipLaunchKernelGGL(colstats_finish_kernel, dim3(dim), dim3(kWG), 0, st,
                      part, gy, dim, rows, mode, osum, osq, cnt);
   return check_launch("colstats_finish_kernel");
 }
@@ -393,8 +552,12 @@ int launch_diag_gauss(const float* a, const float* p0, const float* p1, int64_t 
                       float* ll, float* lik, float* kl, float* ent, hipStream_t st) {
   const float c_ll = (float)(0.5 * log(2.0 * 3.141592653589793) * (double)A);
   const float c_ent = (float)(0.5 * log(2.0 * 3.141592653589793 * 2.718281828459045) * (double)A);
-  hipLaunchKernelGGL(diag_gauss_kernel, dim3(grid_for(rows)), dim3(kWG), 0, st, a, p0, p1, rows,
-                     A, c_ll, c_ent, ll, lik, kl, ent);
+  if (rows <= 0) return SMI_OK;
+  const size_t lds = (size_t)DG_R * ((A | 1) + 2 * ((2 * A) | 1)) * 4;
+  if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "diag_gauss: act_dim too large");
+  allow_lds(diag_gauss_kernel, lds);
+  hipLaunchKernelGGL(diag_gauss_kernel, dim3(grid_for(rows, 4096)), dim3(kWG), lds, st, a, p0, p1,
+                     rows, A, c_ll, c_ent, ll, lik, kl, ent);
   return check_launch("diag_gauss_kernel");
 }
 
@@ -422,22 +585,36 @@ int launch_mlp_forward(const float* params, int in, int h1, int h2, int out, int
 
 int launch_moments(const float* x, int64_t n, const double* part, int np, double* out,
                    hipStream_t st) {
-  hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(kWG), 0, st, x, n, part, np, out);
+  if ((part && np > 0) || n <= (int64_t)1 << 16) {
+    hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(kWG), 0, st, x, n, part, np, out);
+    return check_launch("moments_kernel");
+  }
+  const int grid = grid_for((n + 7) / 8, 1024);
+  double* ws = reinterpret_cast<double*>(workspace_f32(4 * grid));
+  if (!ws) return set_error(SMI_E_ARG, "moments: workspace unavailable");
+  hipLaunchKernelGGL(moments_partial_kernel, dim3(grid), dim3(kWG), 0, st, x, n, ws);
+  int rc = check_launch("moments_partial_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(kWG), 0, st, nullptr, n, ws, grid, out);
   return check_launch("moments_kernel");
 }
 
 int launch_adam_clip(float* p, const float* g, float* m, float* v, int64_t n, int* step,
                      const float* lr, float b1, float b2, float eps, float wd, float max_norm,
                      float clip_value, const int* skip, float* norm_out, hipStream_t st) {
-  const int grid = grid_for(n, 512);
-  double* part = reinterpret_cast<double*>(workspace_f32(2 * 512));
-  if (!part) return set_error(SMI_E_ARG, "adam: workspace unavailable");
-  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kWG), 0, st, g, n, clip_value, part);
-  int rc = check_launch("sumsq_partial_kernel");
-  if (rc) return rc;
+  const int grid = grid_for((n + 3) / 4, 2048);
+  const bool need_norm = max_norm > 0.f || norm_out != nullptr;
+  double* part = nullptr;
+  if (need_norm) {
+    part = reinterpret_cast<double*>(workspace_f32(2 * 2048));
+    if (!part) return set_error(SMI_E_ARG, "adam: workspace unavailable");
+    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kWG), 0, st, g, n, clip_value, part);
+    const int rc0 = check_launch("sumsq_partial_kernel");
+    if (rc0) return rc0;
+  }
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kWG), 0, st, p, g, m, v, n, step, lr, b1, b2,
-                     eps, wd, max_norm, clip_value, part, grid, skip, norm_out);
-  rc = check_launch("adam_kernel");
+                     eps, wd, max_norm, clip_value, part, need_norm ? grid : 0, skip, norm_out);
+  int rc = check_launch("adam_kernel");
   if (rc) return rc;
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step, skip);
   return check_launch("step_inc_kernel");

@@ -115,68 +115,255 @@ critic_gae_kernel(CriticGaeArgs a) {
 }
 
 // ===================================================== streaming GAE windows
-// values [B][T+1] (masked in place), rewards/dones [B][T] -> adv/ret [B][E].
-// A workgroup stages a contiguous block of SB segments of r, d, V through LDS
-// with coalesced loads (the three arrays are contiguous per segment block),
-// computes the windows from LDS and writes adv/ret coalesced.
+// values [B][T+1], rewards/dones [B][T] -> adv/ret [B][E]  (ppo.py:387-406).
+// HBM-bound.  A workgroup stages a contiguous block of SB segments of r, d, V
+// through LDS with 16-byte coalesced loads (the three arrays are contiguous per
+// segment block; SB is a multiple of 4, so every block starts 16-byte aligned).
+//   pass 1 (row-mapped: TPR = 2^k >= T threads per segment row, no divides):
+//          td[s][t] = r + gamma * V[t+1](1-d[t]) - V[t](1-d[t-1])   (done mask
+//          of ppo.py:387 applied on the fly; optionally written out)
+//   pass 2 (item = (segment, window), LG lanes per item, window index fixed
+//          per thread): ret = sum g[k] r[s+k] + Vm[s+H] gamma^H,
+//          adv = sum (td[s+k] g[k]) l[k]; LG > 1 splits long (non-RNN) windows.
 struct GaeWinArgs {
-  float* values; const float *rewards, *dones;
-  int64_t B; int T, H, E, SB;
+  const float* values; float* values_masked; const float *rewards, *dones;
+  int64_t B; int T, H, E, SB, LG, TPR;
   const float *gtab, *ltab; float gamma, gamma_H;
   float *adv, *ret; double* partials;
 };
+
+__device__ __forceinline__ void stage_f32(const float* __restrict__ src, float* __restrict__ dst,
+                                          int n, bool vec) {
+  if (vec) {
+    const int n4 = n >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    int i = threadIdx.x;
+    for (; i + 3 * kWG < n4; i += 4 * kWG) {
+      const float4 a = s4[i], b = s4[i + kWG], c = s4[i + 2 * kWG], d = s4[i + 3 * kWG];
+      d4[i] = a; d4[i + kWG] = b; d4[i + 2 * kWG] = c; d4[i + 3 * kWG] = d;
+    }
+    for (; i < n4; i += kWG) d4[i] = s4[i];
+    for (int j = (n4 << 2) + threadIdx.x; j < n; j += kWG) dst[j] = src[j];
+  } else {
+    for (int j = threadIdx.x; j < n; j += kWG) dst[j] = src[j];
+  }
+}
+
+// Register prefetch of one full segment block ([r | d | V] as float4s, at most
+// GAE_PF per thread): the next block's loads are in flight while the current
+// block computes, so HBM sees a continuous stream.
+constexpr int GAE_PF = 8;   // the SMI_GAE_PF_* macros below are unrolled for 8
+
+// (8 named registers rather than an array: the compiler kept an array in scratch)
+#define SMI_GAE_PF_LOAD(j)                                               \
+  {                                                                      \
+    const int q = threadIdx.x + (j) * kWG;                               \
+    const float4* src = q < pf_nr4 ? pf_r4 : (q < 2 * pf_nr4 ? pf_d4 : pf_v4); \
+    if (q < pf_tot4) pf##j = src[q];                                     \
+  }
+#define SMI_GAE_PREFETCH(b0)                                                                   \
+  {                                                                                            \
+    const float4* pf_r4 = reinterpret_cast<const float4*>(a.rewards + (b0) * T);               \
+    const float4* pf_d4 = reinterpret_cast<const float4*>(a.dones + (b0) * T) - pf_nr4;        \
+    const float4* pf_v4 = reinterpret_cast<const float4*>(a.values + (b0) * T1) - 2 * pf_nr4;  \
+    SMI_GAE_PF_LOAD(0) SMI_GAE_PF_LOAD(1) SMI_GAE_PF_LOAD(2) SMI_GAE_PF_LOAD(3)                \
+    SMI_GAE_PF_LOAD(4) SMI_GAE_PF_LOAD(5) SMI_GAE_PF_LOAD(6) SMI_GAE_PF_LOAD(7)                \
+  }
+#define SMI_GAE_PF_STORE(j)                                              \
+  {                                                                      \
+    const int q = threadIdx.x + (j) * kWG;                               \
+    if (q < pf_tot4) l4[q] = pf##j;                                      \
+  }
 
 __global__ void __launch_bounds__(kWG)
 gae_windows_kernel(GaeWinArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ double red[kNW];
-  const int T = a.T, T1 = T + 1, H = a.H, E = a.E;
-  float* sr = sm;                         // [SB*T]
-  float* sd = sr + a.SB * T;              // [SB*T]
-  float* sv = sd + a.SB * T;              // [SB*T1]
-  float* sg = sv + a.SB * T1;             // [H] gamma table
+  const int T = a.T, T1 = T + 1, H = a.H, E = a.E, LG = a.LG, TPR = a.TPR;
+  const int SBT4 = (a.SB * T + 3) & ~3, SBT14 = (a.SB * T1 + 3) & ~3;
+  float* sr = sm;                         // [SB*T] rewards
+  float* sd = sr + SBT4;                  // [SB*T] dones
+  float* sv = sd + SBT4;                  // [SB*T1] values (raw)
+  float* st = sv + SBT14;                 // [SB*T] td
+  float* sg = st + SBT4;                  // [H] gamma table
   float* sl = sg + H;                     // [H] lambda table
   for (int k = threadIdx.x; k < H; k += kWG) { sg[k] = a.gtab[k]; sl[k] = a.ltab[k]; }
+  // pass-1 mapping: thread -> (row lane, t)
+  const int tcol = threadIdx.x & (TPR - 1);
+  const int trow = threadIdx.x / TPR;
+  const int RPP = kWG / TPR;
+  // pass-2 mapping: thread -> (segment offset, window w) fixed across passes
+  const int lane_g = threadIdx.x & (LG - 1);
+  const int it0 = threadIdx.x / LG;
+  const int SPP = (kWG / LG) / E;          // segments per pass (>= 1 by construction)
+  const int s_off = it0 / E, w = it0 - s_off * E;
+  const bool p2_active = s_off < SPP;
   double psum = 0.0, psq = 0.0;
   const int64_t nblk = (a.B + a.SB - 1) / a.SB;
+  const bool vec = ((reinterpret_cast<uintptr_t>(a.rewards) | reinterpret_cast<uintptr_t>(a.dones) |
+                     reinterpret_cast<uintptr_t>(a.values)) & 15) == 0;
+  const float gamma = a.gamma;
+  // full blocks (nseg == SB, 16-byte aligned arrays) go through the register
+  // prefetch; the ragged last block is staged directly
+  const int64_t nfull = vec ? a.B / a.SB : 0;
+  const int nr4 = a.SB * T / 4, nv4 = a.SB * T1 / 4;
+  const int pf_nr4 = nr4, pf_tot4 = 2 * nr4 + nv4;
+  float4 pf0, pf1, pf2, pf3, pf4, pf5, pf6, pf7;
+  if (blockIdx.x < nfull) SMI_GAE_PREFETCH((int64_t)blockIdx.x * a.SB)
   for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     const int64_t b0 = blk * a.SB;
     const int nseg = (int)min((int64_t)a.SB, a.B - b0);
-    const int nrd = nseg * T, nv = nseg * T1;
-    const float* gr = a.rewards + b0 * T;
-    const float* gd = a.dones + b0 * T;
-    float* gv = a.values + b0 * T1;
     __syncthreads();
-    for (int i = threadIdx.x; i < nrd; i += kWG) { sr[i] = gr[i]; sd[i] = gd[i]; }
-    for (int i = threadIdx.x; i < nv; i += kWG) sv[i] = gv[i];
+    if (blk < nfull) {
+      // sr, sd, sv are contiguous in LDS (SB*T is a multiple of 4)
+      float4* l4 = reinterpret_cast<float4*>(sr);
+      SMI_GAE_PF_STORE(0) SMI_GAE_PF_STORE(1) SMI_GAE_PF_STORE(2) SMI_GAE_PF_STORE(3)
+      SMI_GAE_PF_STORE(4) SMI_GAE_PF_STORE(5) SMI_GAE_PF_STORE(6) SMI_GAE_PF_STORE(7)
+      const int64_t nxt = blk + gridDim.x;
+      if (nxt < nfull) SMI_GAE_PREFETCH(nxt * a.SB)
+    } else {
+      stage_f32(a.rewards + b0 * T, sr, nseg * T, vec);
+      stage_f32(a.dones + b0 * T, sd, nseg * T, vec);
+      stage_f32(a.values + b0 * T1, sv, nseg * T1, vec);
+    }
     __syncthreads();
-    // mask values[:,1:] *= 1-dones and write back
-    for (int i = threadIdx.x; i < nv; i += kWG) {
-      const int s = i / T1, t = i - s * T1;
-      if (t > 0) {
-        const float m = sv[i] * (1.f - sd[s * T + t - 1]);
-        sv[i] = m;
-        gv[i] = m;
+    for (int s = trow; s < nseg; s += RPP) {
+      const float* r = sr + s * T;
+      const float* d = sd + s * T;
+      const float* v = sv + s * T1;
+      for (int t = tcol; t < T1; t += TPR) {
+        const float vm = t > 0 ? v[t] * (1.f - d[t - 1]) : v[0];
+        if (a.values_masked) a.values_masked[(b0 + s) * T1 + t] = vm;
+        if (t < T) {
+          const float vm1 = v[t + 1] * (1.f - d[t]);
+          st[s * T + t] = (r[t] + gamma * vm1) - vm;
+        }
       }
     }
     __syncthreads();
-    // windows: item = (segment s, window w)
-    const int nitems = nseg * E;
-    for (int it = threadIdx.x; it < nitems; it += kWG) {
-      const int s = it / E, w = it - s * E;
-      const float* r = sr + s * T + w;
-      const float* v = sv + s * T1 + w;
-      float rs = 0.f, as = 0.f;
-      for (int k = 0; k < H; ++k) {
-        rs += sg[k] * r[k];
-        const float td = (r[k] + a.gamma * v[k + 1]) - v[k];
-        as += (td * sg[k]) * sl[k];
+    if (p2_active) {
+      for (int s = s_off; s < nseg; s += SPP) {
+        const float* r = sr + s * T + w;
+        const float* td = st + s * T + w;
+        float rs = 0.f, as = 0.f;
+        for (int k = lane_g; k < H; k += LG) {
+          rs += sg[k] * r[k];
+          as += (td[k] * sg[k]) * sl[k];
+        }
+        for (int o = LG >> 1; o > 0; o >>= 1) {
+          rs += __shfl_xor(rs, o, 64);
+          as += __shfl_xor(as, o, 64);
+        }
+        if (lane_g == 0) {
+          const float vH = sv[s * T1 + w + H] * (1.f - sd[s * T + w + H - 1]);
+          const int64_t o = (b0 + s) * E + w;
+          a.ret[o] = rs + vH * a.gamma_H;
+          a.adv[o] = as;
+          psum += (double)as;
+          psq += (double)as * (double)as;
+        }
       }
-      const int64_t o = (b0 + s) * E + w;
-      a.ret[o] = rs + v[H] * a.gamma_H;
-      a.adv[o] = as;
-      psum += (double)as;
-      psq += (double)as * (double)as;
+    }
+  }
+  const double s1 = block_sum_d(psum, red);
+  const double s2 = block_sum_d(psq, red);
+  if (threadIdx.x == 0 && a.partials) {
+    a.partials[2 * blockIdx.x] = s1;
+    a.partials[2 * blockIdx.x + 1] = s2;
+  }
+}
+
+// ---------------------------------------------------- lane-per-step variant
+// For T + 1 <= 64 (every BASELINE config): no LDS, no barriers.  A segment row
+// is mapped onto TPR = 2^k >= T+1 lanes of a wave (lane t holds step t), so a
+// wave's loads of r, d, V cover 64/TPR consecutive segments — contiguous
+// memory, coalesced — and U row groups are loaded before any is used (24
+// loads in flight per lane).  Neighbouring steps come from lane shuffles:
+//   V[t+1] <- lane t+1,  d[t-1] <- lane t-1,
+//   td_t = r_t + gamma * V[t+1](1-d[t]) - V[t](1-d[t-1])    (ppo.py:387,390)
+// Windows: E == 1 (non-RNN, H == T) is a lane reduction over the row; E > 1
+// (RNN, H <= 16) sums H shuffled-down terms, lane w writing window w.
+template <int TPR>
+__global__ void __launch_bounds__(kWG)
+gae_rows_kernel(GaeWinArgs a) {
+  constexpr int RPW = 64 / TPR;           // segment rows per wave-row-group
+  constexpr int U = 8;                    // row groups in flight per wave
+  __shared__ double red[kNW];
+  const int T = a.T, T1 = T + 1, H = a.H, E = a.E;
+  const int lane = threadIdx.x & 63;
+  const int t = lane & (TPR - 1);
+  const int rsub = lane / TPR;
+  const int64_t nwaves = (int64_t)gridDim.x * kNW;
+  const int64_t wid = (int64_t)blockIdx.x * kNW + (threadIdx.x >> 6);
+  const int64_t ngroups = (a.B + RPW - 1) / RPW;
+  const float gamma = a.gamma, gamma_H = a.gamma_H;
+  // per-lane window coefficients: lane t needs g[t], l[t] (E == 1) or the
+  // whole H-table (E > 1, read from the constant tables in the loop)
+  const float gt_raw = a.gtab[t < H ? t : H - 1], lt_raw = a.ltab[t < H ? t : H - 1];
+  const float gt = t < H ? gt_raw : 0.f;
+  const float lt = t < H ? lt_raw : 0.f;
+  double psum = 0.0, psq = 0.0;
+  for (int64_t g0 = wid; g0 < ngroups; g0 += U * nwaves) {
+    float r[U], d[U], v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      // unconditional loads from clamped addresses (a predicated load makes
+      // hipcc branch and wait per element); out-of-range lanes are zeroed after
+      const int64_t row = (g0 + u * nwaves) * RPW + rsub;
+      const int64_t rr = row < a.B ? row : a.B - 1;
+      const int tc = t < T ? t : T - 1, tv = t < T1 ? t : T;
+      r[u] = a.rewards[rr * T + tc];
+      d[u] = a.dones[rr * T + tc];
+      v[u] = a.values[rr * T1 + tv];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t >= T) { r[u] = 0.f; d[u] = 0.f; }
+      if (t >= T1) v[u] = 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = (g0 + u * nwaves) * RPW + rsub;
+      const float v1 = __shfl_down(v[u], 1, TPR);       // V[t+1]
+      const float dm1 = __shfl_up(d[u], 1, TPR);        // d[t-1]
+      const float vm = t > 0 ? v[u] * (1.f - dm1) : v[u];
+      const float vm1 = v1 * (1.f - d[u]);
+      if (a.values_masked && row < a.B && t < T1) a.values_masked[row * T1 + t] = vm;
+      const float td = t < T ? (r[u] + gamma * vm1) - vm : 0.f;
+      if (E == 1) {
+        float rs = gt * r[u];
+        float as = (td * gt) * lt;
+#pragma unroll
+        for (int o = TPR >> 1; o > 0; o >>= 1) {
+          rs += __shfl_xor(rs, o, TPR);
+          as += __shfl_xor(as, o, TPR);
+        }
+        const float vH = __shfl(vm, H, TPR);              // Vm[H]
+        if (t == 0 && row < a.B) {
+          a.ret[row] = rs + vH * gamma_H;
+          a.adv[row] = as;
+          psum += (double)as;
+          psq += (double)as * (double)as;
+        }
+      } else {
+        float rs = 0.f, as = 0.f;
+        for (int k = 0; k < H; ++k) {
+          const float rk = __shfl_down(r[u], k, TPR);
+          const float tk = __shfl_down(td, k, TPR);
+          const float gk = __shfl(gt, k, TPR), lk = __shfl(lt, k, TPR);
+          rs += gk * rk;
+          as += (tk * gk) * lk;
+        }
+        const float vH = __shfl_down(vm, H, TPR);         // Vm[w+H]
+        if (t < E && row < a.B) {
+          const int64_t o = row * E + t;
+          a.ret[o] = rs + vH * gamma_H;
+          a.adv[o] = as;
+          psum += (double)as;
+          psq += (double)as * (double)as;
+        }
+      }
     }
   }
   const double s1 = block_sum_d(psum, red);
@@ -232,23 +419,63 @@ int gae_windows_max_partials(int64_t B, int T) {
   return 2048;
 }
 
-int launch_gae_windows(float* values, const float* rewards, const float* dones, int64_t B,
-                       int T, int H, const float* gtab, const float* ltab, float gamma,
-                       float gamma_H, float* adv, float* ret, double* partials,
-                       int* n_partials, hipStream_t stream) {
+int launch_gae_windows(const float* values, float* values_masked, const float* rewards,
+                       const float* dones, int64_t B, int T, int H, const float* gtab,
+                       const float* ltab, float gamma, float gamma_H, float* adv, float* ret,
+                       double* partials, int* n_partials, hipStream_t stream) {
   if (H < 1 || H > T) return set_error(SMI_E_ARG, "gae_windows: horizon must be in [1, T]");
   GaeWinArgs a;
-  a.values = values; a.rewards = rewards; a.dones = dones; a.B = B; a.T = T; a.H = H;
+  a.values = values; a.values_masked = values_masked; a.rewards = rewards; a.dones = dones;
+  a.B = B; a.T = T; a.H = H;
   a.E = T - H + 1;
-  // segment block: ~16 KB of r/d/V per block
-  int SB = 4096 / (3 * T + 1);
-  if (SB < 1) SB = 1;
+  a.gtab = gtab; a.ltab = ltab; a.gamma = gamma; a.gamma_H = gamma_H;
+  a.adv = adv; a.ret = ret; a.partials = partials;
+  if (T + 1 <= 64 && (a.E == 1 || H <= 16)) {
+    int TPR = 8;
+    while (TPR < T + 1) TPR *= 2;
+    const int64_t groups = (B + 64 / TPR - 1) / (64 / TPR);
+    int64_t g = (groups + kNW * 8 - 1) / (kNW * 8);
+    static int cap[4] = {0, 0, 0, 0};
+    const int ci = TPR == 8 ? 0 : TPR == 16 ? 1 : TPR == 32 ? 2 : 3;
+    if (!cap[ci]) {
+      cap[ci] = TPR == 8 ? resident_grid(gae_rows_kernel<8>, kWG, 0)
+              : TPR == 16 ? resident_grid(gae_rows_kernel<16>, kWG, 0)
+              : TPR == 32 ? resident_grid(gae_rows_kernel<32>, kWG, 0)
+                          : resident_grid(gae_rows_kernel<64>, kWG, 0);
+      if (cap[ci] > 2048) cap[ci] = 2048;         // <= smi_gae_windows_max_partials
+    }
+    const int grid = (int)(g < cap[ci] ? (g < 1 ? 1 : g) : cap[ci]);
+    if (TPR == 8) hipLaunchKernelGGL(gae_rows_kernel<8>, dim3(grid), dim3(kWG), 0, stream, a);
+    else if (TPR == 16) hipLaunchKernelGGL(gae_rows_kernel<16>, dim3(grid), dim3(kWG), 0, stream, a);
+    else if (TPR == 32) hipLaunchKernelGGL(gae_rows_kernel<32>, dim3(grid), dim3(kWG), 0, stream, a);
+    else hipLaunchKernelGGL(gae_rows_kernel<64>, dim3(grid), dim3(kWG), 0, stream, a);
+    if (n_partials) *n_partials = grid;
+    return check_launch("gae_rows_kernel");
+  }
+  // lanes per window: split long windows so a block pass keeps every lane busy
+  int LG = 1;
+  while (LG < 16 && 2 * LG <= H / 3) LG *= 2;
+  while (LG > 1 && (kWG / LG) < a.E) LG >>= 1;
+  if ((kWG / LG) < a.E) return set_error(SMI_E_ARG, "gae_windows: more than 256 windows per segment");
+  a.LG = LG;
+  int TPR = 1;
+  while (TPR < 64 && TPR < T + 1) TPR *= 2;
+  a.TPR = TPR;
+  // segments per block: ~1024 lane-items per pass, a multiple of 4 (16-byte
+  // aligned staging), LDS <= 40 KB so several blocks share a CU
+  int SB = (1024 + a.E * LG - 1) / (a.E * LG);
+  int max_sb = (40 * 1024 / 4 - 2 * H - 16) / (4 * T + 1);
+  const int max_pf = GAE_PF * kWG * 4 / (3 * T + 1);     // register prefetch capacity
+  if (max_sb > max_pf) max_sb = max_pf;
+  if (SB > max_sb) SB = max_sb;
+  SB = SB & ~3;
+  if (SB < 4) SB = 4;
   a.SB = SB;
   a.gtab = gtab; a.ltab = ltab; a.gamma = gamma; a.gamma_H = gamma_H;
   a.adv = adv; a.ret = ret; a.partials = partials;
   const int64_t nblk = (B + SB - 1) / SB;
   const int grid = (int)(nblk < 2048 ? nblk : 2048);
-  const size_t lds = (size_t)(SB * (3 * T + 1) + 2 * H) * 4;
+  const size_t lds = (size_t)(3 * ((SB * T + 3) & ~3) + ((SB * (T + 1) + 3) & ~3) + 2 * H) * 4;
   if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "gae_windows: T too large");
   allow_lds(gae_windows_kernel, lds);
   hipLaunchKernelGGL(gae_windows_kernel, dim3(grid), dim3(kWG), lds, stream, a);

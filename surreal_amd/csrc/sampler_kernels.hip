@@ -179,22 +179,48 @@ int launch_mt_randint(uint32_t* st, int64_t n, int64_t batch, int64_t* out, hipS
 }
 
 // ------------------------------------------------------------ row gather
+// out[i][:] = table[idx[i]][:].  Output-ordered (coalesced stores); 16-byte
+// elements when rows are float4-aligned, 32-bit index arithmetic when the
+// output fits (a 64-bit divide per element costs more than the load), and four
+// independent loads in flight per thread.
+template <typename V, typename I>
+__device__ __forceinline__ void gather_body(const V* __restrict__ table, I cols,
+                                            const int64_t* __restrict__ idx, I total,
+                                            V* __restrict__ out) {
+  const I stride = (I)gridDim.x * kWG;
+  I e = (I)blockIdx.x * kWG + threadIdx.x;
+  for (; e + 3 * stride < total; e += 4 * stride) {
+    V v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const I f = e + u * stride;
+      const I i = f / cols, c = f - i * cols;
+      v[u] = table[idx[i] * (int64_t)cols + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) out[e + u * stride] = v[u];
+  }
+  for (; e < total; e += stride) {
+    const I i = e / cols, c = e - i * cols;
+    out[e] = table[idx[i] * (int64_t)cols + c];
+  }
+}
+
 __global__ void __launch_bounds__(kWG)
 gather_rows_kernel(const float* __restrict__ table, int64_t cols, const int64_t* __restrict__ idx,
                    int64_t batch, float* __restrict__ out) {
-  if ((cols & 3) == 0) {
-    const int64_t c4 = cols >> 2;
-    const int64_t total = batch * c4;
-    for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < total; e += (int64_t)gridDim.x * kWG) {
-      const int64_t i = e / c4, c = e - i * c4;
-      reinterpret_cast<float4*>(out)[e] = reinterpret_cast<const float4*>(table + idx[i] * cols)[c];
-    }
+  const bool v4 = (cols & 3) == 0 &&
+                  ((reinterpret_cast<uintptr_t>(table) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  const int64_t c = v4 ? cols >> 2 : cols;
+  const int64_t total = batch * c;
+  if (total < ((int64_t)1 << 31)) {
+    if (v4) gather_body<float4, uint32_t>(reinterpret_cast<const float4*>(table), (uint32_t)c, idx,
+                                          (uint32_t)total, reinterpret_cast<float4*>(out));
+    else gather_body<float, uint32_t>(table, (uint32_t)c, idx, (uint32_t)total, out);
   } else {
-    const int64_t total = batch * cols;
-    for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < total; e += (int64_t)gridDim.x * kWG) {
-      const int64_t i = e / cols, c = e - i * cols;
-      out[e] = table[idx[i] * cols + c];
-    }
+    if (v4) gather_body<float4, int64_t>(reinterpret_cast<const float4*>(table), c, idx, total,
+                                         reinterpret_cast<float4*>(out));
+    else gather_body<float, int64_t>(table, c, idx, total, out);
   }
 }
 
@@ -203,7 +229,9 @@ int launch_gather_rows(const float* table, int64_t cols, const int64_t* idx, int
   const int64_t work = batch * ((cols & 3) == 0 ? cols / 4 : cols);
   if (work <= 0) return SMI_OK;
   int64_t g = (work + kWG - 1) / kWG;
+  g = (g + 3) / 4;
   if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((int)g), dim3(kWG), 0, s, table, cols, idx, batch, out);
   return check_launch("gather_rows_kernel");
 }

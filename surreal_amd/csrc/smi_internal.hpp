@@ -19,6 +19,20 @@ inline void allow_lds(K kernel, size_t bytes) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// Number of workgroups of `kernel` resident on the whole device at once
+// (occupancy x CUs): the grid of a grid-stride streaming kernel, so every
+// workgroup runs in the first and only round (no tail round at 60 % fill).
+template <typename K>
+inline int resident_grid(K kernel, int threads, size_t lds) {
+  int dev = 0, cus = 256, per = 1;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kernel),
+                                                     threads, lds);
+  if (per < 1) per = 1;
+  return cus * per;
+}
+
 int64_t fused_lds_bytes(int B, int D, int H1, int H2, int A, int cH1, int cH2);
 
 int launch_critic_gae(const float* critic_params, int D, int H1, int H2, int use_zf,
@@ -28,7 +42,7 @@ int launch_critic_gae(const float* critic_params, int D, int H1, int H2, int use
                       const float* gtab, const float* ltab, float gamma, float gamma_T,
                       float* values, float* adv, float* ret, hipStream_t stream);
 int gae_windows_max_partials(int64_t B, int T);
-int launch_gae_windows(float* values, const float* rewards, const float* dones, int64_t B,
+int launch_gae_windows(const float* values, float* values_masked, const float* rewards, const float* dones, int64_t B,
                        int T, int H, const float* gtab, const float* ltab, float gamma,
                        float gamma_H, float* adv, float* ret, double* partials,
                        int* n_partials, hipStream_t stream);

@@ -1,0 +1,92 @@
+"""The real data-parallel PPOLearner.learn() (dp=TorchDistAllReduce) in two
+processes that share cuda:0 and exchange over torch.distributed (gloo here:
+RCCL refuses two ranks on one GPU; on a multi-GPU node the same code runs over
+'nccl' = RCCL/xGMI, as bench.py does).  Every rank must end with bit-identical
+parameters, equal to the CPU oracle's learn() on the concatenated global batch
+(tolerances as in test_gpu_ppo.py)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B_LOC, T, D, A = 24, 10, 17, 6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, outdir):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from surreal_amd import synthetic
+    from surreal_amd.learner import PPOLearner, TorchDistAllReduce
+    from tests.helpers import env_config, ppo_config
+    lc = ppo_config(B=B_LOC, T=T, mode=mode, use_z_filter=True)
+    learner = PPOLearner(lc, env_config(D, A), seed=21, device='cuda:0', dp=TorchDistAllReduce())
+    init = {'actor': learner.model.actor.flat.cpu(), 'critic': learner.model.critic.flat.cpu()}
+    res = []
+    for it in range(2):
+        full = synthetic.ppo_batch(B_LOC * world, T, D, A, seed=500 + it)
+        dev = synthetic.to_device(full, 'cuda:0')
+        lo, hi = rank * B_LOC, (rank + 1) * B_LOC
+
+        def cut(x):
+            if x is None:
+                return None
+            if isinstance(x, dict):
+                return {k: cut(v) for k, v in x.items()}
+            if isinstance(x, list):
+                return [cut(v) for v in x]
+            return x[lo:hi].contiguous()
+        learner.learn(cut(dev))
+        st = learner.last_stats()
+        res.append({'actor': learner.model.actor.flat.cpu(), 'critic': learner.model.critic.flat.cpu(),
+                    'zsum': learner.model.z_filter.running_sum.cpu(), 'stats': st})
+    torch.save({'init': init, 'res': res}, os.path.join(outdir, f'rank{rank}.pt'))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('mode', ['adapt', 'clip'])
+def test_two_process_dp_learn_matches_oracle(mode):
+    from oracle import ppo_ref as R
+    from surreal_amd import synthetic
+    from tests.helpers import max_rel_err, oracle_batch, ppo_config
+    from tests.test_gpu_ppo import _compare_params
+    world = 2
+    with tempfile.TemporaryDirectory() as outdir:
+        mp.spawn(_worker, args=(world, _free_port(), mode, outdir), nprocs=world, join=True)
+        out = [torch.load(os.path.join(outdir, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+    ref = R.PPOLearnerRef(ppo_config(B=B_LOC * world, T=T, mode=mode, use_z_filter=True), D, A)
+    ref.model.actor.load_flat(out[0]['init']['actor'])
+    ref.model.critic.load_flat(out[0]['init']['critic'])
+    ref.ref_target_model.actor.load_flat(out[0]['init']['actor'])
+    ref.ref_target_model.critic.load_flat(out[0]['init']['critic'])
+    report = {}
+    for it in range(2):
+        rstats = ref.learn(oracle_batch(synthetic.ppo_batch(B_LOC * world, T, D, A, seed=500 + it)))
+        r0, r1 = out[0]['res'][it], out[1]['res'][it]
+        assert torch.equal(r0['actor'], r1['actor']) and torch.equal(r0['critic'], r1['critic'])
+        assert torch.equal(r0['zsum'], r1['zsum'])
+        assert r0['stats']['epochs_run'] == rstats['epochs_run']
+        for k in ('_surr_loss', '_pol_kl', '_entropy', '_val_loss', 'grad_norm_actor',
+                  'grad_norm_critic'):
+            assert abs(r0['stats'][k] - rstats[k]) <= 1e-4 * abs(rstats[k]) + 1e-6, (it, k)
+        _compare_params(f'actor{it}', r0['actor'], ref.model.actor.flat(), 3e-4,
+                        rstats['epochs_run'], report)
+        _compare_params(f'critic{it}', r0['critic'], ref.model.critic.flat(), 3e-4, 10, report)
+        assert max_rel_err(r0['zsum'], ref.model.z_filter.running_sum) < 1e-5
+    print('two-process dp report:', report)

@@ -163,7 +163,7 @@ def _gae_windows_gpu(values, rewards, dones, gamma, lam, T, H):
     import ctypes
     n = ctypes.c_int(0)
     gtd, ltd = gt.to(DEV), lt.to(DEV)       # keep the device tables alive across the call
-    L.call('smi_gae_windows', L.ptr(vd), L.ptr(rd), L.ptr(dd), B, T, H, L.ptr(gtd),
+    L.call('smi_gae_windows', L.ptr(vd), L.ptr(vd), L.ptr(rd), L.ptr(dd), B, T, H, L.ptr(gtd),
            L.ptr(ltd), float(gamma), float(gamma ** H), L.ptr(adv), L.ptr(ret), L.ptr(part),
            ctypes.byref(n), st())
     return adv.cpu(), ret.cpu(), vd.cpu(), part[:2 * n.value].cpu().view(-1, 2)
