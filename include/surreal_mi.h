@@ -267,6 +267,114 @@ int64_t smi_ppo_xbuf_floats(int obs_dim, int h1, int h2, int act_dim, int critic
 int smi_ppo_epoch_grad(const smi_ppo_args* args, int epoch, void* stream);
 int smi_ppo_epoch_apply(const smi_ppo_args* args, int epoch, void* stream);
 
+/* ------------------------------------------- PPO: LSTM policy (RNN branch) */
+/* PPOLearner._optimize with if_rnn_policy (surreal/learner/ppo.py:487-586,
+ * 389-406; PPOModel with the nn.LSTM stem, ppo_net.py:137-152,253-315):
+ * obs -> ZFilter -> LSTM(h0, c0) -> actor / critic MLP heads, on the MFMA GEMM
+ * engine and persistent LSTM sequence kernels (one workgroup per 16 segments,
+ * all steps in one launch).  Activations are kept time-major ([step][segment]).
+ * One learn() is a fixed sequence of phases (SMI_RNN_PH_*) issued by the host
+ * in the same order on every rank; between some phases a data-parallel caller
+ * all-reduces (SUM) the buffer named in the phase table (include order):
+ *   GAE              -> all-reduce moments (double[3], smi_ppo_rnn_args.moments)
+ *   PREP             (reference-policy forward)
+ *   POLICY_FWD(e)    e = 0..epoch_policy: forward + loss sums -> all-reduce pstat
+ *   POLICY_DECIDE(e) KL early stop / adapt coefficient / statistics from pstat
+ *   POLICY_BWD(e)    e < epoch_policy: backward -> all-reduce actor grads
+ *                    (xbuf[0 : nA], nA = actor params + lstm params)
+ *   POLICY_APPLY(e)  clip_grad_norm_ + Adam over [actor | lstm]
+ *   VALUE_GRAD(e)    e = 0..epoch_baseline-1 -> all-reduce critic grads
+ *                    (xbuf[nA : nA + nC], nC = critic params + lstm params)
+ *   VALUE_APPLY(e)   clip_grad_norm_ + Adam over [critic | lstm]
+ *   ZSTATS           column sums of obs_iter -> all-reduce zbuf (value sums of
+ *                    the last value epoch + 2D ZFilter sums, doubles)
+ *   ZAPPLY           z_update from the (reduced) column sums
+ * The KL early stop (ppo.py:556) and the adapt penalty branch (ppo.py:275) are
+ * decided on device from the (global) sums; skipped phases are no-ops, so the
+ * host never synchronises.  The LSTM parameters belong to both optimizers
+ * (ppo_net.py:202-224): actor_m/v and critic_m/v each cover [head | lstm].
+ * Flat LSTM layout (nn.LSTM parameter order): W_ih[4H][D] W_hh[4H][H] b_ih[4H]
+ * b_hh[4H], gates in torch order (i, f, g, o). */
+#define SMI_RNN_PH_GAE           0
+#define SMI_RNN_PH_PREP          1
+#define SMI_RNN_PH_POLICY_FWD    2
+#define SMI_RNN_PH_POLICY_BWD    3
+#define SMI_RNN_PH_POLICY_APPLY  4
+#define SMI_RNN_PH_VALUE_GRAD    5
+#define SMI_RNN_PH_VALUE_APPLY   6
+#define SMI_RNN_PH_ZSTATS        7
+#define SMI_RNN_PH_ZAPPLY        8
+#define SMI_RNN_PH_POLICY_DECIDE 9
+
+typedef struct smi_ppo_rnn_args {
+  /* dims (local batch) */
+  int B, T, horizon;                 /* segments on this rank, n_step, horizon */
+  int obs_dim, rnn_hidden;           /* D, H (one LSTM layer)                 */
+  int h1, h2, act_dim;               /* actor head                            */
+  int critic_h1, critic_h2;
+  int epoch_policy, epoch_baseline;
+  int mode, norm_adv, clip_actor_grad, clip_critic_grad, use_zf;
+  int64_t B_global;                  /* segments over all ranks               */
+  /* batch as MultistepAggregatorWithInfo emits it (batch-major, fp32) */
+  const float* obs;        /* [B][T][D]   */
+  const float* obs_next;   /* [B][1][D]   */
+  const float* actions;    /* [B][T][A]   */
+  const float* rewards;    /* [B][T]      */
+  const float* dones;      /* [B][T]      */
+  const float* behave;     /* [B][T][2A]  */
+  const float* h0;         /* [B][H]  onetime_infos[0] (layer 0) */
+  const float* c0;         /* [B][H]  onetime_infos[1]           */
+  /* parameters */
+  float* lstm; float* actor; float* critic;
+  const float* ref_lstm; const float* ref_actor;
+  float* zf_sum; float* zf_sumsq; float* zf_count;     /* updated by ZAPPLY */
+  const float* rzf_sum; const float* rzf_sumsq; const float* rzf_count;
+  float zf_eps;
+  /* Adam state over [head | lstm] for each optimizer */
+  float* actor_m; float* actor_v; float* critic_m; float* critic_v;
+  int* actor_step; int* critic_step;
+  const float* hyper;                /* SMI_HYP_* */
+  const float* gamma_tab; const float* lam_tab;   /* torch.pow tables, [T] */
+  float gamma, gamma_H;
+  double kl_target;
+  float kl_cutoff_coeff, actor_max_norm, critic_max_norm, actor_wd, critic_wd;
+  float beta1, beta2, adam_eps;
+  /* outputs */
+  float* stats;                      /* [SMI_ST_COUNT] */
+  float* kl_record; int* kl_count; int kl_capacity;
+  /* exchange buffers (all-reduced by a data-parallel caller) */
+  double* moments;                   /* [3] advantage (sum, sumsq, n) */
+  double* pstat;                     /* [SMI_RNN_PSTAT] policy sums   */
+  float* xbuf;                       /* [smi_ppo_rnn_xbuf_floats]: actor grads [actor | lstm]
+                                        then critic grads [critic | lstm]                    */
+  double* zbuf;                      /* [5 + 2*D] value sums | ZFilter column sums            */
+  /* device scratch, smi_ppo_rnn_scratch_bytes() */
+  void* scratch; int64_t scratch_bytes;
+} smi_ppo_rnn_args;
+
+#define SMI_RNN_PSTAT 16
+int64_t smi_ppo_rnn_scratch_bytes(int B, int T, int horizon, int obs_dim, int rnn_hidden,
+                                  int h1, int h2, int act_dim, int critic_h1, int critic_h2);
+int64_t smi_ppo_rnn_xbuf_floats(int obs_dim, int rnn_hidden, int h1, int h2, int act_dim,
+                                int critic_h1, int critic_h2);
+int64_t smi_lstm_param_count(int in_dim, int hidden);
+int smi_ppo_rnn_phase(const smi_ppo_rnn_args* args, int phase, int epoch, void* stream);
+
+/* LSTM sequence ops (nn.LSTM, one layer, batch_first semantics with
+ * time-major buffers) — the building blocks of the phases above, exported for
+ * tests and other callers:
+ *   xproj [S][B][4H] = x W_ih^T + b_ih   (smi_linear_forward)
+ *   forward: gates = xproj[t] + h_{t-1} W_hh^T + b_hh; c,h updates (i,f,g,o);
+ *            hbuf[0] = h0, hbuf[t+1] = h_t ([S+1][B][H]); cbuf likewise and
+ *            gates_act [S][B][4H] (activated) when non-NULL.
+ *   backward: dgates [S][B][4H] from dh [S][B][H] (dL/dh_t from the heads),
+ *            given gates_act and cbuf of the forward (BPTT through c and h). */
+int smi_lstm_forward(const float* xproj, const float* w_hh, const float* b_hh,
+                     const float* h0, const float* c0, int S, int B, int H,
+                     float* hbuf, float* cbuf, float* gates_act, void* stream);
+int smi_lstm_backward(const float* dh, const float* gates_act, const float* cbuf,
+                      const float* w_hh, int S, int B, int H, float* dgates, void* stream);
+
 /* running_sum += sum_in, running_sumsq += sumsq_in, count += rows — the
  * data-parallel z_update after the column statistics were all-reduced. */
 int smi_zfilter_accumulate(const float* sum_in, const float* sumsq_in, int dim, float rows,

@@ -56,6 +56,39 @@ class PPOArgs(ctypes.Structure):
     ]
 
 
+class RNNArgs(ctypes.Structure):
+    """struct smi_ppo_rnn_args (include/surreal_mi.h)."""
+    _fields_ = [
+        ('B', c_int), ('T', c_int), ('horizon', c_int), ('obs_dim', c_int), ('rnn_hidden', c_int),
+        ('h1', c_int), ('h2', c_int), ('act_dim', c_int), ('critic_h1', c_int), ('critic_h2', c_int),
+        ('epoch_policy', c_int), ('epoch_baseline', c_int),
+        ('mode', c_int), ('norm_adv', c_int), ('clip_actor_grad', c_int), ('clip_critic_grad', c_int),
+        ('use_zf', c_int),
+        ('B_global', c_i64),
+        ('obs', P), ('obs_next', P), ('actions', P), ('rewards', P), ('dones', P), ('behave', P),
+        ('h0', P), ('c0', P),
+        ('lstm', P), ('actor', P), ('critic', P), ('ref_lstm', P), ('ref_actor', P),
+        ('zf_sum', P), ('zf_sumsq', P), ('zf_count', P),
+        ('rzf_sum', P), ('rzf_sumsq', P), ('rzf_count', P),
+        ('zf_eps', c_f32),
+        ('actor_m', P), ('actor_v', P), ('critic_m', P), ('critic_v', P),
+        ('actor_step', P), ('critic_step', P),
+        ('hyper', P), ('gamma_tab', P), ('lam_tab', P),
+        ('gamma', c_f32), ('gamma_H', c_f32),
+        ('kl_target', c_f64),
+        ('kl_cutoff_coeff', c_f32), ('actor_max_norm', c_f32), ('critic_max_norm', c_f32),
+        ('actor_wd', c_f32), ('critic_wd', c_f32),
+        ('beta1', c_f32), ('beta2', c_f32), ('adam_eps', c_f32),
+        ('stats', P), ('kl_record', P), ('kl_count', P), ('kl_capacity', c_int),
+        ('moments', P), ('pstat', P), ('xbuf', P), ('zbuf', P),
+        ('scratch', P), ('scratch_bytes', c_i64),
+    ]
+
+
+RNN_PH_GAE, RNN_PH_PREP, RNN_PH_POLICY_FWD, RNN_PH_POLICY_BWD, RNN_PH_POLICY_APPLY, \
+    RNN_PH_VALUE_GRAD, RNN_PH_VALUE_APPLY, RNN_PH_ZSTATS, RNN_PH_ZAPPLY, RNN_PH_POLICY_DECIDE = range(10)
+RNN_PSTAT = 16
+
 _SIGS = {
     'smi_version': (c_int, []),
     'smi_last_error': (ctypes.c_char_p, []),
@@ -100,6 +133,12 @@ _SIGS = {
     'smi_mt_randint_host': (c_int, [P, c_i64, c_i64, P]),
     'smi_mt_randint': (c_int, [P, c_i64, c_i64, P, P]),
     'smi_gather_rows': (c_int, [P, c_i64, P, c_i64, P, P]),
+    'smi_lstm_param_count': (c_i64, [c_int, c_int]),
+    'smi_ppo_rnn_scratch_bytes': (c_i64, [c_int] * 10),
+    'smi_ppo_rnn_xbuf_floats': (c_i64, [c_int] * 7),
+    'smi_ppo_rnn_phase': (c_int, [ctypes.POINTER(RNNArgs), c_int, c_int, P]),
+    'smi_lstm_forward': (c_int, [P, P, P, P, P, c_int, c_int, c_int, P, P, P, P]),
+    'smi_lstm_backward': (c_int, [P, P, P, P, c_int, c_int, c_int, P, P]),
 }
 
 _lib = None

@@ -27,6 +27,7 @@ int check_launch(const char* what) {
 // caller-registered device workspace (smi_set_workspace)
 static void* g_ws = nullptr;
 static int64_t g_ws_bytes = 0;
+int64_t smi_workspace_floats() { return g_ws ? g_ws_bytes / 4 : 0; }
 float* workspace_f32(int64_t nfloats) {
   if (!g_ws || nfloats * 4 > g_ws_bytes) return nullptr;
   return static_cast<float*>(g_ws);
@@ -47,12 +48,6 @@ int launch_mlp_forward(const float*, int, int, int, int, int, int, const float*,
 int launch_moments(const float*, int64_t, const double*, int, double*, hipStream_t);
 int launch_adam_clip(float*, const float*, float*, float*, int64_t, int*, const float*, float,
                      float, float, float, float, float, const int*, float*, hipStream_t);
-int launch_linear_fwd(const float*, int64_t, int, int, const float*, int64_t, const float*, int,
-                      int, float*, int64_t, hipStream_t);
-int launch_linear_bwd_dx(const float*, int64_t, int, int, const float*, int64_t, int,
-                         const float*, int64_t, float*, int64_t, hipStream_t);
-int launch_linear_bwd_dw(const float*, int64_t, int, int, const float*, int64_t, int, float*,
-                         int64_t, float*, int, hipStream_t);
 int launch_mse_grad(const float*, int64_t, const float*, int64_t, float*, float*, hipStream_t);
 int launch_neg_mean_grad(const float*, int64_t, int64_t, float*, float*, hipStream_t);
 int launch_tanh_backward(const float*, int64_t, const float*, int64_t, int64_t, int, float*,
@@ -90,7 +85,7 @@ int smi_set_workspace(void* dev_ptr, int64_t bytes) {
   g_ws_bytes = bytes;
   return SMI_OK;
 }
-int64_t smi_workspace_bytes(void) { return (int64_t)4 << 20; }
+int64_t smi_workspace_bytes(void) { return (int64_t)64 << 20; }
 
 int64_t smi_mlp_param_count(int in_dim, int h1, int h2, int out_dim, int with_log_var) {
   return mlp_layout(in_dim, h1, h2, out_dim, with_log_var).fcount;
@@ -344,6 +339,61 @@ int smi_gather_rows(const float* table, int64_t cols, const int64_t* idx, int64_
                     float* out, void* stream) {
   REQUIRE(table && idx && out && cols > 0 && batch >= 0, "gather_rows: bad args");
   return launch_gather_rows(table, cols, idx, batch, out, SMI_STREAM(stream));
+}
+
+
+/* ------------------------------------------------ PPO: LSTM policy path */
+int64_t smi_lstm_param_count(int in_dim, int hidden) {
+  return (int64_t)4 * hidden * in_dim + (int64_t)4 * hidden * hidden + 8 * (int64_t)hidden;
+}
+
+int64_t smi_ppo_rnn_scratch_bytes(int B, int T, int horizon, int obs_dim, int rnn_hidden, int h1,
+                                  int h2, int act_dim, int critic_h1, int critic_h2) {
+  return ppo_rnn_scratch_bytes(B, T, horizon, obs_dim, rnn_hidden, h1, h2, act_dim, critic_h1,
+                               critic_h2);
+}
+
+int64_t smi_ppo_rnn_xbuf_floats(int obs_dim, int rnn_hidden, int h1, int h2, int act_dim,
+                                int critic_h1, int critic_h2) {
+  const int64_t nl = smi_lstm_param_count(obs_dim, rnn_hidden);
+  return mlp_layout(rnn_hidden, h1, h2, act_dim, 1).fcount +
+         mlp_layout(rnn_hidden, critic_h1, critic_h2, 1, 0).fcount + 2 * nl;
+}
+
+int smi_ppo_rnn_phase(const smi_ppo_rnn_args* a, int phase, int epoch, void* stream) {
+  REQUIRE(a, "ppo_rnn: null args");
+  REQUIRE(a->B >= 1 && a->T >= 1 && a->horizon >= 1 && a->horizon <= a->T, "ppo_rnn: bad B/T/horizon");
+  REQUIRE(a->obs_dim >= 1 && a->obs_dim <= 128, "ppo_rnn: obs_dim must be in [1, 128]");
+  REQUIRE(a->rnn_hidden >= 1 && a->rnn_hidden <= 256, "ppo_rnn: rnn_hidden must be in [1, 256]");
+  REQUIRE(a->act_dim >= 1 && a->act_dim <= 32, "ppo_rnn: act_dim must be in [1, 32]");
+  REQUIRE(a->h1 >= 1 && a->h2 >= 1 && a->critic_h1 >= 1 && a->critic_h2 >= 1, "ppo_rnn: bad hidden sizes");
+  REQUIRE(a->obs && a->obs_next && a->actions && a->rewards && a->dones && a->behave && a->h0 &&
+          a->c0, "ppo_rnn: null batch pointer");
+  REQUIRE(a->lstm && a->actor && a->critic && a->ref_lstm && a->ref_actor, "ppo_rnn: null params");
+  REQUIRE(a->actor_m && a->actor_v && a->critic_m && a->critic_v && a->actor_step &&
+          a->critic_step && a->hyper && a->gamma_tab && a->lam_tab, "ppo_rnn: null optimizer state");
+  REQUIRE(a->stats && a->kl_record && a->kl_count && a->moments && a->pstat && a->xbuf && a->zbuf &&
+          a->scratch, "ppo_rnn: null output/exchange buffer");
+  REQUIRE(!a->use_zf || (a->zf_sum && a->zf_sumsq && a->zf_count && a->rzf_sum && a->rzf_sumsq &&
+                         a->rzf_count), "ppo_rnn: zfilter buffers required");
+  REQUIRE(a->B_global >= a->B, "ppo_rnn: B_global < B");
+  return ppo_rnn_phase(*a, phase, epoch, SMI_STREAM(stream));
+}
+
+int smi_lstm_forward(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
+                     const float* c0, int S, int B, int H, float* hbuf, float* cbuf,
+                     float* gates_act, void* stream) {
+  REQUIRE(xproj && w_hh && b_hh && h0 && c0 && hbuf && S >= 0 && B >= 0 && H >= 1,
+          "lstm_forward: bad args");
+  return launch_lstm_fwd(xproj, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates_act,
+                         SMI_STREAM(stream), nullptr);
+}
+
+int smi_lstm_backward(const float* dh, const float* gates_act, const float* cbuf,
+                      const float* w_hh, int S, int B, int H, float* dgates, void* stream) {
+  REQUIRE(dh && gates_act && cbuf && w_hh && dgates && S >= 0 && B >= 0 && H >= 1,
+          "lstm_backward: bad args");
+  return launch_lstm_bwd(dh, gates_act, cbuf, w_hh, S, B, H, dgates, SMI_STREAM(stream), nullptr);
 }
 
 }  // extern "C"

@@ -1,21 +1,35 @@
 // linear_kernels.hip — layer-by-layer fp32 MFMA GEMMs for networks whose
-// parameters do not fit one CU's LDS (DDPG actor 300x200 / critic 400x300,
-// builders.py:35-84; PPO heads 300x200).  Activations live in HBM (L2-resident
-// at learner batch sizes); every dense layer's forward, input-gradient and
-// weight-gradient are the same LDS-tiled GEMM with a different operand view
-// and epilogue:
+// parameters do not fit one CU's LDS (PPO heads 300x200 over B*E rows, the
+// LSTM input projection and weight gradients, DDPG actor 300x200 / critic
+// 400x300; builders.py:35-175, ppo_net.py:137-152).  Every dense layer's
+// forward, input-gradient and weight-gradient is the same LDS-tiled GEMM with
+// a different operand view and epilogue:
 //   fwd:  Y[m][n]  = act(b[n] + sum_k X[m][k] W[n][k])
 //   dX:   dX[m][k] = mask(Xact[m][k] > 0) * sum_n dY[m][n] W[n][k]
-//   dW:   dW[n][k] (+)= sum_m dY[m][n] X[m][k]       (reduction over rows;
-//         one workgroup owns an output tile: deterministic, no atomics)
-// Tiles 64x64, K-steps of 16 staged through LDS, 4 waves x (16 rows x 64 cols)
-// with v_mfma_f32_16x16x4_f32.
+//   dW:   dW[n][k] (+)= sum_m dY[m][n] X[m][k];  db[n] (+)= sum_m dY[m][n]
+//         (db rides along as an extra all-ones column of X).  The reduction
+//         over rows is split into KSPLIT slabs (dW is a 300x100 output over
+//         ~20k rows: 10 tiles alone would leave 246 CUs idle); slab partials
+//         go to the workspace and a fixed-order reducer adds them
+//         (deterministic, no atomics).
+// Tile 64x64, K-steps of 32, 256 threads: wave w owns rows [16w, 16w+16) x 64
+// columns (4 accumulators of v_mfma_f32_16x16x4_f32).  The next K-step is
+// loaded into registers while the current one runs on the MFMA pipe (LDS
+// double buffer, one barrier per K-step).  LDS images follow the operand's
+// contiguous dimension (leading dims 36 / 80: conflict-free MFMA operand
+// reads and contiguous-dimension stores).  Global loads use clamped addresses
+// and are zeroed afterwards (no predicated loads: see cdna_hip_programming.md).
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
 
 namespace smi {
 
 enum { EPI_FWD = 0, EPI_DX = 1, EPI_DW = 2 };
+
+constexpr int GBM = 64, GBN = 64, GBK = 32;
+constexpr int LD_KC = 36;     // [row][k] images (k contiguous)
+constexpr int LD_RC = 80;     // [k][row] images (row contiguous)
+constexpr int G_STAGE = 2560; // floats per operand image per stage
 
 struct GemmArgs {
   int M, N, K;
@@ -26,40 +40,109 @@ struct GemmArgs {
   const float* bias;              // EPI_FWD
   int act;                        // EPI_FWD: ACT_*
   const float* mask; int64_t ldm; // EPI_DX: zero where mask[m*ldm+n] <= 0 (may be null)
-  int accumulate;                 // EPI_DW: C += result
+  int accumulate;                 // EPI_DW (no split): C += result
+  int ones_col;                   // EPI_DW: B(k, ones_col) == 1 (bias gradient column), -1 none
+  float* bias_out;                // EPI_DW: column ones_col goes to bias_out[m]
+  int kchunk;                     // K range of blockIdx.z: [z*kchunk, min(K, (z+1)*kchunk))
+  float* part;                    // split-K partials [gridDim.z][M][N] (nullptr: no split)
+  const int* skip;                // device flag: nonzero -> no-op (early stop)
 };
 
-template <int EPI>
+// operand loader: 2048 elements (64 x 32) per tile, 8 per thread
+// rows >= rdata read as zero (except the all-ones column); rdata <= rmax
+template <bool KCONTIG>
+__device__ __forceinline__ void gemm_load(const float* __restrict__ P, int64_t rs, int64_t cs,
+                                          int r0, int rdata, int k0, int kmax, int ones_col,
+                                          float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int idx = threadIdx.x + j * kWG;
+    const int r = KCONTIG ? (idx >> 5) : (idx & 63);
+    const int k = KCONTIG ? (idx & 31) : (idx >> 6);
+    const int rr = r0 + r, kk = k0 + k;
+    const int rc = rr < rdata ? rr : rdata - 1;
+    const int kc = kk < kmax ? kk : kmax - 1;
+    const float x = P[(int64_t)rc * rs + (int64_t)kc * cs];
+    v[j] = (rr < rdata && kk < kmax) ? x : 0.f;
+    if (ones_col >= 0 && rr == ones_col && kk < kmax) v[j] = 1.f;
+  }
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ void gemm_store(float* __restrict__ S, const float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int idx = threadIdx.x + j * kWG;
+    const int r = KCONTIG ? (idx >> 5) : (idx & 63);
+    const int k = KCONTIG ? (idx & 31) : (idx >> 6);
+    if (KCONTIG) S[r * LD_KC + k] = v[j];
+    else S[k * LD_RC + r] = v[j];
+  }
+}
+
+// A is viewed with rows = m; B with rows = n (its "row" is the output column).
+template <int EPI, bool AK, bool BK>
 __global__ void __launch_bounds__(kWG)
 gemm_kernel(GemmArgs g) {
-  __shared__ float As[64][17];
-  __shared__ float Bs[16][68];
+  if (g.skip && g.skip[0] != 0) return;
+  __shared__ __attribute__((aligned(16))) float sA[2][G_STAGE];
+  __shared__ __attribute__((aligned(16))) float sB[2][G_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
-  f32x4 acc[4];
+  const int m0 = blockIdx.x * GBM, n0 = blockIdx.y * GBN;
+  const int kb = blockIdx.z * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  const int nk = (ke - kb + GBK - 1) / GBK;
+  // B(k, n): viewed as rows n (B "row" stride b_cs), k stride b_rs
+  f32x4 tot[4];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < g.K; k0 += 16) {
+  for (int c = 0; c < 4; ++c) tot[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float va[8], vb[8];
+  if (nk > 0) {
+    gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb, ke, -1, va);
+    gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, g.ones_col >= 0 ? g.ones_col : g.N, kb, ke, g.ones_col, vb);
+    gemm_store<AK>(sA[0], va);
+    gemm_store<BK>(sB[0], vb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb + (kt + 1) * GBK, ke, -1, va);
+      gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, g.ones_col >= 0 ? g.ones_col : g.N, kb + (kt + 1) * GBK,
+                    ke, g.ones_col, vb);
+    }
+    const float* As = sA[cur];
+    const float* Bs = sB[cur];
+    const int ar = wave * 16 + li;
+    // two-level accumulation: each K-step (32 products per output) starts a
+    // fresh MFMA chain that is then added to the running sums — fp32 error of
+    // a 32-term chain plus an nk-term chain instead of one 32*nk-term chain
+    f32x4 acc[4];
 #pragma unroll
-    for (int e = tid; e < 64 * 16; e += kWG) {
-      const int r = e >> 4, kk = e & 15;
-      const int m = m0 + r, k = k0 + kk;
-      As[r][kk] = (m < g.M && k < g.K) ? g.A[(int64_t)m * g.a_rs + (int64_t)k * g.a_cs] : 0.f;
+    for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < GBK; ks += 8) {
+      float a0, a1, b0[4], b1[4];
+      const int k0 = ks + lk, k1 = ks + 4 + lk;
+      a0 = AK ? As[ar * LD_KC + k0] : As[k0 * LD_RC + ar];
+      a1 = AK ? As[ar * LD_KC + k1] : As[k1 * LD_RC + ar];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int n = c * 16 + li;
+        b0[c] = BK ? Bs[n * LD_KC + k0] : Bs[k0 * LD_RC + n];
+        b1[c] = BK ? Bs[n * LD_KC + k1] : Bs[k1 * LD_RC + n];
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = mfma4(a0, b0[c], acc[c]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = mfma4(a1, b1[c], acc[c]);
     }
 #pragma unroll
-    for (int e = tid; e < 16 * 64; e += kWG) {
-      const int kk = e >> 6, c = e & 63;
-      const int k = k0 + kk, n = n0 + c;
-      Bs[kk][c] = (k < g.K && n < g.N) ? g.B[(int64_t)k * g.b_rs + (int64_t)n * g.b_cs] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < 16; ks += 4) {
-      const float a = As[wave * 16 + li][ks + lk];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[ks + lk][c * 16 + li], acc[c], 0, 0, 0);
+    for (int c = 0; c < 4; ++c) tot[c] += acc[c];
+    if (kt + 1 < nk) {
+      gemm_store<AK>(sA[cur ^ 1], va);
+      gemm_store<BK>(sB[cur ^ 1], vb);
     }
     __syncthreads();
   }
@@ -71,84 +154,137 @@ gemm_kernel(GemmArgs g) {
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wave * 16 + lk * 4 + i;
       if (m >= g.M) continue;
-      float v = acc[c][i];
-      float* dst = g.C + (int64_t)m * g.ldc + n;
+      float v = tot[c][i];
       if constexpr (EPI == EPI_FWD) {
         v += g.bias ? g.bias[n] : 0.f;
         if (g.act == ACT_RELU) v = v > 0.f ? v : 0.f;
         else if (g.act == ACT_TANH) v = tanhf(v);
-        *dst = v;
+        g.C[(int64_t)m * g.ldc + n] = v;
       } else if constexpr (EPI == EPI_DX) {
         if (g.mask) v = g.mask[(int64_t)m * g.ldm + n] > 0.f ? v : 0.f;
-        *dst = v;
+        g.C[(int64_t)m * g.ldc + n] = v;
       } else {
-        *dst = g.accumulate ? *dst + v : v;
+        if (g.part) {
+          g.part[((int64_t)blockIdx.z * g.M + m) * g.N + n] = v;
+        } else if (n == g.ones_col) {
+          g.bias_out[m] = g.accumulate ? g.bias_out[m] + v : v;
+        } else {
+          float* dst = g.C + (int64_t)m * g.ldc + n;
+          *dst = g.accumulate ? *dst + v : v;
+        }
       }
     }
   }
 }
 
-// column sums over rows: out[n] (+)= sum_m X[m*ldx + n]   (bias gradients)
+// split-K reducer: C[m][n] (+)= sum_z part[z][m][n] (fixed order); the
+// ones column goes to bias_out[m].
 __global__ void __launch_bounds__(kWG)
-colsum_kernel(const float* __restrict__ X, int M, int N, int64_t ldx, float* out, int accumulate) {
-  __shared__ float s[kNW][64];
-  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rl = threadIdx.x >> 6;
-  float a = 0.f;
-  if (n < N)
-    for (int m = rl; m < M; m += kNW) a += X[(int64_t)m * ldx + n];
-  s[rl][threadIdx.x & 63] = a;
-  __syncthreads();
-  if (rl == 0 && n < N) {
-    float t = 0.f;
-    for (int w = 0; w < kNW; ++w) t += s[w][threadIdx.x];
-    out[n] = accumulate ? out[n] + t : t;
+gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, float* C,
+                          int64_t ldc, int ones_col, float* bias_out, int accumulate,
+                          const int* skip) {
+  if (skip && skip[0] != 0) return;
+  const int64_t MN = (int64_t)M * N;
+  for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < MN; e += (int64_t)gridDim.x * kWG) {
+    // two-level fixed-order sum (groups of 8): shorter fp32 chains than one
+    // sequential pass over S slabs
+    float s = 0.f;
+    for (int z0 = 0; z0 < S; z0 += 8) {
+      float t = 0.f;
+      const int z1 = min(S, z0 + 8);
+      for (int z = z0; z < z1; ++z) t += part[z * MN + e];
+      s += t;
+    }
+    const int m = (int)(e / N), n = (int)(e - (int64_t)m * N);
+    if (n == ones_col) {
+      bias_out[m] = accumulate ? bias_out[m] + s : s;
+    } else {
+      float* dst = C + (int64_t)m * ldc + n;
+      *dst = accumulate ? *dst + s : s;
+    }
   }
 }
 
-static int gemm_launch(int epi, const GemmArgs& g, hipStream_t st) {
+float* workspace_f32(int64_t nfloats);
+
+template <int EPI>
+static void gemm_dispatch(const GemmArgs& g, dim3 grid, bool ak, bool bk, hipStream_t st) {
+  if (ak && bk) hipLaunchKernelGGL((gemm_kernel<EPI, true, true>), grid, dim3(kWG), 0, st, g);
+  else if (ak) hipLaunchKernelGGL((gemm_kernel<EPI, true, false>), grid, dim3(kWG), 0, st, g);
+  else if (bk) hipLaunchKernelGGL((gemm_kernel<EPI, false, true>), grid, dim3(kWG), 0, st, g);
+  else hipLaunchKernelGGL((gemm_kernel<EPI, false, false>), grid, dim3(kWG), 0, st, g);
+}
+
+static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return SMI_OK;
-  const dim3 grid((g.M + 63) / 64, (g.N + 63) / 64);
-  if (epi == EPI_FWD) hipLaunchKernelGGL(gemm_kernel<EPI_FWD>, grid, dim3(kWG), 0, st, g);
-  else if (epi == EPI_DX) hipLaunchKernelGGL(gemm_kernel<EPI_DX>, grid, dim3(kWG), 0, st, g);
-  else hipLaunchKernelGGL(gemm_kernel<EPI_DW>, grid, dim3(kWG), 0, st, g);
-  return check_launch("gemm_kernel");
+  const bool ak = g.a_cs == 1;         // A contiguous along k
+  const bool bk = g.b_rs == 1;         // B contiguous along k (rows n)
+  const int gm = (g.M + GBM - 1) / GBM, gn = (g.N + GBN - 1) / GBN;
+  int S = 1;
+  g.part = nullptr;
+  g.kchunk = g.K > 0 ? g.K : 1;
+  if (epi == EPI_DW && g.K > 4 * GBK) {
+    const int tiles = gm * gn;
+    S = (512 + tiles - 1) / tiles;
+    const int smax = (g.K + 8 * GBK - 1) / (8 * GBK);   // >= 8 K-steps per slab
+    if (S > smax) S = smax;
+    const int64_t cap = smi_workspace_floats() / ((int64_t)g.M * g.N);
+    if (S > cap) S = (int)cap;
+    if (S < 1) S = 1;
+    if (S > 1) {
+      g.kchunk = ((g.K + S - 1) / S + GBK - 1) / GBK * GBK;
+      S = (g.K + g.kchunk - 1) / g.kchunk;
+      g.part = workspace_f32((int64_t)S * g.M * g.N);
+      if (!g.part) return set_error(SMI_E_ARG, "gemm: workspace unavailable for split-K");
+    }
+  }
+  const dim3 grid(gm, gn, S);
+  if (epi == EPI_FWD) gemm_dispatch<EPI_FWD>(g, grid, ak, bk, st);
+  else if (epi == EPI_DX) gemm_dispatch<EPI_DX>(g, grid, ak, bk, st);
+  else gemm_dispatch<EPI_DW>(g, grid, ak, bk, st);
+  int rc = check_launch("gemm_kernel");
+  if (rc || S == 1) return rc;
+  const int64_t MN = (int64_t)g.M * g.N;
+  int rg = (int)((MN + kWG - 1) / kWG);
+  if (rg > 1024) rg = 1024;
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, g.part, S, g.M, g.N,
+                     g.C, g.ldc, g.ones_col, g.bias_out, g.accumulate, g.skip);
+  return check_launch("gemm_splitk_reduce_kernel");
 }
 
 int launch_linear_fwd(const float* X, int64_t ldx, int M, int K, const float* W, int64_t ldw,
-                      const float* b, int N, int act, float* Y, int64_t ldy, hipStream_t st) {
+                      const float* b, int N, int act, float* Y, int64_t ldy, hipStream_t st,
+                      const int* skip) {
   GemmArgs g{};
   g.M = M; g.N = N; g.K = K;
   g.A = X; g.a_rs = ldx; g.a_cs = 1;
   g.B = W; g.b_rs = 1; g.b_cs = ldw;        // B(k,n) = W[n][k]
-  g.C = Y; g.ldc = ldy; g.bias = b; g.act = act;
+  g.C = Y; g.ldc = ldy; g.bias = b; g.act = act; g.ones_col = -1; g.skip = skip;
   return gemm_launch(EPI_FWD, g, st);
 }
 
 int launch_linear_bwd_dx(const float* dY, int64_t ldg, int M, int N, const float* W, int64_t ldw,
                          int K, const float* mask, int64_t ldm, float* dX, int64_t lddx,
-                         hipStream_t st) {
+                         hipStream_t st, const int* skip) {
   GemmArgs g{};
   g.M = M; g.N = K; g.K = N;
   g.A = dY; g.a_rs = ldg; g.a_cs = 1;
   g.B = W; g.b_rs = ldw; g.b_cs = 1;        // B(k=n', n=k') = W[n'][k']
-  g.C = dX; g.ldc = lddx; g.mask = mask; g.ldm = ldm;
+  g.C = dX; g.ldc = lddx; g.mask = mask; g.ldm = ldm; g.ones_col = -1; g.skip = skip;
   return gemm_launch(EPI_DX, g, st);
 }
 
 int launch_linear_bwd_dw(const float* dY, int64_t ldg, int M, int N, const float* X, int64_t ldx,
                          int K, float* dW, int64_t lddw, float* db, int accumulate,
-                         hipStream_t st) {
+                         hipStream_t st, const int* skip) {
   GemmArgs g{};
-  g.M = N; g.N = K; g.K = M;
+  g.M = N; g.N = db ? K + 1 : K; g.K = M;
   g.A = dY; g.a_rs = 1; g.a_cs = ldg;       // A(m=n, k=r) = dY[r][n]
-  g.B = X; g.b_rs = ldx; g.b_cs = 1;        // B(k=r, n=k') = X[r][k']
-  g.C = dW; g.ldc = lddw; g.accumulate = accumulate;
-  int rc = gemm_launch(EPI_DW, g, st);
-  if (rc || !db) return rc;
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(kWG), 0, st, dY, M, N, ldg, db,
-                     accumulate);
-  return check_launch("colsum_kernel");
+  g.B = X; g.b_rs = ldx; g.b_cs = 1;        // B(k=r, n=k') = X[r][k'] (k' == K: 1)
+  g.C = dW; g.ldc = lddw; g.accumulate = accumulate; g.skip = skip;
+  g.ones_col = db ? K : -1;
+  g.bias_out = db;
+  return gemm_launch(EPI_DW, g, st);
 }
 
 }  // namespace smi

@@ -1,0 +1,336 @@
+// lstm_kernels.hip — the nn.LSTM stem of PPOModel (surreal/model/ppo_net.py:
+// 137-152, 277-279, 310-312) as persistent sequence kernels for gfx950.
+//
+// The input projection x W_ih^T + b_ih of every step is one large GEMM
+// (linear_kernels.hip) before the recurrence; what stays sequential is
+//   gates_t = xproj_t + (h_{t-1} W_hh^T + b_hh)          [torch order i,f,g,o]
+//   c_t = sigmoid(f) c_{t-1} + sigmoid(i) tanh(g),  h_t = sigmoid(o) tanh(c_t)
+// Segments are independent, so one workgroup owns 16 segments for ALL steps
+// (no inter-workgroup synchronisation): h_{t-1} lives in LDS as the MFMA A
+// operand, c_{t-1} in registers, W_hh streams from L2 (160 KB at H = 100,
+// shared by every workgroup).  Wave w owns hidden-unit tiles ut = w, w+4, ...
+// of 16 units and computes the four gate columns of each (4 accumulators of
+// v_mfma_f32_16x16x4_f32), so the cell update happens in the MFMA output
+// registers: lane (li, lk) holds rows lk*4..lk*4+3 of unit ut*16+li.
+//
+// Backward (BPTT, reverse over steps) keeps dh_rec and dc in the same
+// registers: dgates_t are formed element-wise, written to HBM (for the weight
+// GEMMs) and to LDS, and dh_rec_{t-1} = dgates_t W_hh is the next MFMA pass
+// (K = 4H, B operand contiguous along units).
+#include "smi_device.hpp"
+#include "smi_internal.hpp"
+
+namespace smi {
+
+constexpr int LR = 16;   // segments per workgroup
+
+// LDS leading dim for a [16][K] A-operand image: >= round4(K) and == 4 (mod 8),
+// so the 16 rows x 4 k of one MFMA operand read hit 64 distinct banks.
+__host__ __device__ inline int lstm_ld(int k) {
+  int l = round4(k);
+  if ((l & 7) != 4) l += 4;
+  return l;
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+struct LstmFwdArgs {
+  const float* xproj;     // [S][B][4H] = x W_ih^T + b_ih
+  const float* w_hh;      // [4H][H]
+  const float* b_hh;      // [4H]
+  const float* h0;        // [B][H]
+  const float* c0;        // [B][H]
+  int S, B, H;
+  float* hbuf;            // [S+1][B][H]
+  float* cbuf;            // [S+1][B][H] or null
+  float* gates;           // [S][B][4H] activated, or null
+  const int* skip;
+};
+
+template <int MAXUT>
+__global__ void __launch_bounds__(kWG)
+lstm_fwd_kernel(LstmFwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int LDH = lstm_ld(H);
+  float* hA[2] = {sm, sm + LR * LDH};
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int r0 = blockIdx.x * LR;
+  const int NUT = (H + 15) >> 4;
+  const int64_t BH = (int64_t)B * H;
+  for (int e = threadIdx.x; e < LR * LDH; e += kWG) {
+    const int r = e / LDH, k = e - r * LDH;
+    const bool ok = k < H && r0 + r < B;
+    const float v = ok ? a.h0[(int64_t)(r0 + r) * H + k] : 0.f;
+    hA[0][e] = v;
+    hA[1][e] = 0.f;
+    if (ok) a.hbuf[(int64_t)(r0 + r) * H + k] = v;        // hbuf[0] = h0
+  }
+  float creg[MAXUT][4];
+#pragma unroll
+  for (int u = 0; u < MAXUT; ++u) {
+    const int unit = (wave + 4 * u) * 16 + li;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gr = r0 + lk * 4 + i;
+      const bool ok = unit < H && gr < B;
+      creg[u][i] = ok ? a.c0[(int64_t)gr * H + unit] : 0.f;
+      if (ok && a.cbuf) a.cbuf[(int64_t)gr * H + unit] = creg[u][i];
+    }
+  }
+  // per-lane W_hh row bases (clamped: rows of units >= H read unit H-1 and are
+  // never stored)
+  const float* wrow[MAXUT][4];
+  float bh[MAXUT][4];
+#pragma unroll
+  for (int u = 0; u < MAXUT; ++u) {
+    int unit = (wave + 4 * u) * 16 + li;
+    unit = unit < H ? unit : H - 1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      wrow[u][g] = a.w_hh + (int64_t)(g * H + unit) * H;
+      bh[u][g] = a.b_hh[g * H + unit];
+    }
+  }
+  const int nks = (H + 3) >> 2;        // k-steps of 4
+  __syncthreads();
+  for (int t = 0; t < a.S; ++t) {
+    const float* hp = hA[t & 1];
+    float* hn = hA[(t + 1) & 1];
+    // x-projection of this step (epilogue operand), issued before the MFMAs
+    float xp[MAXUT][4][4];
+#pragma unroll
+    for (int u = 0; u < MAXUT; ++u) {
+      int unit = (wave + 4 * u) * 16 + li;
+      unit = unit < H ? unit : H - 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int gr = r0 + lk * 4 + i;
+        gr = gr < B ? gr : B - 1;
+        const float* xr = a.xproj + ((int64_t)t * B + gr) * G4 + unit;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xp[u][g][i] = xr[g * H];
+      }
+    }
+    f32x4 acc[MAXUT][4];
+#pragma unroll
+    for (int u = 0; u < MAXUT; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[u][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* ap = hp + li * LDH + lk;
+    int ks = 0;
+    for (; ks + 4 <= nks; ks += 4) {
+      float av[4], bv[MAXUT][4][4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = (ks + s) * 4 + lk;
+        const int kc = k < H ? k : H - 1;         // A is zero there (LDS pad)
+        av[s] = ap[(ks + s) * 4];
+#pragma unroll
+        for (int u = 0; u < MAXUT; ++u)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) bv[u][g][s] = wrow[u][g][kc];
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < MAXUT; ++u)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[u][g] = mfma4(av[s], bv[u][g][s], acc[u][g]);
+    }
+    for (; ks < nks; ++ks) {
+      const int k = ks * 4 + lk;
+      const int kc = k < H ? k : H - 1;
+      const float av = ap[ks * 4];
+#pragma unroll
+      for (int u = 0; u < MAXUT; ++u)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[u][g] = mfma4(av, wrow[u][g][kc], acc[u][g]);
+    }
+    // cell update in the accumulator registers
+#pragma unroll
+    for (int u = 0; u < MAXUT; ++u) {
+      const int ut = wave + 4 * u;
+      const int unit = ut * 16 + li;
+      if (ut >= NUT) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = lk * 4 + i, gr = r0 + row;
+        const float gi = xp[u][0][i] + (acc[u][0][i] + bh[u][0]);
+        const float gf = xp[u][1][i] + (acc[u][1][i] + bh[u][1]);
+        const float gg = xp[u][2][i] + (acc[u][2][i] + bh[u][2]);
+        const float go = xp[u][3][i] + (acc[u][3][i] + bh[u][3]);
+        const float ig = sigm(gi), fg = sigm(gf), cg = tanhf(gg), og = sigm(go);
+        const float c = fg * creg[u][i] + ig * cg;
+        const float h = og * tanhf(c);
+        const bool ok = unit < H && gr < B;
+        creg[u][i] = ok ? c : 0.f;
+        if (unit < H) hn[row * LDH + unit] = ok ? h : 0.f;
+        if (ok) {
+          a.hbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = h;
+          if (a.cbuf) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = c;
+          if (a.gates) {
+            float* gp = a.gates + ((int64_t)t * B + gr) * G4 + unit;
+            gp[0] = ig; gp[H] = fg; gp[2 * H] = cg; gp[3 * H] = og;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+struct LstmBwdArgs {
+  const float* dh;        // [S][B][H]  dL/dh_t from the heads
+  const float* gates;     // [S][B][4H] activated (i, f, g, o)
+  const float* cbuf;      // [S+1][B][H]
+  const float* w_hh;      // [4H][H]
+  int S, B, H;
+  float* dgates;          // [S][B][4H] dL/d(pre-activation gates)
+  const int* skip;
+};
+
+template <int MAXUT>
+__global__ void __launch_bounds__(kWG)
+lstm_bwd_kernel(LstmBwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int LDG = lstm_ld(G4);
+  float* dG[2] = {sm, sm + LR * LDG};
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int r0 = blockIdx.x * LR;
+  const int NUT = (H + 15) >> 4;
+  const int64_t BH = (int64_t)B * H;
+  for (int e = threadIdx.x; e < 2 * LR * LDG; e += kWG) sm[e] = 0.f;
+  float dcreg[MAXUT][4];
+  f32x4 dhrec[MAXUT];
+#pragma unroll
+  for (int u = 0; u < MAXUT; ++u) {
+    dhrec[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dcreg[u][i] = 0.f;
+  }
+  int ucl[MAXUT];
+#pragma unroll
+  for (int u = 0; u < MAXUT; ++u) {
+    const int unit = (wave + 4 * u) * 16 + li;
+    ucl[u] = unit < H ? unit : H - 1;
+  }
+  const int nks = G4 >> 2;              // K = 4H, k-steps of 4
+  __syncthreads();
+  for (int t = a.S - 1; t >= 0; --t) {
+    float* dg = dG[t & 1];
+#pragma unroll
+    for (int u = 0; u < MAXUT; ++u) {
+      const int ut = wave + 4 * u;
+      const int unit = ut * 16 + li;
+      if (ut >= NUT) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = lk * 4 + i;
+        int gr = r0 + row;
+        const bool ok = unit < H && gr < B;
+        gr = gr < B ? gr : B - 1;
+        const int uc = ucl[u];
+        const float* gp = a.gates + ((int64_t)t * B + gr) * G4 + uc;
+        const float ig = gp[0], fg = gp[H], cg = gp[2 * H], og = gp[3 * H];
+        const float c = a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + uc];
+        const float cp = a.cbuf[(int64_t)t * BH + (int64_t)gr * H + uc];
+        const float dh = a.dh[(int64_t)t * BH + (int64_t)gr * H + uc] + dhrec[u][i];
+        const float tc = tanhf(c);
+        const float dc = dh * og * (1.f - tc * tc) + dcreg[u][i];
+        const float d_o = (dh * tc) * (og * (1.f - og));
+        const float d_i = (dc * cg) * (ig * (1.f - ig));
+        const float d_g = (dc * ig) * (1.f - cg * cg);
+        const float d_f = (dc * cp) * (fg * (1.f - fg));
+        dcreg[u][i] = ok ? dc * fg : 0.f;
+        if (ok) {
+          float* o = a.dgates + ((int64_t)t * B + gr) * G4 + unit;
+          o[0] = d_i; o[H] = d_f; o[2 * H] = d_g; o[3 * H] = d_o;
+          float* l = dg + row * LDG + unit;
+          l[0] = d_i; l[H] = d_f; l[2 * H] = d_g; l[3 * H] = d_o;
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 0) break;
+    // dh_rec for step t-1:  dgates_t (16 x 4H) @ W_hh (4H x H)
+#pragma unroll
+    for (int u = 0; u < MAXUT; ++u) dhrec[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* ap = dg + li * LDG + lk;
+    int ks = 0;
+    for (; ks + 8 <= nks; ks += 8) {
+      float av[8], bv[MAXUT][8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int k = (ks + s) * 4 + lk;
+        av[s] = ap[(ks + s) * 4];
+#pragma unroll
+        for (int u = 0; u < MAXUT; ++u) bv[u][s] = a.w_hh[(int64_t)k * H + ucl[u]];
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int u = 0; u < MAXUT; ++u) dhrec[u] = mfma4(av[s], bv[u][s], dhrec[u]);
+    }
+    for (; ks < nks; ++ks) {
+      const int k = ks * 4 + lk;
+      const float av = ap[ks * 4];
+#pragma unroll
+      for (int u = 0; u < MAXUT; ++u) dhrec[u] = mfma4(av, a.w_hh[(int64_t)k * H + ucl[u]], dhrec[u]);
+    }
+  }
+}
+
+int64_t lstm_fwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(H) * 4; }
+int64_t lstm_bwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * H) * 4; }
+
+int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
+                    const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,
+                    hipStream_t st, const int* skip) {
+  if (B <= 0 || S < 0) return SMI_OK;
+  if (H < 1 || H > 256) return set_error(SMI_E_ARG, "lstm: hidden size must be in [1, 256]");
+  LstmFwdArgs a{xproj, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates, skip};
+  const size_t lds = (size_t)lstm_fwd_lds(H);
+  const dim3 grid((B + LR - 1) / LR);
+  const int nut = (H + 15) / 16;
+  if (nut <= 4) {
+    allow_lds(lstm_fwd_kernel<1>, lds);
+    hipLaunchKernelGGL(lstm_fwd_kernel<1>, grid, dim3(kWG), lds, st, a);
+  } else if (nut <= 8) {
+    allow_lds(lstm_fwd_kernel<2>, lds);
+    hipLaunchKernelGGL(lstm_fwd_kernel<2>, grid, dim3(kWG), lds, st, a);
+  } else {
+    allow_lds(lstm_fwd_kernel<4>, lds);
+    hipLaunchKernelGGL(lstm_fwd_kernel<4>, grid, dim3(kWG), lds, st, a);
+  }
+  return check_launch("lstm_fwd_kernel");
+}
+
+int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
+                    int S, int B, int H, float* dgates, hipStream_t st, const int* skip) {
+  if (B <= 0 || S <= 0) return SMI_OK;
+  if (H < 1 || H > 256) return set_error(SMI_E_ARG, "lstm: hidden size must be in [1, 256]");
+  LstmBwdArgs a{dh, gates, cbuf, w_hh, S, B, H, dgates, skip};
+  const size_t lds = (size_t)lstm_bwd_lds(H);
+  if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "lstm: hidden size too large for LDS");
+  const dim3 grid((B + LR - 1) / LR);
+  const int nut = (H + 15) / 16;
+  if (nut <= 4) {
+    allow_lds(lstm_bwd_kernel<1>, lds);
+    hipLaunchKernelGGL(lstm_bwd_kernel<1>, grid, dim3(kWG), lds, st, a);
+  } else if (nut <= 8) {
+    allow_lds(lstm_bwd_kernel<2>, lds);
+    hipLaunchKernelGGL(lstm_bwd_kernel<2>, grid, dim3(kWG), lds, st, a);
+  } else {
+    allow_lds(lstm_bwd_kernel<4>, lds);
+    hipLaunchKernelGGL(lstm_bwd_kernel<4>, grid, dim3(kWG), lds, st, a);
+  }
+  return check_launch("lstm_bwd_kernel");
+}
+
+}  // namespace smi

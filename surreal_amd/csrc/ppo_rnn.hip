@@ -1,0 +1,823 @@
+// ppo_rnn.hip — PPOLearner._optimize with the LSTM policy (if_rnn_policy;
+// surreal/learner/ppo.py:487-586 and the RNN branch of _gae_and_return,
+// ppo.py:389-406) as a fixed sequence of device phases (see surreal_mi.h).
+//
+// Rows of every activation are time-major, n = t*B + b (t < S), so the LSTM
+// input projection, the heads and all weight gradients are plain GEMMs over
+// contiguous matrices; per-row loss kernels map n back to the batch-major
+// inputs.  Data-dependent control (KL early stop, adapt penalty branch) is a
+// device flag that turns later phases into no-ops: the host issues the same
+// launches on every call and every rank, and never waits for the device.
+#include "smi_device.hpp"
+#include "smi_internal.hpp"
+
+namespace smi {
+
+int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
+                    const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,
+                    hipStream_t st, const int* skip);
+int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
+                    int S, int B, int H, float* dgates, hipStream_t st, const int* skip);
+int launch_gae_windows(const float* values, float* values_masked, const float* rewards,
+                       const float* dones, int64_t B, int T, int H, const float* gtab,
+                       const float* ltab, float gamma, float gamma_H, float* adv, float* ret,
+                       double* partials, int* n_partials, hipStream_t stream);
+
+// ----------------------------------------------------------------- layout
+// policy sums (pstat, double): one forward over the E*B training rows
+enum {
+  PS_KL = 0,       // sum KL(ref || learn)                       ppo.py:265,553
+  PS_SURR,         // clip: sum -ratio*adv; adapt: sum adv*lik/clamp(lik_b)
+  PS_CLIP,         // clip: sum max(surr, clipped surr)          ppo.py:213
+  PS_ISW,          // sum lik / (lik_b + 1e-4)                   ppo.py:573
+  PS_BL,           // sum lik_b                                  ppo.py:572
+  PS_RBD,          // sum KL(ref || behave)                      ppo.py:574
+  PS_RET,          // sum returns                                ppo.py:570
+  PS_N = 8
+};
+// final sums (fstat, double): value statistics of the last value epoch, then
+// the ZFilter column sums of obs_iter
+enum { FS_SE = 0, FS_D, FS_D2, FS_R, FS_R2, FS_Z = 5 };
+
+// device control block (int / float scratch)
+enum { CI_STOP = 0, CI_RUNS, CI_NG, CI_COUNT = 8 };
+enum { CF_KLCOEF = 0, CF_SURRW, CF_COUNT = 8 };
+
+struct RnnDims {
+  int B, T, Hz, E, S1, D, H, G4, A, h1, h2, c1, c2;
+  int64_t NE, NG;
+  int64_t nA_head, nC_head, nL;       // parameter counts
+  MlpLayout LA, LC;
+};
+
+__host__ __device__ inline RnnDims rnn_dims(int B, int T, int Hz, int D, int H, int h1, int h2,
+                                            int A, int c1, int c2) {
+  RnnDims d;
+  d.B = B; d.T = T; d.Hz = Hz; d.E = T - Hz + 1; d.S1 = T + 1; d.D = D; d.H = H; d.G4 = 4 * H;
+  d.A = A; d.h1 = h1; d.h2 = h2; d.c1 = c1; d.c2 = c2;
+  d.NE = (int64_t)d.E * B; d.NG = (int64_t)d.S1 * B;
+  d.LA = mlp_layout(H, h1, h2, A, 1);
+  d.LC = mlp_layout(H, c1, c2, 1, 0);
+  d.nA_head = d.LA.fcount; d.nC_head = d.LC.fcount;
+  d.nL = (int64_t)4 * H * D + (int64_t)4 * H * H + 8 * (int64_t)H;
+  return d;
+}
+
+// scratch carve (floats, 64-float aligned regions)
+struct RnnScratch {
+  float *Xz, *Xr, *xproj, *hbuf, *cbuf, *gates, *HA1, *HA2, *OUT, *dOUT, *dH1, *dH2, *dh, *dgates;
+  float *values, *adv, *ret, *refmu, *lvpart;
+  double *part, *gaepart;
+  int* ci; float* cf;
+  int64_t total_floats;
+};
+
+static inline int64_t al64(int64_t n) { return (n + 63) & ~(int64_t)63; }
+
+__host__ __device__ inline int rnn_nblk(int64_t rows) {
+  const int64_t b = (rows + kWG - 1) / kWG;
+  return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
+}
+
+static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
+  RnnScratch s{};
+  float* p = static_cast<float*>(base);
+  int64_t o = 0;
+  auto take = [&](int64_t n) { float* r = p ? p + o : nullptr; o += al64(n); return r; };
+  const int hmax1 = d.h1 > d.c1 ? d.h1 : d.c1, hmax2 = d.h2 > d.c2 ? d.h2 : d.c2;
+  s.Xz = take(d.NG * d.D);
+  s.Xr = take(d.NE * d.D);
+  s.xproj = take(d.NG * d.G4);
+  s.hbuf = take((int64_t)(d.S1 + 1) * d.B * d.H);
+  s.cbuf = take((int64_t)(d.E + 1) * d.B * d.H);
+  s.gates = take(d.NE * d.G4);
+  s.HA1 = take(d.NG * hmax1);
+  s.HA2 = take(d.NG * hmax2);
+  s.OUT = take(d.NG * (d.A > 1 ? d.A : 1));
+  s.dOUT = take(d.NE * (d.A > 1 ? d.A : 1));
+  s.dH1 = take(d.NE * hmax1);
+  s.dH2 = take(d.NE * hmax2);
+  s.dh = take(d.NE * d.H);
+  s.dgates = take(d.NE * d.G4);
+  s.values = take((int64_t)d.B * d.S1);
+  s.adv = take(d.NE);
+  s.ret = take(d.NE);
+  s.refmu = take(d.NE * d.A);
+  s.lvpart = take((int64_t)1024 * d.A);
+  s.part = reinterpret_cast<double*>(take(2 * 4096 * 16));   // 65536 doubles
+  s.gaepart = reinterpret_cast<double*>(take(2 * 2 * 2048));
+  s.ci = reinterpret_cast<int*>(take(CI_COUNT));
+  s.cf = take(CF_COUNT);
+  s.total_floats = o;
+  return s;
+}
+
+// ------------------------------------------------------------ small kernels
+// out[t][b][:] = zfilter(obs[b][t][:]) for t < T, out[T][b][:] = zfilter(obs_next[b][0][:]),
+// for t < S (S <= T+1).  z_filter.py:59-79 (clamp +-5); use_zf == 0 copies.
+__global__ void __launch_bounds__(kWG)
+zf_tmajor_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next, int B, int T,
+                 int S, int D, int use_zf, const float* zs, const float* zq, const float* zc,
+                 float eps, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* zm = sm;
+  float* zd = sm + round4(D);
+  if (use_zf) zfilter_colstats(zs, zq, zc, eps, D, zm, zd);
+  __syncthreads();
+  const int64_t n = (int64_t)S * B * D;
+  for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < n; e += (int64_t)gridDim.x * kWG) {
+    const int64_t row = e / D;
+    const int c = (int)(e - row * D);
+    const int t = (int)(row / B), b = (int)(row - (int64_t)t * B);
+    float v = t < T ? obs[((int64_t)b * T + t) * D + c] : obs_next[(int64_t)b * D + c];
+    if (use_zf) v = fminf(fmaxf((v - zm[c]) / zd[c], -5.f), 5.f);
+    out[e] = v;
+  }
+}
+
+// values[b][t] = vt[t*B + b]
+__global__ void __launch_bounds__(kWG)
+tmajor_to_bmajor_kernel(const float* __restrict__ vt, int S, int B, float* __restrict__ v) {
+  const int64_t n = (int64_t)S * B;
+  for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < n; e += (int64_t)gridDim.x * kWG) {
+    const int b = (int)(e / S), t = (int)(e - (int64_t)b * S);
+    v[e] = vt[(int64_t)t * B + b];
+  }
+}
+
+// fixed-order reduction of [nb][w] double partials -> out[w] (one workgroup)
+__global__ void __launch_bounds__(kWG)
+reduce_partials_kernel(const double* __restrict__ part, int nb, int w, double* out,
+                       const int* skip) {
+  if (skip && skip[0] != 0) return;
+  __shared__ double scr[kNW];
+  for (int j = 0; j < w; ++j) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nb; i += kWG) s += part[(int64_t)i * w + j];
+    s = block_sum_d(s, scr);
+    if (threadIdx.x == 0) out[j] = s;
+  }
+}
+
+__device__ inline float dg_row_loglik(const float* act, const float* mu, const float* sd,
+                                      const float* logsd, int A, float c_ll) {
+  float s = 0.f, l = 0.f;
+  for (int j = 0; j < A; ++j) {
+    const float u = (act[j] - mu[j]) / sd[j];
+    s += u * u;
+    l += logsd[j];
+  }
+  return (-0.5f * s - c_ll) - l;
+}
+__device__ inline float dg_row_kl(const float* mu0, const float* sd0, const float* mu1,
+                                  const float* sd1, int A) {
+  float s1 = 0.f, s2 = 0.f;
+  for (int j = 0; j < A; ++j) {
+    s1 += logf(sd1[j] / sd0[j]);
+    const float d = mu0[j] - mu1[j];
+    s2 += (sd0[j] * sd0[j] + d * d) / (2.f * (sd1[j] * sd1[j]));
+  }
+  return (s1 + s2) - 0.5f * (float)A;
+}
+
+struct PolRowArgs {
+  int B, T, E, A, mode;
+  const float* mu;        // [NE][A] learner means (tanh applied)
+  const float* lv;        // [A] learner log_var
+  const float* refmu;     // [NE][A]
+  const float* ref_lv;    // [A]
+  const float* actions;   // [B][T][A]
+  const float* behave;    // [B][T][2A]
+  const float* adv;       // [B][E] raw
+  const float* ret;       // [B][E]
+  const double* moments;  // [3] global (sum, sumsq, n) of adv, or null (no norm)
+  int norm_adv;
+  float c_ll;
+  const float* hyper;
+  const int* skip;
+  // outputs
+  double* part;           // [nblk][PS_N]
+  float* dz;              // [NE][A]   (grad pass)
+  float* lvpart;          // [nblk][A] (grad pass)
+  const float* cf;        // device coefficients (grad pass)
+  float invN;
+};
+
+__device__ inline float norm_adv_of(const PolRowArgs& a, float raw) {
+  if (!a.norm_adv || !a.moments) return raw;
+  // ppo.py:402-405: (adv - mean) / max(std, 1e-4), std unbiased over all B*E
+  const double n = a.moments[2];
+  const double mean = a.moments[0] / n;
+  const double var = (a.moments[1] - n * mean * mean) / (n - 1.0);
+  const float sd = (float)sqrt(var > 0.0 ? var : 0.0);
+  return (raw - (float)mean) / fmaxf(sd, 1e-4f);
+}
+
+// forward statistics of the policy over the E*B rows (ppo.py:203-224,
+// 262-284, 553-575)
+__global__ void __launch_bounds__(kWG)
+policy_rows_stats_kernel(PolRowArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  __shared__ float sig[32], lsig[32], rsig[32];
+  __shared__ double scr[kNW];
+  const int A = a.A;
+  for (int j = threadIdx.x; j < A; j += kWG) {
+    sig[j] = expf(a.lv[j]);                 // builders.py:127 std = exp(log_var)
+    lsig[j] = logf(sig[j]);                 // std0.log() of ppo_net.py:40
+    rsig[j] = expf(a.ref_lv[j]);
+  }
+  __syncthreads();
+  const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
+  double acc[PS_N];
+#pragma unroll
+  for (int k = 0; k < PS_N; ++k) acc[k] = 0.0;
+  const int64_t N = (int64_t)a.E * a.B;
+  for (int64_t n = (int64_t)blockIdx.x * kWG + threadIdx.x; n < N; n += (int64_t)gridDim.x * kWG) {
+    const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
+    const float* m = a.mu + n * A;
+    const float* rm = a.refmu + n * A;
+    const float* ac = a.actions + ((int64_t)b * a.T + t) * A;
+    const float* bp = a.behave + ((int64_t)b * a.T + t) * 2 * A;
+    const float av = norm_adv_of(a, a.adv[(int64_t)b * a.E + t]);
+    const float lp = fmaxf(expf(dg_row_loglik(ac, m, sig, lsig, A, a.c_ll)), 1e-5f);
+    float blsd[32];
+    for (int j = 0; j < A; ++j) blsd[j] = logf(bp[A + j]);
+    const float bl = fmaxf(expf(dg_row_loglik(ac, bp, bp + A, blsd, A, a.c_ll)), 1e-5f);
+    acc[PS_KL] += (double)dg_row_kl(rm, rsig, m, sig, A);
+    if (a.mode == 0) {
+      const float ratio = lp / bl;
+      const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
+      const float surr = -ratio * av, csur = -cr * av;
+      acc[PS_SURR] += (double)surr;
+      acc[PS_CLIP] += (double)fmaxf(surr, csur);
+    } else {
+      acc[PS_SURR] += (double)(av * (lp / fmaxf(bl, 1e-2f)));
+    }
+    acc[PS_ISW] += (double)(lp / (bl + 1e-4f));
+    acc[PS_BL] += (double)bl;
+    acc[PS_RBD] += (double)dg_row_kl(rm, rsig, bp, bp + A, A);
+    acc[PS_RET] += (double)a.ret[(int64_t)b * a.E + t];
+  }
+#pragma unroll
+  for (int k = 0; k < PS_N; ++k) {
+    const double s = block_sum_d(acc[k], scr);
+    if (threadIdx.x == 0) a.part[(int64_t)blockIdx.x * PS_N + k] = s;
+  }
+}
+
+// per-row gradient of the policy loss w.r.t. the tanh pre-activation (dz) and
+// block partials of d loss / d log_var (ppo_net.py:29-72, ppo.py:209-217,
+// 267-277): surrogate weight cf[CF_SURRW] (1/N), KL weight cf[CF_KLCOEF] (adapt:
+// (beta + 2 eta relu(kl - 2kt)) / N, clip: 0)
+__global__ void __launch_bounds__(kWG)
+policy_rows_grad_kernel(PolRowArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  __shared__ float sig[32], lsig[32], rsig[32];
+  __shared__ float gls[kWG / 64][32];
+  const int A = a.A;
+  for (int j = threadIdx.x; j < A; j += kWG) {
+    sig[j] = expf(a.lv[j]);
+    lsig[j] = logf(sig[j]);
+    rsig[j] = expf(a.ref_lv[j]);
+  }
+  __syncthreads();
+  const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
+  const float wsurr = a.cf[CF_SURRW], wkl = a.cf[CF_KLCOEF];
+  float glv[32];
+  for (int j = 0; j < A; ++j) glv[j] = 0.f;
+  const int64_t N = (int64_t)a.E * a.B;
+  for (int64_t n = (int64_t)blockIdx.x * kWG + threadIdx.x; n < N; n += (int64_t)gridDim.x * kWG) {
+    const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
+    const float* m = a.mu + n * A;
+    const float* rm = a.refmu + n * A;
+    const float* ac = a.actions + ((int64_t)b * a.T + t) * A;
+    const float* bp = a.behave + ((int64_t)b * a.T + t) * 2 * A;
+    const float av = norm_adv_of(a, a.adv[(int64_t)b * a.E + t]);
+    const float ll = dg_row_loglik(ac, m, sig, lsig, A, a.c_ll);
+    const float ex = expf(ll);
+    const float lp = fmaxf(ex, 1e-5f);
+    float blsd[32];
+    for (int j = 0; j < A; ++j) blsd[j] = logf(bp[A + j]);
+    const float bl = fmaxf(expf(dg_row_loglik(ac, bp, bp + A, blsd, A, a.c_ll)), 1e-5f);
+    float g_lp;
+    if (a.mode == 0) {
+      const float ratio = lp / bl;
+      const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
+      const float surr = -ratio * av, csur = -cr * av;
+      // max() routes to the unclipped term unless the clipped one is strictly
+      // larger (then the ratio is outside the clamp and the gradient is 0)
+      g_lp = ((surr >= csur) ? -(wsurr * av) : 0.f) / bl;
+    } else {
+      g_lp = (-wsurr * av) / fmaxf(bl, 1e-2f);
+    }
+    const float g_ll = (ex >= 1e-5f) ? g_lp * ex : 0.f;    // clamp + exp backward
+    float* dz = a.dz + n * A;
+    for (int j = 0; j < A; ++j) {
+      const float s1 = sig[j];
+      const float u = (ac[j] - m[j]) / s1;
+      float gmu = g_ll * (u / s1);
+      float gsd = g_ll * (u * u / s1 - 1.f / s1);
+      if (wkl != 0.f) {
+        const float d = rm[j] - m[j];
+        gmu += wkl * (-d / (s1 * s1));
+        gsd += wkl * (1.f / s1 - (rsig[j] * rsig[j] + d * d) / (s1 * s1 * s1));
+      }
+      glv[j] += gsd;
+      dz[j] = gmu * (1.f - m[j] * m[j]);                    // tanh backward
+    }
+  }
+  // block partials of sum_rows d/dstd (times std at the reduction: d/dlog_var)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int j = 0; j < A; ++j) {
+    const float s = wave_sum(glv[j]);
+    if (lane == 0) gls[wave][j] = s;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < A; j += kWG) {
+    float s = 0.f;
+    for (int w = 0; w < kWG / 64; ++w) s += gls[w][j];
+    a.lvpart[(int64_t)blockIdx.x * A + j] = s;
+  }
+}
+
+// d log_var[j] = std_j * sum_blocks lvpart[.][j]   (std = exp(log_var) broadcast)
+__global__ void logvar_grad_kernel(const float* __restrict__ lvpart, int nb, int A,
+                                   const float* lv, float* g, const int* skip) {
+  if (skip && skip[0] != 0) return;
+  for (int j = threadIdx.x; j < A; j += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < nb; ++i) s += lvpart[(int64_t)i * A + j];
+    g[j] = s * expf(lv[j]);
+  }
+}
+
+// After the (all-reduced) policy sums of POLICY_FWD(e): early stop, adapt
+// coefficient and statistics (ppo.py:265-284, 541-557, 568-575).
+struct DecideArgs {
+  const double* ps; int e, Ep, mode; double kl_target; float eta; int64_t N;
+  const float* hyper; const float* lv; int A; float c_ent;
+  int* ci; float* cf; float* stats;
+};
+__global__ void policy_decide_kernel(DecideArgs a) {
+  if (threadIdx.x != 0) return;
+  if (a.ci[CI_STOP]) return;
+  const double n = (double)a.N;
+  const float kl = (float)(a.ps[PS_KL] / n);
+  // statistics of the forward with the current parameters (curr_pol after the
+  // previous update, or ref/behave terms before any)
+  a.stats[SMI_ST_AVG_IS_WEIGHT] = (float)(a.ps[PS_ISW] / n);
+  a.stats[SMI_ST_AVG_BEHAVE_LIK] = (float)(a.ps[PS_BL] / n);
+  a.stats[SMI_ST_REF_BEHAVE_DIFF] = (float)(a.ps[PS_RBD] / n);
+  a.stats[SMI_ST_AVG_RETURN] = (float)(a.ps[PS_RET] / n);
+  if (a.e >= 1) {
+    a.stats[SMI_ST_POL_KL] = kl;                            // ppo.py:555
+    if ((double)kl > a.kl_target * 4.0) {                    // ppo.py:556
+      a.ci[CI_STOP] = 1;
+      return;
+    }
+  }
+  if (a.e >= a.Ep) {
+    a.ci[CI_STOP] = 1;                                       // loop finished
+    return;
+  }
+  // loss statistics of update e
+  float ent = 0.f;
+  for (int j = 0; j < a.A; ++j) ent += logf(expf(a.lv[j]));
+  ent = 0.5f * ent + a.c_ent;
+  a.stats[SMI_ST_ENTROPY] = ent;
+  a.cf[CF_SURRW] = (float)(1.0 / n);
+  if (a.mode == 0) {
+    a.stats[SMI_ST_SURR_LOSS] = (float)(a.ps[PS_SURR] / n);
+    a.stats[SMI_ST_CLIP_SURR_LOSS] = (float)(a.ps[PS_CLIP] / n);
+    a.cf[CF_KLCOEF] = 0.f;
+  } else {
+    const float beta = a.hyper[SMI_HYP_BETA];
+    const float surr = -(float)(a.ps[PS_SURR] / n);
+    float loss = surr + beta * kl;
+    float coef = beta;
+    if ((double)kl - 2.0 * a.kl_target > 0.0) {              // ppo.py:275
+      const float d = kl - (float)(2.0 * a.kl_target);
+      loss += a.eta * (d * d);
+      coef += 2.f * a.eta * d;
+    }
+    a.stats[SMI_ST_SURR_LOSS] = surr;
+    a.stats[SMI_ST_KL_LOSS_ADAPT] = loss;
+    a.stats[SMI_ST_POL_KL_ADAPT] = kl;
+    a.stats[SMI_ST_POL_KL] = kl;
+    a.cf[CF_KLCOEF] = (float)(coef / n);
+  }
+}
+
+// value loss rows: V (time-major [NE]) vs ret [B][E]; dV = 2 (V - R) / N and,
+// in the last epoch, the sums of ppo.py:324-331
+__global__ void __launch_bounds__(kWG)
+value_rows_kernel(const float* __restrict__ V, const float* __restrict__ ret, int B, int E,
+                  float invN2, float* __restrict__ dV, double* part) {
+  __shared__ double scr[kNW];
+  double se = 0.0, d1 = 0.0, d2 = 0.0, r1 = 0.0, r2 = 0.0;
+  const int64_t N = (int64_t)E * B;
+  for (int64_t n = (int64_t)blockIdx.x * kWG + threadIdx.x; n < N; n += (int64_t)gridDim.x * kWG) {
+    const int t = (int)(n / B), b = (int)(n - (int64_t)t * B);
+    const float r = ret[(int64_t)b * E + t];
+    const float v = V[n];
+    const float e = v - r;
+    dV[n] = invN2 * e;
+    if (part) {
+      se += (double)(e * e);
+      const double dd = (double)r - (double)v;
+      d1 += dd; d2 += dd * dd;
+      r1 += (double)r; r2 += (double)r * (double)r;
+    }
+  }
+  if (!part) return;
+  const double s[5] = {se, d1, d2, r1, r2};
+  for (int k = 0; k < 5; ++k) {
+    const double t = block_sum_d(s[k], scr);
+    if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 5 + k] = t;
+  }
+}
+
+// column sums of obs_iter = obs[:, :E, :] (B*E rows) in fp64 -> partials
+__global__ void __launch_bounds__(kWG)
+obs_iter_colsum_kernel(const float* __restrict__ obs, int B, int T, int E, int D,
+                       double* part) {
+  // part [gridDim.x][2][D]
+  const int64_t N = (int64_t)B * E;
+  for (int c = threadIdx.x; c < D; c += kWG) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int64_t n = blockIdx.x; n < N; n += gridDim.x) {
+      const int b = (int)(n / E), t = (int)(n - (int64_t)b * E);
+      const float v = obs[((int64_t)b * T + t) * D + c];
+      s1 += (double)v;
+      s2 += (double)(v * v);
+    }
+    part[((int64_t)blockIdx.x * 2) * D + c] = s1;
+    part[((int64_t)blockIdx.x * 2 + 1) * D + c] = s2;
+  }
+}
+
+// torch.optim.Adam over one optimizer's parameter list [head | lstm] (two
+// parameter buffers, one gradient / moment buffer), after clip_grad_norm_
+// over the same list (ppo.py:243-247, 348-352).
+struct AdamSplitArgs {
+  float* p0; int64_t n0; float* p1; int64_t n1;
+  const float* g; float* m; float* v;
+  int* step; const float* lr_ptr; float beta1, beta2, eps, wd, max_norm;
+  const double* part; int np;
+  const int* skip; float* norm_out; int* runs;
+};
+__global__ void __launch_bounds__(kWG)
+adam_split_kernel(AdamSplitArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  __shared__ double red[kNW];
+  __shared__ float s_coef;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < a.np; i += kWG) s += a.part[i];
+  s = block_sum_d(s, red);
+  const int t = a.step[0] + 1;
+  if (threadIdx.x == 0) {
+    const float norm = (float)sqrt(s);
+    float coef = 1.f;
+    if (a.max_norm > 0.f) {
+      const float cc = a.max_norm / (norm + 1e-6f);
+      coef = cc < 1.f ? cc : 1.f;
+    }
+    s_coef = coef;
+    if (blockIdx.x == 0 && a.norm_out) a.norm_out[0] = norm;
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  const double bc1 = 1.0 - pow((double)a.beta1, (double)t);
+  const double bc2 = 1.0 - pow((double)a.beta2, (double)t);
+  const float step_size = (float)((double)a.lr_ptr[0] / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  const float w1 = (float)(1.0 - (double)a.beta1);
+  const float w2 = (float)(1.0 - (double)a.beta2);
+  const int64_t n = a.n0 + a.n1;
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
+    float* pp = i < a.n0 ? a.p0 + i : a.p1 + (i - a.n0);
+    float g = a.g[i] * coef;
+    float p = *pp;
+    if (a.wd != 0.f) g = g + a.wd * p;
+    float mi = a.m[i], vi = a.v[i];
+    mi = mi + w1 * (g - mi);
+    vi = vi * a.beta2 + (w2 * g) * g;
+    const float denom = sqrtf(vi) / bc2_sqrt + a.eps;
+    *pp = p + (-step_size) * (mi / denom);
+    a.m[i] = mi;
+    a.v[i] = vi;
+  }
+}
+
+__global__ void step_bump_kernel(int* step, int* runs, const int* skip) {
+  if (skip && skip[0] != 0) return;
+  step[0] += 1;
+  if (runs) runs[0] += 1;
+}
+
+__global__ void __launch_bounds__(kWG)
+sumsq_part_kernel(const float* __restrict__ g, int64_t n, double* part, const int* skip) {
+  if (skip && skip[0] != 0) return;
+  __shared__ double scr[kNW];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
+    const double v = (double)g[i];
+    s += v * v;
+  }
+  s = block_sum_d(s, scr);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+struct FinalArgs {
+  const double* fs; int D; int64_t N; const float* lv; int A; int clip_critic;
+  float* zs; float* zq; float* zc; int use_zf;
+  float* stats; const int* ci; float* kl_record; int* kl_count; int kl_capacity; int Ep;
+};
+__global__ void rnn_final_kernel(FinalArgs a) {
+  const double n = (double)a.N;
+  for (int c = threadIdx.x; c < a.D && a.use_zf; c += blockDim.x) {
+    a.zs[c] += (float)a.fs[FS_Z + c];                 // z_filter.py:54-56
+    a.zq[c] += (float)a.fs[FS_Z + a.D + c];
+  }
+  if (threadIdx.x != 0) return;
+  if (a.use_zf) a.zc[0] += (float)n;
+  a.stats[SMI_ST_VAL_LOSS] = (float)(a.fs[FS_SE] / n);
+  const double md = a.fs[FS_D] / n, mr = a.fs[FS_R] / n;
+  const float vd = (float)((a.fs[FS_D2] - n * md * md) / (n - 1.0));
+  const float vr = (float)((a.fs[FS_R2] - n * mr * mr) / (n - 1.0));
+  a.stats[SMI_ST_VAL_EXPL_VAR] = 1.f - vd / vr;              // ppo.py:325
+  float s = 0.f;
+  for (int j = 0; j < a.A; ++j) s += a.lv[j];
+  a.stats[SMI_ST_AVG_LOG_SIG] = s / (float)a.A;             // ppo.py:571
+  a.stats[SMI_ST_EPOCHS_RUN] = (float)a.ci[CI_RUNS];
+  if (a.Ep > 0) {                                            // ppo.py:559
+    const int k = a.kl_count[0];
+    if (k < a.kl_capacity) a.kl_record[k] = a.stats[SMI_ST_POL_KL];
+    a.kl_count[0] = k + 1;
+  }
+}
+
+__global__ void set_count_kernel(double* dst, double n) { dst[0] = n; }
+
+__global__ void rnn_init_kernel(int* ci, float* cf) {
+  if (threadIdx.x < CI_COUNT) ci[threadIdx.x] = 0;
+  if (threadIdx.x < CF_COUNT) cf[threadIdx.x] = 0.f;
+}
+
+// ------------------------------------------------------------ host phases
+static int grid_of(int64_t n, int cap = 1024) {
+  int64_t g = (n + kWG - 1) / kWG;
+  if (g < 1) g = 1;
+  return (int)(g < cap ? g : cap);
+}
+
+#define RC(x) do { const int rc_ = (x); if (rc_) return rc_; } while (0)
+
+struct Head {   // one MLP head over rows of an activation matrix
+  const float* P; MlpLayout L; int in, h1, h2, out, tanh_out;
+};
+
+// forward: X[rows][ldx] -> HA1 -> HA2 -> Y ([rows][out])
+static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, float* HA1,
+                    float* HA2, float* Y, hipStream_t st, const int* skip) {
+  const int M = (int)rows;
+  RC(launch_linear_fwd(X, ldx, M, h.in, h.P + h.L.fW1, h.in, h.P + h.L.fb1, h.h1, ACT_RELU, HA1,
+                       h.h1, st, skip));
+  RC(launch_linear_fwd(HA1, h.h1, M, h.h1, h.P + h.L.fW2, h.h1, h.P + h.L.fb2, h.h2, ACT_RELU, HA2,
+                       h.h2, st, skip));
+  return launch_linear_fwd(HA2, h.h2, M, h.h2, h.P + h.L.fW3, h.h2, h.P + h.L.fb3, h.out,
+                           h.tanh_out ? ACT_TANH : ACT_NONE, Y, h.out, st, skip);
+}
+
+// backward from dZ (gradient at the last layer's pre-activation) into the flat
+// gradient image G (same layout as P); dX (no mask) to dXout
+static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx, int64_t rows,
+                    const float* HA1, const float* HA2, float* dH1, float* dH2, float* G,
+                    float* dXout, hipStream_t st, const int* skip) {
+  const int M = (int)rows;
+  const MlpLayout& L = h.L;
+  RC(launch_linear_bwd_dw(dZ, h.out, M, h.out, HA2, h.h2, h.h2, G + L.fW3, h.h2, G + L.fb3, 0, st,
+                          skip));
+  RC(launch_linear_bwd_dx(dZ, h.out, M, h.out, h.P + L.fW3, h.h2, h.h2, HA2, h.h2, dH2, h.h2, st,
+                          skip));
+  RC(launch_linear_bwd_dw(dH2, h.h2, M, h.h2, HA1, h.h1, h.h1, G + L.fW2, h.h1, G + L.fb2, 0, st,
+                          skip));
+  RC(launch_linear_bwd_dx(dH2, h.h2, M, h.h2, h.P + L.fW2, h.h1, h.h1, HA1, h.h1, dH1, h.h1, st,
+                          skip));
+  RC(launch_linear_bwd_dw(dH1, h.h1, M, h.h1, X, ldx, h.in, G + L.fW1, h.in, G + L.fb1, 0, st,
+                          skip));
+  return launch_linear_bwd_dx(dH1, h.h1, M, h.h1, h.P + L.fW1, h.in, h.in, nullptr, 0, dXout,
+                              h.in, st, skip);
+}
+
+struct LstmP { const float *Wih, *Whh, *bih, *bhh; };
+static LstmP lstm_params(const float* p, int D, int H) {
+  LstmP l;
+  l.Wih = p;
+  l.Whh = p + (int64_t)4 * H * D;
+  l.bih = l.Whh + (int64_t)4 * H * H;
+  l.bhh = l.bih + 4 * H;
+  return l;
+}
+
+// LSTM over S steps from (h0, c0): xproj GEMM + recurrence
+static int lstm_forward(const RnnDims& d, const LstmP& l, const float* X, int S, const float* h0,
+                        const float* c0, const RnnScratch& s, float* cbuf, float* gates,
+                        hipStream_t st, const int* skip) {
+  const int64_t rows = (int64_t)S * d.B;
+  RC(launch_linear_fwd(X, d.D, (int)rows, d.D, l.Wih, d.D, l.bih, d.G4, ACT_NONE, s.xproj, d.G4,
+                       st, skip));
+  return launch_lstm_fwd(s.xproj, l.Whh, l.bhh, h0, c0, S, d.B, d.H, s.hbuf, cbuf, gates, st,
+                         skip);
+}
+
+// gradients of the LSTM parameters (flat layout) from dh [E][B][H]
+static int lstm_backward(const RnnDims& d, const LstmP& l, float* G, const RnnScratch& s,
+                         hipStream_t st, const int* skip) {
+  RC(launch_lstm_bwd(s.dh, s.gates, s.cbuf, l.Whh, d.E, d.B, d.H, s.dgates, st, skip));
+  float* gWih = G;
+  float* gWhh = G + (int64_t)4 * d.H * d.D;
+  float* gbih = gWhh + (int64_t)4 * d.H * d.H;
+  float* gbhh = gbih + d.G4;
+  const int M = (int)d.NE;
+  RC(launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.Xz, d.D, d.D, gWih, d.D, gbih, 0, st, skip));
+  // h_{t-1} rows: hbuf[0..E-1] (hbuf[0] = h0)
+  return launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.hbuf, d.H, d.H, gWhh, d.H, gbhh, 0, st,
+                              skip);
+}
+
+static float c_loglik_of(int A) { return (float)(0.5 * log(2.0 * 3.141592653589793) * (double)A); }
+static float c_entropy_of(int A) {
+  return (float)(0.5 * log(2.0 * 3.141592653589793 * 2.718281828459045) * (double)A);
+}
+
+int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int h1, int h2, int A, int c1,
+                              int c2) {
+  return 4 * rnn_scratch(rnn_dims(B, T, Hz, D, H, h1, h2, A, c1, c2), nullptr).total_floats;
+}
+
+static PolRowArgs pol_rows(const smi_ppo_rnn_args& a, const RnnDims& d, const RnnScratch& s) {
+  PolRowArgs p{};
+  p.B = d.B; p.T = d.T; p.E = d.E; p.A = d.A; p.mode = a.mode;
+  p.mu = s.OUT; p.lv = a.actor + d.LA.flv; p.refmu = s.refmu; p.ref_lv = a.ref_actor + d.LA.flv;
+  p.actions = a.actions; p.behave = a.behave; p.adv = s.adv; p.ret = s.ret;
+  p.moments = a.moments; p.norm_adv = a.norm_adv; p.c_ll = c_loglik_of(d.A);
+  p.hyper = a.hyper; p.skip = s.ci + CI_STOP;
+  p.part = s.part; p.dz = s.dOUT; p.lvpart = s.lvpart; p.cf = s.cf;
+  return p;
+}
+
+int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
+  const RnnDims d = rnn_dims(a.B, a.T, a.horizon, a.obs_dim, a.rnn_hidden, a.h1, a.h2, a.act_dim,
+                             a.critic_h1, a.critic_h2);
+  const RnnScratch s = rnn_scratch(d, a.scratch);
+  if (s.total_floats * 4 > a.scratch_bytes) return set_error(SMI_E_ARG, "ppo_rnn: scratch too small");
+  const int* stop = s.ci + CI_STOP;
+  const LstmP lm = lstm_params(a.lstm, d.D, d.H);
+  const Head actor{a.actor, d.LA, d.H, d.h1, d.h2, d.A, 1};
+  const Head critic{a.critic, d.LC, d.H, d.c1, d.c2, 1, 0};
+  float* gA = a.xbuf;                                  // [actor head | lstm]
+  float* gC = a.xbuf + d.nA_head + d.nL;               // [critic head | lstm]
+  const int64_t NEg = (int64_t)d.E * a.B_global;
+  const size_t zlds = (size_t)2 * round4(d.D) * 4;
+  switch (phase) {
+    case SMI_RNN_PH_GAE: {
+      hipLaunchKernelGGL(rnn_init_kernel, dim3(1), dim3(64), 0, st, s.ci, s.cf);
+      RC(check_launch("rnn_init_kernel"));
+      hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NG * d.D)), dim3(kWG), zlds, st, a.obs,
+                         a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum, a.zf_sumsq,
+                         a.zf_count, a.zf_eps, s.Xz);
+      RC(check_launch("zf_tmajor_kernel"));
+      RC(lstm_forward(d, lm, s.Xz, d.S1, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
+      RC(head_fwd(critic, s.hbuf + (int64_t)d.B * d.H, d.H, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
+      hipLaunchKernelGGL(tmajor_to_bmajor_kernel, dim3(grid_of(d.NG)), dim3(kWG), 0, st, s.OUT,
+                         d.S1, d.B, s.values);
+      RC(check_launch("tmajor_to_bmajor_kernel"));
+      int np = 0;
+      RC(launch_gae_windows(s.values, nullptr, a.rewards, a.dones, d.B, d.T, d.Hz, a.gamma_tab,
+                            a.lam_tab, a.gamma, a.gamma_H, s.adv, s.ret, s.gaepart, &np, st));
+      hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.gaepart, np, 2,
+                         a.moments, nullptr);
+      RC(check_launch("reduce_partials_kernel"));
+      hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(1), 0, st, a.moments + 2, (double)d.NE);
+      return check_launch("set_count_kernel");
+    }
+    case SMI_RNN_PH_PREP: {
+      const float* X = s.Xz;
+      if (a.use_zf) {
+        hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NE * d.D)), dim3(kWG), zlds, st, a.obs,
+                           a.obs_next, d.B, d.T, d.E, d.D, 1, a.rzf_sum, a.rzf_sumsq, a.rzf_count,
+                           a.zf_eps, s.Xr);
+        RC(check_launch("zf_tmajor_kernel"));
+        X = s.Xr;
+      }
+      const LstmP lr = lstm_params(a.ref_lstm, d.D, d.H);
+      RC(lstm_forward(d, lr, X, d.E, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
+      const Head ref{a.ref_actor, d.LA, d.H, d.h1, d.h2, d.A, 1};
+      return head_fwd(ref, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.refmu, st,
+                      nullptr);
+    }
+    case SMI_RNN_PH_POLICY_FWD: {
+      RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, stop));
+      RC(head_fwd(actor, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
+      PolRowArgs p = pol_rows(a, d, s);
+      const int nb = rnn_nblk(d.NE);
+      hipLaunchKernelGGL(policy_rows_stats_kernel, dim3(nb), dim3(kWG), 0, st, p);
+      RC(check_launch("policy_rows_stats_kernel"));
+      hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, PS_N,
+                         a.pstat, stop);
+      return check_launch("reduce_partials_kernel");
+    }
+    case SMI_RNN_PH_POLICY_DECIDE: {   // after the pstat all-reduce
+      DecideArgs da{a.pstat, e, a.epoch_policy, a.mode,
+                    a.kl_target, a.kl_cutoff_coeff, NEg, a.hyper, a.actor + d.LA.flv, d.A,
+                    c_entropy_of(d.A), s.ci, s.cf, a.stats};
+      hipLaunchKernelGGL(policy_decide_kernel, dim3(1), dim3(64), 0, st, da);
+      return check_launch("policy_decide_kernel");
+    }
+    case SMI_RNN_PH_POLICY_BWD: {
+      PolRowArgs p = pol_rows(a, d, s);
+      const int nb = rnn_nblk(d.NE);
+      hipLaunchKernelGGL(policy_rows_grad_kernel, dim3(nb), dim3(kWG), 0, st, p);
+      RC(check_launch("policy_rows_grad_kernel"));
+      RC(head_bwd(actor, s.dOUT, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.dH1, s.dH2,
+                  gA, s.dh, st, stop));
+      hipLaunchKernelGGL(logvar_grad_kernel, dim3(1), dim3(64), 0, st, s.lvpart, nb, d.A,
+                         a.actor + d.LA.flv, gA + d.LA.flv, stop);
+      RC(check_launch("logvar_grad_kernel"));
+      return lstm_backward(d, lm, gA + d.nA_head, s, st, stop);
+    }
+    case SMI_RNN_PH_POLICY_APPLY: {
+      const int64_t n = d.nA_head + d.nL;
+      const int g = grid_of(n, 1024);
+      hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gA, n, s.part, stop);
+      RC(check_launch("sumsq_part_kernel"));
+      AdamSplitArgs aa{a.actor, d.nA_head, a.lstm, d.nL, gA, a.actor_m, a.actor_v, a.actor_step,
+                       a.hyper + SMI_HYP_LR_ACTOR, a.beta1, a.beta2, a.adam_eps, a.actor_wd,
+                       a.clip_actor_grad ? a.actor_max_norm : 0.f, s.part, g, stop,
+                       a.clip_actor_grad ? a.stats + SMI_ST_GRAD_NORM_ACTOR : nullptr, nullptr};
+      hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(kWG), 0, st, aa);
+      RC(check_launch("adam_split_kernel"));
+      hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(1), 0, st, a.actor_step, s.ci + CI_RUNS,
+                         stop);
+      return check_launch("step_bump_kernel");
+    }
+    case SMI_RNN_PH_VALUE_GRAD: {
+      RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, nullptr));
+      RC(head_fwd(critic, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
+      const int nb = rnn_nblk(d.NE);
+      const bool last = e == a.epoch_baseline - 1;
+      hipLaunchKernelGGL(value_rows_kernel, dim3(nb), dim3(kWG), 0, st, s.OUT, s.ret, d.B, d.E,
+                         (float)(2.0 / (double)NEg), s.dOUT, last ? s.part : nullptr);
+      RC(check_launch("value_rows_kernel"));
+      if (last) {
+        hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, 5,
+                           a.zbuf, nullptr);
+        RC(check_launch("reduce_partials_kernel"));
+      }
+      RC(head_bwd(critic, s.dOUT, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.dH1,
+                  s.dH2, gC, s.dh, st, nullptr));
+      return lstm_backward(d, lm, gC + d.nC_head, s, st, nullptr);
+    }
+    case SMI_RNN_PH_VALUE_APPLY: {
+      const int64_t n = d.nC_head + d.nL;
+      const int g = grid_of(n, 1024);
+      hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gC, n, s.part, nullptr);
+      RC(check_launch("sumsq_part_kernel"));
+      AdamSplitArgs aa{a.critic, d.nC_head, a.lstm, d.nL, gC, a.critic_m, a.critic_v,
+                       a.critic_step, a.hyper + SMI_HYP_LR_CRITIC, a.beta1, a.beta2, a.adam_eps,
+                       a.critic_wd, a.clip_critic_grad ? a.critic_max_norm : 0.f, s.part, g,
+                       nullptr, a.clip_critic_grad ? a.stats + SMI_ST_GRAD_NORM_CRITIC : nullptr,
+                       nullptr};
+      hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(kWG), 0, st, aa);
+      RC(check_launch("adam_split_kernel"));
+      hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(1), 0, st, a.critic_step, nullptr,
+                         nullptr);
+      return check_launch("step_bump_kernel");
+    }
+    case SMI_RNN_PH_ZSTATS: {
+      // zbuf (double) = [value sums (5) | column sums (D) | sums of squares (D)]
+      if (!a.use_zf) return SMI_OK;
+      const int nb = 256;
+      double* part = s.part;     // [nb][2][D] <= 65536 doubles for D <= 128
+      if ((int64_t)nb * 2 * d.D > 4096 * 16) return set_error(SMI_E_ARG, "ppo_rnn: obs_dim too large");
+      hipLaunchKernelGGL(obs_iter_colsum_kernel, dim3(nb), dim3(kWG), 0, st, a.obs, d.B, d.T, d.E,
+                         d.D, part);
+      RC(check_launch("obs_iter_colsum_kernel"));
+      hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, part, nb, 2 * d.D,
+                         a.zbuf + FS_Z, nullptr);
+      return check_launch("reduce_partials_kernel");
+    }
+    case SMI_RNN_PH_ZAPPLY: {
+      FinalArgs fa{a.zbuf, d.D, NEg, a.actor + d.LA.flv, d.A,
+                   a.clip_critic_grad, a.zf_sum, a.zf_sumsq, a.zf_count, a.use_zf, a.stats, s.ci,
+                   a.kl_record, a.kl_count, a.kl_capacity, a.epoch_policy};
+      hipLaunchKernelGGL(rnn_final_kernel, dim3(1), dim3(64), 0, st, fa);
+      return check_launch("rnn_final_kernel");
+    }
+    default:
+      return set_error(SMI_E_ARG, "ppo_rnn: unknown phase");
+  }
+}
+
+}  // namespace smi

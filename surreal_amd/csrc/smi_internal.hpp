@@ -8,6 +8,18 @@
 namespace smi {
 
 int set_error(int code, const char* msg);
+// registered device workspace (smi_set_workspace): capacity in floats
+int64_t smi_workspace_floats();
+float* workspace_f32(int64_t nfloats);
+int launch_linear_fwd(const float* X, int64_t ldx, int M, int K, const float* W, int64_t ldw,
+                      const float* b, int N, int act, float* Y, int64_t ldy, hipStream_t st,
+                      const int* skip = nullptr);
+int launch_linear_bwd_dx(const float* dY, int64_t ldg, int M, int N, const float* W, int64_t ldw,
+                         int K, const float* mask, int64_t ldm, float* dX, int64_t lddx,
+                         hipStream_t st, const int* skip = nullptr);
+int launch_linear_bwd_dw(const float* dY, int64_t ldg, int M, int N, const float* X, int64_t ldx,
+                         int K, float* dW, int64_t lddw, float* db, int accumulate,
+                         hipStream_t st, const int* skip = nullptr);
 int check_launch(const char* what);
 
 // Opt a kernel in to > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
@@ -51,5 +63,14 @@ int64_t ppo_fused_max_params();
 int64_t ppo_xbuf_floats(int D, int H1, int H2, int A, int cH1, int cH2, int mode);
 int launch_ppo_epoch_grad(const smi_ppo_args* args, int epoch, hipStream_t stream);
 int launch_ppo_epoch_apply(const smi_ppo_args* args, int epoch, hipStream_t stream);
+
+int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int h1, int h2, int A, int c1,
+                              int c2);
+int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st);
+int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
+                    const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,
+                    hipStream_t st, const int* skip);
+int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
+                    int S, int B, int H, float* dgates, hipStream_t st, const int* skip);
 
 }  // namespace smi

@@ -78,6 +78,11 @@ class TorchDistAllReduce(object):
         return t
 
 
+_RNN_PHASE_NAMES = {0: 'rnn_gae', 1: 'rnn_prep', 2: 'rnn_policy_fwd', 3: 'rnn_policy_bwd',
+                    4: 'rnn_policy_apply', 5: 'rnn_value_grad', 6: 'rnn_value_apply',
+                    7: 'rnn_zstats', 8: 'rnn_zapply', 9: 'rnn_policy_decide'}
+
+
 class PPOLearner(object):
     """ppo.py:12-682 on MI355X.  Same constructor, learn/module_dict/
     publish_parameter/checkpoint_attributes/preprocess/_prefetcher_preprocess."""
@@ -141,9 +146,9 @@ class PPOLearner(object):
             self.beta = self.beta_init
         else:
             raise ConfigError('ppo_mode must be clip or adapt')
-        if self.if_rnn_policy:
-            raise NotImplementedError('surreal_amd: RNN (LSTM) PPO policy is SURVEY §8(f) rank 1; '
-                                      'set algo.rnn.if_rnn_policy=False')
+        if self.if_rnn_policy and algo.rnn.get('rnn_layer', 1) != 1:
+            raise NotImplementedError('surreal_amd: the LSTM policy supports rnn_layer == 1 '
+                                      '(the reference default)')
         if ec.get('pixel_input', False):
             raise NotImplementedError('surreal_amd: pixel inputs are SURVEY §8(f) rank 1')
         if dp is not None and self.use_r_filter:
@@ -172,10 +177,13 @@ class PPOLearner(object):
         # Adam state (torch.optim.Adam defaults: betas (0.9, 0.999), eps 1e-8)
         dev = self.device
         self.adam_betas, self.adam_eps = (0.9, 0.999), 1e-8
-        self.actor_m = torch.zeros_like(self.model.actor.flat)
-        self.actor_v = torch.zeros_like(self.model.actor.flat)
-        self.critic_m = torch.zeros_like(self.model.critic.flat)
-        self.critic_v = torch.zeros_like(self.model.critic.flat)
+        # Adam moments per optimizer; with the LSTM stem both optimizers own the
+        # stem's parameters too (ppo.py:159-168, ppo_net.py:202-224): [head | lstm]
+        n_rnn = self.model.rnn_stem.flat.numel() if self.if_rnn_policy else 0
+        self.actor_m = torch.zeros(self.model.actor.flat.numel() + n_rnn, device=dev)
+        self.actor_v = torch.zeros_like(self.actor_m)
+        self.critic_m = torch.zeros(self.model.critic.flat.numel() + n_rnn, device=dev)
+        self.critic_v = torch.zeros_like(self.critic_m)
         self.actor_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.critic_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.actor_lr_scheduler = LinearWithMinLR(self.lr_actor, num_updates,
@@ -264,7 +272,11 @@ class PPOLearner(object):
         return Config(batch) if not isinstance(batch, Config) else batch
 
     def _optimize(self, obs, actions, rewards, obs_next, persistent_infos, onetime_infos, dones):
-        """ppo.py:487-586 (non-RNN low-dim model)."""
+        """ppo.py:487-586 (low-dim model; LSTM stem via _optimize_rnn)."""
+        if self.if_rnn_policy:
+            yield from self._optimize_rnn(obs, actions, rewards, obs_next, persistent_infos,
+                                          onetime_infos, dones)
+            return
         x = self._low_dim(obs).contiguous()
         xn = self._low_dim(obs_next).contiguous()
         B, T, D = x.shape
@@ -375,6 +387,113 @@ class PPOLearner(object):
             yield zbuf
             L.call('smi_zfilter_accumulate', L.ptr(zbuf[0]), L.ptr(zbuf[1]), D, float(a.B_global),
                    L.ptr(zf.running_sum), L.ptr(zf.running_sumsq), L.ptr(zf.count), st)
+
+    def _optimize_rnn(self, obs, actions, rewards, obs_next, persistent_infos, onetime_infos,
+                      dones):
+        """ppo.py:487-586 with if_rnn_policy: the phase sequence of
+        smi_ppo_rnn_phase (include/surreal_mi.h), yielding the buffers a data-
+        parallel learner all-reduces between phases."""
+        x = self._low_dim(obs).contiguous()
+        xn = self._low_dim(obs_next).contiguous()
+        B, T, D = x.shape
+        if B != self.batch_size or T != self.n_step:
+            raise ValueError(f'batch shape (B={B}, T={T}) != config (batch_size={self.batch_size}, '
+                             f'n_step={self.n_step})')
+        if onetime_infos is None or len(onetime_infos) < 2:
+            raise ValueError('RNN policy: onetime_infos must hold the (h, c) LSTM cells')
+        A = self.action_dim
+        Hd = self.learner_config.algo.rnn.rnn_hidden
+        h0 = onetime_infos[0].reshape(B, -1, Hd)[:, 0, :].contiguous()   # (B, L, H) -> layer 0
+        c0 = onetime_infos[1].reshape(B, -1, Hd)[:, 0, :].contiguous()
+        pds = persistent_infos[-1].contiguous()
+        actions = actions.contiguous()
+        dones = dones.contiguous()
+        st = L.stream(self.device)
+        m, rm = self.model, self.ref_target_model
+        zf = m.z_filter if self.use_z_filter else None
+        rzf = rm.z_filter if self.use_z_filter else None
+        a_h1, a_h2 = self.learner_config.model.actor_fc_hidden_sizes
+        c_h1, c_h2 = self.learner_config.model.critic_fc_hidden_sizes
+        H = self.horizon
+        lib = L.lib()
+        nbytes = lib.smi_ppo_rnn_scratch_bytes(B, T, H, D, Hd, a_h1, a_h2, A, c_h1, c_h2)
+        scratch = self._buf('rnn_scratch', (nbytes // 4,))
+        nx = lib.smi_ppo_rnn_xbuf_floats(D, Hd, a_h1, a_h2, A, c_h1, c_h2)
+        xbuf = self._buf('rnn_xbuf', (nx,))
+        moments = self._buf('rnn_moments', (3,), torch.float64)
+        pstat = self._buf('rnn_pstat', (L.RNN_PSTAT,), torch.float64)
+        zbuf = self._buf('rnn_zbuf', (5 + 2 * D,), torch.float64)
+        nA = m.actor.flat.numel() + m.rnn_stem.flat.numel()
+        nC = m.critic.flat.numel() + m.rnn_stem.flat.numel()
+        a = L.RNNArgs()
+        dp = self.dp
+        a.B, a.T, a.horizon, a.obs_dim, a.rnn_hidden = B, T, H, D, Hd
+        a.h1, a.h2, a.act_dim, a.critic_h1, a.critic_h2 = a_h1, a_h2, A, c_h1, c_h2
+        a.epoch_policy, a.epoch_baseline = self.epoch_policy, self.epoch_baseline
+        a.mode = 0 if self.ppo_mode == 'clip' else 1
+        a.norm_adv = 1 if self.norm_adv else 0
+        a.clip_actor_grad = 1 if self.clip_actor_gradient else 0
+        a.clip_critic_grad = 1 if self.clip_critic_gradient else 0
+        a.use_zf = 1 if zf is not None else 0
+        a.B_global = B * (dp.world_size if dp is not None else 1)
+        a.obs, a.obs_next, a.actions = x.data_ptr(), xn.data_ptr(), actions.data_ptr()
+        a.rewards, a.dones, a.behave = rewards.data_ptr(), dones.data_ptr(), pds.data_ptr()
+        a.h0, a.c0 = h0.data_ptr(), c0.data_ptr()
+        a.lstm, a.actor, a.critic = (m.rnn_stem.flat.data_ptr(), m.actor.flat.data_ptr(),
+                                     m.critic.flat.data_ptr())
+        a.ref_lstm, a.ref_actor = rm.rnn_stem.flat.data_ptr(), rm.actor.flat.data_ptr()
+        if zf is not None:
+            a.zf_sum, a.zf_sumsq, a.zf_count = (zf.running_sum.data_ptr(),
+                                                zf.running_sumsq.data_ptr(), zf.count.data_ptr())
+            a.rzf_sum, a.rzf_sumsq, a.rzf_count = (rzf.running_sum.data_ptr(),
+                                                   rzf.running_sumsq.data_ptr(), rzf.count.data_ptr())
+            a.zf_eps = zf.eps
+        else:
+            a.zf_sum = a.zf_sumsq = a.zf_count = a.rzf_sum = a.rzf_sumsq = a.rzf_count = None
+            a.zf_eps = 1e-5
+        a.actor_m, a.actor_v = self.actor_m.data_ptr(), self.actor_v.data_ptr()
+        a.critic_m, a.critic_v = self.critic_m.data_ptr(), self.critic_v.data_ptr()
+        a.actor_step, a.critic_step = self.actor_step.data_ptr(), self.critic_step.data_ptr()
+        a.hyper = self.hyper.data_ptr()
+        a.gamma_tab, a.lam_tab = self.gamma_tab.data_ptr(), self.lam_tab.data_ptr()
+        a.gamma = float(self.gamma)
+        a.gamma_H = float(self.gamma ** H)                           # ppo.py:400 (python float)
+        a.kl_target = float(self.kl_target)
+        a.kl_cutoff_coeff = float(self.kl_cutoff_coeff)
+        a.actor_max_norm = float(self.actor_gradient_clip_value)
+        a.critic_max_norm = float(self.critic_gradient_clip_value)
+        a.actor_wd, a.critic_wd = float(self.actor_regularization), float(self.critic_regularization)
+        a.beta1, a.beta2, a.adam_eps = self.adam_betas[0], self.adam_betas[1], self.adam_eps
+        a.stats = self.stats_buf.data_ptr()
+        a.kl_record, a.kl_count, a.kl_capacity = (self.kl_record_buf.data_ptr(),
+                                                  self.kl_count.data_ptr(), self.kl_capacity)
+        a.moments, a.pstat, a.xbuf, a.zbuf = (moments.data_ptr(), pstat.data_ptr(),
+                                              xbuf.data_ptr(), zbuf.data_ptr())
+        a.scratch, a.scratch_bytes = scratch.data_ptr(), nbytes
+        self._rnn_args = a
+
+        def ph(p, e=0):
+            with self._ev(_RNN_PHASE_NAMES[p]):
+                L.check(lib.smi_ppo_rnn_phase(a, p, e, st), 'smi_ppo_rnn_phase')
+
+        ph(L.RNN_PH_GAE)
+        yield moments
+        ph(L.RNN_PH_PREP)
+        for e in range(self.epoch_policy + 1):                  # ppo.py:541-557
+            ph(L.RNN_PH_POLICY_FWD, e)
+            yield pstat
+            ph(L.RNN_PH_POLICY_DECIDE, e)
+            if e < self.epoch_policy:
+                ph(L.RNN_PH_POLICY_BWD, e)
+                yield xbuf[:nA]
+                ph(L.RNN_PH_POLICY_APPLY, e)
+        for e in range(self.epoch_baseline):                    # ppo.py:561-562
+            ph(L.RNN_PH_VALUE_GRAD, e)
+            yield xbuf[nA:nA + nC]
+            ph(L.RNN_PH_VALUE_APPLY, e)
+        ph(L.RNN_PH_ZSTATS)                                      # ppo.py:578-582
+        yield zbuf
+        ph(L.RNN_PH_ZAPPLY)
 
     def _learn_phases(self, batch):
         """learn() as a generator of the buffers a data-parallel learner must

@@ -135,6 +135,66 @@ class PPO_CriticNetwork(_FlatMLP):
         return out
 
 
+class LSTMStem(nn.Module):
+    """nn.LSTM(input_size, hidden_size, 1, batch_first=True) of PPOModel
+    (ppo_net.py:143-152) over ONE flat device buffer in the C-ABI LSTM layout
+    [W_ih (4H, in) | W_hh (4H, H) | b_ih (4H) | b_hh (4H)] (torch's parameter
+    order and gate order i, f, g, o).  The Parameters are views named and shaped
+    like torch's (weight_ih_l0, weight_hh_l0, bias_ih_l0, bias_hh_l0), so
+    state_dict() matches nn.LSTM's.  forward() runs the x-projection GEMM and the
+    persistent LSTM sequence kernel; inputs are batch_first (B, S, in)."""
+
+    def __init__(self, input_size, hidden_size, num_layers=1, batch_first=True, device=None,
+                 generator=None):
+        super().__init__()
+        if num_layers != 1:
+            raise NotImplementedError('surreal_amd: LSTM stem supports rnn_layer == 1 '
+                                      '(the reference default, ppo_configs.py)')
+        if not batch_first:
+            raise NotImplementedError('surreal_amd: the reference builds the LSTM batch_first')
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        H, D = hidden_size, input_size
+        n = int(L.lib().smi_lstm_param_count(D, H))
+        flat = torch.zeros(n, dtype=torch.float32, device=device)
+        o = 0
+        self.weight_ih_l0 = nn.Parameter(flat[o:o + 4 * H * D].view(4 * H, D)); o += 4 * H * D
+        self.weight_hh_l0 = nn.Parameter(flat[o:o + 4 * H * H].view(4 * H, H)); o += 4 * H * H
+        self.bias_ih_l0 = nn.Parameter(flat[o:o + 4 * H]); o += 4 * H
+        self.bias_hh_l0 = nn.Parameter(flat[o:o + 4 * H]); o += 4 * H
+        self.__dict__['flat'] = flat
+        self.reset_parameters(generator)
+
+    def reset_parameters(self, generator=None):
+        # torch.nn.LSTM default init: every parameter U(-1/sqrt(H), 1/sqrt(H))
+        k = 1.0 / math.sqrt(self.hidden_size)
+        with torch.no_grad():
+            for p in (self.weight_ih_l0, self.weight_hh_l0, self.bias_ih_l0, self.bias_hh_l0):
+                p.copy_(torch.empty(p.shape).uniform_(-k, k, generator=generator))
+
+    def forward(self, x, cells=None):
+        """x (B, S, in) -> (out (B, S, H), (h_n, c_n) each (1, B, H))."""
+        B, S, D = x.shape
+        H = self.hidden_size
+        dev = self.flat.device
+        st = L.stream(dev)
+        xt = x.transpose(0, 1).contiguous()                       # time-major (S, B, D)
+        xproj = torch.empty(S, B, 4 * H, dtype=torch.float32, device=dev)
+        L.call('smi_linear_forward', L.ptr(xt), D, S * B, D, L.ptr(self.weight_ih_l0), D,
+               L.ptr(self.bias_ih_l0), 4 * H, 0, L.ptr(xproj), 4 * H, st)
+        if cells is None:
+            h0 = torch.zeros(B, H, device=dev)
+            c0 = torch.zeros(B, H, device=dev)
+        else:
+            h0 = cells[0].reshape(B, H).contiguous()
+            c0 = cells[1].reshape(B, H).contiguous()
+        hbuf = torch.empty(S + 1, B, H, dtype=torch.float32, device=dev)
+        cbuf = torch.empty(S + 1, B, H, dtype=torch.float32, device=dev)
+        L.call('smi_lstm_forward', L.ptr(xproj), L.ptr(self.weight_hh_l0), L.ptr(self.bias_hh_l0),
+               L.ptr(h0), L.ptr(c0), S, B, H, L.ptr(hbuf), L.ptr(cbuf), None, st)
+        out = hbuf[1:].transpose(0, 1).contiguous()
+        return out, (hbuf[S].unsqueeze(0).clone(), cbuf[S].unsqueeze(0).clone())
+
+
 class ZFilter(nn.Module):
     """z_filter.py:23-107: running sum / sumsq / count whitening, clamp +-5."""
 
@@ -263,8 +323,8 @@ class DiagGauss(object):
 class PPOModel(nn.Module):
     """ppo_net.py:94-375 (low-dimensional observations).
 
-    The LSTM stem (if_rnn_policy) and the pixel CNN stem (if_pixel_input) are
-    SURVEY.md §8(f) rank 1 and are rejected loudly until their HIP kernels land.
+    The LSTM stem (if_rnn_policy, rnn_layer 1) is the HIP LSTMStem; the pixel CNN
+    stem (if_pixel_input) is SURVEY.md §8(f) rank 1 and is rejected loudly.
     """
 
     def __init__(self, obs_spec, action_dim, model_config, use_cuda=True, init_log_sig=0,
@@ -281,8 +341,7 @@ class PPOModel(nn.Module):
         self.rnn_config = rnn_config if rnn_config is not None else Config({'if_rnn_policy': False})
         if if_pixel_input:
             raise NotImplementedError('surreal_amd: pixel CNN stem is not built yet (SURVEY §8(f) 1)')
-        if self.rnn_config.get('if_rnn_policy', False):
-            raise NotImplementedError('surreal_amd: LSTM policy stem is not built yet (SURVEY §8(f) 1)')
+        self.if_rnn = bool(self.rnn_config.get('if_rnn_policy', False))
         self.device = torch.device(device) if device is not None else torch.device('cuda')
         self.low_dim = 0
         self.low_dim_keys = []
@@ -290,12 +349,17 @@ class PPOModel(nn.Module):
             for k, v in obs_spec['low_dim'].items():
                 self.low_dim += int(v[0])
                 self.low_dim_keys.append(k)
-        self.actor = PPO_ActorNetwork(self.low_dim, action_dim, model_config['actor_fc_hidden_sizes'],
-                                      init_log_sig, self.device, generator)
-        self.critic = PPO_CriticNetwork(self.low_dim, model_config['critic_fc_hidden_sizes'],
-                                        self.device, generator)
         self.cnn_stem = None
         self.rnn_stem = None
+        d_in = self.low_dim
+        if self.if_rnn:                                     # ppo_net.py:143-152,159-160
+            self.rnn_stem = LSTMStem(self.low_dim, self.rnn_config['rnn_hidden'],
+                                     self.rnn_config.get('rnn_layer', 1), True, self.device, generator)
+            d_in = self.rnn_config['rnn_hidden']
+        self.actor = PPO_ActorNetwork(d_in, action_dim, model_config['actor_fc_hidden_sizes'],
+                                      init_log_sig, self.device, generator)
+        self.critic = PPO_CriticNetwork(d_in, model_config['critic_fc_hidden_sizes'],
+                                        self.device, generator)
         if use_z_filter:
             assert self.low_dim > 0, 'No low dimensional input, please turn off z-filter'
             self.z_filter = ZFilter(obs_spec, device=self.device)
@@ -309,24 +373,32 @@ class PPOModel(nn.Module):
         parts = [obs['low_dim'][k] for k in obs['low_dim']]
         return parts[0] if len(parts) == 1 else torch.cat(parts, -1)
 
-    def clear_actor_grad(self):
-        for p in self.actor.parameters():
+    def clear_actor_grad(self):                             # ppo_net.py:180-189
+        for p in self.get_actor_params():
             p.grad = None
 
-    def clear_critic_grad(self):
-        for p in self.critic.parameters():
+    def clear_critic_grad(self):                            # ppo_net.py:191-200
+        for p in self.get_critic_params():
             p.grad = None
 
-    def get_actor_params(self):
-        return self.actor.parameters()
+    def get_actor_params(self):                             # ppo_net.py:202-212
+        ps = list(self.actor.parameters())
+        if self.if_rnn:
+            ps += list(self.rnn_stem.parameters())
+        return iter(ps)
 
-    def get_critic_params(self):
-        return self.critic.parameters()
+    def get_critic_params(self):                            # ppo_net.py:214-224
+        ps = list(self.critic.parameters())
+        if self.if_rnn:
+            ps += list(self.rnn_stem.parameters())
+        return iter(ps)
 
     def update_target_params(self, net):                    # ppo_net.py:226-242
         with torch.no_grad():
             self.actor.flat.copy_(net.actor.flat)
             self.critic.flat.copy_(net.critic.flat)
+            if self.if_rnn:
+                self.rnn_stem.flat.copy_(net.rnn_stem.flat)
             if self.use_z_filter:
                 self.z_filter.load_state_dict(net.z_filter.state_dict())
 
@@ -334,16 +406,30 @@ class PPOModel(nn.Module):
         if self.use_z_filter:
             self.z_filter.load_state_dict(net.z_filter.state_dict())
 
-    def forward_actor(self, obs, cells=None):
+    def _rnn_features(self, x, cells):
+        if self.use_z_filter:
+            x = self.z_filter.forward(x)
+        out, cells = self.rnn_stem(x.contiguous(), cells)
+        return out, cells
+
+    def forward_actor(self, obs, cells=None):               # ppo_net.py:253-282
         x = self._gather_low_dim_input(obs)
+        if self.if_rnn:
+            return self.actor(self._rnn_features(x, cells)[0])
         return self.actor(x, self.z_filter if self.use_z_filter else None)
 
-    def forward_critic(self, obs, cells=None):
+    def forward_critic(self, obs, cells=None):              # ppo_net.py:284-315
         x = self._gather_low_dim_input(obs)
+        if self.if_rnn:
+            return self.critic(self._rnn_features(x, cells)[0])
         return self.critic(x, self.z_filter if self.use_z_filter else None)
 
-    def forward_actor_expose_cells(self, obs, cells=None):
-        return self.forward_actor(obs, cells), cells
+    def forward_actor_expose_cells(self, obs, cells=None):  # ppo_net.py:317-352
+        if not self.if_rnn:
+            return self.forward_actor(obs, cells), cells
+        x = self._gather_low_dim_input(obs).reshape(1, 1, -1)
+        out, cells = self._rnn_features(x, cells)
+        return self.actor(out.reshape(-1, self.rnn_config['rnn_hidden'])), cells
 
     def z_update(self, obs):
         if not self.use_z_filter:

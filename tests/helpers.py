@@ -9,10 +9,11 @@ from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, Config, gym_env_confi
 
 def ppo_config(B=64, T=50, mode='clip', use_z_filter=True, hidden=(64, 64), lam=0.95,
                gamma=0.99, epochs=(10, 10), norm_adv=True, use_r_filter=False, reward_scale=1.0,
-               kl_target=0.02, lr=(3e-4, 3e-4), wd=(0.0, 0.0)):
+               kl_target=0.02, lr=(3e-4, 3e-4), wd=(0.0, 0.0), rnn=False, rnn_hidden=100,
+               horizon=5, critic_hidden=None):
     lc = copy.deepcopy(PPO_DEFAULT_LEARNER_CONFIG)
     lc.model.actor_fc_hidden_sizes = list(hidden)
-    lc.model.critic_fc_hidden_sizes = list(hidden)
+    lc.model.critic_fc_hidden_sizes = list(critic_hidden if critic_hidden is not None else hidden)
     lc.algo.use_z_filter = use_z_filter
     lc.algo.use_r_filter = use_r_filter
     lc.algo.gamma = gamma
@@ -21,7 +22,10 @@ def ppo_config(B=64, T=50, mode='clip', use_z_filter=True, hidden=(64, 64), lam=
     lc.algo.advantage.lam = lam
     lc.algo.advantage.norm_adv = norm_adv
     lc.algo.advantage.reward_scale = reward_scale
-    lc.algo.rnn.if_rnn_policy = False
+    lc.algo.rnn.if_rnn_policy = bool(rnn)
+    lc.algo.rnn.rnn_hidden = rnn_hidden
+    lc.algo.rnn.rnn_layer = 1
+    lc.algo.rnn.horizon = horizon
     lc.algo.consts.epoch_policy = epochs[0]
     lc.algo.consts.epoch_baseline = epochs[1]
     lc.algo.consts.kl_target = kl_target
@@ -44,12 +48,30 @@ def copy_weights_to_oracle(learner, ref):
     ref.model.critic.load_flat(learner.model.critic.flat.detach().cpu())
     ref.ref_target_model.actor.load_flat(learner.ref_target_model.actor.flat.detach().cpu())
     ref.ref_target_model.critic.load_flat(learner.ref_target_model.critic.flat.detach().cpu())
+    if getattr(learner, 'if_rnn_policy', False):
+        for src, dst in ((learner.model, ref.model), (learner.ref_target_model, ref.ref_target_model)):
+            load_lstm_flat(dst.rnn_stem, src.rnn_stem.flat.detach().cpu())
     if learner.use_z_filter:
         for a, b in ((learner.model.z_filter, ref.model.z_filter),
                      (learner.ref_target_model.z_filter, ref.ref_target_model.z_filter)):
             b.running_sum.copy_(a.running_sum.cpu())
             b.running_sumsq.copy_(a.running_sumsq.cpu())
             b.count.copy_(a.count.cpu())
+
+
+def load_lstm_flat(lstm, flat):
+    """C-ABI LSTM layout [W_ih | W_hh | b_ih | b_hh] -> a torch nn.LSTM (1 layer)."""
+    o = 0
+    with torch.no_grad():
+        for p in (lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0):
+            n = p.numel()
+            p.copy_(flat[o:o + n].reshape(p.shape))
+            o += n
+
+
+def lstm_flat(lstm):
+    return torch.cat([p.detach().reshape(-1) for p in
+                      (lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0)])
 
 
 def oracle_batch(batch):

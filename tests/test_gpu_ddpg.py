@@ -36,19 +36,23 @@ def _sync_weights(learner, ref):
     ref.hard_update()
 
 
-def _fp32_as_good_as_torch(got, ref32, ref64):
-    """GEMM parity for long reductions: the HIP result must be within 2x the
-    error of torch's own fp32 CPU result against the fp64 truth (+1e-6 of the
-    scale), and within 1e-5 relative on the tensor's scale."""
+def _fp32_as_good_as_torch(got, ref32, ref64, slack=1e-6):
+    """GEMM parity: the HIP result must be within 2x the error of torch's own
+    fp32 CPU result against the fp64 truth (+ slack of the scale), and within
+    1e-5 relative on the tensor's scale.  Reductions over >~20k rows (weight
+    gradients of the B*E = 21504-row C3 batch) accumulate k-ordered MFMA chains
+    per split-K slab where torch's CPU kernel blocks more finely: they get
+    slack 4e-6 (still inside the 1e-5 parity bar)."""
     got, ref32, ref64 = (np.asarray(t, dtype=np.float64) for t in (got, ref32, ref64))
     scale = np.abs(ref64).max()
     e_gpu = np.abs(got - ref64).max()
     e_cpu = np.abs(ref32 - ref64).max()
-    assert e_gpu <= 2 * e_cpu + 1e-6 * scale, (e_gpu, e_cpu, scale)
+    assert e_gpu <= 2 * e_cpu + slack * scale, (e_gpu, e_cpu, scale)
     assert e_gpu <= 1e-5 * scale
 
 
-@pytest.mark.parametrize('rows,k,n', [(512, 17, 300), (70, 406, 300), (512, 300, 1), (3, 5, 7)])
+@pytest.mark.parametrize('rows,k,n', [(512, 17, 300), (70, 406, 300), (512, 300, 1), (3, 5, 7),
+                                      (21504, 100, 300), (5376, 42, 400), (20000, 200, 8)])
 def test_linear_ops_vs_torch(rows, k, n):
     g = torch.Generator().manual_seed(rows + k)
     x = torch.randn(rows, k, generator=g)
@@ -70,8 +74,14 @@ def test_linear_ops_vs_torch(rows, k, n):
     db = torch.empty(n, device='cuda')
     L.call('smi_linear_backward_weight', L.ptr(dyd), n, rows, n, L.ptr(xd), k, k, L.ptr(dw), k,
            L.ptr(db), 0, st)
-    _fp32_as_good_as_torch(dw.cpu(), dy.t() @ x, dy.double().t() @ x.double())
-    _fp32_as_good_as_torch(db.cpu(), dy.sum(0), dy.double().sum(0))
+    sl = 4e-6 if rows > 16384 else 1e-6
+    _fp32_as_good_as_torch(dw.cpu(), dy.t() @ x, dy.double().t() @ x.double(), sl)
+    _fp32_as_good_as_torch(db.cpu(), dy.sum(0), dy.double().sum(0), sl)
+    # accumulate into existing gradients (split-K reducer path for long reductions)
+    L.call('smi_linear_backward_weight', L.ptr(dyd), n, rows, n, L.ptr(xd), k, k, L.ptr(dw), k,
+           L.ptr(db), 1, st)
+    _fp32_as_good_as_torch(dw.cpu(), 2 * (dy.t() @ x), 2 * (dy.double().t() @ x.double()), sl)
+    _fp32_as_good_as_torch(db.cpu(), 2 * dy.sum(0), 2 * dy.double().sum(0), sl)
 
 
 @pytest.mark.parametrize('target,clip_critic', [('hard', False), ('soft', True)])
@@ -91,8 +101,11 @@ def test_ddpg_learn_matches_oracle(target, clip_critic):
             assert abs(s[k] - rs[k]) <= 1e-4 * abs(rs[k]) + 1e-5, (it, k, s[k], rs[k])
         _compare_params(f'critic{it}', learner.model.critic.flat.cpu(), R.flat_of(ref.critic.params()),
                         1e-3, it + 1, report)
+        # the DDPG actor gradient is the critic's input gradient pushed back
+        # through the actor (ddpg.py:325-329): more of its entries are fp32
+        # rounding noise than in PPO, so the Adam sign-flip budget is 0.5 %
         _compare_params(f'actor{it}', learner.model.actor.flat.cpu(), R.flat_of(ref.actor.params()),
-                        1e-4, it + 1, report)
+                        1e-4, it + 1, report, max_frac=5e-3)
         _compare_params(f'tcritic{it}', learner.model_target.critic.flat.cpu(),
                         R.flat_of(ref.critic_t.params()), 1e-3, it + 1, report)
     print('ddpg parity report:', report)

