@@ -46,14 +46,52 @@ struct GemmArgs {
   int kchunk;                     // K range of blockIdx.z: [z*kchunk, min(K, (z+1)*kchunk))
   float* part;                    // split-K partials [gridDim.z][M][N] (nullptr: no split)
   const int* skip;                // device flag: nonzero -> no-op (early stop)
+  int avec, bvec;                 // 16-byte operand loads (set by gemm_launch)
 };
 
-// operand loader: 2048 elements (64 x 32) per tile, 8 per thread
-// rows >= rdata read as zero (except the all-ones column); rdata <= rmax
+// Operand loader: one 64 (rows) x 32 (k) tile, 2048 elements, 8 per thread
+// (scalar) or 2 float4 per thread (VEC: along the contiguous dimension, when
+// that dimension's extent and the other stride are multiples of 4 and the base
+// is 16-byte aligned — decided once per launch, a uniform branch).  Rows >=
+// rdata and k >= kmax read as zero (clamped addresses, then masked); the
+// all-ones column (dW bias gradient) is synthesised, never loaded.
+struct TileRegs { float v[8]; };
+
 template <bool KCONTIG>
 __device__ __forceinline__ void gemm_load(const float* __restrict__ P, int64_t rs, int64_t cs,
                                           int r0, int rdata, int k0, int kmax, int ones_col,
-                                          float (&v)[8]) {
+                                          bool vec, TileRegs& t) {
+  if (vec) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = threadIdx.x + j * kWG;
+      if (KCONTIG) {            // 64 rows x 8 float4 along k
+        const int r = q >> 3, k = (q & 7) << 2;
+        const int rr = r0 + r, kk = k0 + k;
+        const int rc = rr < rdata ? rr : rdata - 1;
+        const int kc = kk < kmax ? kk : kmax - 4;
+        const float4 x = *reinterpret_cast<const float4*>(P + (int64_t)rc * rs + kc);
+        const bool ok = rr < rdata && kk < kmax;
+        t.v[4 * j + 0] = ok ? x.x : 0.f; t.v[4 * j + 1] = ok ? x.y : 0.f;
+        t.v[4 * j + 2] = ok ? x.z : 0.f; t.v[4 * j + 3] = ok ? x.w : 0.f;
+      } else {                  // 32 k x 16 float4 along rows
+        const int k = q >> 4, r = (q & 15) << 2;
+        const int rr = r0 + r, kk = k0 + k;
+        const int rc = rr < rdata ? rr : rdata - 4;
+        const int kc = kk < kmax ? kk : kmax - 1;
+        const float4 x = *reinterpret_cast<const float4*>(P + (int64_t)kc * cs + rc);
+        const bool okk = kk < kmax, ok = okk && rr < rdata;
+        t.v[4 * j + 0] = ok ? x.x : 0.f; t.v[4 * j + 1] = ok ? x.y : 0.f;
+        t.v[4 * j + 2] = ok ? x.z : 0.f; t.v[4 * j + 3] = ok ? x.w : 0.f;
+        if (ones_col >= 0 && okk) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (rr + e == ones_col) t.v[4 * j + e] = 1.f;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int idx = threadIdx.x + j * kWG;
@@ -63,20 +101,35 @@ __device__ __forceinline__ void gemm_load(const float* __restrict__ P, int64_t r
     const int rc = rr < rdata ? rr : rdata - 1;
     const int kc = kk < kmax ? kk : kmax - 1;
     const float x = P[(int64_t)rc * rs + (int64_t)kc * cs];
-    v[j] = (rr < rdata && kk < kmax) ? x : 0.f;
-    if (ones_col >= 0 && rr == ones_col && kk < kmax) v[j] = 1.f;
+    t.v[j] = (rr < rdata && kk < kmax) ? x : 0.f;
+    if (ones_col >= 0 && rr == ones_col && kk < kmax) t.v[j] = 1.f;
   }
 }
 
 template <bool KCONTIG>
-__device__ __forceinline__ void gemm_store(float* __restrict__ S, const float (&v)[8]) {
+__device__ __forceinline__ void gemm_store(float* __restrict__ S, bool vec, const TileRegs& t) {
+  if (vec) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = threadIdx.x + j * kWG;
+      const float4 x = float4{t.v[4 * j], t.v[4 * j + 1], t.v[4 * j + 2], t.v[4 * j + 3]};
+      if (KCONTIG) {
+        const int r = q >> 3, k = (q & 7) << 2;
+        *reinterpret_cast<float4*>(S + r * LD_KC + k) = x;
+      } else {
+        const int k = q >> 4, r = (q & 15) << 2;
+        *reinterpret_cast<float4*>(S + k * LD_RC + r) = x;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int idx = threadIdx.x + j * kWG;
     const int r = KCONTIG ? (idx >> 5) : (idx & 63);
     const int k = KCONTIG ? (idx & 31) : (idx >> 6);
-    if (KCONTIG) S[r * LD_KC + k] = v[j];
-    else S[k * LD_RC + r] = v[j];
+    if (KCONTIG) S[r * LD_KC + k] = t.v[j];
+    else S[k * LD_RC + r] = t.v[j];
   }
 }
 
@@ -97,20 +150,21 @@ gemm_kernel(GemmArgs g) {
   f32x4 tot[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) tot[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float va[8], vb[8];
+  TileRegs va, vb;
+  const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
   if (nk > 0) {
-    gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb, ke, -1, va);
-    gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, g.ones_col >= 0 ? g.ones_col : g.N, kb, ke, g.ones_col, vb);
-    gemm_store<AK>(sA[0], va);
-    gemm_store<BK>(sB[0], vb);
+    gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb, ke, -1, g.avec, va);
+    gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, bdata, kb, ke, g.ones_col, g.bvec, vb);
+    gemm_store<AK>(sA[0], g.avec, va);
+    gemm_store<BK>(sB[0], g.bvec, vb);
   }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb + (kt + 1) * GBK, ke, -1, va);
-      gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, g.ones_col >= 0 ? g.ones_col : g.N, kb + (kt + 1) * GBK,
-                    ke, g.ones_col, vb);
+      gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb + (kt + 1) * GBK, ke, -1, g.avec, va);
+      gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, bdata, kb + (kt + 1) * GBK, ke, g.ones_col, g.bvec,
+                    vb);
     }
     const float* As = sA[cur];
     const float* Bs = sB[cur];
@@ -141,8 +195,8 @@ gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) tot[c] += acc[c];
     if (kt + 1 < nk) {
-      gemm_store<AK>(sA[cur ^ 1], va);
-      gemm_store<BK>(sB[cur ^ 1], vb);
+      gemm_store<AK>(sA[cur ^ 1], g.avec, va);
+      gemm_store<BK>(sB[cur ^ 1], g.bvec, vb);
     }
     __syncthreads();
   }
@@ -219,14 +273,20 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return SMI_OK;
   const bool ak = g.a_cs == 1;         // A contiguous along k
   const bool bk = g.b_rs == 1;         // B contiguous along k (rows n)
+  auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  // VEC needs the contiguous extent and the other stride in multiples of 4
+  // (every K-slab boundary is then a multiple of 4 too: kchunk % 32 == 0)
+  g.avec = al16(g.A) && (ak ? (g.K % 4 == 0 && g.a_rs % 4 == 0) : (g.a_rs == 1 && g.M % 4 == 0 && g.a_cs % 4 == 0));
+  const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
+  g.bvec = al16(g.B) && (bk ? (g.K % 4 == 0 && g.b_cs % 4 == 0) : (g.b_cs == 1 && bdata % 4 == 0 && g.b_rs % 4 == 0));
   const int gm = (g.M + GBM - 1) / GBM, gn = (g.N + GBN - 1) / GBN;
   int S = 1;
   g.part = nullptr;
   g.kchunk = g.K > 0 ? g.K : 1;
   if (epi == EPI_DW && g.K > 4 * GBK) {
     const int tiles = gm * gn;
-    S = (512 + tiles - 1) / tiles;
-    const int smax = (g.K + 8 * GBK - 1) / (8 * GBK);   // >= 8 K-steps per slab
+    S = (1024 + tiles - 1) / tiles;                   // ~4 workgroups per CU
+    const int smax = (g.K + 4 * GBK - 1) / (4 * GBK);   // >= 4 K-steps per slab
     if (S > smax) S = smax;
     const int64_t cap = smi_workspace_floats() / ((int64_t)g.M * g.N);
     if (S > cap) S = (int)cap;

@@ -32,7 +32,14 @@ __host__ __device__ inline int lstm_ld(int k) {
   return l;
 }
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// Activations on the hardware transcendental units (v_exp_f32, v_rcp_f32: ~1
+// ulp each): sigmoid(x) = 1/(1 + 2^(-x log2 e)), tanh(x) = 2 sigmoid(2x) - 1.
+// Absolute error ~1e-7 (fp32 rounding level of the gate values); the libm
+// forms cost ~4x the VALU issue slots and made the sequence kernels VALU-bound.
+__device__ __forceinline__ float sigm(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float ftanh(float x) { return 2.f * sigm(2.f * x) - 1.f; }
 
 struct LstmFwdArgs {
   const float* xproj;     // [S][B][4H] = x W_ih^T + b_ih
@@ -162,9 +169,9 @@ lstm_fwd_kernel(LstmFwdArgs a) {
         const float gf = xp[u][1][i] + (acc[u][1][i] + bh[u][1]);
         const float gg = xp[u][2][i] + (acc[u][2][i] + bh[u][2]);
         const float go = xp[u][3][i] + (acc[u][3][i] + bh[u][3]);
-        const float ig = sigm(gi), fg = sigm(gf), cg = tanhf(gg), og = sigm(go);
+        const float ig = sigm(gi), fg = sigm(gf), cg = ftanh(gg), og = sigm(go);
         const float c = fg * creg[u][i] + ig * cg;
-        const float h = og * tanhf(c);
+        const float h = og * ftanh(c);
         const bool ok = unit < H && gr < B;
         creg[u][i] = ok ? c : 0.f;
         if (unit < H) hn[row * LDH + unit] = ok ? h : 0.f;
@@ -241,7 +248,7 @@ lstm_bwd_kernel(LstmBwdArgs a) {
         const float c = a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + uc];
         const float cp = a.cbuf[(int64_t)t * BH + (int64_t)gr * H + uc];
         const float dh = a.dh[(int64_t)t * BH + (int64_t)gr * H + uc] + dhrec[u][i];
-        const float tc = tanhf(c);
+        const float tc = ftanh(c);
         const float dc = dh * og * (1.f - tc * tc) + dcreg[u][i];
         const float d_o = (dh * tc) * (og * (1.f - og));
         const float d_i = (dc * cg) * (ig * (1.f - ig));
@@ -286,6 +293,182 @@ lstm_bwd_kernel(LstmBwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Register-resident variants (H <= 100, the reference's default H = 100): 8
+// waves, wave w owns unit tile w, and its slice of W_hh (4 gates x 16 units x
+// H for the forward; 16 units x 4H for the backward) is loaded ONCE into
+// registers — every step then runs at the MFMA rate with one LDS read per
+// k-step (the h_{t-1} / dgates operand) instead of streaming 160 KB of W_hh
+// from L2 per step.  KS = k-steps of 4 held per lane (compile-time bound;
+// steps past the runtime count are uniform-branch skipped).
+constexpr int kWG8 = 512;
+
+template <int KS>
+__global__ void __launch_bounds__(kWG8)
+lstm_fwd_reg_kernel(LstmFwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int LDH = lstm_ld(H);
+  float* hA[2] = {sm, sm + LR * LDH};
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int r0 = blockIdx.x * LR;
+  const int NUT = (H + 15) >> 4;
+  const int64_t BH = (int64_t)B * H;
+  const bool active = wave < NUT;
+  const int unit = wave * 16 + li;
+  const int uc = unit < H ? unit : H - 1;
+  for (int e = threadIdx.x; e < LR * LDH; e += kWG8) {
+    const int r = e / LDH, k = e - r * LDH;
+    const bool ok = k < H && r0 + r < B;
+    const float v = ok ? a.h0[(int64_t)(r0 + r) * H + k] : 0.f;
+    hA[0][e] = v;
+    hA[1][e] = 0.f;
+    if (ok) a.hbuf[(int64_t)(r0 + r) * H + k] = v;        // hbuf[0] = h0
+  }
+  const int nks = (H + 3) >> 2;
+  float w[4][KS];
+  float bh[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float* wr = a.w_hh + (int64_t)(g * H + uc) * H;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 4 * s + lk;
+      w[g][s] = wr[k < H ? k : H - 1];
+    }
+    bh[g] = a.b_hh[g * H + uc];
+  }
+  float creg[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gr = r0 + lk * 4 + i;
+    const bool ok = active && unit < H && gr < B;
+    creg[i] = ok ? a.c0[(int64_t)gr * H + unit] : 0.f;
+    if (ok && a.cbuf) a.cbuf[(int64_t)gr * H + unit] = creg[i];
+  }
+  __syncthreads();
+  for (int t = 0; t < a.S; ++t) {
+    const float* hp = hA[t & 1];
+    float* hn = hA[(t + 1) & 1];
+    if (active) {
+      float xp[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int gr = r0 + lk * 4 + i;
+        gr = gr < B ? gr : B - 1;
+        const float* xr = a.xproj + ((int64_t)t * B + gr) * G4 + uc;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xp[g][i] = xr[g * H];
+      }
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* ap = hp + li * LDH + lk;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (s < nks) {
+          const float av = ap[4 * s];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[g] = mfma4(av, w[g][s], acc[g]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = lk * 4 + i, gr = r0 + row;
+        const float gi = xp[0][i] + (acc[0][i] + bh[0]);
+        const float gf = xp[1][i] + (acc[1][i] + bh[1]);
+        const float gg = xp[2][i] + (acc[2][i] + bh[2]);
+        const float go = xp[3][i] + (acc[3][i] + bh[3]);
+        const float ig = sigm(gi), fg = sigm(gf), cg = ftanh(gg), og = sigm(go);
+        const float c = fg * creg[i] + ig * cg;
+        const float h = og * ftanh(c);
+        const bool ok = unit < H && gr < B;
+        creg[i] = ok ? c : 0.f;
+        if (unit < H) hn[row * LDH + unit] = ok ? h : 0.f;
+        if (ok) {
+          a.hbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = h;
+          if (a.cbuf) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = c;
+          if (a.gates) {
+            float* gp = a.gates + ((int64_t)t * B + gr) * G4 + unit;
+            gp[0] = ig; gp[H] = fg; gp[2 * H] = cg; gp[3 * H] = og;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int KS>
+__global__ void __launch_bounds__(kWG8)
+lstm_bwd_reg_kernel(LstmBwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int LDG = lstm_ld(G4);
+  float* dG[2] = {sm, sm + LR * LDG};
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int r0 = blockIdx.x * LR;
+  const int NUT = (H + 15) >> 4;
+  const int64_t BH = (int64_t)B * H;
+  const bool active = wave < NUT;
+  const int unit = wave * 16 + li;
+  const int uc = unit < H ? unit : H - 1;
+  for (int e = threadIdx.x; e < 2 * LR * LDG; e += kWG8) sm[e] = 0.f;
+  const int nks = H;                    // K = 4H in k-steps of 4
+  float w[KS];                          // W_hh[4s + lk][unit]
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + lk;
+    w[s] = a.w_hh[(int64_t)(k < G4 ? k : G4 - 1) * H + uc];
+  }
+  float dcreg[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 dhrec = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int t = a.S - 1; t >= 0; --t) {
+    float* dg = dG[t & 1];
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = lk * 4 + i;
+        int gr = r0 + row;
+        const bool ok = unit < H && gr < B;
+        gr = gr < B ? gr : B - 1;
+        const float* gp = a.gates + ((int64_t)t * B + gr) * G4 + uc;
+        const float ig = gp[0], fg = gp[H], cg = gp[2 * H], og = gp[3 * H];
+        const float c = a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + uc];
+        const float cp = a.cbuf[(int64_t)t * BH + (int64_t)gr * H + uc];
+        const float dh = a.dh[(int64_t)t * BH + (int64_t)gr * H + uc] + dhrec[i];
+        const float tc = ftanh(c);
+        const float dc = dh * og * (1.f - tc * tc) + dcreg[i];
+        const float d_o = (dh * tc) * (og * (1.f - og));
+        const float d_i = (dc * cg) * (ig * (1.f - ig));
+        const float d_g = (dc * ig) * (1.f - cg * cg);
+        const float d_f = (dc * cp) * (fg * (1.f - fg));
+        dcreg[i] = ok ? dc * fg : 0.f;
+        if (ok) {
+          float* o = a.dgates + ((int64_t)t * B + gr) * G4 + unit;
+          o[0] = d_i; o[H] = d_f; o[2 * H] = d_g; o[3 * H] = d_o;
+          float* l = dg + row * LDG + unit;
+          l[0] = d_i; l[H] = d_f; l[2 * H] = d_g; l[3 * H] = d_o;
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 0) break;
+    if (active) {
+      dhrec = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* ap = dg + li * LDG + lk;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        if (s < nks) dhrec = mfma4(ap[4 * s], w[s], dhrec);
+    }
+  }
+}
+
 int64_t lstm_fwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(H) * 4; }
 int64_t lstm_bwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * H) * 4; }
 
@@ -297,6 +480,16 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
   LstmFwdArgs a{xproj, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates, skip};
   const size_t lds = (size_t)lstm_fwd_lds(H);
   const dim3 grid((B + LR - 1) / LR);
+  if (H <= 64) {
+    allow_lds(lstm_fwd_reg_kernel<16>, lds);
+    hipLaunchKernelGGL(lstm_fwd_reg_kernel<16>, grid, dim3(kWG8), lds, st, a);
+    return check_launch("lstm_fwd_reg_kernel");
+  }
+  if (H <= 100) {                      // the reference default H = 100: 100 W regs/lane
+    allow_lds(lstm_fwd_reg_kernel<25>, lds);
+    hipLaunchKernelGGL(lstm_fwd_reg_kernel<25>, grid, dim3(kWG8), lds, st, a);
+    return check_launch("lstm_fwd_reg_kernel");
+  }
   const int nut = (H + 15) / 16;
   if (nut <= 4) {
     allow_lds(lstm_fwd_kernel<1>, lds);
@@ -319,6 +512,16 @@ int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, cons
   const size_t lds = (size_t)lstm_bwd_lds(H);
   if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "lstm: hidden size too large for LDS");
   const dim3 grid((B + LR - 1) / LR);
+  if (H <= 64) {
+    allow_lds(lstm_bwd_reg_kernel<64>, lds);
+    hipLaunchKernelGGL(lstm_bwd_reg_kernel<64>, grid, dim3(kWG8), lds, st, a);
+    return check_launch("lstm_bwd_reg_kernel");
+  }
+  if (H <= 100) {
+    allow_lds(lstm_bwd_reg_kernel<100>, lds);
+    hipLaunchKernelGGL(lstm_bwd_reg_kernel<100>, grid, dim3(kWG8), lds, st, a);
+    return check_launch("lstm_bwd_reg_kernel");
+  }
   const int nut = (H + 15) / 16;
   if (nut <= 4) {
     allow_lds(lstm_bwd_kernel<1>, lds);
