@@ -1,21 +1,29 @@
-"""Learner throughput benchmark (driver contract: see README/DESIGN.md §Measurement).
+"""Learner throughput benchmark (driver contract: see DESIGN.md §6 Measurement).
 
 A step = one PPOLearner.learn() over one synthetic batch already resident in
-HBM: reward scaling, critic forward over B*(T+1) rows + windowed GAE, the fused
-policy/value epoch loop (ref_pol, <=10 actor updates with KL early stop, 10
-critic updates), z_update.  Workload at N=1 = BASELINE config 2 (HalfCheetah
-dims obs 17 / act 6, 64x64 MLP, 64 segments x 50 steps).  With --gpus N the
-learner is data parallel: each rank holds a 64-segment shard of
-one global N*64-segment batch and the ranks all-reduce advantage moments, the
-per-epoch gradient/statistic exchange buffer and the ZFilter column sums over
-RCCL (torch.distributed 'nccl') — weak scaling, every rank applies the update
-of the global batch.
+HBM (reward scaling, critic forward + windowed GAE, the policy epochs with the
+device-side KL early stop, the value epochs, z_update).
 
-Prints ONE JSON line on rank 0 with the metric, a roofline object for the
-dominant kernel (HIP events on the learner's stream, inside the timed region)
-and the CPU baseline (the oracle restatement timed on this host).
+--config c3 (default; BASELINE configs[2], "1024-actor batch, data parallel
+over 2/4/8 GPUs"): the reference PPO defaults — LSTM policy
+(rnn_hidden 100, horizon 5), heads 300x200, n_step 25, adapt mode, z-filter —
+with robosuite SawyerLift state dims (obs 42, act 8; SURVEY §8 notes 42 is an
+assumption) and 1024 segments per learn() on each GPU.
+--config c2 (BASELINE configs[1]): HalfCheetah dims, 64x64 MLP, 64 x 50.
+
+With --gpus N the learner is data parallel: each rank holds its
+own batch shard and the ranks all-reduce advantage moments, per-epoch
+gradients/statistics and the ZFilter sums over RCCL (torch.distributed
+'nccl') — every rank applies the update of the global batch.  Per-GPU work is
+fixed (weak scaling): the global batch is N x the per-GPU batch.
+
+Prints ONE JSON line on rank 0: the metric, a roofline object for the dominant
+kernel (per-launch HIP events recorded by libsurreal_mi on the learner's stream
+inside the timed region) and the CPU baseline (the oracle restatement, timed on
+this host on a bounded sample).
 """
 import argparse
+import copy
 import json
 import os
 import statistics
@@ -33,20 +41,32 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_* dense peak
 HBM_PEAK_GBS = 8000.0
 
 
-def c2_config():
+def make_config(name):
     from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, gym_env_config
-    import copy
     lc = copy.deepcopy(PPO_DEFAULT_LEARNER_CONFIG)
-    lc.model.actor_fc_hidden_sizes = [64, 64]
-    lc.model.critic_fc_hidden_sizes = [64, 64]
+    if name == 'c2':
+        lc.model.actor_fc_hidden_sizes = [64, 64]
+        lc.model.critic_fc_hidden_sizes = [64, 64]
+        lc.algo.use_z_filter = True
+        lc.algo.n_step = 50
+        lc.algo.gamma = 0.99
+        lc.algo.advantage.lam = 0.95
+        lc.algo.ppo_mode = 'adapt'
+        lc.algo.rnn.if_rnn_policy = False
+        lc.replay.batch_size = 64
+        return lc, gym_env_config(17, 6), dict(D=17, A=6, rnn_hidden=None)
+    # c3: the reference defaults (ppo_configs.py:15-94) + z-filter on
+    lc.model.actor_fc_hidden_sizes = [300, 200]
+    lc.model.critic_fc_hidden_sizes = [300, 200]
     lc.algo.use_z_filter = True
-    lc.algo.n_step = 50
-    lc.algo.gamma = 0.99
-    lc.algo.advantage.lam = 0.95
+    lc.algo.n_step = 25
     lc.algo.ppo_mode = 'adapt'
-    lc.algo.rnn.if_rnn_policy = False
-    lc.replay.batch_size = 64
-    return lc, gym_env_config(17, 6)
+    lc.algo.rnn.if_rnn_policy = True
+    lc.algo.rnn.rnn_hidden = 100
+    lc.algo.rnn.rnn_layer = 1
+    lc.algo.rnn.horizon = 5
+    lc.replay.batch_size = 1024
+    return lc, gym_env_config(42, 8), dict(D=42, A=8, rnn_hidden=100)
 
 
 def mlp_flops_per_row(d, h1, h2, o):
@@ -55,38 +75,48 @@ def mlp_flops_per_row(d, h1, h2, o):
     return fwd, bwd
 
 
-def cpu_baseline(lc, ec, budget_s=12.0):
+def cpu_baseline(name, lc, dims, budget_s=12.0):
+    """The oracle's PPOLearnerRef.learn() (torch CPU fp32) on a bounded sample:
+    C2 = the full 64-segment batch; C3 = a 128-segment slice of the batch
+    (learner throughput in env-steps/s is batch-size independent on CPU at these
+    sizes), one warm-up call then as many timed calls as fit the budget."""
     from oracle import ppo_ref as R
     from surreal_amd import synthetic
     from tests.helpers import oracle_batch
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
+    lc = copy.deepcopy(lc)
+    if name == 'c3':
+        lc.replay.batch_size = 128
     B, T = lc.replay.batch_size, lc.algo.n_step
-    D, A = ec.obs_spec['low_dim']['flat_inputs'][0], ec.action_spec['dim'][0]
+    D, A = dims['D'], dims['A']
     ref = R.PPOLearnerRef(lc, D, A)
-    batches = [oracle_batch(synthetic.ppo_batch(B, T, D, A, seed=i)) for i in range(4)]
-    for i in range(2):
-        ref.learn(batches[i % 4])
+    batches = [oracle_batch(synthetic.ppo_batch(B, T, D, A, seed=i, rnn_hidden=dims['rnn_hidden']))
+               for i in range(2)]
+    ref.learn(batches[1])
     times = []
     t_end = time.perf_counter() + budget_s
     i = 0
-    while time.perf_counter() < t_end or len(times) < 5:
+    while time.perf_counter() < t_end or len(times) < 1:
         t0 = time.perf_counter()
-        ref.learn(batches[i % 4])
+        ref.learn(batches[i % 2])
         times.append(time.perf_counter() - t0)
         i += 1
+        if len(times) >= 200:
+            break
     med = statistics.median(times)
-    return {'value': B * T / med, 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
-            'sample': f'oracle PPOLearnerRef.learn() on the C2 batch, {len(times)} calls '
-                      f'(~{budget_s:.0f} s), median {med * 1e3:.2f} ms, torch CPU fp32, '
-                      f'{threads} threads'}
+    return {'value': round(B * T / med, 1), 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
+            'sample': f'oracle PPOLearnerRef.learn() (torch CPU fp32, {threads} threads) on a '
+                      f'{B}-segment x {T}-step batch of the {name.upper()} workload, {len(times)} '
+                      f'timed calls after 1 warm-up (~{budget_s:.0f} s), median {med * 1e3:.1f} ms'}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=100)
-    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', choices=['c2', 'c3'], default='c3')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
     args = ap.parse_args()
@@ -103,15 +133,17 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device('cuda', torch.cuda.current_device())
 
+    from surreal_amd import _lib as L
     from surreal_amd import synthetic
     from surreal_amd.learner import PPOLearner, TorchDistAllReduce
-    lc, ec = c2_config()
+    lc, ec, dims = make_config(args.config)
     B, T = lc.replay.batch_size, lc.algo.n_step
-    D, A = 17, 6
+    D, A = dims['D'], dims['A']
     dp = TorchDistAllReduce() if dist is not None else None
     learner = PPOLearner(lc, ec, seed=1, device=dev, dp=dp)
-    pool = [synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=rank * 1000 + i), dev)
-            for i in range(8)]
+    pool = [synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=rank * 1000 + i,
+                                                    rnn_hidden=dims['rnn_hidden']), dev)
+            for i in range(4)]
 
     def barrier():
         torch.cuda.synchronize()
@@ -123,12 +155,13 @@ def main():
         learner.learn(pool[i % len(pool)])
     barrier()
     learner.kernel_events = {}
-    epochs = []
+    L.kernel_timing(True)
     t0 = time.perf_counter()
     for k in range(args.steps):
         learner.learn(pool[k % len(pool)])
     barrier()
     elapsed = time.perf_counter() - t0
+    L.kernel_timing(False)
     ev = learner.kernel_events
     learner.kernel_events = None
     if dist is not None:
@@ -137,51 +170,66 @@ def main():
         elapsed = float(t.item())
     epochs_run = learner.last_stats()['epochs_run']
 
-    # per-kernel average durations (ms) from the live events
-    kdur = {n: float(np.mean([s.elapsed_time(e) for s, e in v])) for n, v in ev.items()}
-    dominant = max(kdur, key=kdur.get)
-    a_h1, a_h2 = lc.model.actor_fc_hidden_sizes
-    c_h1, c_h2 = lc.model.critic_fc_hidden_sizes
-    af, ab = mlp_flops_per_row(D, a_h1, a_h2, A)
-    cf, cb = mlp_flops_per_row(D, c_h1, c_h2, 1)
-    E_v = lc.algo.consts.epoch_baseline
-    flops = {
-        # ref fwd + (epochs_run + 1) fwd + epochs_run bwd (policy)  +  E_v (fwd + bwd) (value)
-        'ppo_fused_kernel': B * (af * (epochs_run + 2) + ab * epochs_run) + B * E_v * (cf + cb),
-        'critic_gae_kernel': B * (T + 1) * cf,
-        # data parallel: one grad launch per phase (policy fwd/bwd and/or value fwd/bwd)
-        'ppo_epoch_grad_kernel': B * (af + ab + cf + cb),
-    }
-    if dominant in flops:
-        ach = flops[dominant] / (kdur[dominant] * 1e-3) / 1e12
-        roof = {'kernel': dominant, 'bound': 'mfma', 'achieved': round(ach, 6),
-                'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                'frac': round(ach / FP32_MFMA_PEAK_TFLOPS, 8), 'traffic': None,
-                'avg_ms': round(kdur[dominant], 5),
-                'algorithmic_flops_per_launch': int(flops[dominant])}
+    # per-kernel (MFMA engine) classes from the library's own events, and the
+    # learner-level launches/phases from torch events on the same stream
+    kt = L.kernel_timing_report()
+    kernels = {n: {'launches_per_step': round(c / args.steps, 2), 'avg_ms': round(ms / c, 5),
+                   'ms_per_step': round(ms / args.steps, 4),
+                   'tflops': round(fl / (ms * 1e-3) / 1e12, 3)}
+               for n, (c, ms, fl) in kt.items()}
+    phases = {n: round(float(np.sum([s.elapsed_time(e) for s, e in v])) / args.steps, 4)
+              for n, v in ev.items()}
+    if kt:
+        dom = max(kt, key=lambda n: kt[n][1])
+        c, ms, fl = kt[dom]
+        ach = fl / (ms * 1e-3) / 1e12
+        roof = {'kernel': dom, 'bound': 'mfma', 'achieved': round(ach, 3),
+                'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                'traffic': None, 'avg_ms': round(ms / c, 5),
+                'algorithmic_flops_per_launch': int(fl / c)}
     else:
-        byt = B * D * 4 * 2
-        ach = byt / (kdur[dominant] * 1e-3) / 1e9
-        roof = {'kernel': dominant, 'bound': 'hbm', 'achieved': round(ach, 3), 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'frac': round(ach / HBM_PEAK_GBS, 8), 'traffic': None,
-                'avg_ms': round(kdur[dominant], 5)}
+        # C2: the fused single-CU epoch kernel dominates
+        kdur = {n: float(np.mean([s.elapsed_time(e) for s, e in v])) for n, v in ev.items()}
+        dom = max(kdur, key=kdur.get)
+        a_h1, a_h2 = lc.model.actor_fc_hidden_sizes
+        c_h1, c_h2 = lc.model.critic_fc_hidden_sizes
+        af, ab = mlp_flops_per_row(D, a_h1, a_h2, A)
+        cf, cb = mlp_flops_per_row(D, c_h1, c_h2, 1)
+        E_v = lc.algo.consts.epoch_baseline
+        flops = {
+            'ppo_fused_kernel': B * (af * (epochs_run + 2) + ab * epochs_run) + B * E_v * (cf + cb),
+            'critic_gae_kernel': B * (T + 1) * cf,
+            'ppo_epoch_grad_kernel': B * (af + ab + cf + cb),
+        }
+        fl = flops.get(dom, 0)
+        ach = fl / (kdur[dom] * 1e-3) / 1e12
+        roof = {'kernel': dom, 'bound': 'mfma', 'achieved': round(ach, 6), 'peak': FP32_MFMA_PEAK_TFLOPS,
+                'unit': 'TFLOP/s', 'frac': round(ach / FP32_MFMA_PEAK_TFLOPS, 8), 'traffic': None,
+                'avg_ms': round(kdur[dom], 5), 'algorithmic_flops_per_launch': int(fl)}
     ms = elapsed / args.steps * 1e3
     value = world * B * T * args.steps / elapsed
+    if args.config == 'c3':
+        wl = ('C3: synthetic PPO learner batch, reference PPO defaults (LSTM 100, horizon 5, heads '
+              '300x200, n_step 25, adapt, z-filter, 10/10 epochs), SawyerLift state dims (obs 42, '
+              'act 8), 1024 segments per GPU')
+    else:
+        wl = ('C2: synthetic PPO learner batch, HalfCheetah dims (obs 17, act 6), 64x64 MLP, '
+              '64 segments x n_step 50 per GPU, adapt mode, z-filter, 10/10 epochs')
     out = {
         'metric': METRIC, 'value': round(value, 1), 'unit': 'env-steps/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 4),
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
-        'data': 'synthetic (seeded, SURVEY §8(d)); random-init 64x64 actor/critic',
-        'config': {'workload': 'C2: synthetic PPO learner batch, HalfCheetah dims (obs 17, act 6), '
-                               '64x64 MLP, 64 segments x n_step 50 per GPU, adapt mode, z-filter, '
-                               '10/10 epochs', 'segments_per_gpu': B, 'n_step': T,
-                   'env_steps_per_learn_per_gpu': B * T, 'global_segments': world * B, 'parallelism': f'dp{world}' if world > 1 else 'single',
+        'data': 'synthetic (seeded, SURVEY §8(d)); random-init weights of the named architecture',
+        'config': {'workload': wl, 'segments_per_gpu': B, 'n_step': T,
+                   'env_steps_per_learn_per_gpu': B * T, 'global_segments': world * B,
+                   'parallelism': f'dp{world}' if world > 1 else 'single',
                    'epochs_run_last': epochs_run},
         'roofline': roof,
-        'kernels_avg_ms': {k: round(v, 5) for k, v in kdur.items()},
+        'kernels': kernels,
+        'phase_ms_per_step': phases,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(lc, ec, args.cpu_budget)
+        out['cpu_baseline'] = cpu_baseline(args.config, lc, dims, args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -42,6 +42,19 @@ const char* smi_last_error(void);
 int64_t smi_workspace_bytes(void);
 int     smi_set_workspace(void* dev_ptr, int64_t bytes);
 
+/* Measurement only (not part of the reference API): per-launch HIP-event
+ * timing of the MFMA kernels, by class.  smi_kernel_timing(1) starts a fresh
+ * record, (0) stops; smi_kernel_timing_report(cls, out4) -> {launches, total
+ * ms, total algorithmic flops, 0}. */
+#define SMI_KT_GEMM_FWD    0
+#define SMI_KT_GEMM_DX     1
+#define SMI_KT_GEMM_DW     2
+#define SMI_KT_GEMM_REDUCE 3
+#define SMI_KT_LSTM_FWD    4
+#define SMI_KT_LSTM_BWD    5
+int smi_kernel_timing(int on);
+int smi_kernel_timing_report(int cls, double* out4);
+
 /* --------------------------------------------------------------- layouts */
 /* Number of floats in a flat MLP buffer (in -> h1 -> h2 -> out [+ log_var]). */
 int64_t smi_mlp_param_count(int in_dim, int h1, int h2, int out_dim, int with_log_var);

@@ -88,6 +88,22 @@ class RNNArgs(ctypes.Structure):
 RNN_PH_GAE, RNN_PH_PREP, RNN_PH_POLICY_FWD, RNN_PH_POLICY_BWD, RNN_PH_POLICY_APPLY, \
     RNN_PH_VALUE_GRAD, RNN_PH_VALUE_APPLY, RNN_PH_ZSTATS, RNN_PH_ZAPPLY, RNN_PH_POLICY_DECIDE = range(10)
 RNN_PSTAT = 16
+KT_NAMES = ['gemm_fwd', 'gemm_dx', 'gemm_dw', 'gemm_splitk_reduce', 'lstm_fwd', 'lstm_bwd']
+
+
+def kernel_timing(on):
+    check(lib().smi_kernel_timing(1 if on else 0), 'smi_kernel_timing')
+
+
+def kernel_timing_report():
+    """{class: (launches, total_ms, total_flops)} of the recorded launches."""
+    out = {}
+    buf = (c_f64 * 4)()
+    for i, n in enumerate(KT_NAMES):
+        check(lib().smi_kernel_timing_report(i, ctypes.cast(buf, P)), 'smi_kernel_timing_report')
+        if buf[0] > 0:
+            out[n] = (int(buf[0]), float(buf[1]), float(buf[2]))
+    return out
 
 _SIGS = {
     'smi_version': (c_int, []),
@@ -134,6 +150,8 @@ _SIGS = {
     'smi_mt_randint': (c_int, [P, c_i64, c_i64, P, P]),
     'smi_gather_rows': (c_int, [P, c_i64, P, c_i64, P, P]),
     'smi_lstm_param_count': (c_i64, [c_int, c_int]),
+    'smi_kernel_timing': (c_int, [c_int]),
+    'smi_kernel_timing_report': (c_int, [c_int, P]),
     'smi_ppo_rnn_scratch_bytes': (c_i64, [c_int] * 10),
     'smi_ppo_rnn_xbuf_floats': (c_i64, [c_int] * 7),
     'smi_ppo_rnn_phase': (c_int, [ctypes.POINTER(RNNArgs), c_int, c_int, P]),

@@ -24,6 +24,28 @@ int check_launch(const char* what) {
   return SMI_OK;
 }
 
+// ------------------------------------------------------------ kernel timing
+static bool g_kt = false;
+static const int kKtCap = 16384;
+static hipEvent_t* g_kt_ev = nullptr;        // [2 * kKtCap]
+static int g_kt_n = 0;
+struct KtRec { int cls; double flops; };
+static KtRec g_kt_rec[kKtCap];
+
+bool ktime_on() { return g_kt; }
+int ktime_begin(hipStream_t st) {
+  if (!g_kt || g_kt_n >= kKtCap) return -1;
+  const int slot = g_kt_n++;
+  (void)hipEventRecord(g_kt_ev[2 * slot], st);
+  return slot;
+}
+void ktime_end(int slot, int cls, double flops, hipStream_t st) {
+  if (slot < 0) return;
+  g_kt_rec[slot].cls = cls;
+  g_kt_rec[slot].flops = flops;
+  (void)hipEventRecord(g_kt_ev[2 * slot + 1], st);
+}
+
 // caller-registered device workspace (smi_set_workspace)
 static void* g_ws = nullptr;
 static int64_t g_ws_bytes = 0;
@@ -86,6 +108,35 @@ int smi_set_workspace(void* dev_ptr, int64_t bytes) {
   return SMI_OK;
 }
 int64_t smi_workspace_bytes(void) { return (int64_t)64 << 20; }
+
+/* Per-launch HIP-event timing of the MFMA kernels (GEMM forward / input-grad /
+ * weight-grad / split-K reduce, LSTM forward / backward): on != 0 starts a
+ * fresh record, 0 stops.  Not part of the reference API (measurement only). */
+int smi_kernel_timing(int on) {
+  if (!g_kt_ev) {
+    g_kt_ev = new hipEvent_t[2 * kKtCap];
+    for (int i = 0; i < 2 * kKtCap; ++i)
+      if (hipEventCreate(&g_kt_ev[i]) != hipSuccess) return set_error(SMI_E_LAUNCH, "hipEventCreate");
+  }
+  g_kt = on != 0;
+  if (on) g_kt_n = 0;
+  return SMI_OK;
+}
+/* out4 = {launches, total ms, total algorithmic flops, 0} of class cls
+ * (SMI_KT_*); synchronises with the recorded events. */
+int smi_kernel_timing_report(int cls, double* out4) {
+  if (!out4 || cls < 0 || cls >= KT_COUNT) return set_error(SMI_E_ARG, "kernel_timing_report: bad args");
+  double n = 0, ms = 0, fl = 0;
+  for (int i = 0; i < g_kt_n; ++i) {
+    if (g_kt_rec[i].cls != cls) continue;
+    if (hipEventSynchronize(g_kt_ev[2 * i + 1]) != hipSuccess) return set_error(SMI_E_LAUNCH, "event sync");
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, g_kt_ev[2 * i], g_kt_ev[2 * i + 1]) != hipSuccess) continue;
+    n += 1; ms += t; fl += g_kt_rec[i].flops;
+  }
+  out4[0] = n; out4[1] = ms; out4[2] = fl; out4[3] = 0;
+  return SMI_OK;
+}
 
 int64_t smi_mlp_param_count(int in_dim, int h1, int h2, int out_dim, int with_log_var) {
   return mlp_layout(in_dim, h1, h2, out_dim, with_log_var).fcount;

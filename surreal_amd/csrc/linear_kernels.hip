@@ -231,31 +231,40 @@ gemm_kernel(GemmArgs g) {
   }
 }
 
-// split-K reducer: C[m][n] (+)= sum_z part[z][m][n] (fixed order); the
-// ones column goes to bias_out[m].
+// split-K reducer: C[m][n] (+)= sum_z part[z][m][n]; the ones column goes to
+// bias_out[m].  A workgroup owns 64 consecutive elements x 4 slab lanes: lane
+// zl sums slabs zl, zl+4, ... with 4 independent accumulators (loads in
+// flight), then the 4 lane sums are combined in LDS in a fixed order
+// (deterministic, no atomics).
 __global__ void __launch_bounds__(kWG)
 gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, float* C,
                           int64_t ldc, int ones_col, float* bias_out, int accumulate,
                           const int* skip) {
   if (skip && skip[0] != 0) return;
+  __shared__ float red[4][64];
   const int64_t MN = (int64_t)M * N;
-  for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < MN; e += (int64_t)gridDim.x * kWG) {
-    // two-level fixed-order sum (groups of 8): shorter fp32 chains than one
-    // sequential pass over S slabs
-    float s = 0.f;
-    for (int z0 = 0; z0 < S; z0 += 8) {
-      float t = 0.f;
-      const int z1 = min(S, z0 + 8);
-      for (int z = z0; z < z1; ++z) t += part[z * MN + e];
-      s += t;
-    }
-    const int m = (int)(e / N), n = (int)(e - (int64_t)m * N);
-    if (n == ones_col) {
-      bias_out[m] = accumulate ? bias_out[m] + s : s;
-    } else {
-      float* dst = C + (int64_t)m * ldc + n;
-      *dst = accumulate ? *dst + s : s;
-    }
+  const int el = threadIdx.x & 63, zl = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + el;
+  const int64_t ec = e < MN ? e : MN - 1;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int z = zl;
+  for (; z + 12 < S; z += 16) {
+    s0 += part[(int64_t)z * MN + ec];
+    s1 += part[(int64_t)(z + 4) * MN + ec];
+    s2 += part[(int64_t)(z + 8) * MN + ec];
+    s3 += part[(int64_t)(z + 12) * MN + ec];
+  }
+  for (; z < S; z += 4) s0 += part[(int64_t)z * MN + ec];
+  red[zl][el] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (zl != 0 || e >= MN) return;
+  const float s = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+  const int m = (int)(e / N), n = (int)(e - (int64_t)m * N);
+  if (n == ones_col) {
+    bias_out[m] = accumulate ? bias_out[m] + s : s;
+  } else {
+    float* dst = C + (int64_t)m * ldc + n;
+    *dst = accumulate ? *dst + s : s;
   }
 }
 
@@ -299,16 +308,21 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
     }
   }
   const dim3 grid(gm, gn, S);
+  const int kslot = ktime_begin(st);
   if (epi == EPI_FWD) gemm_dispatch<EPI_FWD>(g, grid, ak, bk, st);
   else if (epi == EPI_DX) gemm_dispatch<EPI_DX>(g, grid, ak, bk, st);
   else gemm_dispatch<EPI_DW>(g, grid, ak, bk, st);
+  const int nreal = g.ones_col >= 0 ? g.N - 1 : g.N;
+  ktime_end(kslot, epi == EPI_FWD ? KT_GEMM_FWD : epi == EPI_DX ? KT_GEMM_DX : KT_GEMM_DW,
+            2.0 * g.M * (double)nreal * g.K + (g.ones_col >= 0 ? (double)g.M * g.K : 0.0), st);
   int rc = check_launch("gemm_kernel");
   if (rc || S == 1) return rc;
+  const int rslot = ktime_begin(st);
   const int64_t MN = (int64_t)g.M * g.N;
-  int rg = (int)((MN + kWG - 1) / kWG);
-  if (rg > 1024) rg = 1024;
+  const int rg = (int)((MN + 63) / 64);
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, g.part, S, g.M, g.N,
                      g.C, g.ldc, g.ones_col, g.bias_out, g.accumulate, g.skip);
+  ktime_end(rslot, KT_GEMM_REDUCE, (double)S * MN, st);
   return check_launch("gemm_splitk_reduce_kernel");
 }
 

@@ -425,6 +425,28 @@ lstm_bwd_reg_kernel(LstmBwdArgs a) {
     const int k = 4 * s + lk;
     w[s] = a.w_hh[(int64_t)(k < G4 ? k : G4 - 1) * H + uc];
   }
+  // per-lane element offsets of the 4 rows (clamped rows read row B-1)
+  int64_t roff[4];
+  bool rok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gr = r0 + lk * 4 + i;
+    rok[i] = unit < H && gr < B;
+    roff[i] = (int64_t)(gr < B ? gr : B - 1);
+  }
+  // step operands, prefetched one step ahead (issued before the dh_rec MFMAs)
+  float pg[4][4], pc[4], pcp[4], pdh[4];
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float* gp = a.gates + ((int64_t)t * B + roff[i]) * G4 + uc;
+      pg[i][0] = gp[0]; pg[i][1] = gp[H]; pg[i][2] = gp[2 * H]; pg[i][3] = gp[3 * H];
+      pc[i] = a.cbuf[(int64_t)(t + 1) * BH + roff[i] * H + uc];
+      pcp[i] = a.cbuf[(int64_t)t * BH + roff[i] * H + uc];
+      pdh[i] = a.dh[(int64_t)t * BH + roff[i] * H + uc];
+    }
+  };
+  if (active && a.S > 0) fetch(a.S - 1);
   float dcreg[4] = {0.f, 0.f, 0.f, 0.f};
   f32x4 dhrec = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
@@ -434,23 +456,18 @@ lstm_bwd_reg_kernel(LstmBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = lk * 4 + i;
-        int gr = r0 + row;
-        const bool ok = unit < H && gr < B;
-        gr = gr < B ? gr : B - 1;
-        const float* gp = a.gates + ((int64_t)t * B + gr) * G4 + uc;
-        const float ig = gp[0], fg = gp[H], cg = gp[2 * H], og = gp[3 * H];
-        const float c = a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + uc];
-        const float cp = a.cbuf[(int64_t)t * BH + (int64_t)gr * H + uc];
-        const float dh = a.dh[(int64_t)t * BH + (int64_t)gr * H + uc] + dhrec[i];
+        const float ig = pg[i][0], fg = pg[i][1], cg = pg[i][2], og = pg[i][3];
+        const float c = pc[i], cp = pcp[i];
+        const float dh = pdh[i] + dhrec[i];
         const float tc = ftanh(c);
         const float dc = dh * og * (1.f - tc * tc) + dcreg[i];
         const float d_o = (dh * tc) * (og * (1.f - og));
         const float d_i = (dc * cg) * (ig * (1.f - ig));
         const float d_g = (dc * ig) * (1.f - cg * cg);
         const float d_f = (dc * cp) * (fg * (1.f - fg));
-        dcreg[i] = ok ? dc * fg : 0.f;
-        if (ok) {
-          float* o = a.dgates + ((int64_t)t * B + gr) * G4 + unit;
+        dcreg[i] = rok[i] ? dc * fg : 0.f;
+        if (rok[i]) {
+          float* o = a.dgates + ((int64_t)t * B + roff[i]) * G4 + unit;
           o[0] = d_i; o[H] = d_f; o[2 * H] = d_g; o[3 * H] = d_o;
           float* l = dg + row * LDG + unit;
           l[0] = d_i; l[H] = d_f; l[2 * H] = d_g; l[3 * H] = d_o;
@@ -460,6 +477,7 @@ lstm_bwd_reg_kernel(LstmBwdArgs a) {
     __syncthreads();
     if (t == 0) break;
     if (active) {
+      fetch(t - 1);
       dhrec = f32x4{0.f, 0.f, 0.f, 0.f};
       const float* ap = dg + li * LDG + lk;
 #pragma unroll
@@ -478,6 +496,10 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
   if (B <= 0 || S < 0) return SMI_OK;
   if (H < 1 || H > 256) return set_error(SMI_E_ARG, "lstm: hidden size must be in [1, 256]");
   LstmFwdArgs a{xproj, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates, skip};
+  const int kslot = ktime_begin(st);
+  // algorithmic flops: the recurrent GEMM h W_hh^T of every step
+  struct End { int s; hipStream_t st; double f;
+               ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{kslot, st, 8.0 * B * H * (double)H * S};
   const size_t lds = (size_t)lstm_fwd_lds(H);
   const dim3 grid((B + LR - 1) / LR);
   if (H <= 64) {
@@ -509,6 +531,10 @@ int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, cons
   if (B <= 0 || S <= 0) return SMI_OK;
   if (H < 1 || H > 256) return set_error(SMI_E_ARG, "lstm: hidden size must be in [1, 256]");
   LstmBwdArgs a{dh, gates, cbuf, w_hh, S, B, H, dgates, skip};
+  const int kslot = ktime_begin(st);
+  struct End { int s; hipStream_t st; double f;
+               ~End() { ktime_end(s, KT_LSTM_BWD, f, st); } } end_{kslot, st,
+                                                                 8.0 * B * H * (double)H * (S - 1)};
   const size_t lds = (size_t)lstm_bwd_lds(H);
   if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "lstm: hidden size too large for LDS");
   const dim3 grid((B + LR - 1) / LR);

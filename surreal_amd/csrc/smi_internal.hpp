@@ -8,6 +8,15 @@
 namespace smi {
 
 int set_error(int code, const char* msg);
+
+// Optional per-launch HIP-event timing of the MFMA kernels (smi_kernel_timing):
+// each launch records (class, algorithmic flops, start/end events) on its own
+// stream.  Off by default; bench.py turns it on over its timed region.
+enum { KT_GEMM_FWD = 0, KT_GEMM_DX, KT_GEMM_DW, KT_GEMM_REDUCE, KT_LSTM_FWD, KT_LSTM_BWD,
+       KT_COUNT };
+bool ktime_on();
+int ktime_begin(hipStream_t st);                       // returns a slot, -1 when off/full
+void ktime_end(int slot, int cls, double flops, hipStream_t st);
 // registered device workspace (smi_set_workspace): capacity in floats
 int64_t smi_workspace_floats();
 float* workspace_f32(int64_t nfloats);

@@ -26,7 +26,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, mode, outdir):
+def _cfg(mode, rnn):
+    from tests.helpers import ppo_config
+    if rnn:
+        return ppo_config(B=B_LOC, T=T, mode=mode, use_z_filter=True, hidden=(32, 48), lam=1.0,
+                          rnn=True, rnn_hidden=40, horizon=3)
+    return ppo_config(B=B_LOC, T=T, mode=mode, use_z_filter=True)
+
+
+def _worker(rank, world, port, mode, outdir, rnn):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     import torch.distributed as dist
@@ -34,13 +42,16 @@ def _worker(rank, world, port, mode, outdir):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from surreal_amd import synthetic
     from surreal_amd.learner import PPOLearner, TorchDistAllReduce
-    from tests.helpers import env_config, ppo_config
-    lc = ppo_config(B=B_LOC, T=T, mode=mode, use_z_filter=True)
+    from tests.helpers import env_config
+    lc = _cfg(mode, rnn)
     learner = PPOLearner(lc, env_config(D, A), seed=21, device='cuda:0', dp=TorchDistAllReduce())
     init = {'actor': learner.model.actor.flat.cpu(), 'critic': learner.model.critic.flat.cpu()}
+    if rnn:
+        init['lstm'] = learner.model.rnn_stem.flat.cpu()
     res = []
     for it in range(2):
-        full = synthetic.ppo_batch(B_LOC * world, T, D, A, seed=500 + it)
+        full = synthetic.ppo_batch(B_LOC * world, T, D, A, seed=500 + it,
+                                   rnn_hidden=40 if rnn else None)
         dev = synthetic.to_device(full, 'cuda:0')
         lo, hi = rank * B_LOC, (rank + 1) * B_LOC
 
@@ -54,30 +65,40 @@ def _worker(rank, world, port, mode, outdir):
             return x[lo:hi].contiguous()
         learner.learn(cut(dev))
         st = learner.last_stats()
-        res.append({'actor': learner.model.actor.flat.cpu(), 'critic': learner.model.critic.flat.cpu(),
-                    'zsum': learner.model.z_filter.running_sum.cpu(), 'stats': st})
+        r = {'actor': learner.model.actor.flat.cpu(), 'critic': learner.model.critic.flat.cpu(),
+             'zsum': learner.model.z_filter.running_sum.cpu(), 'stats': st}
+        if rnn:
+            r['lstm'] = learner.model.rnn_stem.flat.cpu()
+        res.append(r)
     torch.save({'init': init, 'res': res}, os.path.join(outdir, f'rank{rank}.pt'))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('mode', ['adapt', 'clip'])
-def test_two_process_dp_learn_matches_oracle(mode):
+@pytest.mark.parametrize('mode,rnn', [('adapt', False), ('clip', False), ('adapt', True),
+                                      ('clip', True)])
+def test_two_process_dp_learn_matches_oracle(mode, rnn):
     from oracle import ppo_ref as R
     from surreal_amd import synthetic
-    from tests.helpers import max_rel_err, oracle_batch, ppo_config
+    from tests.helpers import load_lstm_flat, lstm_flat, max_rel_err, oracle_batch
     from tests.test_gpu_ppo import _compare_params
     world = 2
     with tempfile.TemporaryDirectory() as outdir:
-        mp.spawn(_worker, args=(world, _free_port(), mode, outdir), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), mode, outdir, rnn), nprocs=world, join=True)
         out = [torch.load(os.path.join(outdir, f'rank{r}.pt'), weights_only=True) for r in range(world)]
-    ref = R.PPOLearnerRef(ppo_config(B=B_LOC * world, T=T, mode=mode, use_z_filter=True), D, A)
+    lc = _cfg(mode, rnn)
+    lc.replay.batch_size = B_LOC * world
+    ref = R.PPOLearnerRef(lc, D, A)
     ref.model.actor.load_flat(out[0]['init']['actor'])
     ref.model.critic.load_flat(out[0]['init']['critic'])
     ref.ref_target_model.actor.load_flat(out[0]['init']['actor'])
     ref.ref_target_model.critic.load_flat(out[0]['init']['critic'])
+    if rnn:
+        load_lstm_flat(ref.model.rnn_stem, out[0]['init']['lstm'])
+        load_lstm_flat(ref.ref_target_model.rnn_stem, out[0]['init']['lstm'])
     report = {}
     for it in range(2):
-        rstats = ref.learn(oracle_batch(synthetic.ppo_batch(B_LOC * world, T, D, A, seed=500 + it)))
+        rstats = ref.learn(oracle_batch(synthetic.ppo_batch(B_LOC * world, T, D, A, seed=500 + it,
+                                                            rnn_hidden=40 if rnn else None)))
         r0, r1 = out[0]['res'][it], out[1]['res'][it]
         assert torch.equal(r0['actor'], r1['actor']) and torch.equal(r0['critic'], r1['critic'])
         assert torch.equal(r0['zsum'], r1['zsum'])
@@ -88,5 +109,9 @@ def test_two_process_dp_learn_matches_oracle(mode):
         _compare_params(f'actor{it}', r0['actor'], ref.model.actor.flat(), 3e-4,
                         rstats['epochs_run'], report)
         _compare_params(f'critic{it}', r0['critic'], ref.model.critic.flat(), 3e-4, 10, report)
+        if rnn:
+            assert torch.equal(r0['lstm'], r1['lstm'])
+            _compare_params(f'lstm{it}', r0['lstm'], lstm_flat(ref.model.rnn_stem), 3e-4,
+                            rstats['epochs_run'] + 10, report)
         assert max_rel_err(r0['zsum'], ref.model.z_filter.running_sum) < 1e-5
     print('two-process dp report:', report)
