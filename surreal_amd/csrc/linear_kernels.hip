@@ -19,6 +19,7 @@
 // contiguous dimension (leading dims 36 / 80: conflict-free MFMA operand
 // reads and contiguous-dimension stores).  Global loads use clamped addresses
 // and are zeroed afterwards (no predicated loads: see cdna_hip_programming.md).
+#include <type_traits>
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
 
@@ -61,6 +62,20 @@ template <bool KCONTIG>
 __device__ __forceinline__ void gemm_load(const float* __restrict__ P, int64_t rs, int64_t cs,
                                           int r0, int rdata, int k0, int kmax, int ones_col,
                                           bool vec, TileRegs& t) {
+  // interior tile (all 64 rows and 32 k valid, no synthesised column): plain
+  // 16-byte loads, no clamps or masks
+  if (vec && ones_col < 0 && r0 + 64 <= rdata && k0 + 32 <= kmax) {
+    const float* base = KCONTIG ? P + (int64_t)r0 * rs + k0 : P + (int64_t)k0 * cs + r0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = threadIdx.x + j * kWG;
+      const float* src = KCONTIG ? base + (int64_t)(q >> 3) * rs + ((q & 7) << 2)
+                                 : base + (int64_t)(q >> 4) * cs + ((q & 15) << 2);
+      const float4 x = *reinterpret_cast<const float4*>(src);
+      t.v[4 * j + 0] = x.x; t.v[4 * j + 1] = x.y; t.v[4 * j + 2] = x.z; t.v[4 * j + 3] = x.w;
+    }
+    return;
+  }
   if (vec) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -150,67 +165,86 @@ gemm_kernel(GemmArgs g) {
   f32x4 tot[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) tot[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  TileRegs va, vb;
+  // two K-steps of operands in flight in registers (R[0], R[1]) ahead of the
+  // LDS double buffer: the global loads of step kt+2 are issued before step
+  // kt's MFMAs, so each load has two compute phases to land
+  TileRegs ra[2], rb[2];
   const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
   if (nk > 0) {
-    gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb, ke, -1, g.avec, va);
-    gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, bdata, kb, ke, g.ones_col, g.bvec, vb);
-    gemm_store<AK>(sA[0], g.avec, va);
-    gemm_store<BK>(sB[0], g.bvec, vb);
+    gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb, ke, -1, g.avec, ra[0]);
+    gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, bdata, kb, ke, g.ones_col, g.bvec, rb[0]);
+  }
+  if (nk > 1) {
+    gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb + GBK, ke, -1, g.avec, ra[1]);
+    gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, bdata, kb + GBK, ke, g.ones_col, g.bvec, rb[1]);
+  }
+  if (nk > 0) {
+    gemm_store<AK>(sA[0], g.avec, ra[0]);
+    gemm_store<BK>(sB[0], g.bvec, rb[0]);
   }
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb + (kt + 1) * GBK, ke, -1, g.avec, va);
-      gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, bdata, kb + (kt + 1) * GBK, ke, g.ones_col, g.bvec,
-                    vb);
+  const int ar = wave * 16 + li;
+  // one K-step from LDS image `cur`; register slot `cur` refills with step
+  // kt+2, slot cur^1 (step kt+1) goes to the other LDS image afterwards.  The
+  // loop is unrolled by two so the slots are compile-time registers.
+  auto kstep = [&](int kt, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value;
+    if (kt + 2 < nk) {
+      gemm_load<AK>(g.A, g.a_rs, g.a_cs, m0, g.M, kb + (kt + 2) * GBK, ke, -1, g.avec, ra[cur]);
+      gemm_load<BK>(g.B, g.b_cs, g.b_rs, n0, bdata, kb + (kt + 2) * GBK, ke, g.ones_col, g.bvec,
+                    rb[cur]);
     }
     const float* As = sA[cur];
     const float* Bs = sB[cur];
-    const int ar = wave * 16 + li;
     // two-level accumulation: each K-step (32 products per output) starts a
     // fresh MFMA chain that is then added to the running sums — fp32 error of
     // a 32-term chain plus an nk-term chain instead of one 32*nk-term chain
     f32x4 acc[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // every operand of the K-step is read from LDS first, then 32 MFMAs run
+    // back to back on 4 independent accumulator chains
+    float av[8], bv[4][8];
 #pragma unroll
-    for (int ks = 0; ks < GBK; ks += 8) {
-      float a0, a1, b0[4], b1[4];
-      const int k0 = ks + lk, k1 = ks + 4 + lk;
-      a0 = AK ? As[ar * LD_KC + k0] : As[k0 * LD_RC + ar];
-      a1 = AK ? As[ar * LD_KC + k1] : As[k1 * LD_RC + ar];
+    for (int u = 0; u < 8; ++u) {
+      const int k = 4 * u + lk;
+      av[u] = AK ? As[ar * LD_KC + k] : As[k * LD_RC + ar];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int n = c * 16 + li;
-        b0[c] = BK ? Bs[n * LD_KC + k0] : Bs[k0 * LD_RC + n];
-        b1[c] = BK ? Bs[n * LD_KC + k1] : Bs[k1 * LD_RC + n];
+        bv[c][u] = BK ? Bs[n * LD_KC + k] : Bs[k * LD_RC + n];
       }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] = mfma4(a0, b0[c], acc[c]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] = mfma4(a1, b1[c], acc[c]);
     }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = mfma4(av[u], bv[c][u], acc[c]);
 #pragma unroll
     for (int c = 0; c < 4; ++c) tot[c] += acc[c];
     if (kt + 1 < nk) {
-      gemm_store<AK>(sA[cur ^ 1], g.avec, va);
-      gemm_store<BK>(sB[cur ^ 1], g.bvec, vb);
+      gemm_store<AK>(sA[cur ^ 1], g.avec, ra[cur ^ 1]);
+      gemm_store<BK>(sB[cur ^ 1], g.bvec, rb[cur ^ 1]);
     }
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    kstep(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < nk) kstep(kt + 1, std::integral_constant<int, 1>{});
   }
+  // epilogue: 4 rows x 4 columns per lane, biases hoisted per column
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int n = n0 + c * 16 + li;
     if (n >= g.N) continue;
+    float bias_n = 0.f;
+    if constexpr (EPI == EPI_FWD) bias_n = g.bias ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wave * 16 + lk * 4 + i;
       if (m >= g.M) continue;
       float v = tot[c][i];
       if constexpr (EPI == EPI_FWD) {
-        v += g.bias ? g.bias[n] : 0.f;
+        v += bias_n;
         if (g.act == ACT_RELU) v = v > 0.f ? v : 0.f;
         else if (g.act == ACT_TANH) v = tanhf(v);
         g.C[(int64_t)m * g.ldc + n] = v;
@@ -292,16 +326,16 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   int S = 1;
   g.part = nullptr;
   g.kchunk = g.K > 0 ? g.K : 1;
-  if (epi == EPI_DW && g.K > 4 * GBK) {
+  if (epi == EPI_DW && g.K > 8 * GBK) {
     const int tiles = gm * gn;
     S = (1024 + tiles - 1) / tiles;                   // ~4 workgroups per CU
-    const int smax = (g.K + 4 * GBK - 1) / (4 * GBK);   // >= 4 K-steps per slab
+    const int smax = (g.K + 8 * GBK - 1) / (8 * GBK);   // >= 8 K-steps per slab
     if (S > smax) S = smax;
     const int64_t cap = smi_workspace_floats() / ((int64_t)g.M * g.N);
     if (S > cap) S = (int)cap;
     if (S < 1) S = 1;
     if (S > 1) {
-      g.kchunk = ((g.K + S - 1) / S + GBK - 1) / GBK * GBK;
+      g.kchunk = ((g.K + S - 1) / S + 31) / 32 * 32;
       S = (g.K + g.kchunk - 1) / g.kchunk;
       g.part = workspace_f32((int64_t)S * g.M * g.N);
       if (!g.part) return set_error(SMI_E_ARG, "gemm: workspace unavailable for split-K");
