@@ -24,6 +24,26 @@ namespace smi {
 
 constexpr int LR = 16;   // segments per workgroup
 
+// Developer phase timer (build variant 'prof', -DSMI_PROF): workgroup 0, wave
+// 0 accumulates wall-clock ticks (100 MHz) per step phase:
+//   [0] fwd MFMA (incl. LDS operand reads)  [1] fwd epilogue  [2] fwd barrier
+//   [3] bwd element-wise + stores           [4] bwd barrier   [5] bwd MFMA
+#ifdef SMI_PROF
+__device__ unsigned long long g_lstm_ticks[8];
+#define LSTM_T0() unsigned long long t_prev_ = wall_clock64()
+#define LSTM_TICK(id)                                                       \
+  do {                                                                      \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                              \
+      const unsigned long long n_ = wall_clock64();                         \
+      g_lstm_ticks[id] += n_ - t_prev_;                                     \
+      t_prev_ = n_;                                                         \
+    }                                                                       \
+  } while (0)
+#else
+#define LSTM_T0() (void)0
+#define LSTM_TICK(id) (void)0
+#endif
+
 // LDS leading dim for a [16][K] A-operand image: >= round4(K) and == 4 (mod 8),
 // so the 16 rows x 4 k of one MFMA operand read hit 64 distinct banks.
 __host__ __device__ inline int lstm_ld(int k) {
@@ -36,6 +56,12 @@ __host__ __device__ inline int lstm_ld(int k) {
 // ulp each): sigmoid(x) = 1/(1 + 2^(-x log2 e)), tanh(x) = 2 sigmoid(2x) - 1.
 // Absolute error ~1e-7 (fp32 rounding level of the gate values); the libm
 // forms cost ~4x the VALU issue slots and made the sequence kernels VALU-bound.
+// k-order of the register kernels: lane group lk (= lane >> 4) owns the
+// contiguous quarter k = lk*KS + s, s < KS, of the (padded) K range, so the A
+// operand of 4 consecutive k-steps is one 16-byte LDS read (the MFMA only needs
+// every k to appear once across the 4 lane groups).
+__host__ __device__ inline int lstm_q(int K) { return (((K + 3) >> 2) + 3) & ~3; }
+
 __device__ __forceinline__ float sigm(float x) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
 }
@@ -60,7 +86,7 @@ lstm_fwd_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int H = a.H, B = a.B, G4 = 4 * H;
-  const int LDH = lstm_ld(H);
+  const int LDH = lstm_ld(4 * lstm_q(H));
   float* hA[2] = {sm, sm + LR * LDH};
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
@@ -309,7 +335,7 @@ lstm_fwd_reg_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int H = a.H, B = a.B, G4 = 4 * H;
-  const int LDH = lstm_ld(H);
+  const int LDH = lstm_ld(4 * KS);
   float* hA[2] = {sm, sm + LR * LDH};
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
@@ -327,7 +353,6 @@ lstm_fwd_reg_kernel(LstmFwdArgs a) {
     hA[1][e] = 0.f;
     if (ok) a.hbuf[(int64_t)(r0 + r) * H + k] = v;        // hbuf[0] = h0
   }
-  const int nks = (H + 3) >> 2;
   float w[4][KS];
   float bh[4];
 #pragma unroll
@@ -335,8 +360,9 @@ lstm_fwd_reg_kernel(LstmFwdArgs a) {
     const float* wr = a.w_hh + (int64_t)(g * H + uc) * H;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int k = 4 * s + lk;
-      w[g][s] = wr[k < H ? k : H - 1];
+      const int k = lk * KS + s;
+      const float x = wr[k < H ? k : H - 1];
+      w[g][s] = k < H ? x : 0.f;
     }
     bh[g] = a.b_hh[g * H + uc];
   }
@@ -349,6 +375,7 @@ lstm_fwd_reg_kernel(LstmFwdArgs a) {
     if (ok && a.cbuf) a.cbuf[(int64_t)gr * H + unit] = creg[i];
   }
   __syncthreads();
+  LSTM_T0();
   for (int t = 0; t < a.S; ++t) {
     const float* hp = hA[t & 1];
     float* hn = hA[(t + 1) & 1];
@@ -365,15 +392,17 @@ lstm_fwd_reg_kernel(LstmFwdArgs a) {
       f32x4 acc[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const float* ap = hp + li * LDH + lk;
+      const float4* ap4 = reinterpret_cast<const float4*>(hp + li * LDH + lk * KS);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        if (s < nks) {
-          const float av = ap[4 * s];
+      for (int s4 = 0; s4 < KS / 4; ++s4) {
+        const float4 av = ap4[s4];
+        const float avs[4] = {av.x, av.y, av.z, av.w};
 #pragma unroll
-          for (int g = 0; g < 4; ++g) acc[g] = mfma4(av, w[g][s], acc[g]);
-        }
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[g] = mfma4(avs[j], w[g][4 * s4 + j], acc[g]);
       }
+      LSTM_TICK(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = lk * 4 + i, gr = r0 + row;
@@ -396,8 +425,10 @@ lstm_fwd_reg_kernel(LstmFwdArgs a) {
           }
         }
       }
+      LSTM_TICK(1);
     }
     __syncthreads();
+    LSTM_TICK(2);
   }
 }
 
@@ -418,11 +449,10 @@ lstm_bwd_reg_kernel(LstmBwdArgs a) {
   const int unit = wave * 16 + li;
   const int uc = unit < H ? unit : H - 1;
   for (int e = threadIdx.x; e < 2 * LR * LDG; e += kWG8) sm[e] = 0.f;
-  const int nks = H;                    // K = 4H in k-steps of 4
-  float w[KS];                          // W_hh[4s + lk][unit]
+  float w[KS];                          // W_hh[lk*KS + s][unit]  (KS == H, K = 4H)
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    const int k = 4 * s + lk;
+    const int k = lk * KS + s;
     w[s] = a.w_hh[(int64_t)(k < G4 ? k : G4 - 1) * H + uc];
   }
   // per-lane element offsets of the 4 rows (clamped rows read row B-1)
@@ -450,6 +480,7 @@ lstm_bwd_reg_kernel(LstmBwdArgs a) {
   float dcreg[4] = {0.f, 0.f, 0.f, 0.f};
   f32x4 dhrec = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
+  LSTM_T0();
   for (int t = a.S - 1; t >= 0; --t) {
     float* dg = dG[t & 1];
     if (active) {
@@ -474,20 +505,43 @@ lstm_bwd_reg_kernel(LstmBwdArgs a) {
         }
       }
     }
+    LSTM_TICK(3);
     __syncthreads();
+    LSTM_TICK(4);
     if (t == 0) break;
     if (active) {
       fetch(t - 1);
-      dhrec = f32x4{0.f, 0.f, 0.f, 0.f};
-      const float* ap = dg + li * LDG + lk;
+      // two accumulator chains (alternating 4-step groups), 16-byte A reads
+      f32x4 h0 = f32x4{0.f, 0.f, 0.f, 0.f}, h1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float4* ap4 = reinterpret_cast<const float4*>(dg + li * LDG + lk * KS);
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        if (s < nks) dhrec = mfma4(ap[4 * s], w[s], dhrec);
+      for (int s4 = 0; s4 < KS / 4; ++s4) {
+        const float4 av = ap4[s4];
+        if (s4 & 1) {
+          h1 = mfma4(av.x, w[4 * s4], h1); h1 = mfma4(av.y, w[4 * s4 + 1], h1);
+          h1 = mfma4(av.z, w[4 * s4 + 2], h1); h1 = mfma4(av.w, w[4 * s4 + 3], h1);
+        } else {
+          h0 = mfma4(av.x, w[4 * s4], h0); h0 = mfma4(av.y, w[4 * s4 + 1], h0);
+          h0 = mfma4(av.z, w[4 * s4 + 2], h0); h0 = mfma4(av.w, w[4 * s4 + 3], h0);
+        }
+      }
+      dhrec = h0 + h1;
+      LSTM_TICK(5);
     }
   }
 }
 
-int64_t lstm_fwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(H) * 4; }
+#ifdef SMI_PROF
+extern "C" int smi_lstm_phase_ticks(unsigned long long* out /* [8] */) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_ticks), sizeof(g_lstm_ticks)) != hipSuccess)
+    return SMI_E_LAUNCH;
+  static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_lstm_ticks), zero, sizeof(zero)) == hipSuccess ? SMI_OK
+                                                                                        : SMI_E_LAUNCH;
+}
+#endif
+
+int64_t lstm_fwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * lstm_q(H)) * 4; }
 int64_t lstm_bwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * H) * 4; }
 
 int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
@@ -503,13 +557,15 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
   const size_t lds = (size_t)lstm_fwd_lds(H);
   const dim3 grid((B + LR - 1) / LR);
   if (H <= 64) {
-    allow_lds(lstm_fwd_reg_kernel<16>, lds);
-    hipLaunchKernelGGL(lstm_fwd_reg_kernel<16>, grid, dim3(kWG8), lds, st, a);
+    const size_t l16 = (size_t)2 * LR * lstm_ld(4 * 16) * 4;
+    allow_lds(lstm_fwd_reg_kernel<16>, l16);
+    hipLaunchKernelGGL(lstm_fwd_reg_kernel<16>, grid, dim3(kWG8), l16, st, a);
     return check_launch("lstm_fwd_reg_kernel");
   }
-  if (H <= 100) {                      // the reference default H = 100: 100 W regs/lane
-    allow_lds(lstm_fwd_reg_kernel<25>, lds);
-    hipLaunchKernelGGL(lstm_fwd_reg_kernel<25>, grid, dim3(kWG8), lds, st, a);
+  if (H <= 112) {                      // the reference default H = 100: 112 W regs/lane
+    const size_t l28 = (size_t)2 * LR * lstm_ld(4 * 28) * 4;
+    allow_lds(lstm_fwd_reg_kernel<28>, l28);
+    hipLaunchKernelGGL(lstm_fwd_reg_kernel<28>, grid, dim3(kWG8), l28, st, a);
     return check_launch("lstm_fwd_reg_kernel");
   }
   const int nut = (H + 15) / 16;
@@ -538,12 +594,12 @@ int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, cons
   const size_t lds = (size_t)lstm_bwd_lds(H);
   if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "lstm: hidden size too large for LDS");
   const dim3 grid((B + LR - 1) / LR);
-  if (H <= 64) {
+  if (H == 64) {
     allow_lds(lstm_bwd_reg_kernel<64>, lds);
     hipLaunchKernelGGL(lstm_bwd_reg_kernel<64>, grid, dim3(kWG8), lds, st, a);
     return check_launch("lstm_bwd_reg_kernel");
   }
-  if (H <= 100) {
+  if (H == 100) {                      // the reference default: KS must equal H
     allow_lds(lstm_bwd_reg_kernel<100>, lds);
     hipLaunchKernelGGL(lstm_bwd_reg_kernel<100>, grid, dim3(kWG8), lds, st, a);
     return check_launch("lstm_bwd_reg_kernel");
