@@ -326,10 +326,10 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   int S = 1;
   g.part = nullptr;
   g.kchunk = g.K > 0 ? g.K : 1;
-  if (epi == EPI_DW && g.K > 8 * GBK) {
+  if (epi == EPI_DW && g.K > 4 * GBK) {
     const int tiles = gm * gn;
     S = (1024 + tiles - 1) / tiles;                   // ~4 workgroups per CU
-    const int smax = (g.K + 8 * GBK - 1) / (8 * GBK);   // >= 8 K-steps per slab
+    const int smax = (g.K + 4 * GBK - 1) / (4 * GBK);   // >= 4 K-steps per slab
     if (S > smax) S = smax;
     const int64_t cap = smi_workspace_floats() / ((int64_t)g.M * g.N);
     if (S > cap) S = (int)cap;
