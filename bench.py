@@ -10,6 +10,9 @@ over 2/4/8 GPUs"): the reference PPO defaults — LSTM policy
 with robosuite SawyerLift state dims (obs 42, act 8; SURVEY §8 notes 42 is an
 assumption) and 1024 segments per learn() on each GPU.
 --config c2 (BASELINE configs[1]): HalfCheetah dims, 64x64 MLP, 64 x 50.
+--config c5 (BASELINE configs[4]): C3 plus the pixel stem — camera0
+3x84x84 uint8 -> conv 16@8s4 -> 32@4s2 -> FC 256, LSTM input 42 + 256 — at
+128 segments per GPU (the 1024-segment batch over 8 GPUs).
 
 With --gpus N the learner is data parallel: each rank holds its
 own batch shard and the ranks all-reduce advantage moments, per-epoch
@@ -42,7 +45,7 @@ HBM_PEAK_GBS = 8000.0
 
 
 def make_config(name):
-    from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, gym_env_config
+    from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, gym_env_config, pixel_env_config
     lc = copy.deepcopy(PPO_DEFAULT_LEARNER_CONFIG)
     if name == 'c2':
         lc.model.actor_fc_hidden_sizes = [64, 64]
@@ -66,6 +69,11 @@ def make_config(name):
     lc.algo.rnn.rnn_layer = 1
     lc.algo.rnn.horizon = 5
     lc.replay.batch_size = 1024
+    if name == 'c5':
+        lc.replay.batch_size = 128
+        lc.model.cnn_feature_dim = 256
+        return lc, pixel_env_config(42, 8, (3, 84, 84)), dict(D=42, A=8, rnn_hidden=100,
+                                                               pixel=(3, 84, 84))
     return lc, gym_env_config(42, 8), dict(D=42, A=8, rnn_hidden=100)
 
 
@@ -88,10 +96,13 @@ def cpu_baseline(name, lc, dims, budget_s=12.0):
     lc = copy.deepcopy(lc)
     if name == 'c3':
         lc.replay.batch_size = 128
+    if name == 'c5':
+        lc.replay.batch_size = 8
     B, T = lc.replay.batch_size, lc.algo.n_step
     D, A = dims['D'], dims['A']
-    ref = R.PPOLearnerRef(lc, D, A)
-    batches = [oracle_batch(synthetic.ppo_batch(B, T, D, A, seed=i, rnn_hidden=dims['rnn_hidden']))
+    ref = R.PPOLearnerRef(lc, D, A, pixel=dims.get('pixel'))
+    batches = [oracle_batch(synthetic.ppo_batch(B, T, D, A, seed=i, rnn_hidden=dims['rnn_hidden'],
+                                                pixel=dims.get('pixel')))
                for i in range(2)]
     ref.learn(batches[1])
     times = []
@@ -116,7 +127,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', choices=['c2', 'c3'], default='c3')
+    ap.add_argument('--config', choices=['c2', 'c3', 'c5'], default='c3')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
     args = ap.parse_args()
@@ -142,7 +153,8 @@ def main():
     dp = TorchDistAllReduce() if dist is not None else None
     learner = PPOLearner(lc, ec, seed=1, device=dev, dp=dp)
     pool = [synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=rank * 1000 + i,
-                                                    rnn_hidden=dims['rnn_hidden']), dev)
+                                                    rnn_hidden=dims['rnn_hidden'],
+                                                    pixel=dims.get('pixel')), dev)
             for i in range(4)]
 
     def barrier():
@@ -208,7 +220,11 @@ def main():
                 'avg_ms': round(kdur[dom], 5), 'algorithmic_flops_per_launch': int(fl)}
     ms = elapsed / args.steps * 1e3
     value = world * B * T * args.steps / elapsed
-    if args.config == 'c3':
+    if args.config == 'c5':
+        wl = ('C5: C3 (LSTM 100, horizon 5, heads 300x200, n_step 25, adapt, z-filter, 10/10 '
+              'epochs, obs 42, act 8) + pixel stem: camera0 3x84x84 uint8 -> conv 16@8s4 -> '
+              '32@4s2 -> FC 256; 128 segments per GPU (1024 over 8 GPUs)')
+    elif args.config == 'c3':
         wl = ('C3: synthetic PPO learner batch, reference PPO defaults (LSTM 100, horizon 5, heads '
               '300x200, n_step 25, adapt, z-filter, 10/10 epochs), SawyerLift state dims (obs 42, '
               'act 8), 1024 segments per GPU')

@@ -52,6 +52,8 @@ int     smi_set_workspace(void* dev_ptr, int64_t bytes);
 #define SMI_KT_GEMM_REDUCE 3
 #define SMI_KT_LSTM_FWD    4
 #define SMI_KT_LSTM_BWD    5
+#define SMI_KT_CNN_FWD     6
+#define SMI_KT_CNN_BWD     7
 int smi_kernel_timing(int on);
 int smi_kernel_timing_report(int cls, double* out4);
 
@@ -363,13 +365,23 @@ typedef struct smi_ppo_rnn_args {
   double* zbuf;                      /* [5 + 2*D] value sums | ZFilter column sums            */
   /* device scratch, smi_ppo_rnn_scratch_bytes() */
   void* scratch; int64_t scratch_bytes;
+  /* optional pixel stem (if_pixel_input, ppo_net.py:137-141,268-275): the
+   * LSTM input is [zfilter(low_dim) | CNN(camera0/255)] (D + cnn_feat wide);
+   * cnn_feat == 0 disables it.  With it, `lstm` / `ref_lstm` point at the
+   * joint stem buffer [lstm (in = D + cnn_feat) | cnn (smi_cnn_param_count)],
+   * and the Adam state / xbuf segments are [head | lstm | cnn]. */
+  int pix_c, pix_h, pix_w, cnn_feat;
+  const uint8_t* pixels;        /* [B][T][C][H][W] uint8 (obs['pixel']['camera0'])      */
+  const uint8_t* pixels_next;   /* [B][1][C][H][W] uint8 (obs_next['pixel']['camera0']) */
 } smi_ppo_rnn_args;
 
 #define SMI_RNN_PSTAT 16
 int64_t smi_ppo_rnn_scratch_bytes(int B, int T, int horizon, int obs_dim, int rnn_hidden,
-                                  int h1, int h2, int act_dim, int critic_h1, int critic_h2);
+                                  int h1, int h2, int act_dim, int critic_h1, int critic_h2,
+                                  int pix_c, int pix_h, int pix_w, int cnn_feat);
 int64_t smi_ppo_rnn_xbuf_floats(int obs_dim, int rnn_hidden, int h1, int h2, int act_dim,
-                                int critic_h1, int critic_h2);
+                                int critic_h1, int critic_h2, int pix_c, int pix_h, int pix_w,
+                                int cnn_feat);
 int64_t smi_lstm_param_count(int in_dim, int hidden);
 int smi_ppo_rnn_phase(const smi_ppo_rnn_args* args, int phase, int epoch, void* stream);
 
@@ -387,6 +399,26 @@ int smi_lstm_forward(const float* xproj, const float* w_hh, const float* b_hh,
                      float* hbuf, float* cbuf, float* gates_act, void* stream);
 int smi_lstm_backward(const float* dh, const float* gates_act, const float* cbuf,
                       const float* w_hh, int S, int B, int H, float* dgates, void* stream);
+
+/* Pixel stem: CNNStemNetwork (builders.py:8-33) on obs/255 (ppo_net.py:368-375)
+ *   conv 8x8/4 (C->16) -> ReLU -> conv 4x4/2 (16->32) -> ReLU -> Flatten -> Linear(F) -> ReLU
+ * Flat parameters [conv1.w (16,C,8,8) | conv1.b | conv2.w (32,16,4,4) | conv2.b |
+ * fc.w (F, 32*H2*W2) | fc.b].  Built for C == 3, W % 4 == 0 (84x84 cameras).
+ * Images are uint8, 16-byte aligned; activation row n = t*B + b reads
+ * pix[b][t] (t < T) or pix_next[b] (t == T) — a plain batch is B = rows, T = 1.
+ *   forward: a1 [rows][16][H1*W1] (optional, needed by backward), a2 [rows][32*H2*W2],
+ *            feat[n*ldf + f] = ReLU output.
+ *   backward: dz = gradient at the Linear pre-activation (ReLU mask applied,
+ *            row stride lddz); writes (not accumulates) the flat gradient. */
+int64_t smi_cnn_param_count(int C, int H, int W, int F);
+int64_t smi_cnn_scratch_bytes(int64_t rows, int C, int H, int W, int F);
+int smi_cnn_forward(const float* params, const uint8_t* pix, const uint8_t* pix_next, int64_t B,
+                    int64_t T, int64_t rows, int C, int H, int W, int F, float* a1, float* a2,
+                    float* feat, int64_t ldf, void* stream);
+int smi_cnn_backward(const float* params, const uint8_t* pix, const uint8_t* pix_next, int64_t B,
+                     int64_t T, int64_t rows, int C, int H, int W, int F, const float* a1,
+                     const float* a2, const float* dz, int64_t lddz, float* grad, void* scratch,
+                     int64_t scratch_bytes, void* stream);
 
 /* running_sum += sum_in, running_sumsq += sumsq_in, count += rows — the
  * data-parallel z_update after the column statistics were all-reduced. */

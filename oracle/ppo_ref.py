@@ -5,7 +5,8 @@ fp32 CPU restatement of the reference PPO learner hot path, op by op:
   ZFilter              surreal/model/z_filter.py:23-79
   RewardFilter         surreal/model/reward_filter.py:5-56 (its '=' bug at :42 kept)
   actor / critic MLPs  surreal/model/model_builders/builders.py:86-175
-  PPOModel forward     surreal/model/ppo_net.py:94-375 (low-dim + optional LSTM)
+  PPOModel forward     surreal/model/ppo_net.py:94-375 (low-dim, optional LSTM and
+                       pixel CNNStemNetwork, builders.py:8-33, on obs/255)
   GAE / returns        surreal/learner/ppo.py:355-418
   clip / adapt / value losses and updates   ppo.py:194-353
   _optimize            ppo.py:487-586
@@ -205,24 +206,47 @@ class CriticRef(nn.Module):
         self.model.load_flat(f)
 
 
+def cnn_stem_ref(C, H, W, F):
+    """CNNStemNetwork (builders.py:8-33) with its default conv_channels [16, 32],
+    kernel_sizes [8, 4], strides [4, 2], no padding (torchx Conv2d default)."""
+    H1, W1 = (H - 8) // 4 + 1, (W - 8) // 4 + 1
+    H2, W2 = (H1 - 4) // 2 + 1, (W1 - 4) // 2 + 1
+    return nn.Sequential(nn.Conv2d(C, 16, 8, 4), nn.ReLU(), nn.Conv2d(16, 32, 4, 2), nn.ReLU(),
+                         nn.Flatten(), nn.Linear(32 * H2 * W2, F), nn.ReLU())
+
+
 class PPOModelRef(nn.Module):
-    """PPOModel (ppo_net.py:94-375) for low-dim observations (+ optional LSTM)."""
+    """PPOModel (ppo_net.py:94-375): low-dim observations, optional LSTM stem and
+    optional pixel stem.  With pixels an observation is the pair (low_dim or
+    None, camera0 uint8 (..., C, H, W))."""
 
     def __init__(self, obs_dim, act_dim, actor_hidden, critic_hidden, init_log_sig,
-                 use_z_filter, rnn=False, rnn_hidden=100, rnn_layer=1):
+                 use_z_filter, rnn=False, rnn_hidden=100, rnn_layer=1, pixel=None, cnn_feat=256):
         super().__init__()
         self.use_z_filter = use_z_filter
         self.rnn = rnn
-        self.rnn_stem = nn.LSTM(obs_dim, rnn_hidden, rnn_layer, batch_first=True) if rnn else None
-        d_in = rnn_hidden if rnn else obs_dim
+        self.pixel = pixel
+        self.cnn_stem = cnn_stem_ref(*pixel, cnn_feat) if pixel is not None else None
+        d_stem = obs_dim + (cnn_feat if pixel is not None else 0)
+        self.rnn_stem = nn.LSTM(d_stem, rnn_hidden, rnn_layer, batch_first=True) if rnn else None
+        d_in = rnn_hidden if rnn else d_stem
         self.actor = ActorRef(d_in, act_dim, actor_hidden, init_log_sig)
         self.critic = CriticRef(d_in, critic_hidden)
         if use_z_filter:
             self.z_filter = ZFilterRef(obs_dim)
 
     def _features(self, x, cells):
-        if self.use_z_filter:
-            x = self.z_filter.forward(x)
+        pix = None
+        if self.pixel is not None:
+            x, pix = x
+        parts = []
+        if x is not None:
+            parts.append(self.z_filter.forward(x) if self.use_z_filter else x)
+        if pix is not None:                                 # ppo_net.py:268-273, 368-375
+            lead = pix.shape[:-3]
+            img = pix.reshape(-1, *pix.shape[-3:]) / 255.0
+            parts.append(self.cnn_stem(img).reshape(*lead, -1))
+        x = parts[0] if len(parts) == 1 else torch.cat(parts, -1)
         if self.rnn:
             x, _ = self.rnn_stem(x, cells)
             x = x.contiguous()
@@ -239,20 +263,39 @@ class PPOModelRef(nn.Module):
         self.critic.load_state_dict(net.critic.state_dict())
         if self.rnn:
             self.rnn_stem.load_state_dict(net.rnn_stem.state_dict())
+        if self.pixel is not None:
+            self.cnn_stem.load_state_dict(net.cnn_stem.state_dict())
         if self.use_z_filter:
             self.z_filter.load_state_dict(net.z_filter.state_dict())
 
     def actor_params(self):                                 # ppo_net.py:202-212
         ps = list(self.actor.parameters())
+        if self.pixel is not None:
+            ps += list(self.cnn_stem.parameters())
         if self.rnn:
             ps += list(self.rnn_stem.parameters())
         return ps
 
     def critic_params(self):                                # ppo_net.py:214-224
         ps = list(self.critic.parameters())
+        if self.pixel is not None:
+            ps += list(self.cnn_stem.parameters())
         if self.rnn:
             ps += list(self.rnn_stem.parameters())
         return ps
+
+
+def _tmap(f, o):
+    """apply f to an observation or to each non-None part of a (low, pixel) pair"""
+    if isinstance(o, tuple):
+        return tuple(None if p is None else f(p) for p in o)
+    return f(o)
+
+
+def _tmap2(f, a, b):
+    if isinstance(a, tuple):
+        return tuple(None if p is None else f(p, q) for p, q in zip(a, b))
+    return f(a, b)
 
 
 # ---------------------------------------------------------------------- GAE
@@ -299,7 +342,7 @@ class PPOLearnerRef:
     surreal_amd.config.Config works).  obs are low-dim tensors (B, T, D).
     """
 
-    def __init__(self, lc, obs_dim, act_dim, seed=0):
+    def __init__(self, lc, obs_dim, act_dim, seed=0, pixel=None):
         torch.manual_seed(seed)
         g = lambda p, d=None: cfg_get(lc, p, d)  # noqa: E731
         self.gamma = g('algo.gamma')
@@ -333,7 +376,7 @@ class PPOLearnerRef:
         mk = lambda: PPOModelRef(  # noqa: E731
             obs_dim, act_dim, g('model.actor_fc_hidden_sizes'), g('model.critic_fc_hidden_sizes'),
             g('algo.consts.init_log_sig'), self.use_z_filter, self.rnn,
-            g('algo.rnn.rnn_hidden'), g('algo.rnn.rnn_layer'))
+            g('algo.rnn.rnn_hidden'), g('algo.rnn.rnn_layer'), pixel, g('model.cnn_feature_dim', 256))
         self.model = mk()
         self.ref_target_model = mk()
         self.ref_target_model.update_target_params(self.model)
@@ -409,10 +452,10 @@ class PPOLearnerRef:
 
     # -- GAE through the critic (ppo.py:355-418) ------------------------------
     def gae_and_return(self, obs, obs_next, rewards, dones):
-        x = torch.cat([obs, obs_next], dim=1)
-        B = x.shape[0]
+        x = _tmap2(lambda a, b: torch.cat([a, b], dim=1), obs, obs_next)
+        B = rewards.shape[0]
         if not self.rnn:
-            x = x.reshape(-1, x.shape[-1])
+            x = _tmap(lambda o: o.reshape(-1, *o.shape[2:]), x)
         values = self.model.forward_critic(x, self.cells).detach()
         values = values.view(B, self.n_step + 1)
         return gae_and_return(values, rewards, dones, self.gamma, self.lam, self.n_step,
@@ -439,11 +482,11 @@ class PPOLearnerRef:
             E = self.n_step - self.horizon + 1
             behave_pol = pds[:, :E, :].contiguous()
             actions_iter = actions[:, :E, :].contiguous()
-            obs_iter = obs[:, :E, :].contiguous()
+            obs_iter = _tmap(lambda o: o[:, :E].contiguous(), obs)
         else:
             behave_pol = pds[:, 0, :].contiguous()
             actions_iter = actions[:, 0, :].contiguous()
-            obs_iter = obs[:, 0, :].contiguous()
+            obs_iter = _tmap(lambda o: o[:, 0].contiguous(), obs)
         with torch.no_grad():
             ref_pol = self.ref_target_model.forward_actor(obs_iter, self.cells)
         epochs_run = 0
@@ -476,12 +519,17 @@ class PPOLearnerRef:
             stats['_ref_behave_diff'] = self.pd.kl(ref_pol, behave_pol).mean().item()
             stats['epochs_run'] = epochs_run
             if self.use_z_filter:                             # :578-582
-                self.model.z_filter.z_update(obs_iter)
+                self.model.z_filter.z_update(obs_iter[0] if isinstance(obs_iter, tuple)
+                                             else obs_iter)
         return stats
 
     def learn(self, batch):                                   # ppo.py:588-613
-        obs = torch.as_tensor(batch['obs'], dtype=torch.float32)
-        obs_next = torch.as_tensor(batch['obs_next'], dtype=torch.float32)
+        f32 = lambda a: None if a is None else torch.as_tensor(a, dtype=torch.float32)  # noqa: E731
+        obs = f32(batch['obs'])
+        obs_next = f32(batch['obs_next'])
+        if 'pixels' in batch:                 # (low_dim or None, camera0 uint8)
+            obs = (obs, torch.as_tensor(batch['pixels']))
+            obs_next = (obs_next, torch.as_tensor(batch['pixels_next']))
         actions = torch.as_tensor(batch['actions'], dtype=torch.float32)
         rewards = self.preprocess_rewards(batch['rewards'])
         dones = torch.as_tensor(batch['dones'], dtype=torch.float32)

@@ -82,13 +82,16 @@ class RNNArgs(ctypes.Structure):
         ('stats', P), ('kl_record', P), ('kl_count', P), ('kl_capacity', c_int),
         ('moments', P), ('pstat', P), ('xbuf', P), ('zbuf', P),
         ('scratch', P), ('scratch_bytes', c_i64),
+        ('pix_c', c_int), ('pix_h', c_int), ('pix_w', c_int), ('cnn_feat', c_int),
+        ('pixels', P), ('pixels_next', P),
     ]
 
 
 RNN_PH_GAE, RNN_PH_PREP, RNN_PH_POLICY_FWD, RNN_PH_POLICY_BWD, RNN_PH_POLICY_APPLY, \
     RNN_PH_VALUE_GRAD, RNN_PH_VALUE_APPLY, RNN_PH_ZSTATS, RNN_PH_ZAPPLY, RNN_PH_POLICY_DECIDE = range(10)
 RNN_PSTAT = 16
-KT_NAMES = ['gemm_fwd', 'gemm_dx', 'gemm_dw', 'gemm_splitk_reduce', 'lstm_fwd', 'lstm_bwd']
+KT_NAMES = ['gemm_fwd', 'gemm_dx', 'gemm_dw', 'gemm_splitk_reduce', 'lstm_fwd', 'lstm_bwd',
+            'cnn_fwd', 'cnn_bwd']
 
 
 def kernel_timing(on):
@@ -152,8 +155,13 @@ _SIGS = {
     'smi_lstm_param_count': (c_i64, [c_int, c_int]),
     'smi_kernel_timing': (c_int, [c_int]),
     'smi_kernel_timing_report': (c_int, [c_int, P]),
-    'smi_ppo_rnn_scratch_bytes': (c_i64, [c_int] * 10),
-    'smi_ppo_rnn_xbuf_floats': (c_i64, [c_int] * 7),
+    'smi_ppo_rnn_scratch_bytes': (c_i64, [c_int] * 14),
+    'smi_ppo_rnn_xbuf_floats': (c_i64, [c_int] * 11),
+    'smi_cnn_param_count': (c_i64, [c_int] * 4),
+    'smi_cnn_scratch_bytes': (c_i64, [c_i64] + [c_int] * 4),
+    'smi_cnn_forward': (c_int, [P, P, P, c_i64, c_i64, c_i64] + [c_int] * 4 + [P, P, P, c_i64, P]),
+    'smi_cnn_backward': (c_int, [P, P, P, c_i64, c_i64, c_i64] + [c_int] * 4 +
+                         [P, P, P, c_i64, P, P, c_i64, P]),
     'smi_ppo_rnn_phase': (c_int, [ctypes.POINTER(RNNArgs), c_int, c_int, P]),
     'smi_lstm_forward': (c_int, [P, P, P, P, P, c_int, c_int, c_int, P, P, P, P]),
     'smi_lstm_backward': (c_int, [P, P, P, P, c_int, c_int, c_int, P, P]),

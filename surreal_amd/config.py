@@ -170,6 +170,22 @@ BASE_SESSION_CONFIG = Config({
 })
 
 
+def pixel_env_config(obs_dim, act_dim, camera=(3, 84, 84)):
+    """env_config of a robosuite-style pixel env: obs_spec
+    {'low_dim': {'flat_inputs': (D,)}, 'pixel': {'camera0': (C, H, W)}} with
+    uint8 camera observations; obs_dim 0 drops the low-dim modality."""
+    spec = {'pixel': {'camera0': tuple(camera)}}
+    if obs_dim:
+        spec['low_dim'] = {'flat_inputs': (obs_dim,)}
+    return Config({
+        'pixel_input': True,
+        'frame_stacks': 1,
+        'frame_stack_concatenate_on_env': True,
+        'obs_spec': spec,
+        'action_spec': {'dim': (act_dim,), 'type': 'continuous'},
+    })
+
+
 def gym_env_config(obs_dim, act_dim, pixel_input=False):
     """env_config with obs_spec/action_spec as make_env_config fills them
     (surreal/env/make_env.py:16-38) for a flat low-dim gym env."""

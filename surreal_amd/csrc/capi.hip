@@ -399,26 +399,67 @@ int64_t smi_lstm_param_count(int in_dim, int hidden) {
 }
 
 int64_t smi_ppo_rnn_scratch_bytes(int B, int T, int horizon, int obs_dim, int rnn_hidden, int h1,
-                                  int h2, int act_dim, int critic_h1, int critic_h2) {
+                                  int h2, int act_dim, int critic_h1, int critic_h2, int pix_c,
+                                  int pix_h, int pix_w, int cnn_feat) {
   return ppo_rnn_scratch_bytes(B, T, horizon, obs_dim, rnn_hidden, h1, h2, act_dim, critic_h1,
-                               critic_h2);
+                               critic_h2, pix_c, pix_h, pix_w, cnn_feat);
 }
 
+int64_t smi_cnn_param_count(int C, int H, int W, int F) { return cnn_geom(C, H, W, F).total; }
+
 int64_t smi_ppo_rnn_xbuf_floats(int obs_dim, int rnn_hidden, int h1, int h2, int act_dim,
-                                int critic_h1, int critic_h2) {
-  const int64_t nl = smi_lstm_param_count(obs_dim, rnn_hidden);
+                                int critic_h1, int critic_h2, int pix_c, int pix_h, int pix_w,
+                                int cnn_feat) {
+  const int F = cnn_feat > 0 ? cnn_feat : 0;
+  const int64_t ns = smi_lstm_param_count(obs_dim + F, rnn_hidden) +
+                     (F > 0 ? smi_cnn_param_count(pix_c, pix_h, pix_w, F) : 0);
   return mlp_layout(rnn_hidden, h1, h2, act_dim, 1).fcount +
-         mlp_layout(rnn_hidden, critic_h1, critic_h2, 1, 0).fcount + 2 * nl;
+         mlp_layout(rnn_hidden, critic_h1, critic_h2, 1, 0).fcount + 2 * ns;
+}
+
+int64_t smi_cnn_scratch_bytes(int64_t rows, int C, int H, int W, int F) {
+  const CnnGeom g = cnn_geom(C, H, W, F);
+  return 4 * (rows * g.flat + (int64_t)cnn_bwd_grid(rows) * g.nconv);
+}
+
+int smi_cnn_forward(const float* params, const uint8_t* pix, const uint8_t* pix_next, int64_t B,
+                    int64_t T, int64_t rows, int C, int H, int W, int F, float* a1, float* a2,
+                    float* feat, int64_t ldf, void* stream) {
+  REQUIRE(params && pix && a2 && feat && B >= 1 && T >= 1 && rows >= 0 && ldf >= F,
+          "cnn_forward: bad args");
+  REQUIRE(rows <= B * T || pix_next, "cnn_forward: rows beyond B*T need pix_next");
+  const PixRows pr{pix, pix_next, B, T, (int64_t)C * H * W};
+  return cnn_forward(params, pr, C, H, W, F, rows, a1, a2, feat, ldf, SMI_STREAM(stream), nullptr);
+}
+
+int smi_cnn_backward(const float* params, const uint8_t* pix, const uint8_t* pix_next, int64_t B,
+                     int64_t T, int64_t rows, int C, int H, int W, int F, const float* a1,
+                     const float* a2, const float* dz, int64_t lddz, float* grad, void* scratch,
+                     int64_t scratch_bytes, void* stream) {
+  REQUIRE(params && pix && a1 && a2 && dz && grad && scratch && B >= 1 && T >= 1 && rows >= 0 &&
+          lddz >= F, "cnn_backward: bad args");
+  REQUIRE(rows <= B * T || pix_next, "cnn_backward: rows beyond B*T need pix_next");
+  REQUIRE(scratch_bytes >= smi_cnn_scratch_bytes(rows, C, H, W, F), "cnn_backward: scratch too small");
+  const CnnGeom g = cnn_geom(C, H, W, F);
+  float* dA2 = static_cast<float*>(scratch);
+  float* part = dA2 + rows * g.flat;
+  const PixRows pr{pix, pix_next, B, T, g.img};
+  return cnn_backward(params, pr, C, H, W, F, rows, a1, a2, dz, lddz, grad, dA2, part,
+                      SMI_STREAM(stream), nullptr);
 }
 
 int smi_ppo_rnn_phase(const smi_ppo_rnn_args* a, int phase, int epoch, void* stream) {
   REQUIRE(a, "ppo_rnn: null args");
   REQUIRE(a->B >= 1 && a->T >= 1 && a->horizon >= 1 && a->horizon <= a->T, "ppo_rnn: bad B/T/horizon");
-  REQUIRE(a->obs_dim >= 1 && a->obs_dim <= 128, "ppo_rnn: obs_dim must be in [1, 128]");
+  REQUIRE(a->obs_dim >= (a->cnn_feat > 0 ? 0 : 1) && a->obs_dim <= 128,
+          "ppo_rnn: obs_dim must be in [1, 128] ([0, 128] with a pixel stem)");
+  REQUIRE(a->cnn_feat <= 0 || (a->pixels && a->pixels_next),
+          "ppo_rnn: pixel stem needs pixels and pixels_next");
+  REQUIRE(!(a->use_zf && a->obs_dim == 0), "ppo_rnn: z-filter needs low-dim observations");
   REQUIRE(a->rnn_hidden >= 1 && a->rnn_hidden <= 256, "ppo_rnn: rnn_hidden must be in [1, 256]");
   REQUIRE(a->act_dim >= 1 && a->act_dim <= 32, "ppo_rnn: act_dim must be in [1, 32]");
   REQUIRE(a->h1 >= 1 && a->h2 >= 1 && a->critic_h1 >= 1 && a->critic_h2 >= 1, "ppo_rnn: bad hidden sizes");
-  REQUIRE(a->obs && a->obs_next && a->actions && a->rewards && a->dones && a->behave && a->h0 &&
+  REQUIRE((a->obs_dim == 0 || (a->obs && a->obs_next)) && a->actions && a->rewards && a->dones && a->behave && a->h0 &&
           a->c0, "ppo_rnn: null batch pointer");
   REQUIRE(a->lstm && a->actor && a->critic && a->ref_lstm && a->ref_actor, "ppo_rnn: null params");
   REQUIRE(a->actor_m && a->actor_v && a->critic_m && a->critic_v && a->actor_step &&

@@ -360,6 +360,16 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   return check_launch("gemm_splitk_reduce_kernel");
 }
 
+// out[i] = sum_{z < S} part[z][i] in a fixed order (no accumulate)
+int launch_slab_reduce(const float* part, int S, int64_t n, float* out, hipStream_t st,
+                       const int* skip) {
+  if (n < 1 || S < 1) return SMI_OK;
+  const int rg = (int)((n + 63) / 64);
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, part, S, 1, (int)n, out,
+                     n, -1, nullptr, 0, skip);
+  return check_launch("gemm_splitk_reduce_kernel");
+}
+
 int launch_linear_fwd(const float* X, int64_t ldx, int M, int K, const float* W, int64_t ldw,
                       const float* b, int N, int act, float* Y, int64_t ldy, hipStream_t st,
                       const int* skip) {

@@ -45,21 +45,28 @@ enum { CF_KLCOEF = 0, CF_SURRW, CF_COUNT = 8 };
 
 struct RnnDims {
   int B, T, Hz, E, S1, D, H, G4, A, h1, h2, c1, c2;
+  int F, Din;                         // pixel features (0: no CNN stem), LSTM input D + F
   int64_t NE, NG;
-  int64_t nA_head, nC_head, nL;       // parameter counts
+  int64_t nA_head, nC_head, nL, nCnn, nS;   // parameter counts; stem = [lstm | cnn]
   MlpLayout LA, LC;
+  CnnGeom G;
 };
 
 __host__ __device__ inline RnnDims rnn_dims(int B, int T, int Hz, int D, int H, int h1, int h2,
-                                            int A, int c1, int c2) {
+                                            int A, int c1, int c2, int pc = 0, int ph = 0,
+                                            int pw = 0, int F = 0) {
   RnnDims d;
+  d.F = F > 0 ? F : 0; d.Din = D + d.F;
+  d.G = cnn_geom(pc, ph, pw, d.F);
+  d.nCnn = d.F > 0 ? d.G.total : 0;
   d.B = B; d.T = T; d.Hz = Hz; d.E = T - Hz + 1; d.S1 = T + 1; d.D = D; d.H = H; d.G4 = 4 * H;
   d.A = A; d.h1 = h1; d.h2 = h2; d.c1 = c1; d.c2 = c2;
   d.NE = (int64_t)d.E * B; d.NG = (int64_t)d.S1 * B;
   d.LA = mlp_layout(H, h1, h2, A, 1);
   d.LC = mlp_layout(H, c1, c2, 1, 0);
   d.nA_head = d.LA.fcount; d.nC_head = d.LC.fcount;
-  d.nL = (int64_t)4 * H * D + (int64_t)4 * H * H + 8 * (int64_t)H;
+  d.nL = (int64_t)4 * H * d.Din + (int64_t)4 * H * H + 8 * (int64_t)H;
+  d.nS = d.nL + d.nCnn;
   return d;
 }
 
@@ -67,6 +74,7 @@ __host__ __device__ inline RnnDims rnn_dims(int B, int T, int Hz, int D, int H, 
 struct RnnScratch {
   float *Xz, *Xr, *xproj, *hbuf, *cbuf, *gates, *HA1, *HA2, *OUT, *dOUT, *dH1, *dH2, *dh, *dgates;
   float *values, *adv, *ret, *refmu, *lvpart;
+  float *A1, *A2, *dA2, *dF, *cpart;        // pixel stem (empty without one)
   double *part, *gaepart;
   int* ci; float* cf;
   int64_t total_floats;
@@ -85,8 +93,8 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   int64_t o = 0;
   auto take = [&](int64_t n) { float* r = p ? p + o : nullptr; o += al64(n); return r; };
   const int hmax1 = d.h1 > d.c1 ? d.h1 : d.c1, hmax2 = d.h2 > d.c2 ? d.h2 : d.c2;
-  s.Xz = take(d.NG * d.D);
-  s.Xr = take(d.NE * d.D);
+  s.Xz = take(d.NG * d.Din);
+  s.Xr = take(d.NE * d.Din);
   s.xproj = take(d.NG * d.G4);
   s.hbuf = take((int64_t)(d.S1 + 1) * d.B * d.H);
   s.cbuf = take((int64_t)(d.E + 1) * d.B * d.H);
@@ -104,6 +112,12 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   s.ret = take(d.NE);
   s.refmu = take(d.NE * d.A);
   s.lvpart = take((int64_t)1024 * d.A);
+  const bool px = d.F > 0;
+  s.A1 = take(px ? d.NE * 16 * d.G.P1 : 0);
+  s.A2 = take(px ? d.NG * d.G.flat : 0);
+  s.dA2 = take(px ? d.NE * d.G.flat : 0);
+  s.dF = take(px ? d.NE * d.F : 0);
+  s.cpart = take(px ? (int64_t)cnn_bwd_grid(d.NE) * d.G.nconv : 0);
   s.part = reinterpret_cast<double*>(take(2 * 4096 * 16));   // 65536 doubles
   s.gaepart = reinterpret_cast<double*>(take(2 * 2 * 2048));
   s.ci = reinterpret_cast<int*>(take(CI_COUNT));
@@ -118,7 +132,7 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
 __global__ void __launch_bounds__(kWG)
 zf_tmajor_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next, int B, int T,
                  int S, int D, int use_zf, const float* zs, const float* zq, const float* zc,
-                 float eps, float* __restrict__ out) {
+                 float eps, float* __restrict__ out, int ldo) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* zm = sm;
   float* zd = sm + round4(D);
@@ -131,7 +145,7 @@ zf_tmajor_kernel(const float* __restrict__ obs, const float* __restrict__ obs_ne
     const int t = (int)(row / B), b = (int)(row - (int64_t)t * B);
     float v = t < T ? obs[((int64_t)b * T + t) * D + c] : obs_next[(int64_t)b * D + c];
     if (use_zf) v = fminf(fmaxf((v - zm[c]) / zd[c], -5.f), 5.f);
-    out[e] = v;
+    out[row * ldo + c] = v;
   }
 }
 
@@ -625,8 +639,8 @@ static int lstm_forward(const RnnDims& d, const LstmP& l, const float* X, int S,
                         const float* c0, const RnnScratch& s, float* cbuf, float* gates,
                         hipStream_t st, const int* skip) {
   const int64_t rows = (int64_t)S * d.B;
-  RC(launch_linear_fwd(X, d.D, (int)rows, d.D, l.Wih, d.D, l.bih, d.G4, ACT_NONE, s.xproj, d.G4,
-                       st, skip));
+  RC(launch_linear_fwd(X, d.Din, (int)rows, d.Din, l.Wih, d.Din, l.bih, d.G4, ACT_NONE, s.xproj,
+                       d.G4, st, skip));
   return launch_lstm_fwd(s.xproj, l.Whh, l.bhh, h0, c0, S, d.B, d.H, s.hbuf, cbuf, gates, st,
                          skip);
 }
@@ -636,14 +650,40 @@ static int lstm_backward(const RnnDims& d, const LstmP& l, float* G, const RnnSc
                          hipStream_t st, const int* skip) {
   RC(launch_lstm_bwd(s.dh, s.gates, s.cbuf, l.Whh, d.E, d.B, d.H, s.dgates, st, skip));
   float* gWih = G;
-  float* gWhh = G + (int64_t)4 * d.H * d.D;
+  float* gWhh = G + (int64_t)4 * d.H * d.Din;
   float* gbih = gWhh + (int64_t)4 * d.H * d.H;
   float* gbhh = gbih + d.G4;
   const int M = (int)d.NE;
-  RC(launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.Xz, d.D, d.D, gWih, d.D, gbih, 0, st, skip));
+  RC(launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.Xz, d.Din, d.Din, gWih, d.Din, gbih, 0, st,
+                          skip));
   // h_{t-1} rows: hbuf[0..E-1] (hbuf[0] = h0)
   return launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.hbuf, d.H, d.H, gWhh, d.H, gbhh, 0, st,
                               skip);
+}
+
+static PixRows pix_rows(const smi_ppo_rnn_args& a, const RnnDims& d) {
+  return PixRows{a.pixels, a.pixels_next, d.B, d.T, d.G.img};
+}
+
+// CNN features of the first S time steps into X[:, D:] (ldx = Din); A1 kept
+// for a backward when non-null
+static int cnn_features(const smi_ppo_rnn_args& a, const RnnDims& d, const float* cnn, int S,
+                        float* X, float* A1, const RnnScratch& s, hipStream_t st,
+                        const int* skip) {
+  if (d.F == 0) return SMI_OK;
+  return cnn_forward(cnn, pix_rows(a, d), d.G.C, d.G.H, d.G.W, d.F, (int64_t)S * d.B, A1, s.A2,
+                     X + d.D, d.Din, st, skip);
+}
+
+// pixel-stem gradient (into Gc) from the LSTM gate gradients of the E steps:
+// dF = relu'(F) * (dgates W_ih[:, D:]), then the CNN backward
+static int cnn_grad(const smi_ppo_rnn_args& a, const RnnDims& d, const LstmP& l, const float* cnn,
+                    float* Gc, const RnnScratch& s, hipStream_t st, const int* skip) {
+  if (d.F == 0) return SMI_OK;
+  RC(launch_linear_bwd_dx(s.dgates, d.G4, (int)d.NE, d.G4, l.Wih + d.D, d.Din, d.F, s.Xz + d.D,
+                          d.Din, s.dF, d.F, st, skip));
+  return cnn_backward(cnn, pix_rows(a, d), d.G.C, d.G.H, d.G.W, d.F, d.NE, s.A1, s.A2, s.dF, d.F,
+                      Gc, s.dA2, s.cpart, st, skip);
 }
 
 static float c_loglik_of(int A) { return (float)(0.5 * log(2.0 * 3.141592653589793) * (double)A); }
@@ -652,8 +692,9 @@ static float c_entropy_of(int A) {
 }
 
 int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int h1, int h2, int A, int c1,
-                              int c2) {
-  return 4 * rnn_scratch(rnn_dims(B, T, Hz, D, H, h1, h2, A, c1, c2), nullptr).total_floats;
+                              int c2, int pc, int ph, int pw, int F) {
+  return 4 * rnn_scratch(rnn_dims(B, T, Hz, D, H, h1, h2, A, c1, c2, pc, ph, pw, F), nullptr)
+                 .total_floats;
 }
 
 static PolRowArgs pol_rows(const smi_ppo_rnn_args& a, const RnnDims& d, const RnnScratch& s) {
@@ -669,15 +710,16 @@ static PolRowArgs pol_rows(const smi_ppo_rnn_args& a, const RnnDims& d, const Rn
 
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
   const RnnDims d = rnn_dims(a.B, a.T, a.horizon, a.obs_dim, a.rnn_hidden, a.h1, a.h2, a.act_dim,
-                             a.critic_h1, a.critic_h2);
+                             a.critic_h1, a.critic_h2, a.pix_c, a.pix_h, a.pix_w, a.cnn_feat);
   const RnnScratch s = rnn_scratch(d, a.scratch);
   if (s.total_floats * 4 > a.scratch_bytes) return set_error(SMI_E_ARG, "ppo_rnn: scratch too small");
   const int* stop = s.ci + CI_STOP;
-  const LstmP lm = lstm_params(a.lstm, d.D, d.H);
+  const LstmP lm = lstm_params(a.lstm, d.Din, d.H);
+  const float* cnn = a.lstm + d.nL;                    // stem = [lstm | cnn]
   const Head actor{a.actor, d.LA, d.H, d.h1, d.h2, d.A, 1};
   const Head critic{a.critic, d.LC, d.H, d.c1, d.c2, 1, 0};
-  float* gA = a.xbuf;                                  // [actor head | lstm]
-  float* gC = a.xbuf + d.nA_head + d.nL;               // [critic head | lstm]
+  float* gA = a.xbuf;                                  // [actor head | lstm | cnn]
+  float* gC = a.xbuf + d.nA_head + d.nS;               // [critic head | lstm | cnn]
   const int64_t NEg = (int64_t)d.E * a.B_global;
   const size_t zlds = (size_t)2 * round4(d.D) * 4;
   switch (phase) {
@@ -686,8 +728,9 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       RC(check_launch("rnn_init_kernel"));
       hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NG * d.D)), dim3(kWG), zlds, st, a.obs,
                          a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum, a.zf_sumsq,
-                         a.zf_count, a.zf_eps, s.Xz);
+                         a.zf_count, a.zf_eps, s.Xz, d.Din);
       RC(check_launch("zf_tmajor_kernel"));
+      RC(cnn_features(a, d, cnn, d.S1, s.Xz, nullptr, s, st, nullptr));
       RC(lstm_forward(d, lm, s.Xz, d.S1, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
       RC(head_fwd(critic, s.hbuf + (int64_t)d.B * d.H, d.H, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
       hipLaunchKernelGGL(tmajor_to_bmajor_kernel, dim3(grid_of(d.NG)), dim3(kWG), 0, st, s.OUT,
@@ -704,20 +747,22 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     }
     case SMI_RNN_PH_PREP: {
       const float* X = s.Xz;
-      if (a.use_zf) {
+      if (a.use_zf || d.F > 0) {   // the reference model's own z-filter / CNN stem
         hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NE * d.D)), dim3(kWG), zlds, st, a.obs,
-                           a.obs_next, d.B, d.T, d.E, d.D, 1, a.rzf_sum, a.rzf_sumsq, a.rzf_count,
-                           a.zf_eps, s.Xr);
+                           a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
+                           a.rzf_count, a.zf_eps, s.Xr, d.Din);
         RC(check_launch("zf_tmajor_kernel"));
+        RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, s, st, nullptr));
         X = s.Xr;
       }
-      const LstmP lr = lstm_params(a.ref_lstm, d.D, d.H);
+      const LstmP lr = lstm_params(a.ref_lstm, d.Din, d.H);
       RC(lstm_forward(d, lr, X, d.E, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
       const Head ref{a.ref_actor, d.LA, d.H, d.h1, d.h2, d.A, 1};
       return head_fwd(ref, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.refmu, st,
                       nullptr);
     }
     case SMI_RNN_PH_POLICY_FWD: {
+      RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, stop));
       RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, stop));
       RC(head_fwd(actor, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
       PolRowArgs p = pol_rows(a, d, s);
@@ -745,14 +790,15 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       hipLaunchKernelGGL(logvar_grad_kernel, dim3(1), dim3(64), 0, st, s.lvpart, nb, d.A,
                          a.actor + d.LA.flv, gA + d.LA.flv, stop);
       RC(check_launch("logvar_grad_kernel"));
-      return lstm_backward(d, lm, gA + d.nA_head, s, st, stop);
+      RC(lstm_backward(d, lm, gA + d.nA_head, s, st, stop));
+      return cnn_grad(a, d, lm, cnn, gA + d.nA_head + d.nL, s, st, stop);
     }
     case SMI_RNN_PH_POLICY_APPLY: {
-      const int64_t n = d.nA_head + d.nL;
+      const int64_t n = d.nA_head + d.nS;
       const int g = grid_of(n, 1024);
       hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gA, n, s.part, stop);
       RC(check_launch("sumsq_part_kernel"));
-      AdamSplitArgs aa{a.actor, d.nA_head, a.lstm, d.nL, gA, a.actor_m, a.actor_v, a.actor_step,
+      AdamSplitArgs aa{a.actor, d.nA_head, a.lstm, d.nS, gA, a.actor_m, a.actor_v, a.actor_step,
                        a.hyper + SMI_HYP_LR_ACTOR, a.beta1, a.beta2, a.adam_eps, a.actor_wd,
                        a.clip_actor_grad ? a.actor_max_norm : 0.f, s.part, g, stop,
                        a.clip_actor_grad ? a.stats + SMI_ST_GRAD_NORM_ACTOR : nullptr, nullptr};
@@ -763,6 +809,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       return check_launch("step_bump_kernel");
     }
     case SMI_RNN_PH_VALUE_GRAD: {
+      RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
       RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, nullptr));
       RC(head_fwd(critic, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
       const int nb = rnn_nblk(d.NE);
@@ -777,14 +824,15 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       }
       RC(head_bwd(critic, s.dOUT, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.dH1,
                   s.dH2, gC, s.dh, st, nullptr));
-      return lstm_backward(d, lm, gC + d.nC_head, s, st, nullptr);
+      RC(lstm_backward(d, lm, gC + d.nC_head, s, st, nullptr));
+      return cnn_grad(a, d, lm, cnn, gC + d.nC_head + d.nL, s, st, nullptr);
     }
     case SMI_RNN_PH_VALUE_APPLY: {
-      const int64_t n = d.nC_head + d.nL;
+      const int64_t n = d.nC_head + d.nS;
       const int g = grid_of(n, 1024);
       hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gC, n, s.part, nullptr);
       RC(check_launch("sumsq_part_kernel"));
-      AdamSplitArgs aa{a.critic, d.nC_head, a.lstm, d.nL, gC, a.critic_m, a.critic_v,
+      AdamSplitArgs aa{a.critic, d.nC_head, a.lstm, d.nS, gC, a.critic_m, a.critic_v,
                        a.critic_step, a.hyper + SMI_HYP_LR_CRITIC, a.beta1, a.beta2, a.adam_eps,
                        a.critic_wd, a.clip_critic_grad ? a.critic_max_norm : 0.f, s.part, g,
                        nullptr, a.clip_critic_grad ? a.stats + SMI_ST_GRAD_NORM_CRITIC : nullptr,

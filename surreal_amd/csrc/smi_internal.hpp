@@ -13,7 +13,7 @@ int set_error(int code, const char* msg);
 // each launch records (class, algorithmic flops, start/end events) on its own
 // stream.  Off by default; bench.py turns it on over its timed region.
 enum { KT_GEMM_FWD = 0, KT_GEMM_DX, KT_GEMM_DW, KT_GEMM_REDUCE, KT_LSTM_FWD, KT_LSTM_BWD,
-       KT_COUNT };
+       KT_CNN_FWD, KT_CNN_BWD, KT_COUNT };
 bool ktime_on();
 int ktime_begin(hipStream_t st);                       // returns a slot, -1 when off/full
 void ktime_end(int slot, int cls, double flops, hipStream_t st);
@@ -30,6 +30,45 @@ int launch_linear_bwd_dw(const float* dY, int64_t ldg, int M, int N, const float
                          int K, float* dW, int64_t lddw, float* db, int accumulate,
                          hipStream_t st, const int* skip = nullptr);
 int check_launch(const char* what);
+
+#define RC_CHECK(x) do { const int rc_ = (x); if (rc_) return rc_; } while (0)
+
+// ---- pixel stem (CNNStemNetwork, builders.py:8-33) -------------------------
+// Flat parameter layout (torch Conv2d / Linear shapes, in module order):
+// [conv1.weight (16,C,8,8) | conv1.bias (16) | conv2.weight (32,16,4,4) |
+//  conv2.bias (32) | fc.weight (F, 32*H2*W2) | fc.bias (F)]
+struct CnnGeom {
+  int C, H, W, H1, W1, P1, H2, W2, P2, K1, flat, F;
+  int64_t img;                                  // bytes per uint8 image
+  int64_t oW1, ob1, oW2, ob2, oWf, obf, total;  // offsets (floats)
+  int64_t nconv;                                // conv parameters = oWf
+};
+__host__ __device__ inline CnnGeom cnn_geom(int C, int H, int W, int F) {
+  CnnGeom g;
+  g.C = C; g.H = H; g.W = W; g.F = F;
+  g.H1 = (H - 8) / 4 + 1; g.W1 = (W - 8) / 4 + 1; g.P1 = g.H1 * g.W1;
+  g.H2 = (g.H1 - 4) / 2 + 1; g.W2 = (g.W1 - 4) / 2 + 1; g.P2 = g.H2 * g.W2;
+  g.K1 = 64 * C; g.flat = 32 * g.P2;
+  g.img = (int64_t)C * H * W;
+  g.oW1 = 0; g.ob1 = 16 * (int64_t)g.K1; g.oW2 = g.ob1 + 16; g.ob2 = g.oW2 + 32 * 256;
+  g.oWf = g.ob2 + 32; g.obf = g.oWf + (int64_t)F * g.flat; g.total = g.obf + F;
+  g.nconv = g.oWf;
+  return g;
+}
+// image of activation row n = t*B + b: t < T -> pix[b][t], else pix_next[b]
+struct PixRows { const unsigned char* pix; const unsigned char* pix_next; int64_t B, T, img_bytes; };
+constexpr int kCnnPartials = 512;               // max workgroups (partial slabs) of the backward
+int cnn_bwd_grid(int64_t rows);
+int cnn_forward(const float* prm, const PixRows& pr, int C, int H, int W, int F, int64_t rows,
+                float* A1, float* A2, float* feat, int64_t ldf, hipStream_t st, const int* skip);
+// dz: gradient at the Linear pre-activation (ReLU mask applied), rows x F
+// (stride lddz); writes the full gradient (not accumulated) into grad; dA2
+// (rows x flat) and part (cnn_bwd_grid(rows) x nconv) are scratch.
+int cnn_backward(const float* prm, const PixRows& pr, int C, int H, int W, int F, int64_t rows,
+                 const float* A1, const float* A2, const float* dz, int64_t lddz, float* grad,
+                 float* dA2, float* part, hipStream_t st, const int* skip);
+int launch_slab_reduce(const float* part, int S, int64_t n, float* out, hipStream_t st,
+                       const int* skip);
 
 // Opt a kernel in to > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
 // Host-only attribute call: no allocation, no stream work (graph-capture safe).
@@ -74,7 +113,7 @@ int launch_ppo_epoch_grad(const smi_ppo_args* args, int epoch, hipStream_t strea
 int launch_ppo_epoch_apply(const smi_ppo_args* args, int epoch, hipStream_t stream);
 
 int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int h1, int h2, int A, int c1,
-                              int c2);
+                              int c2, int pc, int ph, int pw, int F);
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st);
 int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
                     const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,

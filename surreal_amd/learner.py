@@ -149,8 +149,10 @@ class PPOLearner(object):
         if self.if_rnn_policy and algo.rnn.get('rnn_layer', 1) != 1:
             raise NotImplementedError('surreal_amd: the LSTM policy supports rnn_layer == 1 '
                                       '(the reference default)')
-        if ec.get('pixel_input', False):
-            raise NotImplementedError('surreal_amd: pixel inputs are SURVEY §8(f) rank 1')
+        self.if_pixel_input = bool(ec.get('pixel_input', False))
+        if self.if_pixel_input and not self.if_rnn_policy:
+            raise NotImplementedError('surreal_amd: the pixel stem is built for the LSTM policy '
+                                      '(SURVEY C5); pixel + MLP-only learners are not')
         if dp is not None and self.use_r_filter:
             raise NotImplementedError('surreal_amd: RewardFilter under data parallelism needs a '
                                       'global reward all-reduce (not built yet)')
@@ -162,7 +164,7 @@ class PPOLearner(object):
 
         gen = torch.Generator().manual_seed(seed)
         mk = lambda: PPOModel(self.obs_spec, self.action_dim, lc.model, True, self.init_log_sig,  # noqa: E731
-                              self.use_z_filter, False, algo.rnn, self.device, gen)
+                              self.use_z_filter, self.if_pixel_input, algo.rnn, self.device, gen)
         self.model = mk()
         self.ref_target_model = mk()
         self.ref_target_model.update_target_params(self.model)
@@ -179,7 +181,7 @@ class PPOLearner(object):
         self.adam_betas, self.adam_eps = (0.9, 0.999), 1e-8
         # Adam moments per optimizer; with the LSTM stem both optimizers own the
         # stem's parameters too (ppo.py:159-168, ppo_net.py:202-224): [head | lstm]
-        n_rnn = self.model.rnn_stem.flat.numel() if self.if_rnn_policy else 0
+        n_rnn = self.model.stem_flat.numel()          # [lstm | cnn] stems (0 without)
         self.actor_m = torch.zeros(self.model.actor.flat.numel() + n_rnn, device=dev)
         self.actor_v = torch.zeros_like(self.actor_m)
         self.critic_m = torch.zeros(self.model.critic.flat.numel() + n_rnn, device=dev)
@@ -253,6 +255,8 @@ class PPOLearner(object):
     def _low_dim(self, obs):
         if isinstance(obs, torch.Tensor):
             return obs
+        if 'low_dim' not in obs:
+            return None
         parts = [obs['low_dim'][k] for k in obs['low_dim']]
         return parts[0] if len(parts) == 1 else torch.cat(parts, -1)
 
@@ -393,9 +397,21 @@ class PPOLearner(object):
         """ppo.py:487-586 with if_rnn_policy: the phase sequence of
         smi_ppo_rnn_phase (include/surreal_mi.h), yielding the buffers a data-
         parallel learner all-reduces between phases."""
-        x = self._low_dim(obs).contiguous()
-        xn = self._low_dim(obs_next).contiguous()
-        B, T, D = x.shape
+        x = self._low_dim(obs)
+        xn = self._low_dim(obs_next)
+        pix = pixn = None
+        if self.if_pixel_input:
+            pix = obs['pixel']['camera0']
+            pixn = obs_next['pixel']['camera0']
+            if pix.dtype != torch.uint8 or pixn.dtype != torch.uint8:
+                raise TypeError('camera0 observations must be uint8')
+            pix, pixn = pix.contiguous(), pixn.contiguous()
+        if x is not None:
+            x, xn = x.contiguous(), xn.contiguous()
+            B, T, D = x.shape
+        else:
+            B, T = pix.shape[:2]
+            D = 0
         if B != self.batch_size or T != self.n_step:
             raise ValueError(f'batch shape (B={B}, T={T}) != config (batch_size={self.batch_size}, '
                              f'n_step={self.n_step})')
@@ -416,15 +432,18 @@ class PPOLearner(object):
         c_h1, c_h2 = self.learner_config.model.critic_fc_hidden_sizes
         H = self.horizon
         lib = L.lib()
-        nbytes = lib.smi_ppo_rnn_scratch_bytes(B, T, H, D, Hd, a_h1, a_h2, A, c_h1, c_h2)
+        pc, ph, pw = self.obs_spec['pixel']['camera0'] if pix is not None else (0, 0, 0)
+        F = int(self.learner_config.model.cnn_feature_dim) if pix is not None else 0
+        nbytes = lib.smi_ppo_rnn_scratch_bytes(B, T, H, D, Hd, a_h1, a_h2, A, c_h1, c_h2,
+                                               pc, ph, pw, F)
         scratch = self._buf('rnn_scratch', (nbytes // 4,))
-        nx = lib.smi_ppo_rnn_xbuf_floats(D, Hd, a_h1, a_h2, A, c_h1, c_h2)
+        nx = lib.smi_ppo_rnn_xbuf_floats(D, Hd, a_h1, a_h2, A, c_h1, c_h2, pc, ph, pw, F)
         xbuf = self._buf('rnn_xbuf', (nx,))
         moments = self._buf('rnn_moments', (3,), torch.float64)
         pstat = self._buf('rnn_pstat', (L.RNN_PSTAT,), torch.float64)
         zbuf = self._buf('rnn_zbuf', (5 + 2 * D,), torch.float64)
-        nA = m.actor.flat.numel() + m.rnn_stem.flat.numel()
-        nC = m.critic.flat.numel() + m.rnn_stem.flat.numel()
+        nA = m.actor.flat.numel() + m.stem_flat.numel()
+        nC = m.critic.flat.numel() + m.stem_flat.numel()
         a = L.RNNArgs()
         dp = self.dp
         a.B, a.T, a.horizon, a.obs_dim, a.rnn_hidden = B, T, H, D, Hd
@@ -436,12 +455,17 @@ class PPOLearner(object):
         a.clip_critic_grad = 1 if self.clip_critic_gradient else 0
         a.use_zf = 1 if zf is not None else 0
         a.B_global = B * (dp.world_size if dp is not None else 1)
-        a.obs, a.obs_next, a.actions = x.data_ptr(), xn.data_ptr(), actions.data_ptr()
+        a.obs = x.data_ptr() if x is not None else None
+        a.obs_next = xn.data_ptr() if xn is not None else None
+        a.actions = actions.data_ptr()
+        a.pix_c, a.pix_h, a.pix_w, a.cnn_feat = pc, ph, pw, F
+        a.pixels = pix.data_ptr() if pix is not None else None
+        a.pixels_next = pixn.data_ptr() if pixn is not None else None
         a.rewards, a.dones, a.behave = rewards.data_ptr(), dones.data_ptr(), pds.data_ptr()
         a.h0, a.c0 = h0.data_ptr(), c0.data_ptr()
-        a.lstm, a.actor, a.critic = (m.rnn_stem.flat.data_ptr(), m.actor.flat.data_ptr(),
+        a.lstm, a.actor, a.critic = (m.stem_flat.data_ptr(), m.actor.flat.data_ptr(),
                                      m.critic.flat.data_ptr())
-        a.ref_lstm, a.ref_actor = rm.rnn_stem.flat.data_ptr(), rm.actor.flat.data_ptr()
+        a.ref_lstm, a.ref_actor = rm.stem_flat.data_ptr(), rm.actor.flat.data_ptr()
         if zf is not None:
             a.zf_sum, a.zf_sumsq, a.zf_count = (zf.running_sum.data_ptr(),
                                                 zf.running_sumsq.data_ptr(), zf.count.data_ptr())

@@ -145,7 +145,7 @@ class LSTMStem(nn.Module):
     persistent LSTM sequence kernel; inputs are batch_first (B, S, in)."""
 
     def __init__(self, input_size, hidden_size, num_layers=1, batch_first=True, device=None,
-                 generator=None):
+                 generator=None, flat=None):
         super().__init__()
         if num_layers != 1:
             raise NotImplementedError('surreal_amd: LSTM stem supports rnn_layer == 1 '
@@ -155,7 +155,9 @@ class LSTMStem(nn.Module):
         self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
         H, D = hidden_size, input_size
         n = int(L.lib().smi_lstm_param_count(D, H))
-        flat = torch.zeros(n, dtype=torch.float32, device=device)
+        if flat is None:
+            flat = torch.zeros(n, dtype=torch.float32, device=device)
+        assert flat.numel() == n
         o = 0
         self.weight_ih_l0 = nn.Parameter(flat[o:o + 4 * H * D].view(4 * H, D)); o += 4 * H * D
         self.weight_hh_l0 = nn.Parameter(flat[o:o + 4 * H * H].view(4 * H, H)); o += 4 * H * H
@@ -193,6 +195,74 @@ class LSTMStem(nn.Module):
                L.ptr(h0), L.ptr(c0), S, B, H, L.ptr(hbuf), L.ptr(cbuf), None, st)
         out = hbuf[1:].transpose(0, 1).contiguous()
         return out, (hbuf[S].unsqueeze(0).clone(), cbuf[S].unsqueeze(0).clone())
+
+
+class _ParamView(nn.Module):
+    """weight/bias Parameters (torch Conv2d / Linear shapes) viewing a flat buffer."""
+
+    def __init__(self, flat, off, wshape, nbias):
+        super().__init__()
+        nw = int(np.prod(wshape))
+        self.weight = nn.Parameter(flat[off:off + nw].view(*wshape))
+        self.bias = nn.Parameter(flat[off + nw:off + nw + nbias])
+        self.end = off + nw + nbias
+
+    def reset_parameters(self, generator=None):
+        # torch Conv2d / Linear default init: U(+-1/sqrt(fan_in)) for weight and bias
+        bound = 1.0 / math.sqrt(int(np.prod(self.weight.shape[1:])))
+        with torch.no_grad():
+            for p in (self.weight, self.bias):
+                p.copy_(torch.empty(p.shape).uniform_(-bound, bound, generator=generator))
+
+
+class CNNStemNetwork(nn.Module):
+    """builders.py:8-33: conv 8x8/4 (C->16) -> ReLU -> conv 4x4/2 (16->32) -> ReLU
+    -> Flatten -> Linear(D_out) -> ReLU, over ONE flat device buffer in the C-ABI
+    CNN layout (include/surreal_mi.h, smi_cnn_*).  State-dict keys follow the
+    Sequential positions: model.0 (conv), model.2 (conv), model.5 (linear).
+
+    forward() takes the raw uint8 camera tensor, (N, C, H, W) or (B, S, C, H, W)
+    — the obs/255 of ppo_net.py:368-375 is fused into the conv kernel (bit-equal
+    to torch's uint8 / 255.0).  Inference only; the learner's phases run the
+    backward (smi_ppo_rnn_phase)."""
+
+    def __init__(self, D_obs, D_out, conv_channels=(16, 32), kernel_sizes=(8, 4), strides=(4, 2),
+                 device=None, generator=None, flat=None):
+        super().__init__()
+        if list(conv_channels) != [16, 32] or list(kernel_sizes) != [8, 4] or list(strides) != [4, 2]:
+            raise NotImplementedError('surreal_amd: CNN stem is built for the reference defaults '
+                                      '(16@8s4, 32@4s2; builders.py:9)')
+        C, H, W = (int(v) for v in D_obs)
+        self.D_obs, self.D_out = (C, H, W), int(D_out)
+        n = int(L.lib().smi_cnn_param_count(C, H, W, self.D_out))
+        if flat is None:
+            flat = torch.zeros(n, dtype=torch.float32, device=device)
+        assert flat.numel() == n
+        H1, W1 = (H - 8) // 4 + 1, (W - 8) // 4 + 1
+        H2, W2 = (H1 - 4) // 2 + 1, (W1 - 4) // 2 + 1
+        self.flat_dim = 32 * H2 * W2
+        c1 = _ParamView(flat, 0, (16, C, 8, 8), 16)
+        c2 = _ParamView(flat, c1.end, (32, 16, 4, 4), 32)
+        fc = _ParamView(flat, c2.end, (self.D_out, self.flat_dim), self.D_out)
+        self.model = nn.Sequential(c1, nn.ReLU(), c2, nn.ReLU(), nn.Flatten(), fc, nn.ReLU())
+        for m in (c1, c2, fc):
+            m.reset_parameters(generator)
+        self.__dict__['flat'] = flat
+
+    def forward(self, obs):
+        if obs.dtype != torch.uint8:
+            raise TypeError('CNNStemNetwork: camera observations must be uint8 (scaled by 1/255 '
+                            'inside the kernel)')
+        lead = obs.shape[:-3]
+        x = obs.reshape(-1, *self.D_obs).contiguous()
+        rows = x.shape[0]
+        dev = self.flat.device
+        a2 = torch.empty(rows, self.flat_dim, dtype=torch.float32, device=dev)
+        out = torch.empty(rows, self.D_out, dtype=torch.float32, device=dev)
+        C, H, W = self.D_obs
+        L.call('smi_cnn_forward', L.ptr(self.flat), L.ptr(x), None, max(rows, 1), 1, rows,
+               C, H, W, self.D_out, None, L.ptr(a2), L.ptr(out), self.D_out, L.stream(dev))
+        return out.reshape(*lead, self.D_out)
 
 
 class ZFilter(nn.Module):
@@ -323,8 +393,10 @@ class DiagGauss(object):
 class PPOModel(nn.Module):
     """ppo_net.py:94-375 (low-dimensional observations).
 
-    The LSTM stem (if_rnn_policy, rnn_layer 1) is the HIP LSTMStem; the pixel CNN
-    stem (if_pixel_input) is SURVEY.md §8(f) rank 1 and is rejected loudly.
+    The LSTM stem (if_rnn_policy, rnn_layer 1) is the HIP LSTMStem and the pixel
+    stem (if_pixel_input) the HIP CNNStemNetwork on obs['pixel']['camera0']
+    (uint8).  With both, their parameters share one flat `stem_flat` buffer
+    [lstm | cnn] (the layout smi_ppo_rnn_phase and the optimizers use).
     """
 
     def __init__(self, obs_spec, action_dim, model_config, use_cuda=True, init_log_sig=0,
@@ -339,8 +411,6 @@ class PPOModel(nn.Module):
         self.init_log_sig = init_log_sig
         self.if_pixel_input = if_pixel_input
         self.rnn_config = rnn_config if rnn_config is not None else Config({'if_rnn_policy': False})
-        if if_pixel_input:
-            raise NotImplementedError('surreal_amd: pixel CNN stem is not built yet (SURVEY §8(f) 1)')
         self.if_rnn = bool(self.rnn_config.get('if_rnn_policy', False))
         self.device = torch.device(device) if device is not None else torch.device('cuda')
         self.low_dim = 0
@@ -351,11 +421,25 @@ class PPOModel(nn.Module):
                 self.low_dim_keys.append(k)
         self.cnn_stem = None
         self.rnn_stem = None
-        d_in = self.low_dim
+        F = int(model_config['cnn_feature_dim']) if if_pixel_input else 0
+        d_in = self.low_dim + F
+        n_cnn = 0
+        if if_pixel_input:
+            C, H, W = obs_spec['pixel']['camera0']
+            n_cnn = int(L.lib().smi_cnn_param_count(C, H, W, F))
+        n_rnn = 0
+        if self.if_rnn:
+            n_rnn = int(L.lib().smi_lstm_param_count(d_in, self.rnn_config['rnn_hidden']))
+        stem = torch.zeros(n_rnn + n_cnn, dtype=torch.float32, device=self.device)
+        if if_pixel_input:                                  # ppo_net.py:137-141
+            self.cnn_stem = CNNStemNetwork(obs_spec['pixel']['camera0'], F, device=self.device,
+                                           generator=generator, flat=stem[n_rnn:])
         if self.if_rnn:                                     # ppo_net.py:143-152,159-160
-            self.rnn_stem = LSTMStem(self.low_dim, self.rnn_config['rnn_hidden'],
-                                     self.rnn_config.get('rnn_layer', 1), True, self.device, generator)
+            self.rnn_stem = LSTMStem(d_in, self.rnn_config['rnn_hidden'],
+                                     self.rnn_config.get('rnn_layer', 1), True, self.device, generator,
+                                     flat=stem[:n_rnn])
             d_in = self.rnn_config['rnn_hidden']
+        self.__dict__['stem_flat'] = stem          # [lstm | cnn]; empty for a plain MLP model
         self.actor = PPO_ActorNetwork(d_in, action_dim, model_config['actor_fc_hidden_sizes'],
                                       init_log_sig, self.device, generator)
         self.critic = PPO_CriticNetwork(d_in, model_config['critic_fc_hidden_sizes'],
@@ -383,12 +467,16 @@ class PPOModel(nn.Module):
 
     def get_actor_params(self):                             # ppo_net.py:202-212
         ps = list(self.actor.parameters())
+        if self.if_pixel_input:
+            ps += list(self.cnn_stem.parameters())
         if self.if_rnn:
             ps += list(self.rnn_stem.parameters())
         return iter(ps)
 
     def get_critic_params(self):                            # ppo_net.py:214-224
         ps = list(self.critic.parameters())
+        if self.if_pixel_input:
+            ps += list(self.cnn_stem.parameters())
         if self.if_rnn:
             ps += list(self.rnn_stem.parameters())
         return iter(ps)
@@ -397,8 +485,7 @@ class PPOModel(nn.Module):
         with torch.no_grad():
             self.actor.flat.copy_(net.actor.flat)
             self.critic.flat.copy_(net.critic.flat)
-            if self.if_rnn:
-                self.rnn_stem.flat.copy_(net.rnn_stem.flat)
+            self.stem_flat.copy_(net.stem_flat)             # lstm and/or cnn stems
             if self.use_z_filter:
                 self.z_filter.load_state_dict(net.z_filter.state_dict())
 
@@ -406,29 +493,41 @@ class PPOModel(nn.Module):
         if self.use_z_filter:
             self.z_filter.load_state_dict(net.z_filter.state_dict())
 
-    def _rnn_features(self, x, cells):
-        if self.use_z_filter:
-            x = self.z_filter.forward(x)
-        out, cells = self.rnn_stem(x.contiguous(), cells)
+    def _stem_input(self, obs):
+        """cat([zfilter(low_dim), cnn(camera0/255)], -1) (ppo_net.py:262-275)."""
+        x = self._gather_low_dim_input(obs)
+        parts = []
+        if x is not None:
+            parts.append(self.z_filter.forward(x) if self.use_z_filter else x)
+        if self.if_pixel_input:
+            parts.append(self.cnn_stem(obs['pixel']['camera0']))
+        return parts[0] if len(parts) == 1 else torch.cat(parts, -1)
+
+    def _rnn_features(self, obs, cells):
+        out, cells = self.rnn_stem(self._stem_input(obs).contiguous(), cells)
         return out, cells
 
     def forward_actor(self, obs, cells=None):               # ppo_net.py:253-282
-        x = self._gather_low_dim_input(obs)
         if self.if_rnn:
-            return self.actor(self._rnn_features(x, cells)[0])
-        return self.actor(x, self.z_filter if self.use_z_filter else None)
+            return self.actor(self._rnn_features(obs, cells)[0])
+        if self.if_pixel_input:
+            return self.actor(self._stem_input(obs))
+        return self.actor(self._gather_low_dim_input(obs),
+                          self.z_filter if self.use_z_filter else None)
 
     def forward_critic(self, obs, cells=None):              # ppo_net.py:284-315
-        x = self._gather_low_dim_input(obs)
         if self.if_rnn:
-            return self.critic(self._rnn_features(x, cells)[0])
-        return self.critic(x, self.z_filter if self.use_z_filter else None)
+            return self.critic(self._rnn_features(obs, cells)[0])
+        if self.if_pixel_input:
+            return self.critic(self._stem_input(obs))
+        return self.critic(self._gather_low_dim_input(obs),
+                           self.z_filter if self.use_z_filter else None)
 
     def forward_actor_expose_cells(self, obs, cells=None):  # ppo_net.py:317-352
         if not self.if_rnn:
             return self.forward_actor(obs, cells), cells
-        x = self._gather_low_dim_input(obs).reshape(1, 1, -1)
-        out, cells = self._rnn_features(x, cells)
+        x = self._stem_input(obs).reshape(1, 1, -1)
+        out, cells = self.rnn_stem(x.contiguous(), cells)
         return self.actor(out.reshape(-1, self.rnn_config['rnn_hidden'])), cells
 
     def z_update(self, obs):

@@ -6,14 +6,16 @@ dones ~ Bernoulli(0.02) with the last step forced to 1 for 5% of segments;
 behaviour policy: mu ~ U(-0.5, 0.5), sigma = exp(init_log_sig) * U(0.8, 1.2);
 actions are drawn from the behaviour policy (what PPOAgent.act samples,
 surreal/agent/ppo_agent.py:103-151, via DiagGauss.sample) and clipped to
-[-1, 1]; LSTM h, c ~ N(0, 0.1).
+[-1, 1]; LSTM h, c ~ N(0, 0.1).  With pixel=(C, H, W), camera0 frames are
+uniform uint8 (drawn after everything else, so the low-dim streams do not
+change); D == 0 drops the low-dim modality.
 """
 import numpy as np
 import torch
 
 
 def ppo_batch(B, T, D, A, seed=0, init_log_sig=-1.0, rnn_hidden=None, rnn_layers=1,
-              obs_key='flat_inputs'):
+              obs_key='flat_inputs', pixel=None):
     g = torch.Generator().manual_seed(seed)
     scale = 1.0 + torch.arange(D, dtype=torch.float32) / D
     obs = torch.randn(B, T, D, generator=g) * scale
@@ -30,9 +32,18 @@ def ppo_batch(B, T, D, A, seed=0, init_log_sig=-1.0, rnn_hidden=None, rnn_layers
     if rnn_hidden:
         onetime = [0.1 * torch.randn(B, rnn_layers, rnn_hidden, generator=g),
                    0.1 * torch.randn(B, rnn_layers, rnn_hidden, generator=g)]
+    o, on = {}, {}
+    if D:
+        o['low_dim'] = {obs_key: obs}
+        on['low_dim'] = {obs_key: obs_next}
+    if pixel is not None:
+        o['pixel'] = {'camera0': torch.randint(0, 256, (B, T) + tuple(pixel), generator=g,
+                                               dtype=torch.uint8)}
+        on['pixel'] = {'camera0': torch.randint(0, 256, (B, 1) + tuple(pixel), generator=g,
+                                                dtype=torch.uint8)}
     return {
-        'obs': {'low_dim': {obs_key: obs}},
-        'obs_next': {'low_dim': {obs_key: obs_next}},
+        'obs': o,
+        'obs_next': on,
         'actions': actions,
         'rewards': rewards,
         'dones': dones,

@@ -10,7 +10,7 @@ from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, Config, gym_env_confi
 def ppo_config(B=64, T=50, mode='clip', use_z_filter=True, hidden=(64, 64), lam=0.95,
                gamma=0.99, epochs=(10, 10), norm_adv=True, use_r_filter=False, reward_scale=1.0,
                kl_target=0.02, lr=(3e-4, 3e-4), wd=(0.0, 0.0), rnn=False, rnn_hidden=100,
-               horizon=5, critic_hidden=None):
+               horizon=5, critic_hidden=None, cnn_feat=256):
     lc = copy.deepcopy(PPO_DEFAULT_LEARNER_CONFIG)
     lc.model.actor_fc_hidden_sizes = list(hidden)
     lc.model.critic_fc_hidden_sizes = list(critic_hidden if critic_hidden is not None else hidden)
@@ -35,6 +35,7 @@ def ppo_config(B=64, T=50, mode='clip', use_z_filter=True, hidden=(64, 64), lam=
     lc.algo.network.actor_regularization = wd[0]
     lc.algo.network.critic_regularization = wd[1]
     lc.replay.batch_size = B
+    lc.model.cnn_feature_dim = cnn_feat
     return lc
 
 
@@ -51,6 +52,9 @@ def copy_weights_to_oracle(learner, ref):
     if getattr(learner, 'if_rnn_policy', False):
         for src, dst in ((learner.model, ref.model), (learner.ref_target_model, ref.ref_target_model)):
             load_lstm_flat(dst.rnn_stem, src.rnn_stem.flat.detach().cpu())
+    if getattr(learner, 'if_pixel_input', False):
+        for src, dst in ((learner.model, ref.model), (learner.ref_target_model, ref.ref_target_model)):
+            load_seq_flat(dst.cnn_stem, src.cnn_stem.flat.detach().cpu())
     if learner.use_z_filter:
         for a, b in ((learner.model.z_filter, ref.model.z_filter),
                      (learner.ref_target_model.z_filter, ref.ref_target_model.z_filter)):
@@ -69,6 +73,21 @@ def load_lstm_flat(lstm, flat):
             o += n
 
 
+def load_seq_flat(module, flat):
+    """flat buffer -> module.parameters() in order (the C-ABI CNN layout)."""
+    o = 0
+    with torch.no_grad():
+        for p in module.parameters():
+            n = p.numel()
+            p.copy_(flat[o:o + n].reshape(p.shape))
+            o += n
+    assert o == flat.numel()
+
+
+def seq_flat(module):
+    return torch.cat([p.detach().reshape(-1) for p in module.parameters()])
+
+
 def lstm_flat(lstm):
     return torch.cat([p.detach().reshape(-1) for p in
                       (lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0)])
@@ -76,10 +95,17 @@ def lstm_flat(lstm):
 
 def oracle_batch(batch):
     """Synthetic batch (surreal_amd.synthetic layout) -> oracle learn() dict."""
-    key = list(batch['obs']['low_dim'])[0]
-    return {'obs': batch['obs']['low_dim'][key], 'obs_next': batch['obs_next']['low_dim'][key],
-            'actions': batch['actions'], 'rewards': batch['rewards'], 'dones': batch['dones'],
-            'pds': batch['persistent_infos'][-1], 'onetime': batch['onetime_infos']}
+    out = {'obs': None, 'obs_next': None,
+           'actions': batch['actions'], 'rewards': batch['rewards'], 'dones': batch['dones'],
+           'pds': batch['persistent_infos'][-1], 'onetime': batch['onetime_infos']}
+    if 'low_dim' in batch['obs']:
+        key = list(batch['obs']['low_dim'])[0]
+        out['obs'] = batch['obs']['low_dim'][key]
+        out['obs_next'] = batch['obs_next']['low_dim'][key]
+    if 'pixel' in batch['obs']:
+        out['pixels'] = batch['obs']['pixel']['camera0']
+        out['pixels_next'] = batch['obs_next']['pixel']['camera0']
+    return out
 
 
 def max_rel_err(x, ref, floor=None):
