@@ -17,9 +17,12 @@
 // gradients accumulate in registers across the images of a workgroup and are
 // summed over workgroups by the fixed-order slab reducer: deterministic.
 //
-// Pixel scaling: torch computes uint8/255.0 as fl(u / 255) (correctly rounded
-// fp32 division).  u8_scale() gets the same bits with one multiply and two
-// FMAs (checked for all 256 values in tests/test_gpu_cnn.py).
+// Pixel scaling: torch computes conv(fl(u / 255)).  The kernels feed the raw
+// byte values (exact in fp32) to the MFMAs and divide the conv-1 sums by 255
+// (IEEE division) in the epilogue — one v_cvt per operand instead of a
+// correctly rounded division.  Same result up to fp32 rounding of the sum
+// (the parity bar); a one-hot filter gives exactly fl(u / 255)
+// (test_u8_scaling_bit_exact).
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
 
@@ -28,11 +31,8 @@ namespace smi {
 int launch_slab_reduce(const float* part, int S, int64_t n, float* out, hipStream_t st,
                        const int* skip);
 
-__device__ __forceinline__ float u8_scale(float u) {
-  const float r = 1.0f / 255.0f;
-  const float q = u * r;
-  const float e = __builtin_fmaf(-q, 255.0f, u);
-  return __builtin_fmaf(e, r, q);
+__device__ __forceinline__ float u8f(unsigned u, int byte) {
+  return (float)((u >> (8 * byte)) & 0xffu);
 }
 
 __device__ __forceinline__ const unsigned char* pix_of(const PixRows& pr, int64_t n) {
@@ -50,8 +50,13 @@ __host__ __device__ inline int64_t lds_img_bytes(const CnnGeom& g) { return (g.i
 //   conv2: M = P2 pixels, N = 32, K = 256; wave w owns channel tile w>>1 and
 //          pixel tiles (w&1), (w&1)+2, ...; one lane reads 4 consecutive A1
 //          floats (kx = 0..3) per 4 MFMAs.
+#ifndef SMI_EXP
+#define CNN_FWD_ATTR __attribute__((amdgpu_waves_per_eu(3, 3)))
+#else
+#define CNN_FWD_ATTR
+#endif
 template <int C>
-__global__ void __launch_bounds__(kWG)
+__global__ void __launch_bounds__(kWG) CNN_FWD_ATTR
 cnn_fwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t rows,
                float* __restrict__ A1g, float* __restrict__ A2g, const int* skip) {
   if (skip && skip[0] != 0) return;
@@ -86,35 +91,48 @@ cnn_fwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
       for (int i = tid; i < nv; i += kWG) dst[i] = src[i];
     }
     __syncthreads();
-    // ---- conv 1
-    for (int pt = w; pt < nt1; pt += 4) {
-      int p = pt * 16 + lm;
-      p = p < g.P1 ? p : g.P1 - 1;
-      const int oy = p / g.W1, ox = p - oy * g.W1;
-      const unsigned char* base = img + oy * 4 * W + ox * 4;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // ---- conv 1: two pixel tiles (two independent MFMA chains) per pass
+    for (int pt = w; pt < nt1; pt += 8) {
+      const int ptb = pt + 4 < nt1 ? pt + 4 : pt;      // second tile (dup when odd)
+      int pa = pt * 16 + lm, pb2 = ptb * 16 + lm;
+      pa = pa < g.P1 ? pa : g.P1 - 1;
+      pb2 = pb2 < g.P1 ? pb2 : g.P1 - 1;
+      const int oya = pa / g.W1, oxa = pa - oya * g.W1;
+      const int oyb = pb2 / g.W1, oxb = pb2 - oyb * g.W1;
+      const unsigned char* basea = img + oya * 4 * W + oxa * 4;
+      const unsigned char* baseb = img + oyb * 4 * W + oxb * 4;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int rb = 0; rb < 2 * C; ++rb) {
         const int r = rb * 4 + lg;
-        const unsigned* q = reinterpret_cast<const unsigned*>(base + (r >> 3) * HW + (r & 7) * W);
-        const unsigned u0 = q[0], u1 = q[1];
-        acc = mfma4(u8_scale((float)(u0 & 0xffu)), w1r[rb * 8 + 0], acc);
-        acc = mfma4(u8_scale((float)((u0 >> 8) & 0xffu)), w1r[rb * 8 + 1], acc);
-        acc = mfma4(u8_scale((float)((u0 >> 16) & 0xffu)), w1r[rb * 8 + 2], acc);
-        acc = mfma4(u8_scale((float)(u0 >> 24)), w1r[rb * 8 + 3], acc);
-        acc = mfma4(u8_scale((float)(u1 & 0xffu)), w1r[rb * 8 + 4], acc);
-        acc = mfma4(u8_scale((float)((u1 >> 8) & 0xffu)), w1r[rb * 8 + 5], acc);
-        acc = mfma4(u8_scale((float)((u1 >> 16) & 0xffu)), w1r[rb * 8 + 6], acc);
-        acc = mfma4(u8_scale((float)(u1 >> 24)), w1r[rb * 8 + 7], acc);
+        const int ro = (r >> 3) * HW + (r & 7) * W;
+        const unsigned* qa = reinterpret_cast<const unsigned*>(basea + ro);
+        const unsigned* qb = reinterpret_cast<const unsigned*>(baseb + ro);
+        const unsigned a0 = qa[0], a1w = qa[1], b0 = qb[0], b1w = qb[1];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc = mfma4(u8f(a0, u), w1r[rb * 8 + u], acc);
+          acc2 = mfma4(u8f(b0, u), w1r[rb * 8 + u], acc2);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc = mfma4(u8f(a1w, u), w1r[rb * 8 + 4 + u], acc);
+          acc2 = mfma4(u8f(b1w, u), w1r[rb * 8 + 4 + u], acc2);
+        }
       }
-      // D[pixel pt*16 + lg*4 + i][channel lm]; P1 % 4 == 0 (checked on the host)
-      const int p0 = pt * 16 + lg * 4;
-      if (p0 < g.P1) {
-        float4 v;
-        v.x = fmaxf(acc[0] + b1, 0.f); v.y = fmaxf(acc[1] + b1, 0.f);
-        v.z = fmaxf(acc[2] + b1, 0.f); v.w = fmaxf(acc[3] + b1, 0.f);
-        *reinterpret_cast<float4*>(a1 + lm * g.P1 + p0) = v;
-        if (A1g) *reinterpret_cast<float4*>(A1g + n * (int64_t)(16 * g.P1) + lm * g.P1 + p0) = v;
+      // D[pixel tile*16 + lg*4 + i][channel lm]; P1 % 4 == 0 (checked on the host)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && ptb == pt) break;
+        const f32x4 s4 = h == 0 ? acc : acc2;
+        const int p0 = (h == 0 ? pt : ptb) * 16 + lg * 4;
+        if (p0 < g.P1) {
+          float4 v;
+          v.x = fmaxf(s4[0] / 255.0f + b1, 0.f); v.y = fmaxf(s4[1] / 255.0f + b1, 0.f);
+          v.z = fmaxf(s4[2] / 255.0f + b1, 0.f); v.w = fmaxf(s4[3] / 255.0f + b1, 0.f);
+          *reinterpret_cast<float4*>(a1 + lm * g.P1 + p0) = v;
+          if (A1g) *reinterpret_cast<float4*>(A1g + n * (int64_t)(16 * g.P1) + lm * g.P1 + p0) = v;
+        }
       }
     }
     __syncthreads();
@@ -169,6 +187,16 @@ cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
   float* a1 = reinterpret_cast<float*>(smem + lds_img_bytes(g));       // A1, then dA1
   float* da2 = a1 + 16 * g.P1;
   float* red = da2 + round4(g.flat);
+  int* ofs1 = reinterpret_cast<int*>(red + kWG);       // conv-1 pixel p -> byte offset
+  int* ofs2 = ofs1 + g.P1;                              // conv-2 pixel p -> A1 offset
+  for (int p = threadIdx.x; p < g.P1; p += kWG) {
+    const int oy = p / g.W1;
+    ofs1[p] = oy * 4 * W + (p - oy * g.W1) * 4;
+  }
+  for (int p = threadIdx.x; p < g.P2; p += kWG) {
+    const int oy = p / g.W2;
+    ofs2[p] = oy * 2 * g.W1 + (p - oy * g.W2) * 2;
+  }
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lg = l >> 4, lm = l & 15;
   const int HW = H * W;
 
@@ -222,8 +250,7 @@ cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
       const int p = 4 * j + lg;
       const bool ok = p < g.P2;
       const int pc = ok ? p : g.P2 - 1;
-      const int oy = pc / g.W2, ox = pc - oy * g.W2;
-      const int pb = oy * 2 * g.W1 + ox * 2;
+      const int pb = ofs2[pc];
       const float av = da2[(ct * 16 + lm) * g.P2 + pc];
       const float a = ok ? av : 0.f;
 #pragma unroll
@@ -234,27 +261,39 @@ cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
       for (int p = tid & 7; p < g.P2; p += 8) db2p += da2[ch * g.P2 + p];
     }
     __syncthreads();
-    // ---- (c) conv-2 input gradient, in place over A1 (ReLU mask from A1)
-    for (int qt = 0; qt < (Q + 15) >> 4; ++qt) {
-      const int q = qt * 16 + lm;
-      const int qc = q < Q ? q : Q - 1;
-      const int yy = qc / NX, xx = qc - yy * NX;
-      const int oy = yy - ty, ox = xx - tx;
-      const bool ok = q < Q && oy >= 0 && oy < g.H2 && ox >= 0 && ox < g.W2;
-      const int off = ok ? oy * g.W2 + ox : 0;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // ---- (c) conv-2 input gradient, in place over A1 (ReLU mask from A1);
+    // two position tiles per pass (two independent MFMA chains)
+    for (int qt = 0; qt < (Q + 15) >> 4; qt += 2) {
+      int off[2];
+      bool okq[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = (qt + h) * 16 + lm;
+        const int qc = q < Q ? q : Q - 1;
+        const int yy = qc / NX, xx = qc - yy * NX;
+        const int oy = yy - ty, ox = xx - tx;
+        okq[h] = q < Q && oy >= 0 && oy < g.H2 && ox >= 0 && ox < g.W2;
+        off[h] = okq[h] ? oy * g.W2 + ox : 0;
+      }
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < 32; ++j) {
-        const float av = da2[j * g.P2 + off];
-        acc = mfma4(ok ? av : 0.f, w2c[j], acc);
+        const float v0 = da2[j * g.P2 + off[0]];
+        const float v1 = da2[j * g.P2 + off[1]];
+        acc0 = mfma4(okq[0] ? v0 : 0.f, w2c[j], acc0);
+        acc1c = mfma4(okq[1] ? v1 : 0.f, w2c[j], acc1c);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int qq = qt * 16 + lg * 4 + i;
-        if (qq < Q) {
-          const int y2 = qq / NX, x2 = qq - y2 * NX;
-          const int idx = lm * g.P1 + (2 * y2 + py) * g.W1 + (2 * x2 + px);
-          a1[idx] = a1[idx] > 0.f ? acc[i] : 0.f;
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 s4 = h == 0 ? acc0 : acc1c;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qq = (qt + h) * 16 + lg * 4 + i;
+          if (qq < Q) {
+            const int y2 = qq / NX, x2 = qq - y2 * NX;
+            const int idx = lm * g.P1 + (2 * y2 + py) * g.W1 + (2 * x2 + px);
+            a1[idx] = a1[idx] > 0.f ? s4[i] : 0.f;
+          }
         }
       }
     }
@@ -264,13 +303,12 @@ cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
       const int p = 4 * j + lg;
       const bool ok = p < g.P1;
       const int pc = ok ? p : g.P1 - 1;
-      const int oy = pc / g.W1, ox = pc - oy * g.W1;
-      const int pb = oy * 4 * W + ox * 4;
+      const int pb = ofs1[pc];
       const float av = a1[lm * g.P1 + pc];
       const float a = ok ? av : 0.f;
 #pragma unroll
-      for (int t = 0; t < C; ++t)
-        acc1[t] = mfma4(a, u8_scale((float)img[koff1[t] + pb]), acc1[t]);
+      for (int t = 0; t < C; ++t)           // raw bytes; / 255 when the partial is written
+        acc1[t] = mfma4(a, (float)img[koff1[t] + pb], acc1[t]);
     }
     {
       const int ch = tid >> 4;
@@ -293,7 +331,7 @@ cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int co = lg * 4 + i, k = (w * C + t) * 16 + lm;
-      out[g.oW1 + co * g.K1 + k] = acc1[t][i];
+      out[g.oW1 + co * g.K1 + k] = acc1[t][i] / 255.0f;
     }
   red[tid] = db2p;
   __syncthreads();
@@ -317,6 +355,8 @@ static int cnn_check(const CnnGeom& g) {
   if (g.C != 3) return set_error(SMI_E_ARG, "cnn: only 3-channel cameras are built (camera0 RGB)");
   if (g.H1 < 4 || g.W1 < 4 || g.H2 < 1 || g.W2 < 1)
     return set_error(SMI_E_ARG, "cnn: image smaller than the two convolutions");
+  if ((g.P2 + 15) / 16 > 6)
+    return set_error(SMI_E_ARG, "cnn: conv-2 output larger than 96 pixels (84x84 gives 81)");
   if (g.W % 4 != 0 || g.img % 16 != 0 || g.P1 % 4 != 0 || g.W1 % 2 != 0 || g.flat % 4 != 0)
     return set_error(SMI_E_ARG, "cnn: need W % 4 == 0, C*H*W % 16 == 0, even conv-1 width, "
                                 "conv-1 pixels % 4 == 0 (84x84 qualifies)");
@@ -326,7 +366,8 @@ static int cnn_check(const CnnGeom& g) {
 
 static size_t cnn_fwd_lds(const CnnGeom& g) { return (size_t)lds_img_bytes(g) + (size_t)64 * g.P1; }
 static size_t cnn_bwd_lds(const CnnGeom& g) {
-  return (size_t)lds_img_bytes(g) + (size_t)64 * g.P1 + 4 * (size_t)round4(g.flat) + 4 * kWG;
+  return (size_t)lds_img_bytes(g) + (size_t)64 * g.P1 + 4 * (size_t)round4(g.flat) + 4 * kWG +
+         4 * (size_t)(g.P1 + g.P2);
 }
 
 int cnn_bwd_grid(int64_t rows) { return (int)(rows < kCnnPartials ? rows : kCnnPartials); }
