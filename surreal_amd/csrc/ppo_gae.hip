@@ -374,6 +374,214 @@ gae_rows_kernel(GaeWinArgs a) {
   }
 }
 
+// ------------------------------------------------ segment-per-thread variant
+// The RNN windows of the reference defaults (n_step T, horizon H compile-time;
+// ppo_configs.py: 25 / 5).  A workgroup owns SEG = 256 consecutive segments,
+// one per thread.  Their r, d, V are contiguous in HBM ([SEG][T], [SEG][T],
+// [SEG][T+1]) and move as ONE stream of 16-byte loads into LDS, register-
+// prefetched one block ahead; each thread then runs its row from LDS (stride
+// T floats: conflict-free for odd T) with the window sums in registers
+// (fully unrolled, H-deep ring), and the block's adv/ret leave through LDS as
+// 16-byte coalesced stores.  Same fp32 op order as gae_rows_kernel.
+template <int T, int H, int SEG_>
+struct GaeSeg {
+  static constexpr int SEG = SEG_, T1 = T + 1, E = T - H + 1;
+  static constexpr int NF4 = SEG * (3 * T + 1) / 4;            // float4s of one block
+  static constexpr int NPF = (NF4 + SEG - 1) / SEG;            // per thread
+  static constexpr size_t LDS = ((size_t)SEG * (3 * T + 1) + 2 * H) * 4;   // + gamma/lambda tables
+};
+
+template <int T, int H, int SEG_>
+__global__ void __launch_bounds__(SEG_)
+gae_seg_kernel(GaeWinArgs a, int64_t nblocks) {
+  using G = GaeSeg<T, H, SEG_>;
+  constexpr int SEG = G::SEG, T1 = G::T1, E = G::E, NPF = G::NPF, NF4 = G::NF4;
+  constexpr int NT = SEG;                                       // threads = segments
+  constexpr int NR4 = SEG * T / 4;                              // float4s of r (and of d)
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ double red[NT / 64];
+  float* sr = sm;                  // [SEG][T]
+  float* sd = sr + SEG * T;        // [SEG][T]
+  float* sv = sd + SEG * T;        // [SEG][T1]
+  const int tid = threadIdx.x;
+  float* sg = sv + SEG * T1;       // [H] gamma^k, [H] lambda^k (E == 1 reads them per step)
+  for (int k = tid; k < H; k += NT) { sg[k] = a.gtab[k]; sg[H + k] = a.ltab[k]; }
+  constexpr int HK = E > 1 ? H : 1;
+  float gk[HK], lk[HK];
+#pragma unroll
+  for (int k = 0; k < HK; ++k) { gk[k] = a.gtab[k]; lk[k] = a.ltab[k]; }
+  const float gamma = a.gamma, gamma_H = a.gamma_H;
+  double psum = 0.0, psq = 0.0;
+  // prefetch registers as named variables (an indexed float4 array stays in
+  // scratch whatever its shape)
+  static_assert(NPF <= 40, "gae_seg: prefetch depth");
+#define SMI_GAE_X24(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
+  X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26)   \
+  X(27) X(28) X(29) X(30) X(31) X(32) X(33) X(34) X(35) X(36) X(37) X(38) X(39)
+#define SMI_GAE_DECL(j) float4 pf##j = make_float4(0.f, 0.f, 0.f, 0.f);
+  SMI_GAE_X24(SMI_GAE_DECL)
+#define SMI_GAE_LD(j)                                                          \
+  if ((j) < NPF) {                                                             \
+    const int q = tid + (j) * NT;                                              \
+    const float4* src = q < NR4 ? r4 : (q < 2 * NR4 ? d4 : v4);                \
+    if (q < NF4) pf##j = src[q];                                               \
+  }
+#define SMI_GAE_ST(j)                                                          \
+  if ((j) < NPF) {                                                             \
+    const int q = tid + (j) * NT;                                              \
+    if (q < NF4) l4[q] = pf##j;                                                \
+  }
+#define SMI_GAE_SEG_PREFETCH(BLK)                                                              \
+  {                                                                                            \
+    const float4* r4 = reinterpret_cast<const float4*>(a.rewards + (BLK) * SEG * T);           \
+    const float4* d4 = reinterpret_cast<const float4*>(a.dones + (BLK) * SEG * T) - NR4;       \
+    const float4* v4 = reinterpret_cast<const float4*>(a.values + (BLK) * SEG * T1) - 2 * NR4; \
+    SMI_GAE_X24(SMI_GAE_LD)                                                                    \
+  }
+  if (blockIdx.x < nblocks) SMI_GAE_SEG_PREFETCH((int64_t)blockIdx.x)
+  for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    __syncthreads();                        // previous block's outputs have left LDS
+    {
+      float4* l4 = reinterpret_cast<float4*>(sm);
+      SMI_GAE_X24(SMI_GAE_ST)
+    }
+    if (blk + gridDim.x < nblocks) SMI_GAE_SEG_PREFETCH(blk + gridDim.x)
+    __syncthreads();
+    // ---- one segment row per thread
+    const float* r = sr + tid * T;
+    const float* d = sd + tid * T;
+    const float* v = sv + tid * T1;
+    float adv[E], ret[E];
+    constexpr int HR = E > 1 ? H : 1;
+    float rr[HR], tt[HR];                  // ring: index k = step (t - H + 1 + k)
+    float rs1 = 0.f, as1 = 0.f;            // E == 1: the single window, summed in k order
+    float vm = v[0];                       // Vm[t]
+    float dprev = 0.f;
+    // E > 1: fully unrolled (register-indexed windows); E == 1: partial unroll
+    // keeps the row's LDS reads from being hoisted into registers all at once
+#pragma unroll (E > 1 ? T : 5)
+    for (int t = 0; t < T; ++t) {
+      const float rt = r[t], dt = d[t];
+      if (t > 0) vm = v[t] * (1.f - dprev);
+      const float vm1 = v[t + 1] * (1.f - dt);
+      if (a.values_masked) a.values_masked[(blk * SEG + tid) * T1 + t] = vm;
+      const float td = (rt + gamma * vm1) - vm;
+      if constexpr (E == 1) {
+        const float g = sg[t], l = sg[H + t];
+        rs1 += g * rt;
+        as1 += (td * g) * l;
+        if (t == T - 1) {
+          ret[0] = rs1 + vm1 * gamma_H;
+          adv[0] = as1;
+          psum += (double)as1;
+          psq += (double)as1 * (double)as1;
+        }
+      } else {
+#pragma unroll
+      for (int k = 0; k < H - 1; ++k) { rr[k] = rr[k + 1]; tt[k] = tt[k + 1]; }
+      rr[H - 1] = rt;
+      tt[H - 1] = td;
+      if (t >= H - 1) {
+        float rs = 0.f, as = 0.f;
+#pragma unroll
+        for (int k = 0; k < H; ++k) {
+          rs += gk[k] * rr[k];
+          as += (tt[k] * gk[k]) * lk[k];
+        }
+        // window w = t - H + 1 needs Vm[w + H] = Vm[t + 1]
+        ret[t - H + 1] = rs + vm1 * gamma_H;
+        adv[t - H + 1] = as;
+        psum += (double)as;
+        psq += (double)as * (double)as;
+      }
+      }
+      dprev = dt;
+    }
+    if (a.values_masked) a.values_masked[(blk * SEG + tid) * T1 + T] = v[T] * (1.f - dprev);
+    __syncthreads();                        // every row has been read
+    float* oa = sr;                         // [SEG][E] adv   (E <= T)
+    float* orr = sd;                        // [SEG][E] ret
+#pragma unroll
+    for (int w = 0; w < E; ++w) { oa[tid * E + w] = adv[w]; orr[tid * E + w] = ret[w]; }
+    __syncthreads();
+    {
+      constexpr int NO4 = SEG * E / 4;
+      float4* ga = reinterpret_cast<float4*>(a.adv + blk * SEG * E);
+      float4* gr = reinterpret_cast<float4*>(a.ret + blk * SEG * E);
+      const float4* la = reinterpret_cast<const float4*>(oa);
+      const float4* lr = reinterpret_cast<const float4*>(orr);
+      for (int q = tid; q < NO4; q += NT) { ga[q] = la[q]; gr[q] = lr[q]; }
+      if constexpr ((SEG * E) % 4 != 0) {
+        for (int q = NO4 * 4 + tid; q < SEG * E; q += NT) {
+          a.adv[blk * SEG * E + q] = oa[q];
+          a.ret[blk * SEG * E + q] = orr[q];
+        }
+      }
+    }
+  }
+#undef SMI_GAE_SEG_PREFETCH
+#undef SMI_GAE_X24
+#undef SMI_GAE_DECL
+#undef SMI_GAE_LD
+#undef SMI_GAE_ST
+  const double s1 = block_sum_d<NT>(psum, red);
+  const double s2 = block_sum_d<NT>(psq, red);
+  if (threadIdx.x == 0 && a.partials) {
+    a.partials[2 * blockIdx.x] = s1;
+    a.partials[2 * blockIdx.x + 1] = s2;
+  }
+}
+
+// Launch the segment-per-thread kernel over the full 256-segment blocks; the
+// ragged tail goes to gae_rows_kernel (partials appended).  Returns false when
+// (T, H) has no instantiation or the buffers are not 16-byte aligned.
+template <int T, int H, int SEG>
+static bool try_gae_seg(const GaeWinArgs& a, int* n_partials, hipStream_t stream, int* rc) {
+  using G = GaeSeg<T, H, SEG>;
+  if (a.T != T || a.H != H) return false;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(a.rewards) | reinterpret_cast<uintptr_t>(a.dones) |
+                       reinterpret_cast<uintptr_t>(a.values) | reinterpret_cast<uintptr_t>(a.adv) |
+                       reinterpret_cast<uintptr_t>(a.ret);
+  if (al & 15) return false;
+  const int64_t nblk = a.B / G::SEG;
+  if (nblk < 1) return false;
+  auto k = gae_seg_kernel<T, H, SEG>;
+  allow_lds(k, G::LDS);
+  static int cap = 0;
+  if (!cap) {
+    cap = resident_grid(k, SEG, G::LDS);
+    if (cap > 1024) cap = 1024;
+  }
+  const int grid = (int)(nblk < cap ? nblk : cap);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(SEG), G::LDS, stream, a, nblk);
+  *rc = check_launch("gae_seg_kernel");
+  if (*rc) return true;
+  int np = grid;
+  const int64_t done = nblk * G::SEG;
+  if (done < a.B) {
+    GaeWinArgs t = a;
+    t.B = a.B - done;
+    t.values = a.values + done * (T + 1);
+    t.values_masked = a.values_masked ? a.values_masked + done * (T + 1) : nullptr;
+    t.rewards = a.rewards + done * T;
+    t.dones = a.dones + done * T;
+    t.adv = a.adv + done * G::E;
+    t.ret = a.ret + done * G::E;
+    t.partials = a.partials ? a.partials + 2 * grid : nullptr;
+    int TPR = 8;
+    while (TPR < T + 1) TPR *= 2;
+    const int64_t groups = (t.B + 64 / TPR - 1) / (64 / TPR);
+    int g2 = (int)((groups + kNW * 8 - 1) / (kNW * 8));
+    g2 = g2 < 1 ? 1 : (g2 > 1024 ? 1024 : g2);
+    if (TPR == 32) hipLaunchKernelGGL(gae_rows_kernel<32>, dim3(g2), dim3(kWG), 0, stream, t);
+    else hipLaunchKernelGGL(gae_rows_kernel<64>, dim3(g2), dim3(kWG), 0, stream, t);
+    *rc = check_launch("gae_rows_kernel");
+    np += g2;
+  }
+  if (n_partials) *n_partials = np;
+  return true;
+}
+
 // ============================================================ host launchers
 int launch_critic_gae(const float* critic_params, int D, int H1, int H2, int use_zf,
                       const float* zf_sum, const float* zf_sumsq, const float* zf_count,
@@ -430,6 +638,12 @@ int launch_gae_windows(const float* values, float* values_masked, const float* r
   a.E = T - H + 1;
   a.gtab = gtab; a.ltab = ltab; a.gamma = gamma; a.gamma_H = gamma_H;
   a.adv = adv; a.ret = ret; a.partials = partials;
+  {
+    int rc = 0;
+    // the reference defaults: RNN n_step 25 / horizon 5; non-RNN n_step 50
+    if (try_gae_seg<25, 5, 256>(a, n_partials, stream, &rc)) return rc;
+    if (try_gae_seg<50, 50, 128>(a, n_partials, stream, &rc)) return rc;
+  }
   if (T + 1 <= 64 && (a.E == 1 || H <= 16)) {
     int TPR = 8;
     while (TPR < T + 1) TPR *= 2;

@@ -180,7 +180,9 @@ def test_gae_known_answers():
         assert np.allclose(ret[:, 0].numpy(), case['ret'], rtol=1e-5, atol=1e-5), case['name']
 
 
-@pytest.mark.parametrize('B,T,H', [(64, 50, 50), (33, 25, 5), (1, 7, 1), (200, 25, 25), (5, 1, 1)])
+@pytest.mark.parametrize('B,T,H', [(64, 50, 50), (33, 25, 5), (1, 7, 1), (200, 25, 25), (5, 1, 1),
+                                   (256, 25, 5), (600, 25, 5), (3077, 25, 5), (300, 50, 50),
+                                   (1029, 50, 50)])
 def test_gae_windows_vs_oracle(B, T, H):
     g = torch.Generator().manual_seed(B + T)
     v = torch.randn(B, T + 1, generator=g)
