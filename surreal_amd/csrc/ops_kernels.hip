@@ -269,6 +269,84 @@ diag_gauss_kernel(const float* __restrict__ a, const float* __restrict__ p0,
   }
 }
 
+// Row-direct variant for A <= 8 (every BASELINE config): no LDS, no barriers.
+// Each thread owns whole rows and reads them with the widest aligned vector
+// loads (a row is 4A / 8A / 8A bytes); consecutive lanes read consecutive
+// rows, so the lines a wave touches are fully consumed from L1 by its next
+// vector loads.  U rows per thread are loaded before any is used.
+template <int W>
+struct VecT;
+template <> struct VecT<1> { typedef float T; };
+template <> struct VecT<2> { typedef float2 T; };
+template <> struct VecT<4> { typedef float4 T; };
+
+template <int N, int W>
+__device__ __forceinline__ void load_row(const float* __restrict__ src, float (&out)[N]) {
+  typedef typename VecT<W>::T V;
+  const V* s = reinterpret_cast<const V*>(src);
+#pragma unroll
+  for (int i = 0; i < N / W; ++i) {
+    const V v = s[i];
+    const float* f = reinterpret_cast<const float*>(&v);
+#pragma unroll
+    for (int k = 0; k < W; ++k) out[i * W + k] = f[k];
+  }
+}
+
+template <int A>
+__global__ void __launch_bounds__(kWG)
+diag_gauss_rows_kernel(const float* __restrict__ a, const float* __restrict__ p0,
+                       const float* __restrict__ p1, int64_t rows, float c_ll, float c_ent,
+                       float* loglik, float* lik, float* kl, float* ent) {
+  constexpr int WA = (A % 4 == 0) ? 4 : (A % 2 == 0) ? 2 : 1;
+  constexpr int WP = (A % 2 == 0) ? 4 : 2;
+  constexpr int U = 2;
+  const bool need_a = loglik || lik;
+  const bool need_p1 = kl && p1;
+  const int64_t nth = (int64_t)gridDim.x * kWG;
+  for (int64_t r0 = (int64_t)blockIdx.x * kWG + threadIdx.x; r0 < rows; r0 += U * nth) {
+    float ar[U][A], q0[U][2 * A], q1[U][2 * A];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t r = r0 + u * nth;
+      r = r < rows ? r : rows - 1;                   // clamped: every load is unconditional
+      load_row<2 * A, WP>(p0 + r * 2 * A, q0[u]);
+      if (need_a) load_row<A, WA>(a + r * A, ar[u]);
+      if (need_p1) load_row<2 * A, WP>(p1 + r * 2 * A, q1[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = r0 + u * nth;
+      if (r >= rows) break;
+      float lsum = 0.f;
+#pragma unroll
+      for (int j = 0; j < A; ++j) lsum += logf(q0[u][A + j]);
+      if (need_a) {
+        float sq = 0.f;
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+          const float z = (ar[u][j] - q0[u][j]) / q0[u][A + j];
+          sq += z * z;
+        }
+        const float ll = (-0.5f * sq - c_ll) - lsum;
+        if (loglik) loglik[r] = ll;
+        if (lik) lik[r] = fmaxf(expf(ll), 1e-5f);
+      }
+      if (need_p1) {
+        float k1 = 0.f, k2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+          k1 += logf(q1[u][A + j] / q0[u][A + j]);
+          const float d = q0[u][j] - q1[u][j];
+          k2 += (q0[u][A + j] * q0[u][A + j] + d * d) / (2.f * (q1[u][A + j] * q1[u][A + j]));
+        }
+        kl[r] = (k1 + k2) - 0.5f * (float)A;
+      }
+      if (ent) ent[r] = 0.5f * lsum + c_ent;
+    }
+  }
+}
+
 // -------------------------------------------------------------- MLP forward
 struct MlpFwdArgs {
   const float* params; int in, h1, h2, out, act, lv;
@@ -553,6 +631,23 @@ int launch_diag_gauss(const float* a, const float* p0, const float* p1, int64_t 
   const float c_ll = (float)(0.5 * log(2.0 * 3.141592653589793) * (double)A);
   const float c_ent = (float)(0.5 * log(2.0 * 3.141592653589793 * 2.718281828459045) * (double)A);
   if (rows <= 0) return SMI_OK;
+  const bool al = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(p0) |
+                    reinterpret_cast<uintptr_t>(p1)) & 15) == 0;
+  if (al && A >= 1 && A <= 8) {
+    const int64_t want = (rows + 2 * kWG - 1) / (2 * kWG);
+    const int grid = (int)(want < 8192 ? (want < 1 ? 1 : want) : 8192);
+#define SMI_DG_CASE(N)                                                                          \
+    case N:                                                                                     \
+      hipLaunchKernelGGL(diag_gauss_rows_kernel<N>, dim3(grid), dim3(kWG), 0, st, a, p0, p1,   \
+                         rows, c_ll, c_ent, ll, lik, kl, ent);                                  \
+      break;
+    switch (A) {
+      SMI_DG_CASE(1) SMI_DG_CASE(2) SMI_DG_CASE(3) SMI_DG_CASE(4)
+      SMI_DG_CASE(5) SMI_DG_CASE(6) SMI_DG_CASE(7) SMI_DG_CASE(8)
+    }
+#undef SMI_DG_CASE
+    return check_launch("diag_gauss_rows_kernel");
+  }
   const size_t lds = (size_t)DG_R * ((A | 1) + 2 * ((2 * A) | 1)) * 4;
   if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "diag_gauss: act_dim too large");
   allow_lds(diag_gauss_kernel, lds);
