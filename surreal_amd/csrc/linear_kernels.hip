@@ -302,6 +302,144 @@ gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, f
   }
 }
 
+// Small-K forward (K <= 64: the LSTM input projection x W_ih^T over the
+// observation width, the first layer of the DDPG nets).  The tiled kernel is
+// latency-bound there (two K-steps per 64x64 tile, prologue and epilogue
+// dominate); this one stages the whole weight W[N][K] (zero-padded to 4*NKU
+// k) in LDS once per workgroup, keeps a 64-row tile of X in registers as MFMA
+// A operands, and sweeps all N columns in groups of four 16-column blocks
+// (four independent NKU-long MFMA chains).  Workgroups are persistent over row
+// tiles.
+template <int NKU>
+__global__ void __launch_bounds__(kWG)
+gemm_smallk_fwd_kernel(const float* __restrict__ X, int64_t ldx, int M, int K,
+                       const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
+                       int N, int act, float* __restrict__ Y, int64_t ldy, const int* skip) {
+  if (skip && skip[0] != 0) return;
+  extern __shared__ __attribute__((aligned(16))) float sW[];
+  constexpr int LDK = 4 * NKU + 1;                  // odd: conflict-free B reads
+  constexpr int LDO = 68;                           // output staging [16][68] per wave
+  float* sb = sW + N * LDK;
+  float* so = sb + ((N + 3) & ~3) + (threadIdx.x >> 6) * 16 * LDO;
+  // staging: 8 independent loads in flight per thread (a plain loop waits for
+  // each load before the next: ~80 serialised L2 round trips per thread)
+  {
+    const int tot = N * LDK;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += 8 * kWG) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = e0 + j * kWG;
+        const int ec = e < tot ? e : tot - 1;
+        const int n = ec / LDK, k = ec - n * LDK;
+        const float x = W[(int64_t)n * ldw + (k < K ? k : K - 1)];
+        v[j] = k < K ? x : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = e0 + j * kWG;
+        if (e < tot) sW[e] = v[j];
+      }
+    }
+  }
+  for (int n = threadIdx.x; n < N; n += kWG) sb[n] = bias ? bias[n] : 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, lk = lane >> 4;
+  const bool vec_out = ((reinterpret_cast<uintptr_t>(Y) & 15) == 0) && (ldy % 4 == 0);
+  for (int tile = blockIdx.x; tile * 64 < M; tile += gridDim.x) {
+    const int m = tile * 64 + wave * 16 + li;
+    const int mc = m < M ? m : M - 1;
+    float a[NKU];
+#pragma unroll
+    for (int u = 0; u < NKU; ++u) {
+      const int k = 4 * u + lk;
+      const float x = X[(int64_t)mc * ldx + (k < K ? k : K - 1)];
+      a[u] = k < K ? x : 0.f;
+    }
+    for (int nb = 0; nb < N; nb += 64) {
+      f32x4 acc[4];
+      const float* w[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int n = nb + c * 16 + li;
+        w[c] = sW + (n < N ? n : N - 1) * LDK + lk;
+      }
+      // all B operands of the group first (one LDS round trip), then the MFMAs
+      float bw[4][NKU];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int u = 0; u < NKU; ++u) bw[c][u] = w[c][4 * u];
+#ifndef SMI_EXP
+#pragma unroll
+      for (int u = 0; u < NKU; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = mfma4(a[u], bw[c][u], acc[c]);
+#else
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c][0] = a[0] + bw[c][NKU - 1];
+#endif
+      // epilogue through the wave's LDS slab: rows leave as 16-byte stores
+      // (a wave-instruction writes 4 rows x 256 contiguous bytes)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = nb + c * 16 + li;
+        const float bn = col < N ? sb[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = acc[c][i] + bn;
+          if (act == ACT_RELU) v = v > 0.f ? v : 0.f;
+          else if (act == ACT_TANH) v = tanhf(v);
+          so[(lk * 4 + i) * LDO + c * 16 + li] = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = j * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+        const int row = tile * 64 + wave * 16 + r, col = nb + c4;
+        const float4 v = *reinterpret_cast<const float4*>(so + r * LDO + c4);
+        if (row < M) {
+          float* dst = Y + (int64_t)row * ldy + col;
+          if (vec_out && col + 3 < N) {
+            *reinterpret_cast<float4*>(dst) = v;
+          } else {
+            if (col < N) dst[0] = v.x;
+            if (col + 1 < N) dst[1] = v.y;
+            if (col + 2 < N) dst[2] = v.z;
+            if (col + 3 < N) dst[3] = v.w;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+static int launch_smallk_fwd(const float* X, int64_t ldx, int M, int K, const float* W,
+                             int64_t ldw, const float* b, int N, int act, float* Y, int64_t ldy,
+                             hipStream_t st, const int* skip) {
+  const int nku = (K + 3) / 4 <= 4 ? 4 : (K + 3) / 4 <= 8 ? 8 : (K + 3) / 4 <= 12 ? 12 : 16;
+  const size_t lds = ((size_t)N * (4 * nku + 1) + ((N + 3) & ~3) + 4 * 16 * 68) * 4;
+  const int tiles = (M + 63) / 64;
+  const int kslot = ktime_begin(st);
+#define SMI_SK_CASE(V)                                                                         \
+  if (nku == V) {                                                                              \
+    auto k = gemm_smallk_fwd_kernel<V>;                                                        \
+    allow_lds(k, lds);                                                                         \
+    static int cap = 0;                                                                        \
+    if (!cap) cap = resident_grid(k, kWG, lds);                                                \
+    const int grid = tiles < cap ? tiles : cap;                                                \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kWG), lds, st, X, ldx, M, K, W, ldw, b, N, act, Y, \
+                       ldy, skip);                                                             \
+  }
+  SMI_SK_CASE(4) SMI_SK_CASE(8) SMI_SK_CASE(12) SMI_SK_CASE(16)
+#undef SMI_SK_CASE
+  ktime_end(kslot, KT_GEMM_FWD, 2.0 * M * (double)N * K, st);
+  return check_launch("gemm_smallk_fwd_kernel");
+}
+
 float* workspace_f32(int64_t nfloats);
 
 template <int EPI>
@@ -373,6 +511,8 @@ int launch_slab_reduce(const float* part, int S, int64_t n, float* out, hipStrea
 int launch_linear_fwd(const float* X, int64_t ldx, int M, int K, const float* W, int64_t ldw,
                       const float* b, int N, int act, float* Y, int64_t ldy, hipStream_t st,
                       const int* skip) {
+  if (K >= 1 && K <= 64 && N >= 32 && N <= 512 && M >= 2048)
+    return launch_smallk_fwd(X, ldx, M, K, W, ldw, b, N, act, Y, ldy, st, skip);
   GemmArgs g{};
   g.M = M; g.N = N; g.K = K;
   g.A = X; g.a_rs = ldx; g.a_cs = 1;
