@@ -35,7 +35,7 @@ def _mtime(p):
 # Developer variants: 'prof' adds the epoch-kernel phase timer (-DSMI_PROF,
 # tools/fused_breakdown.py --phases); 'noinl' keeps the dense helpers out of line.  The product library is variant None.
 VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
-            'noinl_prof': ['-DSMI_DENSE_NOINLINE', '-DSMI_PROF'], 'exp': ['-DSMI_EXP']}
+            'noinl_prof': ['-DSMI_DENSE_NOINLINE', '-DSMI_PROF']}
 
 
 def lib_path(variant=None):

@@ -50,13 +50,10 @@ __host__ __device__ inline int64_t lds_img_bytes(const CnnGeom& g) { return (g.i
 //   conv2: M = P2 pixels, N = 32, K = 256; wave w owns channel tile w>>1 and
 //          pixel tiles (w&1), (w&1)+2, ...; one lane reads 4 consecutive A1
 //          floats (kx = 0..3) per 4 MFMAs.
-#ifndef SMI_EXP
-#define CNN_FWD_ATTR __attribute__((amdgpu_waves_per_eu(3, 3)))
-#else
-#define CNN_FWD_ATTR
-#endif
+// 3 waves per SIMD (168 VGPRs, a few bytes of scratch) beat 2 waves at 176:
+// 132 vs 143 us per 2688-image forward (tools/bench_cnn.py)
 template <int C>
-__global__ void __launch_bounds__(kWG) CNN_FWD_ATTR
+__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(3, 3)))
 cnn_fwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t rows,
                float* __restrict__ A1g, float* __restrict__ A2g, const int* skip) {
   if (skip && skip[0] != 0) return;

@@ -244,6 +244,10 @@ gemm_kernel(GemmArgs g) {
       if (m >= g.M) continue;
       float v = tot[c][i];
       if constexpr (EPI == EPI_FWD) {
+        if (g.part) {                           // split-K slab: raw sums
+          g.part[((int64_t)blockIdx.z * g.M + m) * g.N + n] = v;
+          continue;
+        }
         v += bias_n;
         if (g.act == ACT_RELU) v = v > 0.f ? v : 0.f;
         else if (g.act == ACT_TANH) v = tanhf(v);
@@ -273,7 +277,7 @@ gemm_kernel(GemmArgs g) {
 __global__ void __launch_bounds__(kWG)
 gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, float* C,
                           int64_t ldc, int ones_col, float* bias_out, int accumulate,
-                          const int* skip) {
+                          const int* skip, const float* bias, int act) {
   if (skip && skip[0] != 0) return;
   __shared__ float red[4][64];
   const int64_t MN = (int64_t)M * N;
@@ -292,8 +296,11 @@ gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, f
   red[zl][el] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (zl != 0 || e >= MN) return;
-  const float s = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+  float s = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
   const int m = (int)(e / N), n = (int)(e - (int64_t)m * N);
+  if (bias) s += bias[n];                       // split-K forward epilogue
+  if (act == ACT_RELU) s = s > 0.f ? s : 0.f;
+  else if (act == ACT_TANH) s = tanhf(s);
   if (n == ones_col) {
     bias_out[m] = accumulate ? bias_out[m] + s : s;
   } else {
@@ -371,15 +378,10 @@ gemm_smallk_fwd_kernel(const float* __restrict__ X, int64_t ldx, int M, int K,
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int u = 0; u < NKU; ++u) bw[c][u] = w[c][4 * u];
-#ifndef SMI_EXP
 #pragma unroll
       for (int u = 0; u < NKU; ++u)
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = mfma4(a[u], bw[c][u], acc[c]);
-#else
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c][0] = a[0] + bw[c][NKU - 1];
-#endif
       // epilogue through the wave's LDS slab: rows leave as 16-byte stores
       // (a wave-instruction writes 4 rows x 256 contiguous bytes)
 #pragma unroll
@@ -464,7 +466,10 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   int S = 1;
   g.part = nullptr;
   g.kchunk = g.K > 0 ? g.K : 1;
-  if (epi == EPI_DW && g.K > 4 * GBK) {
+  // split-K: weight gradients (K = rows), and forwards whose output has too
+  // few tiles to fill the GPU over a long K (the pixel stem's 2592 -> 256 FC)
+  const bool split_fwd = epi == EPI_FWD && gm * gn < 256 && g.K >= 16 * GBK;
+  if ((epi == EPI_DW && g.K > 4 * GBK) || split_fwd) {
     const int tiles = gm * gn;
     S = (1024 + tiles - 1) / tiles;                   // ~4 workgroups per CU
     const int smax = (g.K + 4 * GBK - 1) / (4 * GBK);   // >= 4 K-steps per slab
@@ -492,8 +497,10 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   const int rslot = ktime_begin(st);
   const int64_t MN = (int64_t)g.M * g.N;
   const int rg = (int)((MN + 63) / 64);
+  const bool fwd = epi == EPI_FWD;
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, g.part, S, g.M, g.N,
-                     g.C, g.ldc, g.ones_col, g.bias_out, g.accumulate, g.skip);
+                     g.C, g.ldc, g.ones_col, g.bias_out, g.accumulate, g.skip,
+                     fwd ? g.bias : nullptr, fwd ? g.act : ACT_NONE);
   ktime_end(rslot, KT_GEMM_REDUCE, (double)S * MN, st);
   return check_launch("gemm_splitk_reduce_kernel");
 }
@@ -504,7 +511,7 @@ int launch_slab_reduce(const float* part, int S, int64_t n, float* out, hipStrea
   if (n < 1 || S < 1) return SMI_OK;
   const int rg = (int)((n + 63) / 64);
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, part, S, 1, (int)n, out,
-                     n, -1, nullptr, 0, skip);
+                     n, -1, nullptr, 0, skip, nullptr, ACT_NONE);
   return check_launch("gemm_splitk_reduce_kernel");
 }
 
