@@ -19,6 +19,7 @@
 // contiguous dimension (leading dims 36 / 80: conflict-free MFMA operand
 // reads and contiguous-dimension stores).  Global loads use clamped addresses
 // and are zeroed afterwards (no predicated loads: see cdna_hip_programming.md).
+#include <stdlib.h>
 #include <type_traits>
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
@@ -442,7 +443,142 @@ static int launch_smallk_fwd(const float* X, int64_t ldx, int M, int K, const fl
   return check_launch("gemm_smallk_fwd_kernel");
 }
 
+// Weight-gradient GEMM with 128x128 output tiles (dW[m][n] = sum_r dY[r][m]
+// X[r][n], r = the B*E rows).  The 64x64 kernel re-reads dY once per 64
+// output columns and X once per 64 output rows (5x / 4x for the 300x200
+// head): at these shapes the launch moves ~5x its unique bytes through L2 and
+// is bound by that, not by the MFMAs.  128x128 halves both re-read factors
+// and raises MFMAs per LDS operand read (16 MFMAs per 10 reads).  Both
+// operands are row-contiguous slabs of 32 rows: float4 loads straight into
+// [k][col] LDS images (row pitch 144: a half-wave's 32 lanes hit 32 banks),
+// one K-step of register prefetch, one barrier per K-step.  Wave w owns
+// output rows [32w, 32w+32) x 128 columns (16 accumulators).  The reduction
+// is one MFMA chain per K-slab (split-K keeps slabs <= 512 rows); slab
+// partials go to the fixed-order reducer as in gemm_kernel.
+constexpr int D2_T = 128, D2_LD = 144;
+
+__device__ __forceinline__ void dw2_load(const float* __restrict__ P, int64_t rs, int c0,
+                                         int cdata, int ones_col, int k0, int kmax, float4 (&r)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = threadIdx.x + j * kWG;            // 32 rows x 32 float4
+    const int k = q >> 5, c = c0 + ((q & 31) << 2);
+    const int kk = k0 + k;
+    const int kc = kk < kmax ? kk : kmax - 1;
+    const int cc = c + 3 < cdata ? c : (cdata >= 4 ? cdata - 4 : 0);
+    float4 v = *reinterpret_cast<const float4*>(P + (int64_t)kc * rs + cc);
+    const bool okk = kk < kmax;
+    v.x = okk && c < cdata ? v.x : 0.f;
+    v.y = okk && c + 1 < cdata ? v.y : 0.f;
+    v.z = okk && c + 2 < cdata ? v.z : 0.f;
+    v.w = okk && c + 3 < cdata ? v.w : 0.f;
+    if (ones_col >= 0 && okk) {
+      if (c == ones_col) v.x = 1.f;
+      if (c + 1 == ones_col) v.y = 1.f;
+      if (c + 2 == ones_col) v.z = 1.f;
+      if (c + 3 == ones_col) v.w = 1.f;
+    }
+    r[j] = v;
+  }
+}
+
+__device__ __forceinline__ void dw2_store(float* __restrict__ S, const float4 (&r)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = threadIdx.x + j * kWG;
+    *reinterpret_cast<float4*>(S + (q >> 5) * D2_LD + ((q & 31) << 2)) = r[j];
+  }
+}
+
+__global__ void __launch_bounds__(kWG)
+gemm_dw128_kernel(GemmArgs g) {
+  if (g.skip && g.skip[0] != 0) return;
+  __shared__ __attribute__((aligned(16))) float sA[2][32 * D2_LD];
+  __shared__ __attribute__((aligned(16))) float sB[2][32 * D2_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int m0 = blockIdx.x * D2_T, n0 = blockIdx.y * D2_T;
+  const int kb = blockIdx.z * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  const int nk = (ke - kb + 31) / 32;
+  const int bdata = g.ones_col >= 0 ? g.ones_col + 1 : g.N;   // the ones column is synthesised
+  const int bload = g.ones_col >= 0 ? g.ones_col : g.N;       // real columns of X
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 ra[4], rb[4];
+  (void)bdata;
+  if (nk > 0) {
+    dw2_load(g.A, g.a_cs, m0, g.M, -1, kb, ke, ra);
+    dw2_load(g.B, g.b_rs, n0, bload, g.ones_col, kb, ke, rb);
+    dw2_store(sA[0], ra);
+    dw2_store(sB[0], rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      dw2_load(g.A, g.a_cs, m0, g.M, -1, kb + (kt + 1) * 32, ke, ra);
+      dw2_load(g.B, g.b_rs, n0, bload, g.ones_col, kb + (kt + 1) * 32, ke, rb);
+    }
+    const float* As = sA[cur];
+    const float* Bs = sB[cur];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int kr = (4 * u + lk) * D2_LD;
+      float av[2], bv[8];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) av[a] = As[kr + wave * 32 + a * 16 + li];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) bv[b] = Bs[kr + b * 16 + li];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = mfma4(av[a], bv[b], acc[a][b]);
+    }
+    if (kt + 1 < nk) {
+      dw2_store(sA[cur ^ 1], ra);
+      dw2_store(sB[cur ^ 1], rb);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const int n = n0 + b * 16 + li;
+    if (n >= g.N) continue;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wave * 32 + a * 16 + lk * 4 + i;
+        if (m >= g.M) continue;
+        const float v = acc[a][b][i];
+        if (g.part) {
+          g.part[((int64_t)blockIdx.z * g.M + m) * g.N + n] = v;
+        } else if (n == g.ones_col) {
+          g.bias_out[m] = g.accumulate ? g.bias_out[m] + v : v;
+        } else {
+          float* dst = g.C + (int64_t)m * g.ldc + n;
+          *dst = g.accumulate ? *dst + v : v;
+        }
+      }
+  }
+}
+
 float* workspace_f32(int64_t nfloats);
+
+// split-K target workgroup count (SMI_SPLITK_TARGET overrides; tuning knob)
+static int smi_splitk_target() {
+  static int t = 0;
+  if (!t) {
+    const char* e = getenv("SMI_SPLITK_TARGET");
+    t = e ? atoi(e) : 512;
+    if (t < 64) t = 64;
+  }
+  return t;
+}
 
 template <int EPI>
 static void gemm_dispatch(const GemmArgs& g, dim3 grid, bool ak, bool bk, hipStream_t st) {
@@ -462,7 +598,15 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   g.avec = al16(g.A) && (ak ? (g.K % 4 == 0 && g.a_rs % 4 == 0) : (g.a_rs == 1 && g.M % 4 == 0 && g.a_cs % 4 == 0));
   const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
   g.bvec = al16(g.B) && (bk ? (g.K % 4 == 0 && g.b_cs % 4 == 0) : (g.b_cs == 1 && bdata % 4 == 0 && g.b_rs % 4 == 0));
-  const int gm = (g.M + GBM - 1) / GBM, gn = (g.N + GBN - 1) / GBN;
+  // 128x128 weight-gradient tiles when both operands are row-contiguous
+  // float4-able slabs and the output is large enough to need them
+  const int breal = g.ones_col >= 0 ? g.ones_col : g.N;
+  const bool dw128 = epi == EPI_DW && !ak && !bk && g.a_rs == 1 && g.b_cs == 1 &&
+                     al16(g.A) && al16(g.B) && g.M % 4 == 0 && breal % 4 == 0 &&
+                     g.a_cs % 4 == 0 && g.b_rs % 4 == 0 && g.M >= 96 && g.N >= 96 &&
+                     g.K >= 1024;
+  const int TM = dw128 ? D2_T : GBM, TN = dw128 ? D2_T : GBN;
+  const int gm = (g.M + TM - 1) / TM, gn = (g.N + TN - 1) / TN;
   int S = 1;
   g.part = nullptr;
   g.kchunk = g.K > 0 ? g.K : 1;
@@ -471,10 +615,15 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   const bool split_fwd = epi == EPI_FWD && gm * gn < 256 && g.K >= 16 * GBK;
   if ((epi == EPI_DW && g.K > 4 * GBK) || split_fwd) {
     const int tiles = gm * gn;
-    S = (1024 + tiles - 1) / tiles;                   // ~4 workgroups per CU
+    S = (smi_splitk_target() + tiles - 1) / tiles;    // ~2-4 workgroups per CU
     const int smax = (g.K + 4 * GBK - 1) / (4 * GBK);   // >= 4 K-steps per slab
     if (S > smax) S = smax;
     const int64_t cap = smi_workspace_floats() / ((int64_t)g.M * g.N);
+    if (S > cap) S = (int)cap;
+    if (S < 1) S = 1;
+    // one MFMA chain per slab: <= 512 rows (longer fixed slabs measured slower:
+    // fewer workgroups in flight outweigh the smaller partial traffic)
+    if (dw128 && (g.K + S - 1) / S > 512) S = (g.K + 511) / 512;
     if (S > cap) S = (int)cap;
     if (S < 1) S = 1;
     if (S > 1) {
@@ -486,7 +635,8 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   }
   const dim3 grid(gm, gn, S);
   const int kslot = ktime_begin(st);
-  if (epi == EPI_FWD) gemm_dispatch<EPI_FWD>(g, grid, ak, bk, st);
+  if (dw128) hipLaunchKernelGGL(gemm_dw128_kernel, grid, dim3(kWG), 0, st, g);
+  else if (epi == EPI_FWD) gemm_dispatch<EPI_FWD>(g, grid, ak, bk, st);
   else if (epi == EPI_DX) gemm_dispatch<EPI_DX>(g, grid, ak, bk, st);
   else gemm_dispatch<EPI_DW>(g, grid, ak, bk, st);
   const int nreal = g.ones_col >= 0 ? g.N - 1 : g.N;
