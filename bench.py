@@ -140,8 +140,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        ndev = torch.cuda.device_count()
+        local_rank = local_rank % max(ndev, 1)       # rehearsal: several ranks per GPU
         torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        # 'nccl' = RCCL over xGMI; SMI_DIST_BACKEND=gloo rehearses the same
+        # code path with several ranks on one GPU (RCCL refuses that)
+        backend = os.environ.get('SMI_DIST_BACKEND', 'nccl')
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device('cuda', torch.cuda.current_device())
