@@ -324,7 +324,11 @@ int smi_ppo_epoch_apply(const smi_ppo_args* args, int epoch, void* stream);
 typedef struct smi_ppo_rnn_args {
   /* dims (local batch) */
   int B, T, horizon;                 /* segments on this rank, n_step, horizon */
-  int obs_dim, rnn_hidden;           /* D, H (one LSTM layer)                 */
+  int obs_dim, rnn_hidden;           /* D, H (one LSTM layer).  H == 0: no LSTM — the heads
+                                        read the stem input [zfilter(low) | cnn] directly
+                                        (the non-RNN pixel model); then horizon == T (one
+                                        window: ppo.py:408-418) and only step 0 of each
+                                        segment trains (ppo.py:532-535) */
   int h1, h2, act_dim;               /* actor head                            */
   int critic_h1, critic_h2;
   int epoch_policy, epoch_baseline;

@@ -411,10 +411,11 @@ int64_t smi_ppo_rnn_xbuf_floats(int obs_dim, int rnn_hidden, int h1, int h2, int
                                 int critic_h1, int critic_h2, int pix_c, int pix_h, int pix_w,
                                 int cnn_feat) {
   const int F = cnn_feat > 0 ? cnn_feat : 0;
-  const int64_t ns = smi_lstm_param_count(obs_dim + F, rnn_hidden) +
+  const int hin = rnn_hidden > 0 ? rnn_hidden : obs_dim + F;     // 0: MLP policy on the stem
+  const int64_t ns = (rnn_hidden > 0 ? smi_lstm_param_count(obs_dim + F, rnn_hidden) : 0) +
                      (F > 0 ? smi_cnn_param_count(pix_c, pix_h, pix_w, F) : 0);
-  return mlp_layout(rnn_hidden, h1, h2, act_dim, 1).fcount +
-         mlp_layout(rnn_hidden, critic_h1, critic_h2, 1, 0).fcount + 2 * ns;
+  return mlp_layout(hin, h1, h2, act_dim, 1).fcount +
+         mlp_layout(hin, critic_h1, critic_h2, 1, 0).fcount + 2 * ns;
 }
 
 int64_t smi_cnn_scratch_bytes(int64_t rows, int C, int H, int W, int F) {
@@ -456,12 +457,17 @@ int smi_ppo_rnn_phase(const smi_ppo_rnn_args* a, int phase, int epoch, void* str
   REQUIRE(a->cnn_feat <= 0 || (a->pixels && a->pixels_next),
           "ppo_rnn: pixel stem needs pixels and pixels_next");
   REQUIRE(!(a->use_zf && a->obs_dim == 0), "ppo_rnn: z-filter needs low-dim observations");
-  REQUIRE(a->rnn_hidden >= 1 && a->rnn_hidden <= 256, "ppo_rnn: rnn_hidden must be in [1, 256]");
+  REQUIRE(a->rnn_hidden >= 0 && a->rnn_hidden <= 256,
+          "ppo_rnn: rnn_hidden must be in [0, 256] (0: MLP policy over the stem input)");
+  REQUIRE(a->rnn_hidden > 0 || a->horizon == a->T,
+          "ppo_rnn: the MLP policy (rnn_hidden 0) uses horizon == n_step (one window)");
   REQUIRE(a->act_dim >= 1 && a->act_dim <= 32, "ppo_rnn: act_dim must be in [1, 32]");
   REQUIRE(a->h1 >= 1 && a->h2 >= 1 && a->critic_h1 >= 1 && a->critic_h2 >= 1, "ppo_rnn: bad hidden sizes");
-  REQUIRE((a->obs_dim == 0 || (a->obs && a->obs_next)) && a->actions && a->rewards && a->dones && a->behave && a->h0 &&
-          a->c0, "ppo_rnn: null batch pointer");
-  REQUIRE(a->lstm && a->actor && a->critic && a->ref_lstm && a->ref_actor, "ppo_rnn: null params");
+  REQUIRE((a->obs_dim == 0 || (a->obs && a->obs_next)) && a->actions && a->rewards && a->dones &&
+          a->behave && (a->rnn_hidden == 0 || (a->h0 && a->c0)), "ppo_rnn: null batch pointer");
+  REQUIRE(a->actor && a->critic && a->ref_actor &&
+          ((a->rnn_hidden == 0 && a->cnn_feat <= 0) || (a->lstm && a->ref_lstm)),
+          "ppo_rnn: null params");
   REQUIRE(a->actor_m && a->actor_v && a->critic_m && a->critic_v && a->actor_step &&
           a->critic_step && a->hyper && a->gamma_tab && a->lam_tab, "ppo_rnn: null optimizer state");
   REQUIRE(a->stats && a->kl_record && a->kl_count && a->moments && a->pstat && a->xbuf && a->zbuf &&

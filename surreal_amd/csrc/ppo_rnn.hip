@@ -46,6 +46,7 @@ enum { CF_KLCOEF = 0, CF_SURRW, CF_COUNT = 8 };
 struct RnnDims {
   int B, T, Hz, E, S1, D, H, G4, A, h1, h2, c1, c2;
   int F, Din;                         // pixel features (0: no CNN stem), LSTM input D + F
+  int Hin;                            // head input width: H (LSTM) or Din (H == 0: MLP policy)
   int64_t NE, NG;
   int64_t nA_head, nC_head, nL, nCnn, nS;   // parameter counts; stem = [lstm | cnn]
   MlpLayout LA, LC;
@@ -62,10 +63,11 @@ __host__ __device__ inline RnnDims rnn_dims(int B, int T, int Hz, int D, int H, 
   d.B = B; d.T = T; d.Hz = Hz; d.E = T - Hz + 1; d.S1 = T + 1; d.D = D; d.H = H; d.G4 = 4 * H;
   d.A = A; d.h1 = h1; d.h2 = h2; d.c1 = c1; d.c2 = c2;
   d.NE = (int64_t)d.E * B; d.NG = (int64_t)d.S1 * B;
-  d.LA = mlp_layout(H, h1, h2, A, 1);
-  d.LC = mlp_layout(H, c1, c2, 1, 0);
+  d.Hin = H > 0 ? H : d.Din;
+  d.LA = mlp_layout(d.Hin, h1, h2, A, 1);
+  d.LC = mlp_layout(d.Hin, c1, c2, 1, 0);
   d.nA_head = d.LA.fcount; d.nC_head = d.LC.fcount;
-  d.nL = (int64_t)4 * H * d.Din + (int64_t)4 * H * H + 8 * (int64_t)H;
+  d.nL = H > 0 ? (int64_t)4 * H * d.Din + (int64_t)4 * H * H + 8 * (int64_t)H : 0;
   d.nS = d.nL + d.nCnn;
   return d;
 }
@@ -604,10 +606,12 @@ static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, fl
 }
 
 // backward from dZ (gradient at the last layer's pre-activation) into the flat
-// gradient image G (same layout as P); dX (no mask) to dXout
+// gradient image G (same layout as P); input-gradient columns [dx0, dx0+dxn)
+// to dXout ([rows][dxn], masked by dxmask > 0 when given; dxn == 0: none)
 static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx, int64_t rows,
                     const float* HA1, const float* HA2, float* dH1, float* dH2, float* G,
-                    float* dXout, hipStream_t st, const int* skip) {
+                    int dx0, int dxn, const float* dxmask, int64_t ldm, float* dXout,
+                    hipStream_t st, const int* skip) {
   const int M = (int)rows;
   const MlpLayout& L = h.L;
   RC(launch_linear_bwd_dw(dZ, h.out, M, h.out, HA2, h.h2, h.h2, G + L.fW3, h.h2, G + L.fb3, 0, st,
@@ -620,8 +624,9 @@ static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx,
                           skip));
   RC(launch_linear_bwd_dw(dH1, h.h1, M, h.h1, X, ldx, h.in, G + L.fW1, h.in, G + L.fb1, 0, st,
                           skip));
-  return launch_linear_bwd_dx(dH1, h.h1, M, h.h1, h.P + L.fW1, h.in, h.in, nullptr, 0, dXout,
-                              h.in, st, skip);
+  if (dxn <= 0) return SMI_OK;
+  return launch_linear_bwd_dx(dH1, h.h1, M, h.h1, h.P + L.fW1 + dx0, h.in, dxn, dxmask, ldm, dXout,
+                              dxn, st, skip);
 }
 
 struct LstmP { const float *Wih, *Whh, *bih, *bhh; };
@@ -675,6 +680,13 @@ static int cnn_features(const smi_ppo_rnn_args& a, const RnnDims& d, const float
                      X + d.D, d.Din, st, skip);
 }
 
+// CNN backward from dF = dL/d(features) * relu'(features) in s.dF
+static int cnn_bwd_from_dF(const smi_ppo_rnn_args& a, const RnnDims& d, const float* cnn,
+                           float* Gc, const RnnScratch& s, hipStream_t st, const int* skip) {
+  return cnn_backward(cnn, pix_rows(a, d), d.G.C, d.G.H, d.G.W, d.F, d.NE, s.A1, s.A2, s.dF, d.F,
+                      Gc, s.dA2, s.cpart, st, skip);
+}
+
 // pixel-stem gradient (into Gc) from the LSTM gate gradients of the E steps:
 // dF = relu'(F) * (dgates W_ih[:, D:]), then the CNN backward
 static int cnn_grad(const smi_ppo_rnn_args& a, const RnnDims& d, const LstmP& l, const float* cnn,
@@ -682,8 +694,31 @@ static int cnn_grad(const smi_ppo_rnn_args& a, const RnnDims& d, const LstmP& l,
   if (d.F == 0) return SMI_OK;
   RC(launch_linear_bwd_dx(s.dgates, d.G4, (int)d.NE, d.G4, l.Wih + d.D, d.Din, d.F, s.Xz + d.D,
                           d.Din, s.dF, d.F, st, skip));
-  return cnn_backward(cnn, pix_rows(a, d), d.G.C, d.G.H, d.G.W, d.F, d.NE, s.A1, s.A2, s.dF, d.F,
-                      Gc, s.dA2, s.cpart, st, skip);
+  return cnn_bwd_from_dF(a, d, cnn, Gc, s, st, skip);
+}
+
+// the policy / value features the heads read: LSTM outputs hbuf[1..] ([S][B][H])
+// or, without the LSTM (MLP policy), the stem input itself ([S][B][Din])
+static const float* head_in(const RnnDims& d, const RnnScratch& s, const float* X) {
+  return d.H > 0 ? s.hbuf + (int64_t)d.B * d.H : X;
+}
+
+// backward of one head into G (+ the stem below it): LSTM BPTT and/or CNN
+static int stem_backward(const smi_ppo_rnn_args& a, const RnnDims& d, const Head& hd,
+                         const LstmP& lm, const float* cnn, float* G, const RnnScratch& s,
+                         int64_t n_head, hipStream_t st, const int* skip) {
+  const float* X = head_in(d, s, s.Xz);
+  if (d.H > 0) {
+    RC(head_bwd(hd, s.dOUT, X, d.Hin, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, 0, d.H, nullptr, 0,
+                s.dh, st, skip));
+    RC(lstm_backward(d, lm, G + n_head, s, st, skip));
+    return cnn_grad(a, d, lm, cnn, G + n_head + d.nL, s, st, skip);
+  }
+  // MLP policy: the first head layer's input gradient over the CNN columns only
+  RC(head_bwd(hd, s.dOUT, X, d.Hin, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, d.D, d.F, s.Xz + d.D,
+              d.Din, s.dF, st, skip));
+  if (d.F == 0) return SMI_OK;
+  return cnn_bwd_from_dF(a, d, cnn, G + n_head, s, st, skip);
 }
 
 static float c_loglik_of(int A) { return (float)(0.5 * log(2.0 * 3.141592653589793) * (double)A); }
@@ -716,8 +751,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
   const int* stop = s.ci + CI_STOP;
   const LstmP lm = lstm_params(a.lstm, d.Din, d.H);
   const float* cnn = a.lstm + d.nL;                    // stem = [lstm | cnn]
-  const Head actor{a.actor, d.LA, d.H, d.h1, d.h2, d.A, 1};
-  const Head critic{a.critic, d.LC, d.H, d.c1, d.c2, 1, 0};
+  const Head actor{a.actor, d.LA, d.Hin, d.h1, d.h2, d.A, 1};
+  const Head critic{a.critic, d.LC, d.Hin, d.c1, d.c2, 1, 0};
   float* gA = a.xbuf;                                  // [actor head | lstm | cnn]
   float* gC = a.xbuf + d.nA_head + d.nS;               // [critic head | lstm | cnn]
   const int64_t NEg = (int64_t)d.E * a.B_global;
@@ -731,8 +766,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                          a.zf_count, a.zf_eps, s.Xz, d.Din);
       RC(check_launch("zf_tmajor_kernel"));
       RC(cnn_features(a, d, cnn, d.S1, s.Xz, nullptr, s, st, nullptr));
-      RC(lstm_forward(d, lm, s.Xz, d.S1, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
-      RC(head_fwd(critic, s.hbuf + (int64_t)d.B * d.H, d.H, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
+      if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.S1, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
+      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hin, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
       hipLaunchKernelGGL(tmajor_to_bmajor_kernel, dim3(grid_of(d.NG)), dim3(kWG), 0, st, s.OUT,
                          d.S1, d.B, s.values);
       RC(check_launch("tmajor_to_bmajor_kernel"));
@@ -756,15 +791,15 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
         X = s.Xr;
       }
       const LstmP lr = lstm_params(a.ref_lstm, d.Din, d.H);
-      RC(lstm_forward(d, lr, X, d.E, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
-      const Head ref{a.ref_actor, d.LA, d.H, d.h1, d.h2, d.A, 1};
-      return head_fwd(ref, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.refmu, st,
+      if (d.H > 0) RC(lstm_forward(d, lr, X, d.E, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
+      const Head ref{a.ref_actor, d.LA, d.Hin, d.h1, d.h2, d.A, 1};
+      return head_fwd(ref, head_in(d, s, X), d.Hin, d.NE, s.HA1, s.HA2, s.refmu, st,
                       nullptr);
     }
     case SMI_RNN_PH_POLICY_FWD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, stop));
-      RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, stop));
-      RC(head_fwd(actor, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
+      if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, stop));
+      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hin, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE);
       hipLaunchKernelGGL(policy_rows_stats_kernel, dim3(nb), dim3(kWG), 0, st, p);
@@ -785,13 +820,10 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       const int nb = rnn_nblk(d.NE);
       hipLaunchKernelGGL(policy_rows_grad_kernel, dim3(nb), dim3(kWG), 0, st, p);
       RC(check_launch("policy_rows_grad_kernel"));
-      RC(head_bwd(actor, s.dOUT, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.dH1, s.dH2,
-                  gA, s.dh, st, stop));
+      RC(stem_backward(a, d, actor, lm, cnn, gA, s, d.nA_head, st, stop));
       hipLaunchKernelGGL(logvar_grad_kernel, dim3(1), dim3(64), 0, st, s.lvpart, nb, d.A,
                          a.actor + d.LA.flv, gA + d.LA.flv, stop);
-      RC(check_launch("logvar_grad_kernel"));
-      RC(lstm_backward(d, lm, gA + d.nA_head, s, st, stop));
-      return cnn_grad(a, d, lm, cnn, gA + d.nA_head + d.nL, s, st, stop);
+      return check_launch("logvar_grad_kernel");
     }
     case SMI_RNN_PH_POLICY_APPLY: {
       const int64_t n = d.nA_head + d.nS;
@@ -810,8 +842,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     }
     case SMI_RNN_PH_VALUE_GRAD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
-      RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, nullptr));
-      RC(head_fwd(critic, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
+      if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, nullptr));
+      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hin, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
       const int nb = rnn_nblk(d.NE);
       const bool last = e == a.epoch_baseline - 1;
       hipLaunchKernelGGL(value_rows_kernel, dim3(nb), dim3(kWG), 0, st, s.OUT, s.ret, d.B, d.E,
@@ -822,10 +854,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                            a.zbuf, nullptr);
         RC(check_launch("reduce_partials_kernel"));
       }
-      RC(head_bwd(critic, s.dOUT, s.hbuf + (int64_t)d.B * d.H, d.H, d.NE, s.HA1, s.HA2, s.dH1,
-                  s.dH2, gC, s.dh, st, nullptr));
-      RC(lstm_backward(d, lm, gC + d.nC_head, s, st, nullptr));
-      return cnn_grad(a, d, lm, cnn, gC + d.nC_head + d.nL, s, st, nullptr);
+      return stem_backward(a, d, critic, lm, cnn, gC, s, d.nC_head, st, nullptr);
     }
     case SMI_RNN_PH_VALUE_APPLY: {
       const int64_t n = d.nC_head + d.nS;

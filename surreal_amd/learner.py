@@ -150,9 +150,6 @@ class PPOLearner(object):
             raise NotImplementedError('surreal_amd: the LSTM policy supports rnn_layer == 1 '
                                       '(the reference default)')
         self.if_pixel_input = bool(ec.get('pixel_input', False))
-        if self.if_pixel_input and not self.if_rnn_policy:
-            raise NotImplementedError('surreal_amd: the pixel stem is built for the LSTM policy '
-                                      '(SURVEY C5); pixel + MLP-only learners are not')
         if dp is not None and self.use_r_filter:
             raise NotImplementedError('surreal_amd: RewardFilter under data parallelism needs a '
                                       'global reward all-reduce (not built yet)')
@@ -277,7 +274,7 @@ class PPOLearner(object):
 
     def _optimize(self, obs, actions, rewards, obs_next, persistent_infos, onetime_infos, dones):
         """ppo.py:487-586 (low-dim model; LSTM stem via _optimize_rnn)."""
-        if self.if_rnn_policy:
+        if self.if_rnn_policy or self.if_pixel_input:      # phase path (LSTM and/or CNN stem)
             yield from self._optimize_rnn(obs, actions, rewards, obs_next, persistent_infos,
                                           onetime_infos, dones)
             return
@@ -415,12 +412,15 @@ class PPOLearner(object):
         if B != self.batch_size or T != self.n_step:
             raise ValueError(f'batch shape (B={B}, T={T}) != config (batch_size={self.batch_size}, '
                              f'n_step={self.n_step})')
-        if onetime_infos is None or len(onetime_infos) < 2:
-            raise ValueError('RNN policy: onetime_infos must hold the (h, c) LSTM cells')
         A = self.action_dim
-        Hd = self.learner_config.algo.rnn.rnn_hidden
-        h0 = onetime_infos[0].reshape(B, -1, Hd)[:, 0, :].contiguous()   # (B, L, H) -> layer 0
-        c0 = onetime_infos[1].reshape(B, -1, Hd)[:, 0, :].contiguous()
+        if self.if_rnn_policy:
+            if onetime_infos is None or len(onetime_infos) < 2:
+                raise ValueError('RNN policy: onetime_infos must hold the (h, c) LSTM cells')
+            Hd = self.learner_config.algo.rnn.rnn_hidden
+            h0 = onetime_infos[0].reshape(B, -1, Hd)[:, 0, :].contiguous()   # (B, L, H) -> layer 0
+            c0 = onetime_infos[1].reshape(B, -1, Hd)[:, 0, :].contiguous()
+        else:                       # MLP policy over the pixel stem (ppo.py:532-535: step 0)
+            Hd, h0, c0 = 0, None, None
         pds = persistent_infos[-1].contiguous()
         actions = actions.contiguous()
         dones = dones.contiguous()
@@ -430,7 +430,7 @@ class PPOLearner(object):
         rzf = rm.z_filter if self.use_z_filter else None
         a_h1, a_h2 = self.learner_config.model.actor_fc_hidden_sizes
         c_h1, c_h2 = self.learner_config.model.critic_fc_hidden_sizes
-        H = self.horizon
+        H = self.horizon if self.if_rnn_policy else T      # non-RNN: one window of n_step
         lib = L.lib()
         pc, ph, pw = self.obs_spec['pixel']['camera0'] if pix is not None else (0, 0, 0)
         F = int(self.learner_config.model.cnn_feature_dim) if pix is not None else 0
@@ -462,7 +462,8 @@ class PPOLearner(object):
         a.pixels = pix.data_ptr() if pix is not None else None
         a.pixels_next = pixn.data_ptr() if pixn is not None else None
         a.rewards, a.dones, a.behave = rewards.data_ptr(), dones.data_ptr(), pds.data_ptr()
-        a.h0, a.c0 = h0.data_ptr(), c0.data_ptr()
+        a.h0 = h0.data_ptr() if h0 is not None else None
+        a.c0 = c0.data_ptr() if c0 is not None else None
         a.lstm, a.actor, a.critic = (m.stem_flat.data_ptr(), m.actor.flat.data_ptr(),
                                      m.critic.flat.data_ptr())
         a.ref_lstm, a.ref_actor = rm.stem_flat.data_ptr(), rm.actor.flat.data_ptr()

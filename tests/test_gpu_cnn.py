@@ -143,9 +143,9 @@ def test_cnn_forward_backward_vs_torch(B, T, S, F):
     assert o == got.numel()
 
 
-def _pixel_cfg(mode, B, T, H, Hd, hidden, F, zf=True, epochs=(10, 10), lr=(3e-4, 3e-4)):
-    return ppo_config(B=B, T=T, mode=mode, use_z_filter=zf, hidden=hidden, lam=1.0,
-                      epochs=epochs, rnn=True, rnn_hidden=Hd, horizon=H, lr=lr, cnn_feat=F)
+def _pixel_cfg(mode, B, T, H, Hd, hidden, F, zf=True, epochs=(10, 10), lr=(3e-4, 3e-4), rnn=True):
+    return ppo_config(B=B, T=T, mode=mode, use_z_filter=zf, hidden=hidden, lam=1.0 if rnn else 0.95,
+                      epochs=epochs, rnn=rnn, rnn_hidden=Hd, horizon=H, lr=lr, cnn_feat=F)
 
 
 def test_ppo_model_pixel_forward_vs_oracle():
@@ -180,15 +180,16 @@ def test_ppo_model_pixel_forward_vs_oracle():
 
 
 def _run_pixel(mode, B, T, H, D, A, Hd, hidden, F, iters=2, zf=True, epochs=(10, 10),
-               lr=(3e-4, 3e-4)):
-    lc = _pixel_cfg(mode, B, T, H, Hd, hidden, F, zf and D > 0, epochs, lr)
+               lr=(3e-4, 3e-4), rnn=True):
+    lc = _pixel_cfg(mode, B, T, H, Hd, hidden, F, zf and D > 0, epochs, lr, rnn)
     ec = pixel_env_config(D, A, CAM)
     learner = PPOLearner(lc, ec, seed=9)
     ref = R.PPOLearnerRef(lc, D, A, pixel=CAM)
     copy_weights_to_oracle(learner, ref)
     report = {}
     for it in range(iters):
-        batch = synthetic.ppo_batch(B, T, D, A, seed=50 + it, rnn_hidden=Hd, pixel=CAM)
+        batch = synthetic.ppo_batch(B, T, D, A, seed=50 + it, rnn_hidden=Hd if rnn else None,
+                                    pixel=CAM)
         rstats = ref.learn(oracle_batch(batch))
         learner.learn(synthetic.to_device(batch, DEV))
         stats = learner.last_stats()
@@ -206,8 +207,9 @@ def _run_pixel(mode, B, T, H, D, A, Hd, hidden, F, iters=2, zf=True, epochs=(10,
                         lr[0], ups, report)
         _compare_params(f'critic{it}', learner.model.critic.flat.cpu(), ref.model.critic.flat(),
                         lr[1], epochs[1], report)
-        _compare_params(f'lstm{it}', learner.model.rnn_stem.flat.cpu(),
-                        lstm_flat(ref.model.rnn_stem), max(lr), ups + epochs[1], report)
+        if rnn:
+            _compare_params(f'lstm{it}', learner.model.rnn_stem.flat.cpu(),
+                            lstm_flat(ref.model.rnn_stem), max(lr), ups + epochs[1], report)
         # CNN stem: more entries whose gradient cancels to rounding noise (FC
         # weights of units alive in a handful of rows), which Adam's first steps
         # normalise to +-lr in either implementation; the raw gradients are held
@@ -247,20 +249,23 @@ def test_pixel_rnn_c5_widths_one_update():
     print('pixel rnn C5-widths parity:', rep)
 
 
-def test_pixel_rnn_gradients_match_autograd():
+@pytest.mark.parametrize('rnn', [True, False])
+def test_pixel_gradients_match_autograd(rnn):
     """Raw gradients of the last value update (before Adam) vs the oracle's
-    autograd at C5 widths: critic head, LSTM and CNN stem."""
-    B, T, H, D, A, Hd, F = 16, 25, 5, 42, 8, 100, 256
-    lc = _pixel_cfg('adapt', B, T, H, Hd, (300, 200), F, epochs=(1, 1))
+    autograd at C5 widths: critic head, LSTM (rnn) and CNN stem; rnn=False is
+    the non-RNN pixel model (heads over [zfilter(low_dim) | cnn])."""
+    B, T, D, A, F = 16, 25, 42, 8, 256
+    H, Hd = (5, 100) if rnn else (25, 0)
+    lc = _pixel_cfg('adapt', B, T, H, Hd, (300, 200), F, epochs=(1, 1), rnn=rnn)
     learner = PPOLearner(lc, pixel_env_config(D, A, CAM), seed=9)
     ref = R.PPOLearnerRef(lc, D, A, pixel=CAM)
     copy_weights_to_oracle(learner, ref)
-    batch = synthetic.ppo_batch(B, T, D, A, seed=1, rnn_hidden=Hd, pixel=CAM)
+    batch = synthetic.ppo_batch(B, T, D, A, seed=1, rnn_hidden=Hd if rnn else None, pixel=CAM)
     ref.learn(oracle_batch(batch))
     learner.learn(synthetic.to_device(batch, DEV))
     xbuf = learner._bufs['rnn_xbuf'].cpu().double()
     nAh = learner.model.actor.flat.numel()
-    nL = learner.model.rnn_stem.flat.numel()
+    nL = learner.model.rnn_stem.flat.numel() if rnn else 0
     nK = learner.model.cnn_stem.flat.numel()
     nCh = learner.model.critic.flat.numel()
     o = nAh + nL + nK
@@ -271,12 +276,26 @@ def test_pixel_rnn_gradients_match_autograd():
     def flat_grad(ps):
         return torch.cat([p.grad.detach().reshape(-1) for p in ps]).double()
     rc = flat_grad(ref.model.critic.model.parameters())
-    rl = flat_grad([ref.model.rnn_stem.weight_ih_l0, ref.model.rnn_stem.weight_hh_l0,
-                    ref.model.rnn_stem.bias_ih_l0, ref.model.rnn_stem.bias_hh_l0])
     rk = flat_grad(ref.model.cnn_stem.parameters())
-    for name, got, exp in (('critic', g_critic, rc), ('lstm', g_lstm, rl), ('cnn', g_cnn, rk)):
+    checks = [('critic', g_critic, rc), ('cnn', g_cnn, rk)]
+    if rnn:
+        rl = flat_grad([ref.model.rnn_stem.weight_ih_l0, ref.model.rnn_stem.weight_hh_l0,
+                        ref.model.rnn_stem.bias_ih_l0, ref.model.rnn_stem.bias_hh_l0])
+        checks.append(('lstm', g_lstm, rl))
+    for name, got, exp in checks:
         scale = float(exp.abs().max())
         err = (got - exp).abs()
         print(name, 'max abs err / scale', float(err.max()) / scale,
               'frac > 1e-5 scale', float((err > 1e-5 * scale).double().mean()))
         assert float(err.max()) <= 1e-4 * scale, name
+
+
+@pytest.mark.parametrize('mode', ['clip', 'adapt'])
+def test_pixel_mlp_learn_matches_oracle(mode):
+    # non-RNN pixel model (ppo_net.py:155-166: heads over [zfilter(low_dim) | cnn]),
+    # ppo.py's non-RNN branch: one GAE window of n_step, step 0 trains
+    # (with one training row per segment the CNN gradients sum few terms; the
+    # raw gradients are held to 1e-4 of scale by the autograd test below)
+    rep = _run_pixel(mode, B=24, T=6, H=6, D=7, A=3, Hd=0, hidden=(32, 24), F=32, iters=1,
+                     epochs=(1, 1), rnn=False)
+    print('pixel mlp parity:', rep)
