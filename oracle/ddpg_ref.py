@@ -4,7 +4,9 @@ fp32 CPU restatement of the DDPG learner step (low-dim observations, no
 layernorm — the reference default, ddpg_configs.py:21):
   ActorNetworkX / CriticNetworkX   surreal/model/model_builders/builders.py:35-84
   DDPGModel.forward                surreal/model/ddpg_net.py:86-93
-  DDPGLearner._optimize            surreal/learner/ddpg.py:244-352
+  DDPGLearner._optimize            surreal/learner/ddpg.py:244-352 (incl. the TD3 options:
+                                   twin critic ddpg.py:280-283,312-320; target policy
+                                   smoothing noise from numpy's global RNG :267-277)
   DDPGLearner._target_update       surreal/learner/ddpg.py:403-428
 torchx's nnx.Module.clip_grad_value / soft_update / hard_update are not
 available; they are stated here as torch.nn.utils.clip_grad_value_,
@@ -71,6 +73,11 @@ class DDPGLearnerRef:
         ah, ch = lc['model']['actor_fc_hidden_sizes'], lc['model']['critic_fc_hidden_sizes']
         self.actor, self.critic = ActorX(obs_dim, act_dim, ah), CriticX(obs_dim, act_dim, ch)
         self.actor_t, self.critic_t = ActorX(obs_dim, act_dim, ah), CriticX(obs_dim, act_dim, ch)
+        self.double = bool(net.get('use_double_critic', False))
+        self.action_reg = bool(net.get('use_action_regularization', False))
+        self.act_dim = act_dim
+        if self.double:
+            self.critic2, self.critic2_t = CriticX(obs_dim, act_dim, ch), CriticX(obs_dim, act_dim, ch)
         self.hard_update()
         self.clip_actor = net['clip_actor_gradient']
         self.actor_clip_value = net['actor_gradient_value_clip']
@@ -80,6 +87,9 @@ class DDPGLearnerRef:
                                              weight_decay=net['critic_regularization'])
         self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=net['lr_actor'],
                                             weight_decay=net['actor_regularization'])
+        if self.double:
+            self.critic_optim2 = torch.optim.Adam(self.critic2.parameters(), lr=net['lr_critic'],
+                                                  weight_decay=net['critic_regularization'])
         tu = net['target_update']
         self.target_update_type = tu['type']
         self.tau = tu.get('tau', 1e-3)
@@ -89,13 +99,23 @@ class DDPGLearnerRef:
     def hard_update(self):
         self.actor_t.load_state_dict(self.actor.state_dict())
         self.critic_t.load_state_dict(self.critic.state_dict())
+        if self.double:
+            self.critic2_t.load_state_dict(self.critic2.state_dict())
 
     def optimize(self, obs, actions, rewards, obs_next, done):          # ddpg.py:244-352
         assert actions.max().item() <= 1.0 and actions.min().item() >= -1.0
         with torch.no_grad():
             a_t = self.actor_t(obs_next)
             q_t = self.critic_t(obs_next, a_t)
+            if self.action_reg:
+                noise = np.clip(np.random.normal(0, 0.2, size=(self.batch_size, self.act_dim)),
+                                -0.5, 0.5)
+                a_t = (a_t + torch.tensor(noise, dtype=torch.float32)).clamp(-1, 1)
             y = rewards + pow(self.gamma, self.n_step) * q_t * (1.0 - done)
+            if self.double:
+                q_t2 = self.critic2_t(obs_next, a_t)
+                y2 = rewards + pow(self.gamma, self.n_step) * q_t2 * (1.0 - done)
+                y = torch.min(y, y2)
         q = self.critic(obs, actions)
         self.critic.zero_grad()
         critic_loss = nn.MSELoss()(q, y)
@@ -103,6 +123,15 @@ class DDPGLearnerRef:
         if self.clip_critic:
             nn.utils.clip_grad_value_(self.critic.parameters(), self.critic_clip_value)
         self.critic_optim.step()
+        q2 = None
+        if self.double:
+            q2 = self.critic2(obs, actions)
+            self.critic2.zero_grad()
+            critic_loss = nn.MSELoss()(q2, y)
+            critic_loss.backward()
+            if self.clip_critic:
+                nn.utils.clip_grad_value_(self.critic2.parameters(), self.critic_clip_value)
+            self.critic_optim2.step()
         self.actor.zero_grad()
         actor_loss = -self.critic(obs, self.actor(obs)).mean()
         actor_loss.backward()
@@ -112,14 +141,20 @@ class DDPGLearnerRef:
         stats = {'actor_loss': actor_loss.item(), 'critic_loss': critic_loss.item(),
                  'action_norm': actions.norm(2, 1).mean().item(), 'rewards': rewards.mean().item(),
                  'Q_target': y.mean().item(), 'Q_policy': q.mean().item()}
+        if q2 is not None:
+            stats['Q_policy2'] = q2.mean().item()
         self.target_update()
         return stats
 
     def target_update(self):                                            # ddpg.py:403-428
         if self.target_update_type == 'soft':
             with torch.no_grad():
-                for t, s in zip(list(self.actor_t.parameters()) + list(self.critic_t.parameters()),
-                                list(self.actor.parameters()) + list(self.critic.parameters())):
+                tp = list(self.actor_t.parameters()) + list(self.critic_t.parameters())
+                sp = list(self.actor.parameters()) + list(self.critic.parameters())
+                if self.double:
+                    tp += list(self.critic2_t.parameters())
+                    sp += list(self.critic2.parameters())
+                for t, s in zip(tp, sp):
                     t.copy_(self.tau * s + (1 - self.tau) * t)
         else:
             self.counter += 1

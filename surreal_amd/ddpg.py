@@ -188,9 +188,6 @@ class DDPGLearner(object):
         net = lc.algo.network
         self.use_double_critic = net.use_double_critic
         self.use_action_regularization = net.use_action_regularization
-        if self.use_double_critic or self.use_action_regularization:
-            raise NotImplementedError('surreal_amd: TD3 options (double critic / target noise) '
-                                      'are not built yet')
         tu = net.target_update
         self.target_update_type = tu.type
         if tu.type == 'soft':
@@ -211,16 +208,27 @@ class DDPGLearner(object):
                                device=self.device, generator=gen)
         self.model = mk()
         self.model_target = mk()
+        if self.use_double_critic:                      # ddpg.py:119-145 (critic_only twins)
+            mk2 = lambda: DDPGModel(ec.obs_spec, self.action_dim, self.use_layernorm,  # noqa: E731
+                                    lc.model.actor_fc_hidden_sizes,
+                                    lc.model.critic_fc_hidden_sizes, critic_only=True,
+                                    device=self.device, generator=gen)
+            self.model2 = mk2()
+            self.model_target2 = mk2()
         self._hard_update()
         dev = self.device
         self.opt = {}
-        for name, flat, lr, wd in (('critic', self.model.critic.flat, net.lr_critic, net.critic_regularization),
-                                   ('actor', self.model.actor.flat, net.lr_actor, net.actor_regularization)):
+        groups = [('critic', self.model.critic.flat, net.lr_critic, net.critic_regularization),
+                  ('actor', self.model.actor.flat, net.lr_actor, net.actor_regularization)]
+        if self.use_double_critic:                      # critic_optim2 (ddpg.py:163-168)
+            groups.append(('critic2', self.model2.critic.flat, net.lr_critic,
+                           net.critic_regularization))
+        for name, flat, lr, wd in groups:
             self.opt[name] = {'m': torch.zeros_like(flat), 'v': torch.zeros_like(flat),
                               'step': torch.zeros(1, dtype=torch.int32, device=dev),
                               'lr': torch.tensor([lr], dtype=torch.float32, device=dev),
                               'wd': float(wd), 'g': torch.zeros_like(flat)}
-        self.stats_buf = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.stats_buf = torch.zeros(12, dtype=torch.float32, device=dev)
         self._bufs = {}
         self.kernel_events = None
 
@@ -229,6 +237,8 @@ class DDPGLearner(object):
         with torch.no_grad():
             self.model_target.actor.flat.copy_(self.model.actor.flat)
             self.model_target.critic.flat.copy_(self.model.critic.flat)
+            if self.use_double_critic:
+                self.model_target2.critic.flat.copy_(self.model2.critic.flat)
 
     def _adam(self, name, flat, clip_value, st):
         o = self.opt[name]
@@ -261,11 +271,23 @@ class DDPGLearner(object):
         # target: y = r + gamma^n * Q'(s', mu'(s')) * (1 - d)           (ddpg.py:266-284)
         a_t = tnet.actor_fwd(obs_next, B, store='ta')
         q_t = tnet.critic_fwd(self.model_target.critic, obs_next, a_t, B, store='tc')
+        q_t2 = None
+        if self.use_double_critic:
+            # TD3 (ddpg.py:267-283): target policy smoothing noise is drawn on the
+            # host from numpy's global RNG exactly as the reference does, and only
+            # the twin target sees it (next_Q_target was computed before the noise)
+            a_t2 = a_t
+            if self.use_action_regularization:
+                noise = np.clip(np.random.normal(0, 0.2, size=(self.batch_size, self.action_dim)),
+                                -0.5, 0.5)
+                a_t2 = (a_t + torch.tensor(noise, dtype=torch.float32).to(self.device)).clamp(-1, 1)
+            q_t2 = tnet.critic_fwd(self.model_target2.critic, obs_next, a_t2.contiguous(), B,
+                                   store='t2c')
         y = net.buf('y', (B, 1))
         r1 = rewards if rewards.is_contiguous() else rewards.contiguous()
         d1 = done if done.is_contiguous() else done.contiguous()
-        L.call('smi_ddpg_target', _p(r1), _p(d1), _p(q_t), None, B,
-               float(pow(self.discount_factor, self.n_step)), _p(y), st)
+        L.call('smi_ddpg_target', _p(r1), _p(d1), _p(q_t), _p(q_t2) if q_t2 is not None else None,
+               B, float(pow(self.discount_factor, self.n_step)), _p(y), st)
         # critic update (ddpg.py:287-310)
         crit = self.model.critic
         q = net.critic_fwd(crit, obs, actions, B, store='c')
@@ -275,6 +297,19 @@ class DDPGLearner(object):
         self._critic_backward(net, crit, obs, B, dq, 'c', g, st, need_obs_grad=True)
         self._adam('critic', crit.flat,
                    self.critic_gradient_clip_value if self.clip_critic_gradient else 0.0, st)
+        if self.use_double_critic:                      # second critic (ddpg.py:312-320)
+            crit2 = self.model2.critic
+            q_2 = net.critic_fwd(crit2, obs, actions, B, store='q2c')
+            dq_2 = net.buf('dq_2', (B, 1))
+            # the reference reports this critic's loss as 'critic_loss'
+            L.call('smi_mse_grad', _p(q_2), 1, _p(y), B, _p(dq_2), _p(self.stats_buf[1:2]), st)
+            self._critic_backward(net, crit2, obs, B, dq_2, 'q2c', self.opt['critic2']['g'], st,
+                                  need_obs_grad=True)
+            self._adam('critic2', crit2.flat,
+                       self.critic_gradient_clip_value if self.clip_critic_gradient else 0.0, st)
+            L.call('smi_ddpg_stats', _p(actions), actions.stride(0), self.action_dim, _p(rewards),
+                   rewards.stride(0) if rewards.dim() == 2 else 1, _p(y), _p(q_2), 1, B,
+                   _p(self.stats_buf[8:12]), st)         # [.., .., .., Q_policy2]
         # actor update with the updated critic (ddpg.py:323-333)
         act = self.model.actor
         a = net.actor_fwd(obs, B, store='a')
@@ -347,8 +382,11 @@ class DDPGLearner(object):
     def _target_update(self):                                            # ddpg.py:403-428
         st = L.stream(self.device)
         if self.target_update_type == 'soft':
-            for t, s in ((self.model_target.actor.flat, self.model.actor.flat),
-                         (self.model_target.critic.flat, self.model.critic.flat)):
+            pairs = [(self.model_target.actor.flat, self.model.actor.flat),
+                     (self.model_target.critic.flat, self.model.critic.flat)]
+            if self.use_double_critic:
+                pairs.append((self.model_target2.critic.flat, self.model2.critic.flat))
+            for t, s in pairs:
                 L.call('smi_soft_update', _p(t), _p(s), t.numel(), float(self.target_update_tau), st)
         else:
             self.target_update_counter += 1
@@ -370,14 +408,20 @@ class DDPGLearner(object):
 
     def last_stats(self):
         v = self.stats_buf.cpu().numpy()
-        return {'actor_loss': float(v[0]), 'critic_loss': float(v[1]), 'action_norm': float(v[2]),
-                'rewards': float(v[3]), 'Q_target': float(v[4]), 'Q_policy': float(v[5])}
+        out = {'actor_loss': float(v[0]), 'critic_loss': float(v[1]), 'action_norm': float(v[2]),
+               'rewards': float(v[3]), 'Q_target': float(v[4]), 'Q_policy': float(v[5])}
+        if self.use_double_critic:
+            out['Q_policy2'] = float(v[11])
+        return out
 
     def module_dict(self):
         return {'ddpg': self.model}
 
     def checkpoint_attributes(self):
-        return ['current_iteration', 'model', 'model_target']
+        attrs = ['current_iteration', 'model', 'model_target']
+        if self.use_double_critic:
+            attrs += ['model2', 'model_target2']
+        return attrs
 
     def _prefetcher_preprocess(self, batch):
         from .aggregator import FrameStackPreprocessor, SSARAggregator

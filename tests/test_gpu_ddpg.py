@@ -114,6 +114,44 @@ def test_ddpg_learn_matches_oracle(target, clip_critic):
     print('ddpg parity report:', report)
 
 
+@pytest.mark.parametrize('target,action_reg', [('hard', False), ('soft', True)])
+def test_ddpg_td3_matches_oracle(target, action_reg):
+    """TD3 options (ddpg.py:267-283,312-320): twin critic with min target, and
+    target-policy smoothing noise drawn from numpy's global RNG on the host (the
+    reference's own generator: both sides are seeded identically per step)."""
+    B, D, A = 512, 17, 6
+    lc = _cfg(B, target, False)
+    lc.algo.network.use_double_critic = True
+    lc.algo.network.use_action_regularization = action_reg
+    learner = DDPGLearner(lc, gym_env_config(D, A), seed=2)
+    ref = R.DDPGLearnerRef(lc, D, A)
+    _sync_weights(learner, ref)
+    R.load_flat(ref.critic2.params(), learner.model2.critic.flat.cpu())
+    ref.hard_update()
+    report = {}
+    for it in range(3):
+        b = synthetic.ddpg_batch(B, D, A, seed=it)
+        np.random.seed(100 + it)
+        rs = ref.optimize(b['obs'], b['actions'], b['rewards'], b['obs_next'], b['dones'])
+        np.random.seed(100 + it)
+        learner.learn({k: v.cuda() for k, v in b.items()})
+        s = learner.last_stats()
+        for k in rs:
+            assert abs(s[k] - rs[k]) <= 1e-4 * abs(rs[k]) + 1e-5, (it, k, s[k], rs[k])
+        _compare_params(f'critic{it}', learner.model.critic.flat.cpu(), R.flat_of(ref.critic.params()),
+                        1e-3, it + 1, report)
+        _compare_params(f'critic2_{it}', learner.model2.critic.flat.cpu(),
+                        R.flat_of(ref.critic2.params()), 1e-3, it + 1, report)
+        # min(y1, y2) picks per row; rows with y1 ~ y2 within fp32 noise may pick
+        # differently in any two implementations (like a ReLU mask flip), on
+        # top of the DDPG actor's sign-flip budget: 1 %
+        _compare_params(f'actor{it}', learner.model.actor.flat.cpu(), R.flat_of(ref.actor.params()),
+                        1e-4, it + 1, report, max_frac=1e-2)
+        _compare_params(f'tcritic2_{it}', learner.model_target2.critic.flat.cpu(),
+                        R.flat_of(ref.critic2_t.params()), 1e-3, it + 1, report)
+    print('ddpg td3 parity report:', report)
+
+
 def test_replay_sample_feeds_learner_with_cpython_indices():
     from surreal_amd.replay import UniformReplay
     D, A, B = 17, 6, 512
