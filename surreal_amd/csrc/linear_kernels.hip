@@ -59,6 +59,28 @@ struct GemmArgs {
 // all-ones column (dW bias gradient) is synthesised, never loaded.
 struct TileRegs { float v[8]; };
 
+// XCD-aware tile order (cdna_hip_programming.md T1): the dispatcher deals
+// consecutive workgroups round-robin over the 8 XCDs (private L2 each); the
+// bijective remap gives every XCD a contiguous run of the logical order, in
+// which n-tiles of one m-tile (sharing A rows) and the tiles of one split-K
+// slab (sharing the slab's rows of both operands) are neighbours.
+struct TileIdx { int mt, nt, z; };
+__device__ __forceinline__ TileIdx gemm_tile_index() {
+  const int gm = gridDim.x, gn = gridDim.y;
+  const int nwg = gm * gn * gridDim.z;
+  const int orig = blockIdx.x + gm * (blockIdx.y + gn * blockIdx.z);
+  int w = orig;
+  if (nwg > 8) {
+    const int x = orig & 7, q = nwg >> 3, r = nwg & 7;
+    w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
+  }
+  TileIdx t;
+  t.nt = w % gn;
+  t.mt = (w / gn) % gm;
+  t.z = w / (gn * gm);
+  return t;
+}
+
 template <bool KCONTIG>
 __device__ __forceinline__ void gemm_load(const float* __restrict__ P, int64_t rs, int64_t cs,
                                           int r0, int rdata, int k0, int kmax, int ones_col,
@@ -158,8 +180,9 @@ gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float sB[2][G_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const int m0 = blockIdx.x * GBM, n0 = blockIdx.y * GBN;
-  const int kb = blockIdx.z * g.kchunk;
+  const TileIdx ti = gemm_tile_index();
+  const int m0 = ti.mt * GBM, n0 = ti.nt * GBN;
+  const int kb = ti.z * g.kchunk;
   const int ke = min(g.K, kb + g.kchunk);
   const int nk = (ke - kb + GBK - 1) / GBK;
   // B(k, n): viewed as rows n (B "row" stride b_cs), k stride b_rs
@@ -246,7 +269,7 @@ gemm_kernel(GemmArgs g) {
       float v = tot[c][i];
       if constexpr (EPI == EPI_FWD) {
         if (g.part) {                           // split-K slab: raw sums
-          g.part[((int64_t)blockIdx.z * g.M + m) * g.N + n] = v;
+          g.part[((int64_t)ti.z * g.M + m) * g.N + n] = v;
           continue;
         }
         v += bias_n;
@@ -258,7 +281,7 @@ gemm_kernel(GemmArgs g) {
         g.C[(int64_t)m * g.ldc + n] = v;
       } else {
         if (g.part) {
-          g.part[((int64_t)blockIdx.z * g.M + m) * g.N + n] = v;
+          g.part[((int64_t)ti.z * g.M + m) * g.N + n] = v;
         } else if (n == g.ones_col) {
           g.bias_out[m] = g.accumulate ? g.bias_out[m] + v : v;
         } else {
@@ -497,8 +520,9 @@ gemm_dw128_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float sB[2][32 * D2_LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const int m0 = blockIdx.x * D2_T, n0 = blockIdx.y * D2_T;
-  const int kb = blockIdx.z * g.kchunk;
+  const TileIdx ti = gemm_tile_index();
+  const int m0 = ti.mt * D2_T, n0 = ti.nt * D2_T;
+  const int kb = ti.z * g.kchunk;
   const int ke = min(g.K, kb + g.kchunk);
   const int nk = (ke - kb + 31) / 32;
   const int bdata = g.ones_col >= 0 ? g.ones_col + 1 : g.N;   // the ones column is synthesised
@@ -556,7 +580,7 @@ gemm_dw128_kernel(GemmArgs g) {
         if (m >= g.M) continue;
         const float v = acc[a][b][i];
         if (g.part) {
-          g.part[((int64_t)blockIdx.z * g.M + m) * g.N + n] = v;
+          g.part[((int64_t)ti.z * g.M + m) * g.N + n] = v;
         } else if (n == g.ones_col) {
           g.bias_out[m] = g.accumulate ? g.bias_out[m] + v : v;
         } else {
