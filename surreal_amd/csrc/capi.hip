@@ -47,12 +47,17 @@ void ktime_end(int slot, int cls, double flops, hipStream_t st) {
 }
 
 // caller-registered device workspace (smi_set_workspace)
+// Two halves: slot 0 for launches on the caller's stream, slot 1 for the
+// side stream the RNN phases overlap weight-gradient GEMMs on (ppo_rnn.hip).
 static void* g_ws = nullptr;
 static int64_t g_ws_bytes = 0;
-int64_t smi_workspace_floats() { return g_ws ? g_ws_bytes / 4 : 0; }
+static int g_ws_slot = 0;
+int workspace_slot(int slot) { const int old = g_ws_slot; g_ws_slot = slot; return old; }
+int64_t smi_workspace_floats() { return g_ws ? g_ws_bytes / 8 : 0; }
 float* workspace_f32(int64_t nfloats) {
-  if (!g_ws || nfloats * 4 > g_ws_bytes) return nullptr;
-  return static_cast<float*>(g_ws);
+  const int64_t half = g_ws_bytes / 8;
+  if (!g_ws || nfloats > half) return nullptr;
+  return static_cast<float*>(g_ws) + (g_ws_slot ? half : 0);
 }
 
 // declared in the other translation units
@@ -107,7 +112,7 @@ int smi_set_workspace(void* dev_ptr, int64_t bytes) {
   g_ws_bytes = bytes;
   return SMI_OK;
 }
-int64_t smi_workspace_bytes(void) { return (int64_t)64 << 20; }
+int64_t smi_workspace_bytes(void) { return (int64_t)128 << 20; }
 
 /* Per-launch HIP-event timing of the MFMA kernels (GEMM forward / input-grad /
  * weight-grad / split-K reduce, LSTM forward / backward): on != 0 starts a

@@ -591,6 +591,165 @@ gemm_dw128_kernel(GemmArgs g) {
   }
 }
 
+// Weight gradient with operands straight from global memory into MFMA
+// registers (no LDS staging, no barriers in the main loop).  dW[m][n] =
+// sum_r dY[r][m] * X[r][n] reduces over the rows, which is the MFMA k index;
+// a 16x16x4 MFMA's A operand for lane (li, lk) is (row lk, column li) and its
+// B operand (row lk, column li), so one wave loads a 4-row step of BOTH
+// operands as row-contiguous vectors: lane li takes MT consecutive dY columns
+// m0 + MT*li + t (one per MFMA m-tile t) and 4 consecutive X columns per
+// 64-column half, i.e. 16-byte loads that feed MT x NT MFMAs.  The output
+// columns are thereby interleaved across tiles; the epilogue undoes that.  The
+// four waves of a workgroup take interleaved 4-row steps of one row slab (P
+// steps prefetched in registers) and are combined through LDS in a fixed
+// order; slabs go to the split-K partials.  Row-major dY/X of the heads, the
+// LSTM input/recurrent weights and the DDPG nets all take this path.
+constexpr int DWD_P = 4;   // steps in flight per wave
+
+// Rows past the slab and the synthesised bias column are selected by ADDRESS
+// (a zero row / a {1, 0, 0, 0} vector in device memory), never by masking the
+// loaded value: the loads then feed the MFMAs untouched and the compiler keeps
+// all P steps in flight.  Columns past M / N read clamped addresses; they only
+// reach outputs the epilogue drops.
+constexpr int DWD_ZMAX = 8192;
+__device__ __attribute__((aligned(16))) float g_dwd_zero[DWD_ZMAX];
+__device__ __attribute__((aligned(16))) float g_dwd_one[4] = {1.f, 0.f, 0.f, 0.f};
+
+template <int MT, int NT, bool VA, bool VB>
+__device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m0, int n0, int bdata,
+                                         float (&av)[MT], float (&bv)[NT]) {
+  const int li = threadIdx.x & 15;
+  const bool ok = r < ke;
+  const float* Ar = ok ? g.A + (int64_t)r * g.a_cs : g_dwd_zero;
+  const float* Br = ok ? g.B + (int64_t)r * g.b_rs : g_dwd_zero;
+  const float* one = ok ? g_dwd_one : g_dwd_zero;
+  if constexpr (MT == 4 && VA) {
+    const int c = min(m0 + 4 * li, g.M - 4);
+    const float4 x = *reinterpret_cast<const float4*>(Ar + c);
+    av[0] = x.x; av[1] = x.y; av[2] = x.z; av[3] = x.w;
+  } else {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) av[t] = Ar[min(m0 + MT * li + t, g.M - 1)];
+  }
+#pragma unroll
+  for (int h = 0; h < NT / 4; ++h) {
+    const int cb = n0 + 64 * h + 4 * li;
+    if constexpr (VB) {
+      const float* src = cb < bdata ? Br + cb : (cb == g.ones_col ? one : g_dwd_zero);
+      const float4 x = *reinterpret_cast<const float4*>(src);
+      bv[4 * h] = x.x; bv[4 * h + 1] = x.y; bv[4 * h + 2] = x.z; bv[4 * h + 3] = x.w;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = cb + t;
+        bv[4 * h + t] = *(c < bdata ? Br + c : (c == g.ones_col ? one : g_dwd_zero));
+      }
+    }
+  }
+}
+
+template <int MT, int NT, bool VA, bool VB>
+__global__ void __launch_bounds__(kWG)
+gemm_dwd_kernel(GemmArgs g) {
+  if (g.skip && g.skip[0] != 0) return;
+  extern __shared__ float4 dwd_red[];            // 2 x [MT*NT][64] float4
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const TileIdx ti = gemm_tile_index();
+  const int m0 = ti.mt * 16 * MT, n0 = ti.nt * 16 * NT;
+  const int kb = ti.z * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  const int nsteps = (ke - kb + 15) >> 4;
+  const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
+  const int rw = kb + 4 * wave + lk;              // this lane's row in step 0
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // loads are unconditional (rows past the slab read clamped and zeroed) so
+  // the compiler's vmcnt waits stay partial across the unrolled P steps;
+  // slabs are multiples of 16*P rows, only the last one runs zero steps
+  float av[DWD_P][MT], bv[DWD_P][NT];
+#pragma unroll
+  for (int p = 0; p < DWD_P; ++p)
+    dwd_load<MT, NT, VA, VB>(g, rw + 16 * p, ke, m0, n0, bdata, av[p], bv[p]);
+  for (int s0 = 0; s0 < nsteps; s0 += DWD_P) {
+#pragma unroll
+    for (int p = 0; p < DWD_P; ++p) {
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+#pragma unroll
+        for (int a = 0; a < MT; ++a) acc[a][b] = mfma4(av[p][a], bv[p][b], acc[a][b]);
+      dwd_load<MT, NT, VA, VB>(g, rw + 16 * (s0 + p + DWD_P), ke, m0, n0, bdata, av[p], bv[p]);
+    }
+  }
+  // combine the four waves: (w0 + w2) + (w1 + w3)
+  float4* buf0 = dwd_red;
+  float4* buf1 = dwd_red + MT * NT * 64;
+  auto put = [&](float4* buf) {
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        const f32x4 v = acc[a][b];
+        buf[(a * NT + b) * 64 + lane] = float4{v[0], v[1], v[2], v[3]};
+      }
+  };
+  auto add = [&](const float4* buf) {
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        const float4 v = buf[(a * NT + b) * 64 + lane];
+        acc[a][b] += f32x4{v.x, v.y, v.z, v.w};
+      }
+  };
+  if (wave >= 2) put(wave == 2 ? buf0 : buf1);
+  __syncthreads();
+  if (wave < 2) add(wave == 0 ? buf0 : buf1);
+  __syncthreads();
+  if (wave == 1) put(buf0);
+  __syncthreads();
+  if (wave != 0) return;
+  add(buf0);
+  // D(row lk*4+i, col li) of tile (a, b) is dW[m][n] with
+  // m = m0 + MT*(lk*4+i) + a, n = n0 + 64*(b/4) + 4*li + b%4
+  const bool vec_part = g.part && (g.N & 3) == 0;
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + MT * (lk * 4 + i) + a;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int h = 0; h < NT / 4; ++h) {
+        const int nb = n0 + 64 * h + 4 * li;
+        if (vec_part) {
+          if (nb < g.N)
+            *reinterpret_cast<float4*>(g.part + ((int64_t)ti.z * g.M + m) * g.N + nb) =
+                float4{acc[a][4 * h][i], acc[a][4 * h + 1][i], acc[a][4 * h + 2][i],
+                       acc[a][4 * h + 3][i]};
+          continue;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int n = nb + t;
+          if (n >= g.N) continue;
+          const float v = acc[a][4 * h + t][i];
+          if (g.part) {
+            g.part[((int64_t)ti.z * g.M + m) * g.N + n] = v;
+          } else if (n == g.ones_col) {
+            g.bias_out[m] = g.accumulate ? g.bias_out[m] + v : v;
+          } else {
+            float* dst = g.C + (int64_t)m * g.ldc + n;
+            *dst = g.accumulate ? *dst + v : v;
+          }
+        }
+      }
+    }
+}
+
 float* workspace_f32(int64_t nfloats);
 
 // split-K target workgroup count (SMI_SPLITK_TARGET overrides; tuning knob)
@@ -612,8 +771,76 @@ static void gemm_dispatch(const GemmArgs& g, dim3 grid, bool ak, bool bk, hipStr
   else hipLaunchKernelGGL((gemm_kernel<EPI, false, false>), grid, dim3(kWG), 0, st, g);
 }
 
+static int use_dwd() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("SMI_DWD");
+    u = (e && e[0] == '0') ? 0 : 1;
+  }
+  return u;
+}
+
+template <int MT, int NT>
+static void dwd_dispatch(const GemmArgs& g, dim3 grid, bool va, bool vb, hipStream_t st) {
+  const size_t lds = (size_t)2 * MT * NT * 64 * sizeof(float4);
+  if (va && vb) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, true, true>), grid, dim3(kWG), lds, st, g);
+  else if (va) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, true, false>), grid, dim3(kWG), lds, st, g);
+  else if (vb) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, false, true>), grid, dim3(kWG), lds, st, g);
+  else hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, false, false>), grid, dim3(kWG), lds, st, g);
+}
+
+static int splitk_reduce(const GemmArgs& g, int S, int epi, hipStream_t st);
+
+// weight gradient over row-major dY / X (a_rs == 1, b_cs == 1): gemm_dwd_kernel
+static int dwd_launch(GemmArgs g, hipStream_t st) {
+  auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
+  const int MT = g.M > 32 ? 4 : 1, NT = g.N > 64 ? 8 : 4;
+  const bool va = MT == 4 && al16(g.A) && g.M % 4 == 0 && g.a_cs % 4 == 0;
+  const bool vb = al16(g.B) && bdata >= 4 && bdata % 4 == 0 && g.b_rs % 4 == 0;
+  const int gm = (g.M + 16 * MT - 1) / (16 * MT), gn = (g.N + 16 * NT - 1) / (16 * NT);
+  const int tiles = gm * gn;
+  static int target = 0;
+  if (!target) {    // measured: ~1 workgroup per CU beats deeper splits (partials)
+    const char* e = getenv("SMI_DWD_TARGET");
+    target = e ? atoi(e) : 256;
+    if (target < 16) target = 16;
+  }
+  int S = (target + tiles - 1) / tiles;
+  const int smax = (g.K + 127) / 128;               // >= 8 four-row steps per wave
+  if (S > smax) S = smax;
+  const int64_t cap = smi_workspace_floats() / ((int64_t)g.M * g.N);
+  if (S > cap) S = (int)cap;
+  if (S < 1) S = 1;
+  g.part = nullptr;
+  g.kchunk = g.K;
+  if (S > 1) {
+    g.kchunk = ((g.K + S - 1) / S + 16 * DWD_P - 1) / (16 * DWD_P) * (16 * DWD_P);
+    S = (g.K + g.kchunk - 1) / g.kchunk;
+  }
+  if (S > 1) {
+    g.part = workspace_f32((int64_t)S * g.M * g.N);
+    if (!g.part) return set_error(SMI_E_ARG, "gemm: workspace unavailable for split-K");
+  }
+  const dim3 grid(gm, gn, S);
+  const int kslot = ktime_begin(st);
+  if (MT == 4 && NT == 8) dwd_dispatch<4, 8>(g, grid, va, vb, st);
+  else if (MT == 4) dwd_dispatch<4, 4>(g, grid, va, vb, st);
+  else if (NT == 8) dwd_dispatch<1, 8>(g, grid, false, vb, st);
+  else dwd_dispatch<1, 4>(g, grid, false, vb, st);
+  const int nreal = g.ones_col >= 0 ? g.N - 1 : g.N;
+  ktime_end(kslot, KT_GEMM_DW,
+            2.0 * g.M * (double)nreal * g.K + (g.ones_col >= 0 ? (double)g.M * g.K : 0.0), st);
+  const int rc = check_launch("gemm_dwd_kernel");
+  if (rc || S == 1) return rc;
+  return splitk_reduce(g, S, EPI_DW, st);
+}
+
 static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return SMI_OK;
+  if (epi == EPI_DW && use_dwd() && g.a_rs == 1 && g.b_cs == 1 && g.K >= 1 &&
+      (g.ones_col >= 0 ? g.ones_col : g.N) >= 1 && g.M <= 512 && g.N <= 512)
+    return dwd_launch(g, st);
   const bool ak = g.a_cs == 1;         // A contiguous along k
   const bool bk = g.b_rs == 1;         // B contiguous along k (rows n)
   auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -668,6 +895,10 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
             2.0 * g.M * (double)nreal * g.K + (g.ones_col >= 0 ? (double)g.M * g.K : 0.0), st);
   int rc = check_launch("gemm_kernel");
   if (rc || S == 1) return rc;
+  return splitk_reduce(g, S, epi, st);
+}
+
+static int splitk_reduce(const GemmArgs& g, int S, int epi, hipStream_t st) {
   const int rslot = ktime_begin(st);
   const int64_t MN = (int64_t)g.M * g.N;
   const int rg = (int)((MN + 63) / 64);

@@ -17,6 +17,7 @@
 // registers: dgates_t are formed element-wise, written to HBM (for the weight
 // GEMMs) and to LDS, and dh_rec_{t-1} = dgates_t W_hh is the next MFMA pass
 // (K = 4H, B operand contiguous along units).
+#include <stdlib.h>
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
 
@@ -531,6 +532,244 @@ lstm_bwd_reg_kernel(LstmBwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 4-segment variants (H <= 128, the reference default H = 100 included): a
+// workgroup owns LR4 = 4 segments, so the 1024-segment C3 batch spreads over
+// 256 workgroups — one per CU — instead of 64.  A step's recurrent GEMM is
+// then 4 rows x 4H columns x H, which is exactly the shape of
+// v_mfma_f32_4x4x1_16b_f32 with block 0's A operand (the 4 rows of h_{t-1},
+// lanes 0-3) broadcast to all 16 blocks (cbsz 4): a 4 x 64 outer-product
+// step whose output column is the lane.  Wave w owns gate columns
+// 64w .. 64w+63 with its W_hh column in registers; 8 accumulators over
+// k mod 8 hide the 44-cycle dependent latency (measured: 12 cycles/MFMA at 4
+// chains, tools/exp/mfma4x4.hip).  The cell update runs one (row, unit) per
+// thread after the pre-activations pass through LDS.
+//
+// Backward: dh_rec = dgates_t (4 x 4H) W_hh (4H x H) with units on lanes
+// (ceil(H/64) groups of 64) and K = 4H split over the waves of a group; the
+// partial sums meet in LDS and are added in a fixed order by the cell threads.
+constexpr int LR4 = 4;
+
+__device__ __forceinline__ f32x4 mfma4x64(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 4, 0, 0);
+}
+
+// KP: H rounded up to a multiple of 8 (W_hh registers per lane)
+template <int KP>
+__global__ void __launch_bounds__(kWG8)
+lstm_fwd_r4_kernel(LstmFwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  __shared__ __attribute__((aligned(16))) float hS[2][LR4 * KP];
+  __shared__ float pre[LR4][4 * KP];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * LR4;
+  const int64_t BH = (int64_t)B * H;
+  const int col = wave * 64 + lane;
+  const bool cact = wave * 64 < G4;              // wave-uniform
+  const int colc = col < G4 ? col : G4 - 1;
+  float w[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const float x = a.w_hh[(int64_t)colc * H + (k < H ? k : H - 1)];
+    w[k] = k < H ? x : 0.f;
+  }
+  const float bh = a.b_hh[colc];
+  // cell owned by this thread: (crow, cunit)
+  const bool cell = tid < LR4 * H;
+  const int crow = cell ? tid / H : 0;
+  const int cunit = cell ? tid - crow * H : 0;
+  const int cgr = r0 + crow;
+  const bool cok = cell && cgr < B;
+  float creg = cok ? a.c0[(int64_t)cgr * H + cunit] : 0.f;
+  if (cok && a.cbuf) a.cbuf[(int64_t)cgr * H + cunit] = creg;
+  for (int e = tid; e < LR4 * KP; e += kWG8) {
+    const int r = e / KP, k = e - r * KP;
+    const bool ok = k < H && r0 + r < B;
+    const float v = ok ? a.h0[(int64_t)(r0 + r) * H + k] : 0.f;
+    hS[0][e] = v;
+    hS[1][e] = 0.f;
+    if (ok) a.hbuf[(int64_t)(r0 + r) * H + k] = v;        // hbuf[0] = h0
+  }
+  int64_t xoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gr = r0 + i < B ? r0 + i : B - 1;
+    xoff[i] = (int64_t)gr * G4 + colc;
+  }
+  float xp[4];
+  if (a.S > 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xp[i] = a.xproj[xoff[i]];
+  }
+  __syncthreads();
+  LSTM_T0();
+  for (int t = 0; t < a.S; ++t) {
+    const float* hp = hS[t & 1];
+    float* hn = hS[(t + 1) & 1];
+    if (cact) {
+      f32x4 acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float4* hr = reinterpret_cast<const float4*>(hp + (lane & 3) * KP);
+#pragma unroll
+      for (int k8 = 0; k8 < KP / 8; ++k8) {
+        const float4 u = hr[2 * k8], v = hr[2 * k8 + 1];
+        acc[0] = mfma4x64(u.x, w[8 * k8 + 0], acc[0]);
+        acc[1] = mfma4x64(u.y, w[8 * k8 + 1], acc[1]);
+        acc[2] = mfma4x64(u.z, w[8 * k8 + 2], acc[2]);
+        acc[3] = mfma4x64(u.w, w[8 * k8 + 3], acc[3]);
+        acc[4] = mfma4x64(v.x, w[8 * k8 + 4], acc[4]);
+        acc[5] = mfma4x64(v.y, w[8 * k8 + 5], acc[5]);
+        acc[6] = mfma4x64(v.z, w[8 * k8 + 6], acc[6]);
+        acc[7] = mfma4x64(v.w, w[8 * k8 + 7], acc[7]);
+      }
+      const f32x4 sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
+                        ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+      if (col < G4) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pre[i][col] = xp[i] + (sum[i] + bh);
+      }
+      if (t + 1 < a.S) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xp[i] = a.xproj[(int64_t)(t + 1) * B * G4 + xoff[i]];
+      }
+    }
+    LSTM_TICK(0);
+    __syncthreads();
+    if (cell) {
+      const float ig = sigm(pre[crow][cunit]), fg = sigm(pre[crow][H + cunit]);
+      const float cg = ftanh(pre[crow][2 * H + cunit]), og = sigm(pre[crow][3 * H + cunit]);
+      const float c = fg * creg + ig * cg;
+      const float h = og * ftanh(c);
+      creg = cok ? c : 0.f;
+      hn[crow * KP + cunit] = cok ? h : 0.f;
+      if (cok) {
+        a.hbuf[(int64_t)(t + 1) * BH + (int64_t)cgr * H + cunit] = h;
+        if (a.cbuf) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)cgr * H + cunit] = c;
+        if (a.gates) {
+          float* gp = a.gates + ((int64_t)t * B + cgr) * G4 + cunit;
+          gp[0] = ig; gp[H] = fg; gp[2 * H] = cg; gp[3 * H] = og;
+        }
+      }
+    }
+    LSTM_TICK(1);
+    __syncthreads();
+    LSTM_TICK(2);
+  }
+}
+
+// KW: k range per wave (4H / waves-per-unit-group) rounded up to 8
+template <int KW>
+__global__ void __launch_bounds__(kWG8)
+lstm_bwd_r4_kernel(LstmBwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  constexpr int G4P = 4 * 128 + KW;               // dG row stride (reads run up to KW past 4H)
+  __shared__ __attribute__((aligned(16))) float dG[LR4 * G4P];
+  __shared__ float red[8][LR4][64];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * LR4;
+  const int64_t BH = (int64_t)B * H;
+  const int NU = (H + 63) >> 6;                   // unit groups of 64 lanes
+  const int WPG = 8 / NU;                         // waves per group (NU <= 2)
+  const int kw = (G4 + WPG - 1) / WPG;
+  const int ug = wave / WPG, kp = wave - ug * WPG;
+  const int k0 = kp * kw;
+  const int unit = ug * 64 + lane;
+  const int uc = unit < H ? unit : H - 1;
+  for (int e = tid; e < LR4 * G4P; e += kWG8) dG[e] = 0.f;
+  float w[KW];                                    // W_hh[k0 + j][unit]
+#pragma unroll
+  for (int j = 0; j < KW; ++j) {
+    const int k = k0 + j;
+    const bool ok = j < kw && k < G4 && unit < H;
+    const float x = a.w_hh[(int64_t)(k < G4 ? k : G4 - 1) * H + uc];
+    w[j] = ok ? x : 0.f;
+  }
+  const bool cell = tid < LR4 * H;
+  const int crow = cell ? tid / H : 0;
+  const int cunit = cell ? tid - crow * H : 0;
+  const int cgr = r0 + crow;
+  const bool cok = cell && cgr < B;
+  const int64_t grc = cgr < B ? cgr : B - 1;
+  const int cug = cunit >> 6, cl = cunit & 63;
+  float pg[4], pc = 0.f, pcp = 0.f, pdh = 0.f;
+  auto fetch = [&](int t) {
+    const float* gp = a.gates + ((int64_t)t * B + grc) * G4 + cunit;
+    pg[0] = gp[0]; pg[1] = gp[H]; pg[2] = gp[2 * H]; pg[3] = gp[3 * H];
+    pc = a.cbuf[(int64_t)(t + 1) * BH + grc * H + cunit];
+    pcp = a.cbuf[(int64_t)t * BH + grc * H + cunit];
+    pdh = a.dh[(int64_t)t * BH + grc * H + cunit];
+  };
+  if (cell && a.S > 0) fetch(a.S - 1);
+  float dcreg = 0.f;
+  __syncthreads();
+  LSTM_T0();
+  for (int t = a.S - 1; t >= 0; --t) {
+    if (cell) {
+      float dhr = 0.f;
+      if (t < a.S - 1) {
+        for (int p = 0; p < WPG; ++p) dhr += red[cug * WPG + p][crow][cl];
+      }
+      const float ig = pg[0], fg = pg[1], cg = pg[2], og = pg[3];
+      const float dh = pdh + dhr;
+      const float tc = ftanh(pc);
+      const float dc = dh * og * (1.f - tc * tc) + dcreg;
+      const float d_o = (dh * tc) * (og * (1.f - og));
+      const float d_i = (dc * cg) * (ig * (1.f - ig));
+      const float d_g = (dc * ig) * (1.f - cg * cg);
+      const float d_f = (dc * pcp) * (fg * (1.f - fg));
+      dcreg = cok ? dc * fg : 0.f;
+      float* l = dG + crow * G4P + cunit;
+      l[0] = cok ? d_i : 0.f; l[H] = cok ? d_f : 0.f;
+      l[2 * H] = cok ? d_g : 0.f; l[3 * H] = cok ? d_o : 0.f;
+      if (cok) {
+        float* o = a.dgates + ((int64_t)t * B + cgr) * G4 + cunit;
+        o[0] = d_i; o[H] = d_f; o[2 * H] = d_g; o[3 * H] = d_o;
+      }
+      if (t > 0) fetch(t - 1);
+    }
+    LSTM_TICK(3);
+    __syncthreads();
+    LSTM_TICK(4);
+    if (t == 0) break;
+    if (wave < NU * WPG) {
+      f32x4 acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float4* dr = reinterpret_cast<const float4*>(dG + (lane & 3) * G4P + k0);
+#pragma unroll
+      for (int k8 = 0; k8 < KW / 8; ++k8) {
+        const float4 u = dr[2 * k8], v = dr[2 * k8 + 1];
+        acc[0] = mfma4x64(u.x, w[8 * k8 + 0], acc[0]);
+        acc[1] = mfma4x64(u.y, w[8 * k8 + 1], acc[1]);
+        acc[2] = mfma4x64(u.z, w[8 * k8 + 2], acc[2]);
+        acc[3] = mfma4x64(u.w, w[8 * k8 + 3], acc[3]);
+        acc[4] = mfma4x64(v.x, w[8 * k8 + 4], acc[4]);
+        acc[5] = mfma4x64(v.y, w[8 * k8 + 5], acc[5]);
+        acc[6] = mfma4x64(v.z, w[8 * k8 + 6], acc[6]);
+        acc[7] = mfma4x64(v.w, w[8 * k8 + 7], acc[7]);
+      }
+      const f32x4 sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
+                        ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wave][i][lane] = sum[i];
+    }
+    LSTM_TICK(5);
+    __syncthreads();
+  }
+}
+
+static int use_r4() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("SMI_LSTM_R4");
+    u = (e && e[0] == '0') ? 0 : 1;
+  }
+  return u;
+}
+
 #ifdef SMI_PROF
 extern "C" int smi_lstm_phase_ticks(unsigned long long* out /* [8] */) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_ticks), sizeof(g_lstm_ticks)) != hipSuccess)
@@ -554,6 +793,14 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
   // algorithmic flops: the recurrent GEMM h W_hh^T of every step
   struct End { int s; hipStream_t st; double f;
                ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{kslot, st, 8.0 * B * H * (double)H * S};
+  if (H <= 128 && use_r4()) {
+    const dim3 g4((B + LR4 - 1) / LR4);
+    if (H <= 32) hipLaunchKernelGGL(lstm_fwd_r4_kernel<32>, g4, dim3(kWG8), 0, st, a);
+    else if (H <= 64) hipLaunchKernelGGL(lstm_fwd_r4_kernel<64>, g4, dim3(kWG8), 0, st, a);
+    else if (H <= 104) hipLaunchKernelGGL(lstm_fwd_r4_kernel<104>, g4, dim3(kWG8), 0, st, a);
+    else hipLaunchKernelGGL(lstm_fwd_r4_kernel<128>, g4, dim3(kWG8), 0, st, a);
+    return check_launch("lstm_fwd_r4_kernel");
+  }
   const size_t lds = (size_t)lstm_fwd_lds(H);
   const dim3 grid((B + LR - 1) / LR);
   if (H <= 64) {
@@ -591,6 +838,16 @@ int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, cons
   struct End { int s; hipStream_t st; double f;
                ~End() { ktime_end(s, KT_LSTM_BWD, f, st); } } end_{kslot, st,
                                                                  8.0 * B * H * (double)H * (S - 1)};
+  if (H <= 128 && use_r4()) {
+    const int nu = (H + 63) / 64, wpg = 8 / nu;
+    const int kw = (4 * H + wpg - 1) / wpg;
+    const dim3 g4((B + LR4 - 1) / LR4);
+    if (kw <= 32) hipLaunchKernelGGL(lstm_bwd_r4_kernel<32>, g4, dim3(kWG8), 0, st, a);
+    else if (kw <= 64) hipLaunchKernelGGL(lstm_bwd_r4_kernel<64>, g4, dim3(kWG8), 0, st, a);
+    else if (kw <= 104) hipLaunchKernelGGL(lstm_bwd_r4_kernel<104>, g4, dim3(kWG8), 0, st, a);
+    else hipLaunchKernelGGL(lstm_bwd_r4_kernel<128>, g4, dim3(kWG8), 0, st, a);
+    return check_launch("lstm_bwd_r4_kernel");
+  }
   const size_t lds = (size_t)lstm_bwd_lds(H);
   if (lds > 160 * 1024) return set_error(SMI_E_NOFIT, "lstm: hidden size too large for LDS");
   const dim3 grid((B + LR - 1) / LR);
