@@ -750,6 +750,132 @@ gemm_dwd_kernel(GemmArgs g) {
     }
 }
 
+// Row-panel GEMM for the learner's tall activations (rows >> N, K small):
+//   EPI_FWD: Y = act(X W^T + b)        EPI_DX: dX = (dY W) * [mask > 0]
+// A workgroup owns 64 rows x 16*NTW output columns, one 16-row MFMA tile per
+// wave.  The A operand goes from global memory straight into MFMA registers
+// as 16-byte k-runs (lane (li, lk) loads row li, k 4lk..4lk+3 of a 16-k
+// chunk; B is staged with the same k permutation), so every activation row
+// is read once per column group; the weight chunk B[16 k][16*NTW n] is
+// staged in LDS once per workgroup and shared by the four waves (one barrier
+// per chunk).  k past K reads a zero row by address (g_dwd_zero).
+constexpr int PN_LD = 20;
+
+template <int EPI, int NTW>
+__global__ void __launch_bounds__(kWG)
+gemm_panel_kernel(GemmArgs g) {
+  if (g.skip && g.skip[0] != 0) return;
+  constexpr int NB = 16 * NTW;                    // columns per workgroup
+  constexpr int BQ = (4 * NB + kWG - 1) / kWG;    // staged float4 per thread
+  __shared__ __attribute__((aligned(16))) float sB[2][NB * PN_LD + 4];   // + dummy slot
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const TileIdx ti = gemm_tile_index();
+  const int r0 = ti.mt * 64 + wave * 16;
+  const int n0 = ti.nt * NB;
+  const int nch = (g.K + 15) >> 4;
+  const float* arow = g.A + (int64_t)min(r0 + li, g.M - 1) * g.a_rs;
+  auto load_a = [&](int c) -> float4 {
+    const int k = c * 16 + 4 * lk;
+    return *reinterpret_cast<const float4*>(k < g.K ? arow + k : g_dwd_zero);
+  };
+  // staging: FWD B(k, n) = W[n][k] (k-contiguous rows); DX B(k, n) = W[k][n].
+  // Slot q of this thread is element idx = tid + q*256 of the chunk; slots past
+  // the chunk (idx >= 4*NB) load the zero row and write the dummy LDS slot (no
+  // divergent branches: the staging values stay in named registers)
+  auto load_b = [&](int c, int q) -> float4 {
+    const int idx = tid + q * kWG;
+    const float* src;
+    if constexpr (EPI == EPI_FWD) {
+      const int n = idx >> 2, k = c * 16 + ((idx & 3) << 2);
+      const int nc = min(n0 + n, g.N - 1);
+      src = (idx < 4 * NB && k < g.K) ? g.B + (int64_t)nc * g.b_cs + k : g_dwd_zero;
+    } else {
+      const int k = idx / (NB / 4), nq = (idx - k * (NB / 4)) << 2;
+      const int kk = c * 16 + k;
+      const int nc = min(n0 + nq, g.N - 4);
+      src = (idx < 4 * NB && kk < g.K) ? g.B + (int64_t)kk * g.b_rs + nc : g_dwd_zero;
+    }
+    return *reinterpret_cast<const float4*>(src);
+  };
+  auto store_b = [&](float* S, int q, float4 r) {
+    const int idx = tid + q * kWG;
+    const bool ok = idx < 4 * NB;
+    if constexpr (EPI == EPI_FWD) {
+      const int n = idx >> 2, kq = (idx & 3) << 2;
+      *reinterpret_cast<float4*>(S + (ok ? n * PN_LD + kq : NB * PN_LD)) = r;
+    } else {
+      const int k = idx / (NB / 4), nq = (idx - k * (NB / 4)) << 2;
+      const int base = ok ? nq * PN_LD + k : NB * PN_LD;
+      const int step = ok ? PN_LD : 1;
+      S[base] = r.x; S[base + step] = r.y; S[base + 2 * step] = r.z; S[base + 3 * step] = r.w;
+    }
+  };
+  f32x4 acc[NTW];
+#pragma unroll
+  for (int b = 0; b < NTW; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  static_assert(BQ <= 3, "panel staging: at most 3 float4 per thread");
+  float4 b0, b1, b2;
+  float4 aC = load_a(0), aN;
+  b0 = load_b(0, 0);
+  if constexpr (BQ > 1) b1 = load_b(0, 1);
+  if constexpr (BQ > 2) b2 = load_b(0, 2);
+  store_b(sB[0], 0, b0);
+  if constexpr (BQ > 1) store_b(sB[0], 1, b1);
+  if constexpr (BQ > 2) store_b(sB[0], 2, b2);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+    if (more) {
+      aN = load_a(c + 1);
+      b0 = load_b(c + 1, 0);
+      if constexpr (BQ > 1) b1 = load_b(c + 1, 1);
+      if constexpr (BQ > 2) b2 = load_b(c + 1, 2);
+    }
+    const float* S = sB[c & 1];
+    float4 bq[NTW];
+#pragma unroll
+    for (int b = 0; b < NTW; ++b)
+      bq[b] = *reinterpret_cast<const float4*>(S + (16 * b + li) * PN_LD + 4 * lk);
+#pragma unroll
+    for (int b = 0; b < NTW; ++b) {
+      acc[b] = mfma4(aC.x, bq[b].x, acc[b]);
+      acc[b] = mfma4(aC.y, bq[b].y, acc[b]);
+      acc[b] = mfma4(aC.z, bq[b].z, acc[b]);
+      acc[b] = mfma4(aC.w, bq[b].w, acc[b]);
+    }
+    if (more) {
+      float* S1 = sB[(c + 1) & 1];
+      store_b(S1, 0, b0);
+      if constexpr (BQ > 1) store_b(S1, 1, b1);
+      if constexpr (BQ > 2) store_b(S1, 2, b2);
+      aC = aN;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int b = 0; b < NTW; ++b) {
+    const int n = n0 + 16 * b + li;
+    if (n >= g.N) continue;
+    float bias_n = 0.f;
+    if constexpr (EPI == EPI_FWD) bias_n = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + 4 * lk + i;
+      if (m >= g.M) continue;
+      float v = acc[b][i];
+      if constexpr (EPI == EPI_FWD) {
+        v += bias_n;
+        if (g.act == ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (g.act == ACT_TANH) v = tanhf(v);
+      } else {
+        if (g.mask) v = g.mask[(int64_t)m * g.ldm + n] > 0.f ? v : 0.f;
+      }
+      g.C[(int64_t)m * g.ldc + n] = v;
+    }
+  }
+}
+
 float* workspace_f32(int64_t nfloats);
 
 // split-K target workgroup count (SMI_SPLITK_TARGET overrides; tuning knob)
@@ -836,8 +962,63 @@ static int dwd_launch(GemmArgs g, hipStream_t st) {
   return splitk_reduce(g, S, EPI_DW, st);
 }
 
+static int use_panel() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("SMI_PANEL");
+    u = (e && e[0] == '0') ? 0 : 1;
+  }
+  return u;
+}
+
+template <int EPI>
+static void panel_dispatch(const GemmArgs& g, dim3 grid, int ntw, hipStream_t st) {
+  switch (ntw) {
+    case 1: hipLaunchKernelGGL((gemm_panel_kernel<EPI, 1>), grid, dim3(kWG), 0, st, g); break;
+    case 2: hipLaunchKernelGGL((gemm_panel_kernel<EPI, 2>), grid, dim3(kWG), 0, st, g); break;
+    case 4: hipLaunchKernelGGL((gemm_panel_kernel<EPI, 4>), grid, dim3(kWG), 0, st, g); break;
+    case 5: hipLaunchKernelGGL((gemm_panel_kernel<EPI, 5>), grid, dim3(kWG), 0, st, g); break;
+    case 7: hipLaunchKernelGGL((gemm_panel_kernel<EPI, 7>), grid, dim3(kWG), 0, st, g); break;
+    default: hipLaunchKernelGGL((gemm_panel_kernel<EPI, 10>), grid, dim3(kWG), 0, st, g); break;
+  }
+}
+
+// tall forward / input-gradient GEMMs with 16-byte operands: gemm_panel_kernel
+static bool panel_ok(int epi, const GemmArgs& g) {
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!use_panel() || g.M < 2048 || g.N > 640 || g.K > 1024 || g.K < 1) return false;
+  if (g.a_cs != 1 || g.a_rs % 4 || g.K % 4 || !al16(g.A) || !al16(g.B)) return false;
+  if (epi == EPI_FWD) return g.b_rs == 1 && g.b_cs % 4 == 0;
+  // input gradients: the transposing LDS stage costs more than it saves below
+  // ~192 output columns (measured: 300->100 and 400->100 faster on gemm_kernel)
+  if (epi == EPI_DX)
+    return g.b_cs == 1 && g.b_rs % 4 == 0 && g.N % 4 == 0 && g.N >= 192;
+  return false;
+}
+
+static int panel_launch(int epi, const GemmArgs& g, hipStream_t st) {
+  // column-group width: fewest padded 16-column tiles, then fewer groups
+  static const int cand[6] = {1, 2, 4, 5, 7, 10};
+  const int t16 = (g.N + 15) / 16;
+  int best = 10;
+  double bcost = 1e30;
+  for (int c : cand) {
+    const int groups = (t16 + c - 1) / c;
+    const double cost = groups * c + 0.3 * groups;
+    if (cost < bcost) { bcost = cost; best = c; }
+  }
+  const dim3 grid((g.M + 63) / 64, (g.N + 16 * best - 1) / (16 * best), 1);
+  const int kslot = ktime_begin(st);
+  if (epi == EPI_FWD) panel_dispatch<EPI_FWD>(g, grid, best, st);
+  else panel_dispatch<EPI_DX>(g, grid, best, st);
+  ktime_end(kslot, epi == EPI_FWD ? KT_GEMM_FWD : KT_GEMM_DX, 2.0 * g.M * (double)g.N * g.K, st);
+  return check_launch("gemm_panel_kernel");
+}
+
 static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return SMI_OK;
+  g.part = nullptr;
+  if (epi != EPI_DW && panel_ok(epi, g)) return panel_launch(epi, g, st);
   if (epi == EPI_DW && use_dwd() && g.a_rs == 1 && g.b_cs == 1 && g.K >= 1 &&
       (g.ones_col >= 0 ? g.ones_col : g.N) >= 1 && g.M <= 512 && g.N <= 512)
     return dwd_launch(g, st);
