@@ -79,6 +79,13 @@ struct LstmFwdArgs {
   float* cbuf;            // [S+1][B][H] or null
   float* gates;           // [S][B][4H] activated, or null
   const int* skip;
+  // fused input projection (lstm_fwd_r4_kernel<KP, KX > 0>): x_t W_ih^T + b_ih
+  // inside the step instead of the xproj GEMM
+  const float* x;         // [S][B][ldx]
+  int64_t ldx;
+  int din;
+  const float* w_ih;      // [4H][din]
+  const float* b_ih;      // [4H]
 };
 
 template <int MAXUT>
@@ -554,12 +561,18 @@ __device__ __forceinline__ f32x4 mfma4x64(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 4, 0, 0);
 }
 
-// KP: H rounded up to a multiple of 8 (W_hh registers per lane)
-template <int KP>
+// KP: H rounded up to a multiple of 8 (W_hh registers per lane).  KX > 0:
+// the input projection is fused (din <= KX, a multiple of 8): W_ih's column
+// joins W_hh's in registers, x_t of the 4 segments is staged in LDS one step
+// ahead, and the k loop runs over [x_t | h_{t-1}] — no xproj GEMM and no
+// [S][B][4H] round trip through HBM.
+template <int KP, int KX>
 __global__ void __launch_bounds__(kWG8)
 lstm_fwd_r4_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  constexpr int KXS = KX > 0 ? KX : 8;
   __shared__ __attribute__((aligned(16))) float hS[2][LR4 * KP];
+  __shared__ __attribute__((aligned(16))) float xS[2][LR4 * KXS];
   __shared__ float pre[LR4][4 * KP];
   const int H = a.H, B = a.B, G4 = 4 * H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -574,7 +587,30 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
     const float x = a.w_hh[(int64_t)colc * H + (k < H ? k : H - 1)];
     w[k] = k < H ? x : 0.f;
   }
-  const float bh = a.b_hh[colc];
+  float bh = a.b_hh[colc];
+  float wx[KXS];
+  if constexpr (KX > 0) {
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+      const float x = a.w_ih[(int64_t)colc * a.din + (k < a.din ? k : a.din - 1)];
+      wx[k] = k < a.din ? x : 0.f;
+    }
+    bh += a.b_ih[colc];
+  }
+  // x staging: thread tid < 4*KX owns (row tid / KX, k tid % KX) of x_t
+  const int xr = tid / KXS, xk = tid - (tid / KXS) * KXS;
+  const bool xown = KX > 0 && tid < LR4 * KXS;
+  const int64_t xoff0 = (int64_t)min(r0 + xr, B - 1) * a.ldx + min(xk, a.din - 1);
+  const bool xval = xk < a.din;
+  auto xload = [&](int t) -> float {
+    const float v = a.x[(int64_t)t * B * a.ldx + xoff0];
+    return xval ? v : 0.f;
+  };
+  float xnext = 0.f;
+  if constexpr (KX > 0) {
+    if (xown && a.S > 0) xS[0][xr * KXS + xk] = xload(0);
+    if (xown && a.S > 1) xnext = xload(1);
+  }
   // cell owned by this thread: (crow, cunit)
   const bool cell = tid < LR4 * H;
   const int crow = cell ? tid / H : 0;
@@ -597,8 +633,8 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
     const int gr = r0 + i < B ? r0 + i : B - 1;
     xoff[i] = (int64_t)gr * G4 + colc;
   }
-  float xp[4];
-  if (a.S > 0) {
+  float xp[4] = {0.f, 0.f, 0.f, 0.f};
+  if (KX == 0 && a.S > 0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) xp[i] = a.xproj[xoff[i]];
   }
@@ -611,6 +647,21 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
       f32x4 acc[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (KX > 0) {
+        const float4* xr4 = reinterpret_cast<const float4*>(xS[t & 1] + (lane & 3) * KXS);
+#pragma unroll
+        for (int k8 = 0; k8 < KX / 8; ++k8) {
+          const float4 u = xr4[2 * k8], v = xr4[2 * k8 + 1];
+          acc[0] = mfma4x64(u.x, wx[8 * k8 + 0], acc[0]);
+          acc[1] = mfma4x64(u.y, wx[8 * k8 + 1], acc[1]);
+          acc[2] = mfma4x64(u.z, wx[8 * k8 + 2], acc[2]);
+          acc[3] = mfma4x64(u.w, wx[8 * k8 + 3], acc[3]);
+          acc[4] = mfma4x64(v.x, wx[8 * k8 + 4], acc[4]);
+          acc[5] = mfma4x64(v.y, wx[8 * k8 + 5], acc[5]);
+          acc[6] = mfma4x64(v.z, wx[8 * k8 + 6], acc[6]);
+          acc[7] = mfma4x64(v.w, wx[8 * k8 + 7], acc[7]);
+        }
+      }
       const float4* hr = reinterpret_cast<const float4*>(hp + (lane & 3) * KP);
 #pragma unroll
       for (int k8 = 0; k8 < KP / 8; ++k8) {
@@ -630,10 +681,14 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) pre[i][col] = xp[i] + (sum[i] + bh);
       }
-      if (t + 1 < a.S) {
+      if (KX == 0 && t + 1 < a.S) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) xp[i] = a.xproj[(int64_t)(t + 1) * B * G4 + xoff[i]];
       }
+    }
+    if constexpr (KX > 0) {   // x_{t+1} into the other buffer, x_{t+2} in flight
+      if (xown && t + 1 < a.S) xS[(t + 1) & 1][xr * KXS + xk] = xnext;
+      if (xown && t + 2 < a.S) xnext = xload(t + 2);
     }
     LSTM_TICK(0);
     __syncthreads();
@@ -795,10 +850,10 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
                ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{kslot, st, 8.0 * B * H * (double)H * S};
   if (H <= 128 && use_r4()) {
     const dim3 g4((B + LR4 - 1) / LR4);
-    if (H <= 32) hipLaunchKernelGGL(lstm_fwd_r4_kernel<32>, g4, dim3(kWG8), 0, st, a);
-    else if (H <= 64) hipLaunchKernelGGL(lstm_fwd_r4_kernel<64>, g4, dim3(kWG8), 0, st, a);
-    else if (H <= 104) hipLaunchKernelGGL(lstm_fwd_r4_kernel<104>, g4, dim3(kWG8), 0, st, a);
-    else hipLaunchKernelGGL(lstm_fwd_r4_kernel<128>, g4, dim3(kWG8), 0, st, a);
+    if (H <= 32) hipLaunchKernelGGL((lstm_fwd_r4_kernel<32, 0>), g4, dim3(kWG8), 0, st, a);
+    else if (H <= 64) hipLaunchKernelGGL((lstm_fwd_r4_kernel<64, 0>), g4, dim3(kWG8), 0, st, a);
+    else if (H <= 104) hipLaunchKernelGGL((lstm_fwd_r4_kernel<104, 0>), g4, dim3(kWG8), 0, st, a);
+    else hipLaunchKernelGGL((lstm_fwd_r4_kernel<128, 0>), g4, dim3(kWG8), 0, st, a);
     return check_launch("lstm_fwd_r4_kernel");
   }
   const size_t lds = (size_t)lstm_fwd_lds(H);
@@ -827,6 +882,31 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
     hipLaunchKernelGGL(lstm_fwd_kernel<4>, grid, dim3(kWG), lds, st, a);
   }
   return check_launch("lstm_fwd_kernel");
+}
+
+// LSTM forward with the input projection fused (din <= 64, H <= 104): returns
+// SMI_E_NOFIT when the shape needs the xproj GEMM + launch_lstm_fwd instead
+int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, const float* b_ih,
+                      const float* w_hh, const float* b_hh, const float* h0, const float* c0,
+                      int S, int B, int H, float* hbuf, float* cbuf, float* gates,
+                      hipStream_t st, const int* skip) {
+  if (!use_r4() || din < 1 || din > 64 || H < 1 || H > 104) return SMI_E_NOFIT;
+  if (B <= 0 || S < 0) return SMI_OK;
+  LstmFwdArgs a{nullptr, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates, skip,
+                x, ldx, din, w_ih, b_ih};
+  const int kslot = ktime_begin(st);
+  struct End { int s; hipStream_t st; double f;
+               ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{
+      kslot, st, 8.0 * B * H * (double)(H + din) * S};
+  const dim3 g4((B + LR4 - 1) / LR4);
+  if (din <= 48) {
+    if (H <= 64) hipLaunchKernelGGL((lstm_fwd_r4_kernel<64, 48>), g4, dim3(kWG8), 0, st, a);
+    else hipLaunchKernelGGL((lstm_fwd_r4_kernel<104, 48>), g4, dim3(kWG8), 0, st, a);
+  } else {
+    if (H <= 64) hipLaunchKernelGGL((lstm_fwd_r4_kernel<64, 64>), g4, dim3(kWG8), 0, st, a);
+    else hipLaunchKernelGGL((lstm_fwd_r4_kernel<104, 64>), g4, dim3(kWG8), 0, st, a);
+  }
+  return check_launch("lstm_fwd_r4_kernel");
 }
 
 int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,

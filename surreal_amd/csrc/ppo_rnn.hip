@@ -688,6 +688,9 @@ static LstmP lstm_params(const float* p, int D, int H) {
 static int lstm_forward(const RnnDims& d, const LstmP& l, const float* X, int S, const float* h0,
                         const float* c0, const RnnScratch& s, float* cbuf, float* gates,
                         hipStream_t st, const int* skip) {
+  const int rf = launch_lstm_fwd_x(X, d.Din, d.Din, l.Wih, l.bih, l.Whh, l.bhh, h0, c0, S, d.B,
+                                  d.H, s.hbuf, cbuf, gates, st, skip);
+  if (rf != SMI_E_NOFIT) return rf;
   const int64_t rows = (int64_t)S * d.B;
   RC(launch_linear_fwd(X, d.Din, (int)rows, d.Din, l.Wih, d.Din, l.bih, d.G4, ACT_NONE, s.xproj,
                        d.G4, st, skip));

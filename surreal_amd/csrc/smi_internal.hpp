@@ -121,6 +121,10 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st);
 int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
                     const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,
                     hipStream_t st, const int* skip);
+int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, const float* b_ih,
+                      const float* w_hh, const float* b_hh, const float* h0, const float* c0,
+                      int S, int B, int H, float* hbuf, float* cbuf, float* gates,
+                      hipStream_t st, const int* skip);
 int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
                     int S, int B, int H, float* dgates, hipStream_t st, const int* skip);
 
