@@ -35,7 +35,9 @@ def _mtime(p):
 # Developer variants: 'prof' adds the epoch-kernel phase timer (-DSMI_PROF,
 # tools/fused_breakdown.py --phases); 'noinl' keeps the dense helpers out of line.  The product library is variant None.
 VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
-            'noinl_prof': ['-DSMI_DENSE_NOINLINE', '-DSMI_PROF']}
+            'noinl_prof': ['-DSMI_DENSE_NOINLINE', '-DSMI_PROF'],
+            # dW-kernel experiments (tools/dwd_exp.sh)
+            'p8': ['-DSMI_DWD_P=8'], 'p6': ['-DSMI_DWD_P=6'], 'occ1': ['-DSMI_DWD_OCC=1']}
 
 
 def lib_path(variant=None):

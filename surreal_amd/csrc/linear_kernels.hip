@@ -604,7 +604,13 @@ gemm_dw128_kernel(GemmArgs g) {
 // steps prefetched in registers) and are combined through LDS in a fixed
 // order; slabs go to the split-K partials.  Row-major dY/X of the heads, the
 // LSTM input/recurrent weights and the DDPG nets all take this path.
-constexpr int DWD_P = 4;   // steps in flight per wave
+#ifndef SMI_DWD_P
+#define SMI_DWD_P 4
+#endif
+#ifndef SMI_DWD_OCC
+#define SMI_DWD_OCC 2
+#endif
+constexpr int DWD_P = SMI_DWD_P;   // steps in flight per wave
 
 // Rows past the slab and the synthesised bias column are selected by ADDRESS
 // (a zero row / a {1, 0, 0, 0} vector in device memory), never by masking the
@@ -615,7 +621,7 @@ constexpr int DWD_ZMAX = 8192;
 __device__ __attribute__((aligned(16))) float g_dwd_zero[DWD_ZMAX];
 __device__ __attribute__((aligned(16))) float g_dwd_one[4] = {1.f, 0.f, 0.f, 0.f};
 
-template <int MT, int NT, bool VA, bool VB>
+template <int MT, int NT, bool VA, bool VB, int NB = NT>
 __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m0, int n0, int bdata,
                                          float (&av)[MT], float (&bv)[NT]) {
   const int li = threadIdx.x & 15;
@@ -632,7 +638,7 @@ __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m
     for (int t = 0; t < MT; ++t) av[t] = Ar[min(m0 + MT * li + t, g.M - 1)];
   }
 #pragma unroll
-  for (int h = 0; h < NT / 4; ++h) {
+  for (int h = 0; h < NB / 4; ++h) {
     const int cb = n0 + 64 * h + 4 * li;
     if constexpr (VB) {
       const float* src = cb < bdata ? Br + cb : (cb == g.ones_col ? one : g_dwd_zero);
@@ -649,7 +655,7 @@ __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m
 }
 
 template <int MT, int NT, bool VA, bool VB>
-__global__ void __launch_bounds__(kWG)
+__global__ void __launch_bounds__(kWG, SMI_DWD_OCC)
 gemm_dwd_kernel(GemmArgs g) {
   if (g.skip && g.skip[0] != 0) return;
   extern __shared__ float4 dwd_red[];            // 2 x [MT*NT][64] float4
@@ -670,20 +676,28 @@ gemm_dwd_kernel(GemmArgs g) {
   // loads are unconditional (rows past the slab read clamped and zeroed) so
   // the compiler's vmcnt waits stay partial across the unrolled P steps;
   // slabs are multiples of 16*P rows, only the last one runs zero steps
-  float av[DWD_P][MT], bv[DWD_P][NT];
+  // NB of the NT column sub-tiles carry data: a tile whose upper 64-column
+  // half lies past N (e.g. columns 320..383 of a 301-wide gradient) runs the
+  // half-width loop (wave-uniform choice, no loads or MFMAs for that half)
+  auto mainloop = [&](auto nbc) {
+    constexpr int NB = decltype(nbc)::value;
+    float av[DWD_P][MT], bv[DWD_P][NT];
 #pragma unroll
-  for (int p = 0; p < DWD_P; ++p)
-    dwd_load<MT, NT, VA, VB>(g, rw + 16 * p, ke, m0, n0, bdata, av[p], bv[p]);
-  for (int s0 = 0; s0 < nsteps; s0 += DWD_P) {
+    for (int p = 0; p < DWD_P; ++p)
+      dwd_load<MT, NT, VA, VB, NB>(g, rw + 16 * p, ke, m0, n0, bdata, av[p], bv[p]);
+    for (int s0 = 0; s0 < nsteps; s0 += DWD_P) {
 #pragma unroll
-    for (int p = 0; p < DWD_P; ++p) {
+      for (int p = 0; p < DWD_P; ++p) {
 #pragma unroll
-      for (int b = 0; b < NT; ++b)
+        for (int b = 0; b < NB; ++b)
 #pragma unroll
-        for (int a = 0; a < MT; ++a) acc[a][b] = mfma4(av[p][a], bv[p][b], acc[a][b]);
-      dwd_load<MT, NT, VA, VB>(g, rw + 16 * (s0 + p + DWD_P), ke, m0, n0, bdata, av[p], bv[p]);
+          for (int a = 0; a < MT; ++a) acc[a][b] = mfma4(av[p][a], bv[p][b], acc[a][b]);
+        dwd_load<MT, NT, VA, VB, NB>(g, rw + 16 * (s0 + p + DWD_P), ke, m0, n0, bdata, av[p], bv[p]);
+      }
     }
-  }
+  };
+  if (NT == 8 && n0 + 64 >= g.N) mainloop(std::integral_constant<int, (NT > 4 ? 4 : NT)>{});
+  else mainloop(std::integral_constant<int, NT>{});
   // combine the four waves: (w0 + w2) + (w1 + w3)
   float4* buf0 = dwd_red;
   float4* buf1 = dwd_red + MT * NT * 64;
@@ -1015,9 +1029,102 @@ static int panel_launch(int epi, const GemmArgs& g, hipStream_t st) {
   return check_launch("gemm_panel_kernel");
 }
 
+// Input gradient through a layer with at most 8 outputs (the value head's
+// 200 -> 1, the action head's 200 -> 8): dX = (dY W) * [mask > 0] is a
+// rank-<=8 update, pure streaming (read dY row + mask, write dX), so it skips
+// the MFMA tiles (which pad K to 16/32).  Per element: the k-ordered fmaf
+// chain from 0 (for K = 1 bit-identical to the tiled path).  A thread owns 4
+// consecutive columns of 4 rows (the W slice in registers, 16-byte mask reads
+// and stores, coalesced along the row).  SMI_DX_SMALLK=0 disables it.
+template <int KK, bool V4>
+__global__ void __launch_bounds__(kWG)
+dx_smallk_kernel(GemmArgs g) {
+  if (g.skip && g.skip[0] != 0) return;
+  constexpr int RW = 4;                            // rows per thread
+  const int nq = (g.N + 3) >> 2;
+  const int64_t idx = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (idx >= (int64_t)((g.M + RW - 1) / RW) * nq) return;
+  const int mg = (int)(idx / nq), n0 = (int)(idx - (int64_t)mg * nq) * 4;
+  // W rows k (4 columns each), shared by the thread's RW rows
+  float w[KK][4];
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+    const float* wr = g.B + (int64_t)min(k, g.K - 1) * g.b_rs;
+    if constexpr (V4) {
+      const float4 x = *reinterpret_cast<const float4*>(wr + n0);
+      w[k][0] = x.x; w[k][1] = x.y; w[k][2] = x.z; w[k][3] = x.w;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w[k][t] = wr[min(n0 + t, g.N - 1)];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    const int m = mg * RW + r;
+    if (m >= g.M) break;
+    const float* arow = g.A + (int64_t)m * g.a_rs;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+      if (k >= g.K) break;
+      const float ak = arow[k];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = fmaf(ak, w[k][t], v[t]);
+    }
+    const float* mrow = g.mask ? g.mask + (int64_t)m * g.ldm + n0 : nullptr;
+    float* crow = g.C + (int64_t)m * g.ldc + n0;
+    if constexpr (V4) {
+      if (mrow) {
+        const float4 mk = *reinterpret_cast<const float4*>(mrow);
+        v[0] = mk.x > 0.f ? v[0] : 0.f; v[1] = mk.y > 0.f ? v[1] : 0.f;
+        v[2] = mk.z > 0.f ? v[2] : 0.f; v[3] = mk.w > 0.f ? v[3] : 0.f;
+      }
+      *reinterpret_cast<float4*>(crow) = float4{v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (n0 + t >= g.N) break;
+        crow[t] = (mrow && !(mrow[t] > 0.f)) ? 0.f : v[t];
+      }
+    }
+  }
+}
+
+static int use_dx_smallk() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("SMI_DX_SMALLK");
+    u = (e && e[0] == '0') ? 0 : 1;
+  }
+  return u;
+}
+
+static int dx_smallk_launch(const GemmArgs& g, hipStream_t st) {
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const bool v4 = g.N % 4 == 0 && g.ldc % 4 == 0 && al16(g.C) && g.b_rs % 4 == 0 && al16(g.B) &&
+                  (!g.mask || (g.ldm % 4 == 0 && al16(g.mask)));
+  const int64_t n = (int64_t)((g.M + 3) / 4) * ((g.N + 3) / 4);
+  const dim3 grid((unsigned)((n + kWG - 1) / kWG));
+  const int kslot = ktime_begin(st);
+#define SMI_DXS(KK)                                                                        \
+  do {                                                                                     \
+    if (v4) hipLaunchKernelGGL((dx_smallk_kernel<KK, true>), grid, dim3(kWG), 0, st, g);   \
+    else hipLaunchKernelGGL((dx_smallk_kernel<KK, false>), grid, dim3(kWG), 0, st, g);     \
+  } while (0)
+  if (g.K == 1) SMI_DXS(1);
+  else if (g.K <= 2) SMI_DXS(2);
+  else if (g.K <= 4) SMI_DXS(4);
+  else SMI_DXS(8);
+#undef SMI_DXS
+  ktime_end(kslot, KT_GEMM_DX, 2.0 * g.M * (double)g.N * g.K, st);
+  return check_launch("dx_smallk_kernel");
+}
+
 static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return SMI_OK;
   g.part = nullptr;
+  if (epi == EPI_DX && use_dx_smallk() && g.K >= 1 && g.K <= 8 && g.a_cs == 1 && g.b_cs == 1)
+    return dx_smallk_launch(g, st);
   if (epi != EPI_DW && panel_ok(epi, g)) return panel_launch(epi, g, st);
   if (epi == EPI_DW && use_dwd() && g.a_rs == 1 && g.b_cs == 1 && g.K >= 1 &&
       (g.ones_col >= 0 ? g.ones_col : g.N) >= 1 && g.M <= 512 && g.N <= 512)
