@@ -1004,9 +1004,14 @@ static bool panel_ok(int epi, const GemmArgs& g) {
   if (g.a_cs != 1 || g.a_rs % 4 || g.K % 4 || !al16(g.A) || !al16(g.B)) return false;
   if (epi == EPI_FWD) return g.b_rs == 1 && g.b_cs % 4 == 0;
   // input gradients: the transposing LDS stage costs more than it saves below
-  // ~192 output columns (measured: 300->100 and 400->100 faster on gemm_kernel)
+  // ~96 output columns (in the C3 learner 300->100 runs 16 % faster here than
+  // on gemm_kernel; SMI_PANEL_DX_MIN overrides)
+  static const int dx_min = [] {
+    const char* e = getenv("SMI_PANEL_DX_MIN");
+    return e ? atoi(e) : 96;
+  }();
   if (epi == EPI_DX)
-    return g.b_cs == 1 && g.b_rs % 4 == 0 && g.N % 4 == 0 && g.N >= 192;
+    return g.b_cs == 1 && g.b_rs % 4 == 0 && g.N % 4 == 0 && g.N >= dx_min;
   return false;
 }
 

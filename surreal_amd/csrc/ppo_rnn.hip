@@ -491,7 +491,7 @@ adam_split_kernel(AdamSplitArgs a) {
   double s = 0.0;
   for (int i = threadIdx.x; i < a.np; i += kWG) s += a.part[i];
   s = block_sum_d(s, red);
-  const int t = a.step[0] + 1;
+  const int t = a.step[0];      // already bumped by sumsq_part_kernel
   if (threadIdx.x == 0) {
     const float norm = (float)sqrt(s);
     float coef = 1.f;
@@ -526,15 +526,16 @@ adam_split_kernel(AdamSplitArgs a) {
   }
 }
 
-__global__ void step_bump_kernel(int* step, int* runs, const int* skip) {
-  if (skip && skip[0] != 0) return;
-  step[0] += 1;
-  if (runs) runs[0] += 1;
-}
-
+// also advances the optimizer's step counter (and the applied-epoch count):
+// the Adam kernel that follows in the stream reads the bumped step
 __global__ void __launch_bounds__(kWG)
-sumsq_part_kernel(const float* __restrict__ g, int64_t n, double* part, const int* skip) {
+sumsq_part_kernel(const float* __restrict__ g, int64_t n, double* part, const int* skip,
+                  int* step, int* runs) {
   if (skip && skip[0] != 0) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    step[0] += 1;
+    if (runs) runs[0] += 1;
+  }
   __shared__ double scr[kNW];
   double s = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
@@ -889,17 +890,15 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_POLICY_APPLY: {
       const int64_t n = d.nA_head + d.nS;
       const int g = grid_of(n, 1024);
-      hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gA, n, s.part, stop);
+      hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gA, n, s.part, stop,
+                         a.actor_step, s.ci + CI_RUNS);
       RC(check_launch("sumsq_part_kernel"));
       AdamSplitArgs aa{a.actor, d.nA_head, a.lstm, d.nS, gA, a.actor_m, a.actor_v, a.actor_step,
                        a.hyper + SMI_HYP_LR_ACTOR, a.beta1, a.beta2, a.adam_eps, a.actor_wd,
                        a.clip_actor_grad ? a.actor_max_norm : 0.f, s.part, g, stop,
                        a.clip_actor_grad ? a.stats + SMI_ST_GRAD_NORM_ACTOR : nullptr, nullptr};
       hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(kWG), 0, st, aa);
-      RC(check_launch("adam_split_kernel"));
-      hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(1), 0, st, a.actor_step, s.ci + CI_RUNS,
-                         stop);
-      return check_launch("step_bump_kernel");
+      return check_launch("adam_split_kernel");
     }
     case SMI_RNN_PH_VALUE_GRAD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
@@ -920,7 +919,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_VALUE_APPLY: {
       const int64_t n = d.nC_head + d.nS;
       const int g = grid_of(n, 1024);
-      hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gC, n, s.part, nullptr);
+      hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gC, n, s.part, nullptr,
+                         a.critic_step, nullptr);
       RC(check_launch("sumsq_part_kernel"));
       AdamSplitArgs aa{a.critic, d.nC_head, a.lstm, d.nS, gC, a.critic_m, a.critic_v,
                        a.critic_step, a.hyper + SMI_HYP_LR_CRITIC, a.beta1, a.beta2, a.adam_eps,
@@ -928,10 +928,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                        nullptr, a.clip_critic_grad ? a.stats + SMI_ST_GRAD_NORM_CRITIC : nullptr,
                        nullptr};
       hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(kWG), 0, st, aa);
-      RC(check_launch("adam_split_kernel"));
-      hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(1), 0, st, a.critic_step, nullptr,
-                         nullptr);
-      return check_launch("step_bump_kernel");
+      return check_launch("adam_split_kernel");
     }
     case SMI_RNN_PH_ZSTATS: {
       // zbuf (double) = [value sums (5) | column sums (D) | sums of squares (D)]
