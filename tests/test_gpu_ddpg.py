@@ -58,7 +58,7 @@ def _fp32_as_good_as_torch(got, ref32, ref64, slack=1e-6, mag=None):
                                       (21504, 100, 300), (5376, 42, 400), (20000, 200, 8),
                                       (8192, 17, 300), (4099, 64, 33), (21504, 42, 400),
                                       (300, 2592, 64), (2688, 2592, 256), (4096, 300, 1),
-                                      (3000, 17, 6)])
+                                      (3000, 17, 6), (21504, 200, 1), (777, 100, 3), (9, 256, 5)])
 def test_linear_ops_vs_torch(rows, k, n):
     L.ensure_workspace(torch.device('cuda'))      # split-K paths (dW; few-tile long-K forward)
     g = torch.Generator().manual_seed(rows + k)
