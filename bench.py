@@ -124,16 +124,127 @@ def cpu_baseline(name, lc, dims, budget_s=12.0):
                       f'timed calls after 1 warm-up (~{budget_s:.0f} s), median {med * 1e3:.1f} ms'}
 
 
+DDPG_METRIC = 'DDPG learner env-steps/sec (replay sample + n-step target + critic/actor update)'
+
+
+def run_ddpg(args):
+    """--config c4 (BASELINE configs[3]): DDPGLearner, batch 512,
+    HalfCheetah dims (obs 17, act 6), actor 300x200, critic 400x300, n_step 3,
+    fed by UniformReplay over a 333,333-row shard resident in HBM.  A step =
+    one CPython-exact index draw (MT19937 kernel) + row gather + learn().
+    Single GPU (SURVEY §8(e) DDPG sharding is not built; --gpus > 1 refused)."""
+    if int(os.environ.get('WORLD_SIZE', '1')) > 1:
+        raise SystemExit('bench.py --config c4: single GPU only')
+    from surreal_amd import _lib as L
+    from surreal_amd.config import DDPG_DEFAULT_LEARNER_CONFIG, gym_env_config
+    from surreal_amd.ddpg import DDPGLearner
+    from surreal_amd.replay import UniformReplay
+    torch.cuda.set_device(0)
+    dev = torch.device('cuda', 0)
+    D, A, B, NREP = 17, 6, 512, 333333
+    lc = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
+    lc.replay.batch_size = B
+    lc.replay.memory_size = NREP
+    lc.replay.sampling_start_size = 1000
+    ec = gym_env_config(D, A)
+    rep = UniformReplay(lc, ec, seed=0, device=dev)
+    rows = np.random.RandomState(0).randn(NREP, rep.width).astype(np.float32)
+    rows[:, D:D + A] = np.tanh(rows[:, D:D + A])
+    rows[:, 2 * D + A + 1] = (rows[:, 2 * D + A + 1] > 1.6).astype(np.float32)
+    rep.insert_rows(rows)
+    learner = DDPGLearner(lc, ec, seed=1, device=dev)
+    buf = torch.empty(B, rep.width, device=dev)
+
+    def step():
+        _, got = rep.sample(B, out=buf)
+        learner.learn(rep.split(got))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    n_inst = min(args.steps, 5)
+    L.kernel_timing(True)
+    for _ in range(n_inst):
+        step()
+    torch.cuda.synchronize()
+    L.kernel_timing(False)
+    kt = L.kernel_timing_report()
+    kernels = {n: {'launches_per_step': round(c / n_inst, 2), 'avg_ms': round(ms / c, 5),
+                   'ms_per_step': round(ms / n_inst, 4),
+                   'tflops': round(fl / (ms * 1e-3) / 1e12, 3)}
+               for n, (c, ms, fl) in kt.items()}
+    dom = max(kt, key=lambda n: kt[n][1])
+    c, ms_k, fl = kt[dom]
+    ach = fl / (ms_k * 1e-3) / 1e12
+    out = {
+        'metric': DDPG_METRIC, 'value': round(B * args.steps / elapsed, 1), 'unit': 'env-steps/s',
+        'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'data': 'synthetic replay rows (seeded); random-init weights of the named architecture',
+        'config': {'workload': 'C4: DDPG learner, batch 512 sampled CPython-exactly from a '
+                               '333,333-row replay shard, obs 17, act 6, actor 300x200, critic '
+                               '400x300, n_step 3, hard target update',
+                   'batch': B, 'replay_rows': NREP, 'parallelism': 'single'},
+        'roofline': {'kernel': dom, 'bound': 'mfma', 'achieved': round(ach, 3),
+                     'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': round(ach / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+                     'avg_ms': round(ms_k / c, 5), 'algorithmic_flops_per_launch': int(fl / c)},
+        'kernels': kernels,
+    }
+    if not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline_ddpg(lc, rows, D, A, B, args.cpu_budget)
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_ddpg(lc, rows, D, A, B, budget_s=12.0):
+    """The oracle DDPGLearnerRef.optimize() (torch CPU fp32) fed by CPython
+    random.randint index draws over the same replay rows, timed per step."""
+    import random
+    from oracle import ddpg_ref as R
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    ref = R.DDPGLearnerRef(lc, D, A)
+    table = torch.from_numpy(rows)
+    random.seed(0)
+
+    def step():
+        idx = [random.randint(0, len(rows) - 1) for _ in range(B)]
+        r = table[idx]
+        ref.optimize(r[:, :D], r[:, D:D + A], r[:, D + A:D + A + 1], r[:, D + A + 1:2 * D + A + 1],
+                     r[:, 2 * D + A + 1:2 * D + A + 2])
+
+    step()
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while (time.perf_counter() < t_end or not times) and len(times) < 2000:
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {'value': round(B / med, 1), 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
+            'sample': f'oracle DDPGLearnerRef.optimize() (torch CPU fp32, {threads} threads) + '
+                      f'random.randint sampling, batch {B} of the C4 workload, {len(times)} timed '
+                      f'steps after 1 warm-up (~{budget_s:.0f} s), median {med * 1e3:.2f} ms'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', choices=['c2', 'c3', 'c5'], default='c3')
+    ap.add_argument('--config', choices=['c2', 'c3', 'c4', 'c5'], default='c3')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
     args = ap.parse_args()
 
+    if args.config == 'c4':
+        return run_ddpg(args)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))

@@ -654,8 +654,11 @@ __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m
   }
 }
 
-template <int MT, int NT, bool VA, bool VB>
-__global__ void __launch_bounds__(kWG, SMI_DWD_OCC)
+// WV waves per workgroup (4: one per SIMD; 8: two per SIMD, each wave takes
+// every WV-th 4-row step of the slab, so a SIMD interleaves two waves' loads
+// and MFMAs; the waves' sums meet in LDS in a fixed tree order)
+template <int MT, int NT, bool VA, bool VB, int WV>
+__global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWD_OCC : 1)
 gemm_dwd_kernel(GemmArgs g) {
   if (g.skip && g.skip[0] != 0) return;
   extern __shared__ float4 dwd_red[];            // 2 x [MT*NT][64] float4
@@ -665,7 +668,8 @@ gemm_dwd_kernel(GemmArgs g) {
   const int m0 = ti.mt * 16 * MT, n0 = ti.nt * 16 * NT;
   const int kb = ti.z * g.kchunk;
   const int ke = min(g.K, kb + g.kchunk);
-  const int nsteps = (ke - kb + 15) >> 4;
+  constexpr int RS = 4 * WV;                      // rows per step of the workgroup
+  const int nsteps = (ke - kb + RS - 1) / RS;
   const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
   const int rw = kb + 4 * wave + lk;              // this lane's row in step 0
   f32x4 acc[MT][NT];
@@ -675,7 +679,7 @@ gemm_dwd_kernel(GemmArgs g) {
     for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   // loads are unconditional (rows past the slab read clamped and zeroed) so
   // the compiler's vmcnt waits stay partial across the unrolled P steps;
-  // slabs are multiples of 16*P rows, only the last one runs zero steps
+  // slabs are multiples of 4*WV*P rows, only the last one runs zero steps
   // NB of the NT column sub-tiles carry data: a tile whose upper 64-column
   // half lies past N (e.g. columns 320..383 of a 301-wide gradient) runs the
   // half-width loop (wave-uniform choice, no loads or MFMAs for that half)
@@ -684,7 +688,7 @@ gemm_dwd_kernel(GemmArgs g) {
     float av[DWD_P][MT], bv[DWD_P][NT];
 #pragma unroll
     for (int p = 0; p < DWD_P; ++p)
-      dwd_load<MT, NT, VA, VB, NB>(g, rw + 16 * p, ke, m0, n0, bdata, av[p], bv[p]);
+      dwd_load<MT, NT, VA, VB, NB>(g, rw + RS * p, ke, m0, n0, bdata, av[p], bv[p]);
     for (int s0 = 0; s0 < nsteps; s0 += DWD_P) {
 #pragma unroll
       for (int p = 0; p < DWD_P; ++p) {
@@ -692,15 +696,15 @@ gemm_dwd_kernel(GemmArgs g) {
         for (int b = 0; b < NB; ++b)
 #pragma unroll
           for (int a = 0; a < MT; ++a) acc[a][b] = mfma4(av[p][a], bv[p][b], acc[a][b]);
-        dwd_load<MT, NT, VA, VB, NB>(g, rw + 16 * (s0 + p + DWD_P), ke, m0, n0, bdata, av[p], bv[p]);
+        dwd_load<MT, NT, VA, VB, NB>(g, rw + RS * (s0 + p + DWD_P), ke, m0, n0, bdata, av[p], bv[p]);
       }
     }
   };
   if (NT == 8 && n0 + 64 >= g.N) mainloop(std::integral_constant<int, (NT > 4 ? 4 : NT)>{});
   else mainloop(std::integral_constant<int, NT>{});
-  // combine the four waves: (w0 + w2) + (w1 + w3)
-  float4* buf0 = dwd_red;
-  float4* buf1 = dwd_red + MT * NT * 64;
+  // combine the waves in a fixed tree: at stride h, waves [h, 2h) add into
+  // waves [0, h), two at a time through the two LDS buffers (WV = 4 gives
+  // (w0 + w2) + (w1 + w3))
   auto put = [&](float4* buf) {
 #pragma unroll
     for (int a = 0; a < MT; ++a)
@@ -719,14 +723,17 @@ gemm_dwd_kernel(GemmArgs g) {
         acc[a][b] += f32x4{v.x, v.y, v.z, v.w};
       }
   };
-  if (wave >= 2) put(wave == 2 ? buf0 : buf1);
-  __syncthreads();
-  if (wave < 2) add(wave == 0 ? buf0 : buf1);
-  __syncthreads();
-  if (wave == 1) put(buf0);
-  __syncthreads();
+#pragma unroll
+  for (int h = WV / 2; h >= 1; h >>= 1) {
+#pragma unroll
+    for (int c = 0; c < h; c += 2) {
+      if (wave >= h + c && wave < h + c + 2) put(dwd_red + (wave - h - c) * MT * NT * 64);
+      __syncthreads();
+      if (wave >= c && wave < c + 2 && wave < h) add(dwd_red + (wave - c) * MT * NT * 64);
+      __syncthreads();
+    }
+  }
   if (wave != 0) return;
-  add(buf0);
   // D(row lk*4+i, col li) of tile (a, b) is dW[m][n] with
   // m = m0 + MT*(lk*4+i) + a, n = n0 + 64*(b/4) + 4*li + b%4
   const bool vec_part = g.part && (g.N & 3) == 0;
@@ -920,13 +927,25 @@ static int use_dwd() {
   return u;
 }
 
-template <int MT, int NT>
+template <int MT, int NT, int WV>
 static void dwd_dispatch(const GemmArgs& g, dim3 grid, bool va, bool vb, hipStream_t st) {
   const size_t lds = (size_t)2 * MT * NT * 64 * sizeof(float4);
-  if (va && vb) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, true, true>), grid, dim3(kWG), lds, st, g);
-  else if (va) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, true, false>), grid, dim3(kWG), lds, st, g);
-  else if (vb) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, false, true>), grid, dim3(kWG), lds, st, g);
-  else hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, false, false>), grid, dim3(kWG), lds, st, g);
+  const dim3 blk(64 * WV);
+  if (va && vb) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, true, true, WV>), grid, blk, lds, st, g);
+  else if (va) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, true, false, WV>), grid, blk, lds, st, g);
+  else if (vb) hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, false, true, WV>), grid, blk, lds, st, g);
+  else hipLaunchKernelGGL((gemm_dwd_kernel<MT, NT, false, false, WV>), grid, blk, lds, st, g);
+}
+
+// waves per dW workgroup (SMI_DWD_WAVES=4|8; measured: 8 waves, two per
+// SIMD, 5-10 % slower per launch and 6 % slower end to end at C3)
+static int dwd_waves() {
+  static int w = 0;
+  if (!w) {
+    const char* e = getenv("SMI_DWD_WAVES");
+    w = (e && atoi(e) == 8) ? 8 : 4;
+  }
+  return w;
 }
 
 static int splitk_reduce(const GemmArgs& g, int S, int epi, hipStream_t st);
@@ -947,7 +966,7 @@ static int dwd_launch(GemmArgs g, hipStream_t st) {
     if (target < 16) target = 16;
   }
   int S = (target + tiles - 1) / tiles;
-  const int smax = (g.K + 127) / 128;               // >= 8 four-row steps per wave
+  const int smax = (g.K + 32 * dwd_waves() - 1) / (32 * dwd_waves());   // >= 8 steps per wave
   if (S > smax) S = smax;
   const int64_t cap = smi_workspace_floats() / ((int64_t)g.M * g.N);
   if (S > cap) S = (int)cap;
@@ -955,7 +974,8 @@ static int dwd_launch(GemmArgs g, hipStream_t st) {
   g.part = nullptr;
   g.kchunk = g.K;
   if (S > 1) {
-    g.kchunk = ((g.K + S - 1) / S + 16 * DWD_P - 1) / (16 * DWD_P) * (16 * DWD_P);
+    const int rs = 4 * dwd_waves() * DWD_P;        // rows per prefetch window
+    g.kchunk = ((g.K + S - 1) / S + rs - 1) / rs * rs;
     S = (g.K + g.kchunk - 1) / g.kchunk;
   }
   if (S > 1) {
@@ -964,10 +984,17 @@ static int dwd_launch(GemmArgs g, hipStream_t st) {
   }
   const dim3 grid(gm, gn, S);
   const int kslot = ktime_begin(st);
-  if (MT == 4 && NT == 8) dwd_dispatch<4, 8>(g, grid, va, vb, st);
-  else if (MT == 4) dwd_dispatch<4, 4>(g, grid, va, vb, st);
-  else if (NT == 8) dwd_dispatch<1, 8>(g, grid, false, vb, st);
-  else dwd_dispatch<1, 4>(g, grid, false, vb, st);
+  if (dwd_waves() == 8) {
+    if (MT == 4 && NT == 8) dwd_dispatch<4, 8, 8>(g, grid, va, vb, st);
+    else if (MT == 4) dwd_dispatch<4, 4, 8>(g, grid, va, vb, st);
+    else if (NT == 8) dwd_dispatch<1, 8, 8>(g, grid, false, vb, st);
+    else dwd_dispatch<1, 4, 8>(g, grid, false, vb, st);
+  } else {
+    if (MT == 4 && NT == 8) dwd_dispatch<4, 8, 4>(g, grid, va, vb, st);
+    else if (MT == 4) dwd_dispatch<4, 4, 4>(g, grid, va, vb, st);
+    else if (NT == 8) dwd_dispatch<1, 8, 4>(g, grid, false, vb, st);
+    else dwd_dispatch<1, 4, 4>(g, grid, false, vb, st);
+  }
   const int nreal = g.ones_col >= 0 ? g.N - 1 : g.N;
   ktime_end(kslot, KT_GEMM_DW,
             2.0 * g.M * (double)nreal * g.K + (g.ones_col >= 0 ? (double)g.M * g.K : 0.0), st);
