@@ -152,7 +152,8 @@ def run_ddpg(args):
     rows[:, D:D + A] = np.tanh(rows[:, D:D + A])
     rows[:, 2 * D + A + 1] = (rows[:, 2 * D + A + 1] > 1.6).astype(np.float32)
     rep.insert_rows(rows)
-    learner = DDPGLearner(lc, ec, seed=1, device=dev)
+    graph = os.environ.get('SMI_DDPG_GRAPH', '1') != '0'
+    learner = DDPGLearner(lc, ec, seed=1, device=dev, use_graph=graph)
     buf = torch.empty(B, rep.width, device=dev)
 
     def step():
@@ -167,10 +168,20 @@ def run_ddpg(args):
         step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # instrumented pass on an eager learner (graph replays carry no per-kernel
+    # events): same launches, same shapes
     n_inst = min(args.steps, 5)
+    learner_e = DDPGLearner(lc, ec, seed=1, device=dev) if graph else learner
+
+    def step_e():
+        _, got = rep.sample(B, out=buf)
+        learner_e.learn(rep.split(got))
+
+    step_e()
+    torch.cuda.synchronize()
     L.kernel_timing(True)
     for _ in range(n_inst):
-        step()
+        step_e()
     torch.cuda.synchronize()
     L.kernel_timing(False)
     kt = L.kernel_timing_report()
@@ -190,7 +201,8 @@ def run_ddpg(args):
         'config': {'workload': 'C4: DDPG learner, batch 512 sampled CPython-exactly from a '
                                '333,333-row replay shard, obs 17, act 6, actor 300x200, critic '
                                '400x300, n_step 3, hard target update',
-                   'batch': B, 'replay_rows': NREP, 'parallelism': 'single'},
+                   'batch': B, 'replay_rows': NREP, 'parallelism': 'single',
+                   'update': 'hipGraph replay' if graph else 'eager launches'},
         'roofline': {'kernel': dom, 'bound': 'mfma', 'achieved': round(ach, 3),
                      'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': round(ach / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,

@@ -277,6 +277,10 @@ gemm_kernel(GemmArgs g) {
         else if (g.act == ACT_TANH) v = tanhf(v);
         g.C[(int64_t)m * g.ldc + n] = v;
       } else if constexpr (EPI == EPI_DX) {
+        if (g.part) {                           // split-K slab: raw sums
+          g.part[((int64_t)ti.z * g.M + m) * g.N + n] = v;
+          continue;
+        }
         if (g.mask) v = g.mask[(int64_t)m * g.ldm + n] > 0.f ? v : 0.f;
         g.C[(int64_t)m * g.ldc + n] = v;
       } else {
@@ -301,7 +305,8 @@ gemm_kernel(GemmArgs g) {
 __global__ void __launch_bounds__(kWG)
 gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, float* C,
                           int64_t ldc, int ones_col, float* bias_out, int accumulate,
-                          const int* skip, const float* bias, int act) {
+                          const int* skip, const float* bias, int act, const float* mask,
+                          int64_t ldm) {
   if (skip && skip[0] != 0) return;
   __shared__ float red[4][64];
   const int64_t MN = (int64_t)M * N;
@@ -325,6 +330,7 @@ gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, f
   if (bias) s += bias[n];                       // split-K forward epilogue
   if (act == ACT_RELU) s = s > 0.f ? s : 0.f;
   else if (act == ACT_TANH) s = tanhf(s);
+  if (mask && !(mask[(int64_t)m * ldm + n] > 0.f)) s = 0.f;   // split-K input gradient
   if (n == ones_col) {
     bias_out[m] = accumulate ? bias_out[m] + s : s;
   } else {
@@ -1181,9 +1187,16 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   int S = 1;
   g.part = nullptr;
   g.kchunk = g.K > 0 ? g.K : 1;
-  // split-K: weight gradients (K = rows), and forwards whose output has too
-  // few tiles to fill the GPU over a long K (the pixel stem's 2592 -> 256 FC)
-  const bool split_fwd = epi == EPI_FWD && gm * gn < 256 && g.K >= 16 * GBK;
+  // split-K: weight gradients (K = rows), and forwards / input gradients whose
+  // output has too few tiles to fill the GPU over K >= 128 (the pixel stem's
+  // 2592 -> 256 FC; DDPG's 512-row layers: 40 tiles, a serial K loop per tile
+  // otherwise; C4 +20 %).  The reducer applies bias/activation or the ReLU mask.
+  static const int fwd_split_min = [] {
+    const char* e = getenv("SMI_FWD_SPLITK_MIN");
+    return e ? atoi(e) : 4 * GBK;
+  }();
+  const bool split_fwd = (epi == EPI_FWD || epi == EPI_DX) && gm * gn < 256 &&
+                         g.K >= fwd_split_min;
   if ((epi == EPI_DW && g.K > 4 * GBK) || split_fwd) {
     const int tiles = gm * gn;
     S = (smi_splitk_target() + tiles - 1) / tiles;    // ~2-4 workgroups per CU
@@ -1225,7 +1238,8 @@ static int splitk_reduce(const GemmArgs& g, int S, int epi, hipStream_t st) {
   const bool fwd = epi == EPI_FWD;
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, g.part, S, g.M, g.N,
                      g.C, g.ldc, g.ones_col, g.bias_out, g.accumulate, g.skip,
-                     fwd ? g.bias : nullptr, fwd ? g.act : ACT_NONE);
+                     fwd ? g.bias : nullptr, fwd ? g.act : ACT_NONE,
+                     epi == EPI_DX ? g.mask : nullptr, g.ldm);
   ktime_end(rslot, KT_GEMM_REDUCE, (double)S * MN, st);
   return check_launch("gemm_splitk_reduce_kernel");
 }
@@ -1236,7 +1250,7 @@ int launch_slab_reduce(const float* part, int S, int64_t n, float* out, hipStrea
   if (n < 1 || S < 1) return SMI_OK;
   const int rg = (int)((n + 63) / 64);
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, part, S, 1, (int)n, out,
-                     n, -1, nullptr, 0, skip, nullptr, ACT_NONE);
+                     n, -1, nullptr, 0, skip, nullptr, ACT_NONE, nullptr, 0);
   return check_launch("gemm_splitk_reduce_kernel");
 }
 

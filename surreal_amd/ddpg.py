@@ -170,7 +170,7 @@ class DDPGLearner(object):
     """ddpg.py:12-440 on MI355X (low-dim, no layernorm)."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
-                 device=None, seed=0):
+                 device=None, seed=0, use_graph=False):
         L.require_gpu()
         self.learner_config = lc = learner_config if isinstance(learner_config, Config) else Config(learner_config)
         self.env_config = ec = env_config if isinstance(env_config, Config) else Config(env_config)
@@ -231,6 +231,12 @@ class DDPGLearner(object):
         self.stats_buf = torch.zeros(12, dtype=torch.float32, device=dev)
         self._bufs = {}
         self.kernel_events = None
+        # hipGraph replay of the update (learn() -> _optimize_graphed); the TD3
+        # smoothing noise is a fresh host draw per step, so that option stays eager
+        self.use_graph = bool(use_graph) and not (self.use_double_critic and
+                                                  self.use_action_regularization)
+        self._graph = None
+        self._gin = None
 
     # ------------------------------------------------------------ helpers
     def _hard_update(self):
@@ -260,7 +266,8 @@ class DDPGLearner(object):
         return Config(out)
 
     # --------------------------------------------------------- _optimize
-    def _optimize(self, obs, actions, rewards, obs_next, done):          # ddpg.py:244-352
+    def _optimize(self, obs, actions, rewards, obs_next, done,           # ddpg.py:244-352
+                  target_update=True):
         B = obs.shape[0]
         st = L.stream(self.device)
         net = _Net(self.model, self._bufs)
@@ -323,7 +330,8 @@ class DDPGLearner(object):
         # statistics (ddpg.py:335-345)
         L.call('smi_ddpg_stats', _p(actions), actions.stride(0), A, _p(rewards), rs, _p(y), _p(q), 1,
                B, _p(self.stats_buf[2:6]), st)
-        self._target_update()
+        if target_update:
+            self._target_update()
 
     def _critic_backward(self, net, crit, obs, B, dq, pre, g, st, need_obs_grad):
         """Backward through CriticNetworkX.  With g: weight grads into g (flat).
@@ -402,9 +410,43 @@ class DDPGLearner(object):
         obs = obs['low_dim']['flat_inputs'] if isinstance(obs, dict) else obs
         obs_next = batch['obs_next']
         obs_next = obs_next['low_dim']['flat_inputs'] if isinstance(obs_next, dict) else obs_next
-        self._optimize(obs, batch['actions'], batch['rewards'], obs_next, batch['dones'])
+        ins = (obs, batch['actions'], batch['rewards'], obs_next, batch['dones'])
+        if self.use_graph:
+            self._optimize_graphed(*ins)
+        else:
+            self._optimize(*ins)
         if self.metrics is not None:
             self.metrics(self.last_stats(), self.current_iteration)
+
+    def _optimize_graphed(self, obs, actions, rewards, obs_next, done):
+        """One _optimize as a hipGraph replay (the step is ~40 small launches at
+        batch 512, so host launch overhead, not the GPU, bounds it).  The first
+        call runs eagerly (it is that call's update, and it sizes every scratch
+        buffer), then captures the same launch sequence over static input
+        buffers; later calls copy their inputs in (skipped when the caller
+        already wrote them: graph_inputs()) and replay.  The target update stays
+        on the host, where its interval counter lives (ddpg.py:403-428)."""
+        ins = (obs, actions, rewards, obs_next, done)
+        if self._graph is None:
+            self._optimize(*ins)
+            self._gin = [torch.zeros(tuple(t.shape), dtype=torch.float32, device=self.device)
+                         for t in ins]
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._optimize(*self._gin, target_update=False)
+            self._graph = g
+            return
+        for s, t in zip(self._gin, ins):
+            if s.data_ptr() != t.data_ptr():
+                s.copy_(t)
+        self._graph.replay()
+        self._target_update()
+
+    def graph_inputs(self):
+        """Static (obs, actions, rewards, obs_next, dones) buffers of the captured
+        step (None before the first learn() in graph mode)."""
+        return None if self._gin is None else dict(zip(
+            ('obs', 'actions', 'rewards', 'obs_next', 'dones'), self._gin))
 
     def last_stats(self):
         v = self.stats_buf.cpu().numpy()
