@@ -152,7 +152,7 @@ def run_ddpg(args):
     rows[:, D:D + A] = np.tanh(rows[:, D:D + A])
     rows[:, 2 * D + A + 1] = (rows[:, 2 * D + A + 1] > 1.6).astype(np.float32)
     rep.insert_rows(rows)
-    graph = os.environ.get('SMI_DDPG_GRAPH', '1') != '0'
+    graph = os.environ.get('SMI_DDPG_GRAPH', '0') == '1'      # measured neutral: GPU-bound
     learner = DDPGLearner(lc, ec, seed=1, device=dev, use_graph=graph)
     buf = torch.empty(B, rep.width, device=dev)
 
