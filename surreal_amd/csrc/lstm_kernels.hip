@@ -640,28 +640,36 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
   }
   __syncthreads();
   LSTM_T0();
+  // x_t W_ih^T does not depend on h_{t-1}: its MFMAs for step t+1 are issued
+  // right after step t's pre-activations are published, so the matrix pipe
+  // works through them while the same waves run the cell update (VALU /
+  // transcendentals / stores).  Same chains, same k order as issuing them at
+  // the top of step t+1: bit-identical results.
+  f32x4 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto x_part = [&](int tt) {
+    if constexpr (KX > 0) {
+      const float4* xr4 = reinterpret_cast<const float4*>(xS[tt & 1] + (lane & 3) * KXS);
+#pragma unroll
+      for (int k8 = 0; k8 < KX / 8; ++k8) {
+        const float4 u = xr4[2 * k8], v = xr4[2 * k8 + 1];
+        acc[0] = mfma4x64(u.x, wx[8 * k8 + 0], acc[0]);
+        acc[1] = mfma4x64(u.y, wx[8 * k8 + 1], acc[1]);
+        acc[2] = mfma4x64(u.z, wx[8 * k8 + 2], acc[2]);
+        acc[3] = mfma4x64(u.w, wx[8 * k8 + 3], acc[3]);
+        acc[4] = mfma4x64(v.x, wx[8 * k8 + 4], acc[4]);
+        acc[5] = mfma4x64(v.y, wx[8 * k8 + 5], acc[5]);
+        acc[6] = mfma4x64(v.z, wx[8 * k8 + 6], acc[6]);
+        acc[7] = mfma4x64(v.w, wx[8 * k8 + 7], acc[7]);
+      }
+    }
+  };
+  if (cact && a.S > 0) x_part(0);
   for (int t = 0; t < a.S; ++t) {
     const float* hp = hS[t & 1];
     float* hn = hS[(t + 1) & 1];
     if (cact) {
-      f32x4 acc[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (KX > 0) {
-        const float4* xr4 = reinterpret_cast<const float4*>(xS[t & 1] + (lane & 3) * KXS);
-#pragma unroll
-        for (int k8 = 0; k8 < KX / 8; ++k8) {
-          const float4 u = xr4[2 * k8], v = xr4[2 * k8 + 1];
-          acc[0] = mfma4x64(u.x, wx[8 * k8 + 0], acc[0]);
-          acc[1] = mfma4x64(u.y, wx[8 * k8 + 1], acc[1]);
-          acc[2] = mfma4x64(u.z, wx[8 * k8 + 2], acc[2]);
-          acc[3] = mfma4x64(u.w, wx[8 * k8 + 3], acc[3]);
-          acc[4] = mfma4x64(v.x, wx[8 * k8 + 4], acc[4]);
-          acc[5] = mfma4x64(v.y, wx[8 * k8 + 5], acc[5]);
-          acc[6] = mfma4x64(v.z, wx[8 * k8 + 6], acc[6]);
-          acc[7] = mfma4x64(v.w, wx[8 * k8 + 7], acc[7]);
-        }
-      }
       const float4* hr = reinterpret_cast<const float4*>(hp + (lane & 3) * KP);
 #pragma unroll
       for (int k8 = 0; k8 < KP / 8; ++k8) {
@@ -692,6 +700,11 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
     }
     LSTM_TICK(0);
     __syncthreads();
+    if (cact) {               // next step's chains: x_{t+1} part now (see above)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t + 1 < a.S) x_part(t + 1);
+    }
     if (cell) {
       const float ig = sigm(pre[crow][cunit]), fg = sigm(pre[crow][H + cunit]);
       const float cg = ftanh(pre[crow][2 * H + cunit]), og = sigm(pre[crow][3 * H + cunit]);
