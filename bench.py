@@ -79,6 +79,37 @@ def make_config(name):
     return lc, gym_env_config(42, 8), dict(D=42, A=8, rnn_hidden=100)
 
 
+# kernel class (smi_kernel_timing) -> kernel-name patterns of its launches
+CLASS_KERNELS = {
+    'gemm_dw': ('gemm_dwd_kernel', 'gemm_dw128_kernel', 'gemm_kernel<2,'),
+    'gemm_fwd': ('gemm_panel_kernel<0,', 'gemm_kernel<0,', 'gemm_smallk_fwd_kernel'),
+    'gemm_dx': ('gemm_panel_kernel<1,', 'gemm_kernel<1,', 'dx_smallk_kernel'),
+    'lstm_fwd': ('lstm_fwd',), 'lstm_bwd': ('lstm_bwd',),
+    'cnn_fwd': ('cnn_fwd_kernel',), 'cnn_bwd': ('cnn_bwd_kernel',),
+}
+PMC_TRAFFIC = {'c3': 'profiles/r01/pmc_traffic_c3_final5.json',
+               'c5': 'profiles/r01/pmc_traffic_c5_final5.json'}
+
+
+def pmc_traffic(config, cls):
+    """HBM bytes per launch of a kernel class from the committed PMC passes of
+    this bench command (tools/pmc_bench.sh -> tools/pmc_traffic.py: FETCH_SIZE
+    x2 + WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), launch-weighted over the
+    class's kernels; None when no such profile exists."""
+    path = os.path.join(ROOT, PMC_TRAFFIC.get(config, ''))
+    pats = CLASS_KERNELS.get(cls)
+    if not pats or not os.path.isfile(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    n = b = 0
+    for name, v in d.items():
+        if any(p in name for p in pats) and v.get('launches'):
+            n += v['launches']
+            b += v['launches'] * v['hbm_bytes_per_launch']
+    return (round(b / n) if n else None), os.path.relpath(path, ROOT)
+
+
 def mlp_flops_per_row(d, h1, h2, o):
     fwd = 2 * (d * h1 + h1 * h2 + h2 * o)
     bwd = fwd + 2 * (h1 * h2 + h2 * o)        # dW of all layers + dX of layers 2, 3
@@ -336,10 +367,14 @@ def main():
         dom = max(kt, key=lambda n: kt[n][1])
         c, ms, fl = kt[dom]
         ach = fl / (ms * 1e-3) / 1e12
+        traffic, tsrc = pmc_traffic(args.config, dom)
         roof = {'kernel': dom, 'bound': 'mfma', 'achieved': round(ach, 3),
                 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                'traffic': None, 'avg_ms': round(ms / c, 5),
+                'traffic': traffic, 'avg_ms': round(ms / c, 5),
                 'algorithmic_flops_per_launch': int(fl / c)}
+        if traffic is not None:
+            roof['traffic_unit'] = 'HBM bytes per launch'
+            roof['traffic_source'] = tsrc + ' (PMC passes of this command, launch-weighted over the class)'
     else:
         # C2: the fused single-CU epoch kernel dominates
         kdur = {n: float(np.mean([s.elapsed_time(e) for s, e in v])) for n, v in ev.items()}

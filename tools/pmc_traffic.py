@@ -1,7 +1,7 @@
 """Per-kernel HBM traffic per launch from tools/pmc_bench.sh's two PMC passes.
 FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B,
 MI355X_MICROARCH.md "HBM"); WRITE_SIZE as is.  Counters are in KB.
-Usage: python tools/pmc_traffic.py [gpurun_out] > profiles/.../pmc_traffic.json"""
+Usage: python tools/pmc_traffic.py [gpurun_out] [cfg] > profiles/.../pmc_traffic_<cfg>.json"""
 import collections
 import csv
 import glob
@@ -22,9 +22,9 @@ def load(d, counter):
     return acc
 
 
-def main(root):
-    fe = load(os.path.join(root, 'pmc_bench_fetch'), 'FETCH_SIZE')
-    wr = load(os.path.join(root, 'pmc_bench_write'), 'WRITE_SIZE')
+def main(root, cfg):
+    fe = load(os.path.join(root, f'pmc_{cfg}_fetch'), 'FETCH_SIZE')
+    wr = load(os.path.join(root, f'pmc_{cfg}_write'), 'WRITE_SIZE')
     out = {}
     for k in sorted(set(fe) | set(wr)):
         f, nf = fe.get(k, (0.0, 0))
@@ -37,4 +37,4 @@ def main(root):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1] if len(sys.argv) > 1 else 'gpurun_out')
+    main(sys.argv[1] if len(sys.argv) > 1 else 'gpurun_out', sys.argv[2] if len(sys.argv) > 2 else 'c3')
