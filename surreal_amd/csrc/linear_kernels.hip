@@ -1074,7 +1074,7 @@ static int panel_launch(int epi, const GemmArgs& g, hipStream_t st) {
 // chain from 0 (for K = 1 bit-identical to the tiled path).  A thread owns 4
 // consecutive columns of 4 rows (the W slice in registers, 16-byte mask reads
 // and stores, coalesced along the row).  SMI_DX_SMALLK=0 disables it.
-template <int KK, bool V4>
+template <int KK, bool V4, bool A4 = false>
 __global__ void __launch_bounds__(kWG)
 dx_smallk_kernel(GemmArgs g) {
   if (g.skip && g.skip[0] != 0) return;
@@ -1101,13 +1101,23 @@ dx_smallk_kernel(GemmArgs g) {
     const int m = mg * RW + r;
     if (m >= g.M) break;
     const float* arow = g.A + (int64_t)m * g.a_rs;
+    float av[KK];
+    if (KK % 4 == 0 && A4) {                       // K == KK: 16-byte row loads
+#pragma unroll
+      for (int q = 0; q < KK / 4; ++q) {
+        const float4 x = reinterpret_cast<const float4*>(arow)[q];
+        av[4 * q] = x.x; av[4 * q + 1] = x.y; av[4 * q + 2] = x.z; av[4 * q + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KK; ++k) av[k] = k < g.K ? arow[k] : 0.f;
+    }
     float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < KK; ++k) {
       if (k >= g.K) break;
-      const float ak = arow[k];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) v[t] = fmaf(ak, w[k][t], v[t]);
+      for (int t = 0; t < 4; ++t) v[t] = fmaf(av[k], w[k][t], v[t]);
     }
     const float* mrow = g.mask ? g.mask + (int64_t)m * g.ldm + n0 : nullptr;
     float* crow = g.C + (int64_t)m * g.ldc + n0;
@@ -1149,8 +1159,10 @@ static int dx_smallk_launch(const GemmArgs& g, hipStream_t st) {
     if (v4) hipLaunchKernelGGL((dx_smallk_kernel<KK, true>), grid, dim3(kWG), 0, st, g);   \
     else hipLaunchKernelGGL((dx_smallk_kernel<KK, false>), grid, dim3(kWG), 0, st, g);     \
   } while (0)
+  const bool a4 = (g.K == 4 || g.K == 8) && g.a_rs % 4 == 0 && al16(g.A);
   if (g.K == 1) SMI_DXS(1);
   else if (g.K <= 2) SMI_DXS(2);
+  else if (g.K == 8 && a4 && v4) hipLaunchKernelGGL((dx_smallk_kernel<8, true, true>), grid, dim3(kWG), 0, st, g);
   else if (g.K <= 4) SMI_DXS(4);
   else SMI_DXS(8);
 #undef SMI_DXS

@@ -167,12 +167,13 @@ __global__ void __launch_bounds__(kWG)
 reduce_partials_kernel(const double* __restrict__ part, int nb, int w, double* out,
                        const int* skip) {
   if (skip && skip[0] != 0) return;
-  __shared__ double scr[kNW];
-  for (int j = 0; j < w; ++j) {
+  // one wave per column (fixed lane-strided order + butterfly): no barriers
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int j = wave; j < w; j += kNW) {
     double s = 0.0;
-    for (int i = threadIdx.x; i < nb; i += kWG) s += part[(int64_t)i * w + j];
-    s = block_sum_d(s, scr);
-    if (threadIdx.x == 0) out[j] = s;
+    for (int i = lane; i < nb; i += 64) s += part[(int64_t)i * w + j];
+    s = wave_sum_d(s);
+    if (lane == 0) out[j] = s;
   }
 }
 
@@ -361,10 +362,13 @@ policy_rows_grad_kernel(PolRowArgs a) {
 __global__ void logvar_grad_kernel(const float* __restrict__ lvpart, int nb, int A,
                                    const float* lv, float* g, const int* skip) {
   if (skip && skip[0] != 0) return;
-  for (int j = threadIdx.x; j < A; j += blockDim.x) {
+  // one wave per log_var entry (fixed lane-strided order + butterfly)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int j = wave; j < A; j += nw) {
     float s = 0.f;
-    for (int i = 0; i < nb; ++i) s += lvpart[(int64_t)i * A + j];
-    g[j] = s * expf(lv[j]);
+    for (int i = lane; i < nb; i += 64) s += lvpart[(int64_t)i * A + j];
+    s = wave_sum(s);
+    if (lane == 0) g[j] = s * expf(lv[j]);
   }
 }
 
@@ -883,7 +887,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       hipLaunchKernelGGL(policy_rows_grad_kernel, dim3(nb), dim3(kWG), 0, st, p);
       RC(check_launch("policy_rows_grad_kernel"));
       RC(stem_backward(a, d, actor, lm, cnn, gA, s, d.nA_head, st, stop));
-      hipLaunchKernelGGL(logvar_grad_kernel, dim3(1), dim3(64), 0, st, s.lvpart, nb, d.A,
+      hipLaunchKernelGGL(logvar_grad_kernel, dim3(1), dim3(kWG), 0, st, s.lvpart, nb, d.A,
                          a.actor + d.LA.flv, gA + d.LA.flv, stop);
       return check_launch("logvar_grad_kernel");
     }
