@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(kWG)
 policy_rows_stats_kernel(PolRowArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   __shared__ float sig[32], lsig[32], rsig[32];
-  __shared__ double scr[kNW];
+  __shared__ double scr[kNW][PS_N];
   const int A = a.A;
   for (int j = threadIdx.x; j < A; j += kWG) {
     sig[j] = expf(a.lv[j]);                 // builders.py:127 std = exp(log_var)
@@ -276,10 +276,19 @@ policy_rows_stats_kernel(PolRowArgs a) {
     acc[PS_RBD] += (double)dg_row_kl(rm, rsig, bp, bp + A, A);
     acc[PS_RET] += (double)a.ret[(int64_t)b * a.E + t];
   }
+  // all PS_N sums at once: wave butterflies, one barrier, fixed wave order
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < PS_N; ++k) {
-    const double s = block_sum_d(acc[k], scr);
-    if (threadIdx.x == 0) a.part[(int64_t)blockIdx.x * PS_N + k] = s;
+    const double v = wave_sum_d(acc[k]);
+    if (lane == 0) scr[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < PS_N) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) t += scr[w][threadIdx.x];
+    a.part[(int64_t)blockIdx.x * PS_N + threadIdx.x] = t;
   }
 }
 
