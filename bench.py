@@ -163,46 +163,59 @@ def run_ddpg(args):
     HalfCheetah dims (obs 17, act 6), actor 300x200, critic 400x300, n_step 3,
     fed by UniformReplay over a 333,333-row shard resident in HBM.  A step =
     one CPython-exact index draw (MT19937 kernel) + row gather + learn().
-    Single GPU (SURVEY §8(e) DDPG sharding is not built; --gpus > 1 refused)."""
-    if int(os.environ.get('WORLD_SIZE', '1')) > 1:
-        raise SystemExit('bench.py --config c4: single GPU only')
+    With WORLD_SIZE > 1 (SURVEY §8(e) DDPG row): every rank holds its own
+    333,333-row shard, samples 512 rows per step from it, and the gradients are
+    averaged over the ranks (DDPGLearner dp=TorchDistAllReduce): weak scaling,
+    value = ranks x 512 x steps / max-over-ranks time."""
+    dist, world, rank, _ = init_dist()
     from surreal_amd import _lib as L
     from surreal_amd.config import DDPG_DEFAULT_LEARNER_CONFIG, gym_env_config
     from surreal_amd.ddpg import DDPGLearner
+    from surreal_amd.learner import TorchDistAllReduce
     from surreal_amd.replay import UniformReplay
-    torch.cuda.set_device(0)
-    dev = torch.device('cuda', 0)
+    dev = torch.device('cuda', torch.cuda.current_device())
     D, A, B, NREP = 17, 6, 512, 333333
     lc = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
     lc.replay.batch_size = B
     lc.replay.memory_size = NREP
     lc.replay.sampling_start_size = 1000
     ec = gym_env_config(D, A)
-    rep = UniformReplay(lc, ec, seed=0, device=dev)
-    rows = np.random.RandomState(0).randn(NREP, rep.width).astype(np.float32)
+    rep = UniformReplay(lc, ec, seed=rank, device=dev)
+    rows = np.random.RandomState(rank).randn(NREP, rep.width).astype(np.float32)
     rows[:, D:D + A] = np.tanh(rows[:, D:D + A])
     rows[:, 2 * D + A + 1] = (rows[:, 2 * D + A + 1] > 1.6).astype(np.float32)
     rep.insert_rows(rows)
-    graph = os.environ.get('SMI_DDPG_GRAPH', '0') == '1'      # measured neutral: GPU-bound
-    learner = DDPGLearner(lc, ec, seed=1, device=dev, use_graph=graph)
+    graph = os.environ.get('SMI_DDPG_GRAPH', '0') == '1' and dist is None  # measured neutral
+    dp = TorchDistAllReduce() if dist is not None else None
+    learner = DDPGLearner(lc, ec, seed=1, device=dev, use_graph=graph, dp=dp)
     buf = torch.empty(B, rep.width, device=dev)
 
     def step():
         _, got = rep.sample(B, out=buf)
         learner.learn(rep.split(got))
 
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    barrier()
     elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     # instrumented pass on an eager learner (graph replays carry no per-kernel
     # events): same launches, same shapes
     n_inst = min(args.steps, 5)
-    learner_e = DDPGLearner(lc, ec, seed=1, device=dev) if graph else learner
+    learner_e = DDPGLearner(lc, ec, seed=1, device=dev, dp=dp) if graph else learner
 
     def step_e():
         _, got = rep.sample(B, out=buf)
@@ -224,15 +237,16 @@ def run_ddpg(args):
     c, ms_k, fl = kt[dom]
     ach = fl / (ms_k * 1e-3) / 1e12
     out = {
-        'metric': DDPG_METRIC, 'value': round(B * args.steps / elapsed, 1), 'unit': 'env-steps/s',
-        'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
+        'metric': DDPG_METRIC, 'value': round(world * B * args.steps / elapsed, 1),
+        'unit': 'env-steps/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
         'data': 'synthetic replay rows (seeded); random-init weights of the named architecture',
         'config': {'workload': 'C4: DDPG learner, batch 512 sampled CPython-exactly from a '
                                '333,333-row replay shard, obs 17, act 6, actor 300x200, critic '
                                '400x300, n_step 3, hard target update',
-                   'batch': B, 'replay_rows': NREP, 'parallelism': 'single',
+                   'batch': B, 'replay_rows': NREP,
+                   'parallelism': f'dp{world}' if world > 1 else 'single',
                    'update': 'hipGraph replay' if graph else 'eager launches'},
         'roofline': {'kernel': dom, 'bound': 'mfma', 'achieved': round(ach, 3),
                      'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
@@ -240,7 +254,12 @@ def run_ddpg(args):
                      'avg_ms': round(ms_k / c, 5), 'algorithmic_flops_per_launch': int(fl / c)},
         'kernels': kernels,
     }
-    if not args.no_cpu_baseline:
+    if dist is not None:
+        barrier()
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+    if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline_ddpg(lc, rows, D, A, B, args.cpu_budget)
     print(json.dumps(out), flush=True)
 
@@ -276,18 +295,9 @@ def cpu_baseline_ddpg(lc, rows, D, A, B, budget_s=12.0):
                       f'steps after 1 warm-up (~{budget_s:.0f} s), median {med * 1e3:.2f} ms'}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', choices=['c2', 'c3', 'c4', 'c5'], default='c3')
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-budget', type=float, default=12.0)
-    args = ap.parse_args()
-
-    if args.config == 'c4':
-        return run_ddpg(args)
+def init_dist():
+    """One process per GPU (RANK/LOCAL_RANK/WORLD_SIZE from the launcher).
+    Returns (dist or None, world, rank, device)."""
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
@@ -307,7 +317,22 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device('cuda', torch.cuda.current_device())
+    return dist, world, rank, dev
 
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', choices=['c2', 'c3', 'c4', 'c5'], default='c3')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-budget', type=float, default=12.0)
+    args = ap.parse_args()
+
+    if args.config == 'c4':
+        return run_ddpg(args)
+    dist, world, rank, dev = init_dist()
     from surreal_amd import _lib as L
     from surreal_amd import synthetic
     from surreal_amd.learner import PPOLearner, TorchDistAllReduce

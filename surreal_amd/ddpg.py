@@ -170,8 +170,16 @@ class DDPGLearner(object):
     """ddpg.py:12-440 on MI355X (low-dim, no layernorm)."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
-                 device=None, seed=0, use_graph=False):
+                 device=None, seed=0, use_graph=False, dp=None):
+        """dp: None (one GPU) or a data-parallel group exposing `world_size`,
+        `rank` and `allreduce_(tensor)` (in-place SUM, stream-ordered), e.g.
+        learner.TorchDistAllReduce() over RCCL (SURVEY §8(e) DDPG row).  Each rank
+        passes its own `replay.batch_size` rows; every gradient is averaged over
+        the ranks before clip + Adam, which equals the reference's mean loss on
+        the concatenated global batch (equal shards).  Initial weights are
+        seed-identical, so parameters stay replicated."""
         L.require_gpu()
+        self.dp = dp if dp is not None and dp.world_size > 1 else None
         self.learner_config = lc = learner_config if isinstance(learner_config, Config) else Config(learner_config)
         self.env_config = ec = env_config if isinstance(env_config, Config) else Config(env_config)
         self.session_config = session_config
@@ -233,8 +241,8 @@ class DDPGLearner(object):
         self.kernel_events = None
         # hipGraph replay of the update (learn() -> _optimize_graphed); the TD3
         # smoothing noise is a fresh host draw per step, so that option stays eager
-        self.use_graph = bool(use_graph) and not (self.use_double_critic and
-                                                  self.use_action_regularization)
+        self.use_graph = bool(use_graph) and self.dp is None and not (
+            self.use_double_critic and self.use_action_regularization)
         self._graph = None
         self._gin = None
 
@@ -246,8 +254,15 @@ class DDPGLearner(object):
             if self.use_double_critic:
                 self.model_target2.critic.flat.copy_(self.model2.critic.flat)
 
+    def _dp_mean_(self, t):
+        """Average a per-rank gradient / statistics buffer over the ranks."""
+        if self.dp is not None:
+            self.dp.allreduce_(t)
+            t.mul_(1.0 / self.dp.world_size)
+
     def _adam(self, name, flat, clip_value, st):
         o = self.opt[name]
+        self._dp_mean_(o['g'])
         L.call('smi_adam_clip', _p(flat), _p(o['g']), _p(o['m']), _p(o['v']), flat.numel(),
                _p(o['step']), _p(o['lr']), 0.9, 0.999, 1e-8, o['wd'], 0.0, float(clip_value),
                None, None, st)
@@ -285,8 +300,11 @@ class DDPGLearner(object):
             # the twin target sees it (next_Q_target was computed before the noise)
             a_t2 = a_t
             if self.use_action_regularization:
-                noise = np.clip(np.random.normal(0, 0.2, size=(self.batch_size, self.action_dim)),
-                                -0.5, 0.5)
+                # data parallel: every rank draws the global batch's noise from
+                # the same stream and keeps its own rows
+                W, r = (self.dp.world_size, self.dp.rank) if self.dp is not None else (1, 0)
+                noise = np.clip(np.random.normal(0, 0.2, size=(self.batch_size * W, self.action_dim)),
+                                -0.5, 0.5)[r * self.batch_size:(r + 1) * self.batch_size]
                 a_t2 = (a_t + torch.tensor(noise, dtype=torch.float32).to(self.device)).clamp(-1, 1)
             q_t2 = tnet.critic_fwd(self.model_target2.critic, obs_next, a_t2.contiguous(), B,
                                    store='t2c')
@@ -330,6 +348,7 @@ class DDPGLearner(object):
         # statistics (ddpg.py:335-345)
         L.call('smi_ddpg_stats', _p(actions), actions.stride(0), A, _p(rewards), rs, _p(y), _p(q), 1,
                B, _p(self.stats_buf[2:6]), st)
+        self._dp_mean_(self.stats_buf)                  # shard means -> global means
         if target_update:
             self._target_update()
 
