@@ -230,6 +230,9 @@ typedef struct smi_ppo_args {
   int64_t B_global;            /* rows over all ranks (0: = B)         */
   float* xbuf;                 /* exchange buffer, smi_ppo_xbuf_floats */
   int* dp_state;               /* [4] zeroed by the caller per learn()  */
+  /* optional (NULL: not written): the advantages exactly as the policy epochs
+     use them (normalised on device when norm_adv, ppo.py:413-416), [B] */
+  float* adv_out;
 } smi_ppo_args;
 
 /* device hyper-parameter slots (float) */
@@ -377,6 +380,10 @@ typedef struct smi_ppo_rnn_args {
   int pix_c, pix_h, pix_w, cnn_feat;
   const uint8_t* pixels;        /* [B][T][C][H][W] uint8 (obs['pixel']['camera0'])      */
   const uint8_t* pixels_next;   /* [B][1][C][H][W] uint8 (obs_next['pixel']['camera0']) */
+  /* optional (NULL: not written), filled by PREP: the windowed advantages as the
+     policy epochs use them (normalised over all B_global*E windows when
+     norm_adv, ppo.py:402-405) and the returns, both [B][E] batch-major */
+  float* adv_out; float* ret_out;
 } smi_ppo_rnn_args;
 
 #define SMI_RNN_PSTAT 16

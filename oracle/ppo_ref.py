@@ -167,7 +167,7 @@ class ActorRef(nn.Module):
         if high:
             obs = obs.reshape(-1, shape[2])
         mean = self.model(obs)
-        std = torch.exp(self.log_var) * torch.ones(mean.size())
+        std = torch.exp(self.log_var) * torch.ones_like(mean)
         out = torch.cat((mean, std), dim=1)
         if high:
             out = out.reshape(shape[0], shape[1], -1)
@@ -244,7 +244,9 @@ class PPOModelRef(nn.Module):
             parts.append(self.z_filter.forward(x) if self.use_z_filter else x)
         if pix is not None:                                 # ppo_net.py:268-273, 368-375
             lead = pix.shape[:-3]
-            img = pix.reshape(-1, *pix.shape[-3:]) / 255.0
+            img = pix.reshape(-1, *pix.shape[-3:])
+            dt = self.actor.log_var.dtype
+            img = img / 255.0 if dt == torch.float32 else img.to(dt) / 255.0
             parts.append(self.cnn_stem(img).reshape(*lead, -1))
         x = parts[0] if len(parts) == 1 else torch.cat(parts, -1)
         if self.rnn:
@@ -299,9 +301,13 @@ def _tmap2(f, a, b):
 
 
 # ---------------------------------------------------------------------- GAE
-def gae_and_return(values, rewards, dones, gamma, lam, n_step, horizon, rnn, norm_adv):
+def gae_and_return(values, rewards, dones, gamma, lam, n_step, horizon, rnn, norm_adv,
+                   raw_out=None):
     """ppo.py:371-418 given the critic values (B, T+1).  Returns (adv, ret).
-    `values` is masked in place (values[:,1:] *= 1 - dones, ppo.py:387)."""
+    `values` is masked in place (values[:,1:] *= 1 - dones, ppo.py:387).  The
+    gamma / lambda tables are the reference's fp32 torch.pow tables whatever the
+    dtype of `values` (fp64 runs of the oracle keep the reference's constants).
+    raw_out: optional list that receives the advantages before normalisation."""
     idx = torch.tensor(range(n_step), dtype=torch.float32)
     g = torch.pow(gamma, idx)
     lm = torch.pow(lam, idx)
@@ -311,11 +317,13 @@ def gae_and_return(values, rewards, dones, gamma, lam, n_step, horizon, rnn, nor
         eff_len = n_step - horizon + 1
         g, lm = g[:horizon], lm[:horizon]
         B = values.shape[0]
-        ret = torch.zeros(B, eff_len)
-        adv = torch.zeros(B, eff_len)
+        ret = torch.zeros(B, eff_len, dtype=values.dtype)
+        adv = torch.zeros(B, eff_len, dtype=values.dtype)
         for s in range(eff_len):
             ret[:, s] = torch.sum(g * rewards[:, s:s + horizon], 1) + values[:, s + horizon] * (gamma ** horizon)
             adv[:, s] = torch.sum(tds[:, s:s + horizon] * g * lm, 1)
+        if raw_out is not None:
+            raw_out.append(adv.clone())
         if norm_adv:
             std, mean = adv.std(), adv.mean()
             adv = (adv - mean) / max(std, 1e-4)
@@ -323,6 +331,8 @@ def gae_and_return(values, rewards, dones, gamma, lam, n_step, horizon, rnn, nor
     ret = torch.sum(g * rewards, 1) + values[:, -1] * (gamma ** n_step)   # :409
     tds = rewards + gamma * values[:, 1:] - values[:, :-1]               # :410
     gae = torch.sum(tds * g * lm, 1)                                       # :411
+    if raw_out is not None:
+        raw_out.append(gae.clone())
     if norm_adv:                                                           # :413-416
         std, mean = gae.std(), gae.mean()
         gae = (gae - mean) / max(std, 1e-4)
@@ -340,9 +350,11 @@ class PPOLearnerRef:
 
     `lc` is a learner_config tree with the reference's keys (the product's
     surreal_amd.config.Config works).  obs are low-dim tensors (B, T, D).
+    dtype=torch.float64 runs the same algorithm in double precision: the
+    "truth" the parity tests measure both fp32 implementations against.
     """
 
-    def __init__(self, lc, obs_dim, act_dim, seed=0, pixel=None):
+    def __init__(self, lc, obs_dim, act_dim, seed=0, pixel=None, dtype=torch.float32):
         torch.manual_seed(seed)
         g = lambda p, d=None: cfg_get(lc, p, d)  # noqa: E731
         self.gamma = g('algo.gamma')
@@ -377,8 +389,9 @@ class PPOLearnerRef:
             obs_dim, act_dim, g('model.actor_fc_hidden_sizes'), g('model.critic_fc_hidden_sizes'),
             g('algo.consts.init_log_sig'), self.use_z_filter, self.rnn,
             g('algo.rnn.rnn_hidden'), g('algo.rnn.rnn_layer'), pixel, g('model.cnn_feature_dim', 256))
-        self.model = mk()
-        self.ref_target_model = mk()
+        self.dtype = dtype
+        self.model = mk().to(dtype)
+        self.ref_target_model = mk().to(dtype)
         self.ref_target_model.update_target_params(self.model)
         self.critic_optim = torch.optim.Adam(self.model.critic_params(), lr=g('algo.network.lr_critic'),
                                              weight_decay=g('algo.network.critic_regularization'))
@@ -389,7 +402,7 @@ class PPOLearnerRef:
         self.kl_record = []
         self.exp_counter = 0
         if self.use_r_filter:
-            self.reward_filter = RewardFilterRef()
+            self.reward_filter = RewardFilterRef().to(dtype)
 
     # -- losses -------------------------------------------------------------
     def _clip_loss(self, obs, actions, adv, behave_pol):     # ppo.py:194-225
@@ -458,12 +471,24 @@ class PPOLearnerRef:
             x = _tmap(lambda o: o.reshape(-1, *o.shape[2:]), x)
         values = self.model.forward_critic(x, self.cells).detach()
         values = values.view(B, self.n_step + 1)
-        return gae_and_return(values, rewards, dones, self.gamma, self.lam, self.n_step,
-                              self.horizon, self.rnn, self.norm_adv)
+        raw = []
+        out = gae_and_return(values, rewards, dones, self.gamma, self.lam, self.n_step,
+                             self.horizon, self.rnn, self.norm_adv, raw_out=raw)
+        self.last_adv_raw = raw[0]
+        return out
+
+    def _as_input(self, a):
+        """The reference's FloatTensor conversion of a batch array (ppo.py:420-484):
+        rounded to fp32, then held in the oracle's dtype.  A torch float64 tensor
+        handed to an fp64 oracle is taken as exact (the parity tests' perturbed
+        executions)."""
+        if isinstance(a, torch.Tensor) and a.dtype == torch.float64 and self.dtype == torch.float64:
+            return a
+        return torch.as_tensor(a, dtype=torch.float32).to(self.dtype)
 
     # -- preprocess (ppo.py:420-484, rewards part) ----------------------------
     def preprocess_rewards(self, rewards):
-        rewards = torch.as_tensor(rewards, dtype=torch.float32) * self.reward_scale
+        rewards = self._as_input(rewards) * self.reward_scale
         if self.use_r_filter:
             normed = self.reward_filter.forward(rewards)
             self.reward_filter.update(rewards)
@@ -524,19 +549,19 @@ class PPOLearnerRef:
         return stats
 
     def learn(self, batch):                                   # ppo.py:588-613
-        f32 = lambda a: None if a is None else torch.as_tensor(a, dtype=torch.float32)  # noqa: E731
+        f32 = lambda a: None if a is None else self._as_input(a)  # noqa: E731
         obs = f32(batch['obs'])
         obs_next = f32(batch['obs_next'])
         if 'pixels' in batch:                 # (low_dim or None, camera0 uint8)
             obs = (obs, torch.as_tensor(batch['pixels']))
             obs_next = (obs_next, torch.as_tensor(batch['pixels_next']))
-        actions = torch.as_tensor(batch['actions'], dtype=torch.float32)
+        actions = f32(batch['actions'])
         rewards = self.preprocess_rewards(batch['rewards'])
-        dones = torch.as_tensor(batch['dones'], dtype=torch.float32)
-        pds = torch.as_tensor(batch['pds'], dtype=torch.float32)
+        dones = f32(batch['dones'])
+        pds = f32(batch['pds'])
         onetime = None
         if batch.get('onetime') is not None:
-            onetime = [torch.as_tensor(x, dtype=torch.float32) for x in batch['onetime']]
+            onetime = [f32(x) for x in batch['onetime']]
         stats = self.optimize(obs, actions, rewards, obs_next, pds, onetime, dones)
         self.exp_counter += self.batch_size
         return stats

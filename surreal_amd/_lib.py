@@ -53,6 +53,7 @@ class PPOArgs(ctypes.Structure):
         ('stats', P),
         ('kl_record', P), ('kl_count', P), ('kl_capacity', c_int),
         ('B_global', c_i64), ('xbuf', P), ('dp_state', P),
+        ('adv_out', P),
     ]
 
 
@@ -84,6 +85,7 @@ class RNNArgs(ctypes.Structure):
         ('scratch', P), ('scratch_bytes', c_i64),
         ('pix_c', c_int), ('pix_h', c_int), ('pix_w', c_int), ('cnn_feat', c_int),
         ('pixels', P), ('pixels_next', P),
+        ('adv_out', P), ('ret_out', P),
     ]
 
 

@@ -3,8 +3,8 @@ surreal/learner/aggregator.py: MultistepAggregatorWithInfo (:106-262) for PPO
 and SSARAggregator (:33-103) + FrameStackPreprocessor (:11-31) for DDPG.
 
 Output dictionaries carry the same keys, shapes and dtypes as the reference.
-`stage()` additionally packs an aggregated PPO batch into pinned host buffers
-so the learner issues one async H2D copy per array.
+`StagingArena` packs an aggregated batch into one pinned host buffer and moves
+it to the device with a single async H2D copy.
 """
 import collections
 
@@ -128,43 +128,105 @@ class MultistepAggregatorWithInfo(object):
         return onetime, pers
 
 
-def stage(batch, device, pinned_cache=None):
-    """Pinned-memory staging of an aggregated PPO batch + async H2D copies.
+class StagingArena(object):
+    """Learner-side staging of an aggregated batch (SURVEY.md §8(f) rank 2;
+    the reference converts array by array with torch.tensor, ppo.py:420-484,
+    after LearnerDataPrefetcher hands the batch over, data_fetcher.py:53-58).
 
-    Returns the same nested structure with float32 device tensors.  The copies
-    are enqueued on the current stream (non_blocking) so learn() can follow
-    without a host sync."""
-    cache = pinned_cache if pinned_cache is not None else {}
+    Every array of the batch is packed (converted to float32, camera frames kept
+    uint8) into ONE pinned host buffer at 256-byte aligned offsets, and the
+    whole buffer goes to the device in ONE async H2D copy on the current
+    stream; the returned tensors are views into the device buffer.  Two slots
+    alternate, so packing batch k+1 overlaps the copy / learn() of batch k; a
+    slot's host side is reused only after its previous copy has completed (an
+    event), and its device side is overwritten by a copy that is stream-ordered
+    after every kernel that read it."""
 
-    def put(key, arr):
-        if arr is None:
-            return None
-        # camera observations stay uint8 (4x fewer bytes over PCIe; the conv
-        # kernel applies the /255 of ppo_net.py:368-375)
-        u8 = isinstance(key, tuple) and len(key) == 3 and key[1] == 'pixel'
-        dt, ndt = (torch.uint8, np.uint8) if u8 else (torch.float32, np.float32)
-        if isinstance(arr, torch.Tensor):
-            return arr.to(device=device, dtype=dt, non_blocking=True)
-        a = np.ascontiguousarray(arr, dtype=ndt)
-        ent = cache.get(key)
-        if ent is None or tuple(ent[0].shape) != a.shape:
-            ent = [torch.empty(a.shape, dtype=dt).pin_memory(), torch.cuda.Event()]
-            cache[key] = ent
-        else:
-            ent[1].synchronize()          # the previous async copy out of this buffer is done
-        ent[0].numpy()[...] = a
-        dev = ent[0].to(device=device, non_blocking=True)
-        ent[1].record()
-        return dev
+    ALIGN = 256
 
-    out = {}
-    for name in ('obs', 'obs_next'):
-        out[name] = {m: {k: put((name, m, k), v) for k, v in d.items()}
-                     for m, d in batch[name].items()}
-    for name in ('actions', 'rewards', 'dones'):
-        out[name] = put(name, batch[name])
-    pi = batch.get('persistent_infos')
-    out['persistent_infos'] = None if pi is None else [put(('pi', i), x) for i, x in enumerate(pi)]
-    oi = batch.get('onetime_infos')
-    out['onetime_infos'] = None if oi is None else [put(('oi', i), x) for i, x in enumerate(oi)]
-    return out
+    def __init__(self, device, slots=2):
+        self.device = torch.device(device)
+        self.slots = [None] * slots
+        self.next = 0
+
+    @staticmethod
+    def _leaves(batch):
+        out = []
+
+        def walk(path, v):
+            if v is None:
+                return
+            if isinstance(v, dict):
+                for k in v:
+                    walk(path + (k,), v[k])
+            elif isinstance(v, (list, tuple)):
+                for i, x in enumerate(v):
+                    walk(path + (i,), x)
+            else:
+                out.append((path, v))
+        for name in ('obs', 'obs_next', 'actions', 'rewards', 'dones', 'persistent_infos',
+                     'onetime_infos'):
+            walk((name,), batch.get(name))
+        return out
+
+    @staticmethod
+    def _is_pixel(path):
+        return len(path) == 3 and path[0] in ('obs', 'obs_next') and path[1] == 'pixel'
+
+    def stage(self, batch):
+        leaves = self._leaves(batch)
+        layout, off = [], 0
+        for path, v in leaves:
+            dt = np.uint8 if self._is_pixel(path) else np.float32
+            shape = tuple(v.shape)
+            n = int(np.prod(shape)) * np.dtype(dt).itemsize
+            layout.append((path, shape, dt, off, n))
+            off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        total = max(off, self.ALIGN)
+        key = tuple((p, s, d) for p, s, d, _, _ in layout)
+        slot = self.slots[self.next]
+        if slot is None or slot['key'] != key:
+            slot = {'key': key, 'host': torch.empty(total, dtype=torch.uint8).pin_memory(),
+                    'dev': torch.empty(total, dtype=torch.uint8, device=self.device),
+                    'event': None}
+            self.slots[self.next] = slot
+        elif slot['event'] is not None:
+            slot['event'].synchronize()       # this host buffer's previous copy is done
+        self.next = (self.next + 1) % len(self.slots)
+        hbytes = slot['host'].numpy()
+        for (path, v), (_, shape, dt, o, n) in zip(leaves, layout):
+            dst = hbytes[o:o + n].view(dt).reshape(shape)
+            src = v.numpy() if isinstance(v, torch.Tensor) else v
+            np.copyto(dst, src, casting='unsafe')
+        slot['dev'].copy_(slot['host'], non_blocking=True)        # the single H2D
+        ev = torch.cuda.Event()
+        ev.record()
+        slot['event'] = ev
+        views = {}
+        for path, shape, dt, o, n in layout:
+            t = slot['dev'][o:o + n].view(torch.uint8 if dt == np.uint8 else torch.float32)
+            views[path] = t.view(shape)
+        return self._rebuild(batch, views)
+
+    @staticmethod
+    def _rebuild(batch, views):
+        def build(path, v):
+            if v is None:
+                return None
+            if isinstance(v, dict):
+                return {k: build(path + (k,), v[k]) for k in v}
+            if isinstance(v, (list, tuple)):
+                return [build(path + (i,), x) for i, x in enumerate(v)]
+            return views[path]
+        out = dict(batch)
+        for name in ('obs', 'obs_next', 'actions', 'rewards', 'dones', 'persistent_infos',
+                     'onetime_infos'):
+            out[name] = build((name,), batch.get(name))
+        return out
+
+
+def stage(batch, device, arena=None):
+    """Stage an aggregated (host numpy) PPO batch on `device` through a
+    StagingArena (one pinned buffer, one async H2D on the current stream)."""
+    arena = arena if arena is not None else StagingArena(device)
+    return arena.stage(batch)

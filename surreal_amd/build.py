@@ -37,7 +37,9 @@ def _mtime(p):
 VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             'noinl_prof': ['-DSMI_DENSE_NOINLINE', '-DSMI_PROF'],
             # dW-kernel experiments (tools/dwd_exp.sh)
-            'p8': ['-DSMI_DWD_P=8'], 'p6': ['-DSMI_DWD_P=6'], 'occ1': ['-DSMI_DWD_OCC=1']}
+            'p8': ['-DSMI_DWD_P=8'], 'p6': ['-DSMI_DWD_P=6'], 'occ1': ['-DSMI_DWD_OCC=1'],
+            # LSTM activation A/B (the pre-round-2 cancelling tanh)
+            'oldtanh': ['-DSMI_OLD_TANH']}
 
 
 def lib_path(variant=None):
@@ -50,16 +52,23 @@ def build(verbose=False, force=False, variant=None):
     os.makedirs(build_dir, exist_ok=True)
     deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'surreal_mi.h')]
     dep_t = max(_mtime(d) for d in deps)
-    objs = []
+    objs, cmds = [], []
     for src in SOURCES:
         sp = os.path.join(CSRC, src)
         op = os.path.join(build_dir, src.replace('.hip', '.o'))
         objs.append(op)
         if force or _mtime(op) < max(_mtime(sp), dep_t):
-            cmd = [HIPCC] + CXXFLAGS + VARIANTS[variant] + ['-c', sp, '-o', op]
-            if verbose:
-                print(' '.join(cmd), flush=True)
-            subprocess.run(cmd, check=True)
+            cmds.append([HIPCC] + CXXFLAGS + VARIANTS[variant] + ['-c', sp, '-o', op])
+    # one hipcc per source, run side by side (each is single-threaded)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(cmds), int(os.environ.get('MAX_JOBS', os.cpu_count() or 1))))
+
+    def run(cmd):
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(run, cmds))
     if force or _mtime(lib) < max(_mtime(o) for o in objs):
         tl = torch_lib_dir()
         cmd = ['g++', '-shared', '-o', lib] + objs + [

@@ -54,9 +54,16 @@ __host__ __device__ inline int lstm_ld(int k) {
 }
 
 // Activations on the hardware transcendental units (v_exp_f32, v_rcp_f32: ~1
-// ulp each): sigmoid(x) = 1/(1 + 2^(-x log2 e)), tanh(x) = 2 sigmoid(2x) - 1.
-// Absolute error ~1e-7 (fp32 rounding level of the gate values); the libm
-// forms cost ~4x the VALU issue slots and made the sequence kernels VALU-bound.
+// ulp each).  sigmoid(x) = 1/(1 + 2^(-x log2 e)): a few ulp RELATIVE everywhere
+// (no cancellation).  tanh must also be accurate RELATIVE to its value: the
+// earlier 2 sigmoid(2x) - 1 form cancelled for small |x| (absolute error ~1e-7,
+// i.e. 1e-4 relative at |x| ~ 1e-3), which made the LSTM outputs near zero
+// ~1000x noisier than torch's and showed up as divergence from the fp64 oracle
+// after 10 + 10 epochs (tests/test_gpu_parity_pinned.py).  Now: odd minimax
+// polynomial for |x| < 0.625 (Cephes tanhf coefficients, ~2e-7 relative),
+// 1 - 2/(e^{2|x|} + 1) beyond (no cancellation there: the result is >= 0.55).
+// The libm forms cost ~4x the VALU issue slots and made the sequence kernels
+// VALU-bound; these stay on the transcendental units plus ~6 FMAs.
 // k-order of the register kernels: lane group lk (= lane >> 4) owns the
 // contiguous quarter k = lk*KS + s, s < KS, of the (padded) K range, so the A
 // operand of 4 consecutive k-steps is one 16-byte LDS read (the MFMA only needs
@@ -66,7 +73,19 @@ __host__ __device__ inline int lstm_q(int K) { return (((K + 3) >> 2) + 3) & ~3;
 __device__ __forceinline__ float sigm(float x) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
 }
+#ifdef SMI_OLD_TANH
 __device__ __forceinline__ float ftanh(float x) { return 2.f * sigm(2.f * x) - 1.f; }
+#else
+__device__ __forceinline__ float ftanh(float x) {
+  const float ax = fabsf(x);
+  const float z = x * x;
+  const float p = fmaf(fmaf(fmaf(fmaf(fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f), z,
+                                      -5.37397155531e-2f), z, 1.33314422036e-1f), z,
+                            -3.33332819422e-1f), z * x, x);
+  const float e = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(2.8853900817779268f * ax));
+  return ax < 0.625f ? p : copysignf(e, x);
+}
+#endif
 
 struct LstmFwdArgs {
   const float* xproj;     // [S][B][4H] = x W_ih^T + b_ih

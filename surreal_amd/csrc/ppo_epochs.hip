@@ -282,6 +282,7 @@ SMI_INL void policy_prologue(FusedCtx& c) {
       float v = 0.f;
       if (r < B) v = a.norm_adv ? (a.adv_raw[r] - mean_f) / denom : a.adv_raw[r];
       c.adv[r] = v;
+      if (a.adv_out && r < B) a.adv_out[r] = v;
     }
   }
   __syncthreads();

@@ -231,6 +231,17 @@ __device__ inline float norm_adv_of(const PolRowArgs& a, float raw) {
   return (raw - (float)mean) / fmaxf(sd, 1e-4f);
 }
 
+// optional export of the advantages as the epochs use them and the returns,
+// both [B][E] batch-major (smi_ppo_rnn_args.adv_out / ret_out)
+__global__ void __launch_bounds__(kWG)
+adv_export_kernel(PolRowArgs a, float* __restrict__ adv_out, float* __restrict__ ret_out) {
+  const int64_t n = (int64_t)a.B * a.E;
+  for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < n; e += (int64_t)gridDim.x * kWG) {
+    if (adv_out) adv_out[e] = norm_adv_of(a, a.adv[e]);
+    if (ret_out) ret_out[e] = a.ret[e];
+  }
+}
+
 // forward statistics of the policy over the E*B rows (ppo.py:203-224,
 // 262-284, 553-575)
 __global__ void __launch_bounds__(kWG)
@@ -864,6 +875,11 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
         RC(check_launch("zf_tmajor_kernel"));
         RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, s, st, nullptr));
         X = s.Xr;
+      }
+      if (a.adv_out || a.ret_out) {
+        hipLaunchKernelGGL(adv_export_kernel, dim3(grid_of(d.NE)), dim3(kWG), 0, st,
+                           pol_rows(a, d, s), a.adv_out, a.ret_out);
+        RC(check_launch("adv_export_kernel"));
       }
       const LstmP lr = lstm_params(a.ref_lstm, d.Din, d.H);
       if (d.H > 0) RC(lstm_forward(d, lr, X, d.E, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
-from .aggregator import MultistepAggregatorWithInfo, SSARAggregator, stage
+from .aggregator import MultistepAggregatorWithInfo, SSARAggregator, StagingArena
 from .config import Config, ConfigError
 from .model import DiagGauss, PPOModel, RewardFilter
 
@@ -207,10 +207,13 @@ class PPOLearner(object):
         self.gamma_tab = torch.pow(self.gamma, idx).to(dev)        # ppo.py:372-374
         self.lam_tab = torch.pow(self.lam, idx).to(dev)
         self._bufs = {}
-        self._pinned = {}
+        self._arena = StagingArena(self.device)
         self._args = L.PPOArgs()
         # optional per-kernel HIP event timing: {kernel name: [(start, end), ...]}
         self.kernel_events = None
+        # optional export of the advantages as the policy epochs use them (and
+        # the RNN window returns) into self._bufs['adv_used'] / ['ret_used']
+        self.export_advantages = False
 
     def _ev(self, name):
         """Context for recording a (start, end) event pair around one launch."""
@@ -260,7 +263,7 @@ class PPOLearner(object):
     # ------------------------------------------------------- reference API
     def _preprocess_batch_ppo(self, batch):                 # ppo.py:420-484
         if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
-            batch = stage(batch, self.device, self._pinned)
+            batch = self._arena.stage(batch)          # one pinned buffer, one H2D
         else:
             batch = dict(batch)
         rewards = batch['rewards'].to(torch.float32).contiguous().clone()   # filtered in place
@@ -352,6 +355,7 @@ class PPOLearner(object):
         a.kl_record, a.kl_count, a.kl_capacity = (self.kl_record_buf.data_ptr(),
                                                   self.kl_count.data_ptr(), self.kl_capacity)
         self._last_ret = ret
+        a.adv_out = self._buf('adv_used', (B,)).data_ptr() if self.export_advantages else None
         maxp = L.lib().smi_ppo_fused_max_params()
         fused = dp is None and max(L.lib().smi_mlp_param_count(D, a_h1, a_h2, A, 1),
                                    L.lib().smi_mlp_param_count(D, c_h1, c_h2, 1, 0)) <= maxp
@@ -495,6 +499,9 @@ class PPOLearner(object):
         a.moments, a.pstat, a.xbuf, a.zbuf = (moments.data_ptr(), pstat.data_ptr(),
                                               xbuf.data_ptr(), zbuf.data_ptr())
         a.scratch, a.scratch_bytes = scratch.data_ptr(), nbytes
+        E = T - H + 1
+        a.adv_out = self._buf('adv_used', (B, E)).data_ptr() if self.export_advantages else None
+        a.ret_out = self._buf('ret_used', (B, E)).data_ptr() if self.export_advantages else None
         self._rnn_args = a
 
         def ph(p, e=0):

@@ -9,9 +9,10 @@ surreal/model/ppo_net.py:137-152) on the HIP kernels vs the CPU oracle.
   multiple of 16), and the real C3 layer sizes (D 42, LSTM 100, heads 300x200,
   A 8, T 25, horizon 5) at 128 segments.  Tolerances as test_gpu_ppo.py
   (1e-5 relative with the tensor-scale floor; Adam sign flips bounded).
-* Full C3 batch (1024 segments): finite, deterministic (two learners with the
-  same seed are bit-identical), and the windowed GAE of the RNN branch checked
-  on sampled segments against the oracle given the same critic values.
+* Full C3 batch (1024 segments): finite and deterministic (two learners with
+  the same seed are bit-identical).  Its parity with the oracle — advantages,
+  returns, statistics and post-step parameters after 10 + 10 epochs, against
+  the fp64 oracle — is tests/test_gpu_parity_pinned.py.
 """
 import numpy as np
 import pytest
@@ -166,27 +167,6 @@ def test_rnn_learn_c3_layer_sizes_matches_oracle(mode):
     rep = _run_rnn(mode, B=128, T=25, H=5, D=42, A=8, Hd=100, hidden=(300, 200), iters=1,
                    epochs=(1, 1))
     print('rnn C3-dims parity:', rep)
-
-
-def test_rnn_learn_c3_layer_sizes_statistics_ten_epochs():
-    B, T, H, D, A, Hd = 128, 25, 5, 42, 8, 100
-    lc = _rnn_cfg('adapt', B, T, H, Hd, (300, 200))
-    learner = PPOLearner(lc, env_config(D, A), seed=5)
-    ref = R.PPOLearnerRef(lc, D, A)
-    copy_weights_to_oracle(learner, ref)
-    batch = synthetic.ppo_batch(B, T, D, A, seed=11, rnn_hidden=Hd)
-    rstats = ref.learn(oracle_batch(batch))
-    learner.learn(synthetic.to_device(batch, DEV))
-    stats = learner.last_stats()
-    assert stats['epochs_run'] == rstats['epochs_run']
-    for k in ('_surr_loss', '_entropy', '_pol_kl', '_val_loss', '_avg_return_targ',
-              '_avg_is_weight', '_ref_behave_diff', 'grad_norm_actor', 'grad_norm_critic',
-              '_avg_log_sig', '_kl_loss_adapt'):
-        assert abs(stats[k] - rstats[k]) <= 1e-3 * abs(rstats[k]) + 1e-6, (k, stats[k], rstats[k])
-    for got, exp in ((learner.model.actor.flat.cpu(), ref.model.actor.flat()),
-                     (learner.model.critic.flat.cpu(), ref.model.critic.flat()),
-                     (learner.model.rnn_stem.flat.cpu(), lstm_flat(ref.model.rnn_stem))):
-        assert float((got - exp).abs().max()) <= 2 * 3e-4 * 20     # |dp| <= 2 lr updates
 
 
 def test_rnn_full_c3_batch_deterministic_and_finite():
