@@ -8,17 +8,20 @@ device-side KL early stop, the value epochs, z_update).
 over 2/4/8 GPUs"): the reference PPO defaults — LSTM policy
 (rnn_hidden 100, horizon 5), heads 300x200, n_step 25, adapt mode, z-filter —
 with robosuite SawyerLift state dims (obs 42, act 8; SURVEY §8 notes 42 is an
-assumption) and 1024 segments per learn() on each GPU.
---config c2 (BASELINE configs[1]): HalfCheetah dims, 64x64 MLP, 64 x 50.
+assumption): 1024 segments per learn() in total, split over the GPUs
+(--scaling strong, the default; --scaling weak keeps 1024 per GPU).
+--config c2 (BASELINE configs[1]): HalfCheetah dims, 64x64 MLP, 64 x 50 per GPU.
 --config c5 (BASELINE configs[4]): C3 plus the pixel stem — camera0
-3x84x84 uint8 -> conv 16@8s4 -> 32@4s2 -> FC 256, LSTM input 42 + 256 — at
-128 segments per GPU (the 1024-segment batch over 8 GPUs).
+3x84x84 uint8 -> conv 16@8s4 -> 32@4s2 -> FC 256, LSTM input 42 + 256 — the
+same 1024 segments split over the GPUs.
+--config c4 (BASELINE configs[3]): the DDPG learner (see run_ddpg).
 
-With --gpus N the learner is data parallel: each rank holds its
-own batch shard and the ranks all-reduce advantage moments, per-epoch
-gradients/statistics and the ZFilter sums over RCCL (torch.distributed
-'nccl') — every rank applies the update of the global batch.  Per-GPU work is
-fixed (weak scaling): the global batch is N x the per-GPU batch.
+With --gpus N the learner is data parallel: one process per GPU
+(launched by torch.distributed.run, or spawned by this script when no launcher
+set WORLD_SIZE), each rank holds its shard of the segments and the ranks
+all-reduce advantage moments, per-epoch gradients/statistics and the ZFilter
+sums over RCCL (torch.distributed 'nccl'); every rank applies the update of the
+global batch.
 
 Prints ONE JSON line on rank 0: the metric (timed region = K plain learn()
 calls, no instrumentation), a roofline object for the dominant kernel
@@ -47,6 +50,8 @@ HBM_PEAK_GBS = 8000.0
 
 
 def make_config(name):
+    """(learner_config, env_config, dims) of a bench workload; dims['B_global']
+    is the workload's segment count (the global batch under --scaling strong)."""
     from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, gym_env_config, pixel_env_config
     lc = copy.deepcopy(PPO_DEFAULT_LEARNER_CONFIG)
     if name == 'c2':
@@ -59,7 +64,7 @@ def make_config(name):
         lc.algo.ppo_mode = 'adapt'
         lc.algo.rnn.if_rnn_policy = False
         lc.replay.batch_size = 64
-        return lc, gym_env_config(17, 6), dict(D=17, A=6, rnn_hidden=None)
+        return lc, gym_env_config(17, 6), dict(D=17, A=6, rnn_hidden=None, B_global=64)
     # c3: the reference defaults (ppo_configs.py:15-94) + z-filter on
     lc.model.actor_fc_hidden_sizes = [300, 200]
     lc.model.critic_fc_hidden_sizes = [300, 200]
@@ -72,11 +77,25 @@ def make_config(name):
     lc.algo.rnn.horizon = 5
     lc.replay.batch_size = 1024
     if name == 'c5':
-        lc.replay.batch_size = 128
         lc.model.cnn_feature_dim = 256
         return lc, pixel_env_config(42, 8, (3, 84, 84)), dict(D=42, A=8, rnn_hidden=100,
-                                                               pixel=(3, 84, 84))
-    return lc, gym_env_config(42, 8), dict(D=42, A=8, rnn_hidden=100)
+                                                               pixel=(3, 84, 84), B_global=1024)
+    return lc, gym_env_config(42, 8), dict(D=42, A=8, rnn_hidden=100, B_global=1024)
+
+
+def spawn_ranks(n):
+    """bench.py --gpus N without a launcher: run N ranks under
+    torch.distributed.run as a CHILD process (this parent has made no GPU call:
+    torch is imported, nothing initialised) and exit with its code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(('127.0.0.1', 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 # kernel class (smi_kernel_timing) -> kernel-name patterns of its launches
@@ -110,49 +129,143 @@ def pmc_traffic(config, cls):
     return (round(b / n) if n else None), os.path.relpath(path, ROOT)
 
 
+MFMA_CLASSES = ('gemm_fwd', 'gemm_dx', 'gemm_dw', 'lstm_fwd', 'lstm_bwd', 'cnn_fwd', 'cnn_bwd')
+
+
+def kernel_table(kt, n_inst):
+    """per-class launches / time per step and achieved TFLOP/s (MFMA classes)
+    or GB/s (HBM-bound classes, whose work unit is algorithmic bytes)"""
+    from surreal_amd import _lib as L
+    out = {}
+    for n, (c, ms, w) in kt.items():
+        row = {'launches_per_step': round(c / n_inst, 2), 'avg_ms': round(ms / c, 5),
+               'ms_per_step': round(ms / n_inst, 4)}
+        if n in L.KT_BYTES:
+            gbs = w / (ms * 1e-3) / 1e9
+            row.update({'GBps': round(gbs, 1), 'hbm_frac': round(gbs / HBM_PEAK_GBS, 4),
+                        'bytes_per_launch': int(w / c)})
+        elif n == 'gemm_splitk_reduce':
+            row['note'] = 'split-K partial reducer (memory-bound; work counted = elements reduced)'
+        else:
+            row['tflops'] = round(w / (ms * 1e-3) / 1e12, 3)
+        out[n] = row
+    return out
+
+
+def mfma_dominant(kt):
+    """the MFMA kernel class with the most time (roofline.kernel)"""
+    cands = [n for n in kt if n in MFMA_CLASSES]
+    return max(cands, key=lambda n: kt[n][1]) if cands else None
+
+
+def roofline_hbm(kt, n_inst):
+    """'% HBM roofline' of the streaming kernels inside the benched learn():
+    algorithmic bytes per launch / measured launch time vs 8 TB/s.  At C3 these
+    working sets are cache-resident (<= 10 MB), so the in-workload fraction is
+    bounded by launch latency, not by HBM; tools/bench_hbm.py sweeps the same
+    kernels over > 256 MB working sets."""
+    from surreal_amd import _lib as L
+    rows = {}
+    for n, (c, ms, w) in kt.items():
+        if n not in L.KT_BYTES:
+            continue
+        gbs = w / (ms * 1e-3) / 1e9
+        rows[n] = {'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                   'frac': round(gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': int(w / c),
+                   'avg_us': round(ms / c * 1e3, 2), 'launches_per_step': round(c / n_inst, 2)}
+    if not rows:
+        return None
+    tot_b = sum(kt[n][2] for n in rows)
+    tot_ms = sum(kt[n][1] for n in rows)
+    agg = tot_b / (tot_ms * 1e-3) / 1e9
+    return {'kernels': rows, 'aggregate': {'achieved': round(agg, 1), 'unit': 'GB/s',
+                                           'frac': round(agg / HBM_PEAK_GBS, 4),
+                                           'ms_per_step': round(tot_ms / n_inst, 4)},
+            'note': 'in-workload (cache-resident at these batch sizes); > 256 MB sweeps: '
+                    'tools/bench_hbm.py, profiles/'}
+
+
 def mlp_flops_per_row(d, h1, h2, o):
     fwd = 2 * (d * h1 + h1 * h2 + h2 * o)
     bwd = fwd + 2 * (h1 * h2 + h2 * o)        # dW of all layers + dX of layers 2, 3
     return fwd, bwd
 
 
-def cpu_baseline(name, lc, dims, budget_s=12.0):
-    """The oracle's PPOLearnerRef.learn() (torch CPU fp32) on a bounded sample:
-    C2 = the full 64-segment batch; C3 = a 128-segment slice of the batch
-    (learner throughput in env-steps/s is batch-size independent on CPU at these
-    sizes), one warm-up call then as many timed calls as fit the budget."""
-    from oracle import ppo_ref as R
-    from surreal_amd import synthetic
-    from tests.helpers import oracle_batch
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    lc = copy.deepcopy(lc)
-    if name == 'c3':
-        lc.replay.batch_size = 128
-    if name == 'c5':
-        lc.replay.batch_size = 8
-    B, T = lc.replay.batch_size, lc.algo.n_step
-    D, A = dims['D'], dims['A']
-    ref = R.PPOLearnerRef(lc, D, A, pixel=dims.get('pixel'))
-    batches = [oracle_batch(synthetic.ppo_batch(B, T, D, A, seed=i, rnn_hidden=dims['rnn_hidden'],
-                                                pixel=dims.get('pixel')))
-               for i in range(2)]
-    ref.learn(batches[1])
+def cpu_model():
+    """The host CPU model (lscpu 'Model name', read from /proc/cpuinfo)."""
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def host_threads():
+    """Threads the CPU baseline uses: this process's CPU share (OMP_NUM_THREADS
+    on the GPU box, where os.cpu_count() reports the whole machine)."""
+    env = os.environ.get('OMP_NUM_THREADS')
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _time_oracle(ref, batches, budget_s, max_calls=200):
+    ref.learn(batches[-1])                                 # warm-up
     times = []
     t_end = time.perf_counter() + budget_s
     i = 0
-    while time.perf_counter() < t_end or len(times) < 1:
+    while (time.perf_counter() < t_end or not times) and len(times) < max_calls:
         t0 = time.perf_counter()
-        ref.learn(batches[i % 2])
+        ref.learn(batches[i % len(batches)])
         times.append(time.perf_counter() - t0)
         i += 1
-        if len(times) >= 200:
-            break
-    med = statistics.median(times)
-    return {'value': round(B * T / med, 1), 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
+    return statistics.median(times), len(times)
+
+
+def cpu_baseline(name, lc, dims, budget_s=12.0, one_thread_budget_s=6.0):
+    """The oracle's PPOLearnerRef.learn() (torch CPU fp32) timed on this host:
+    with all the process's threads on the full benched batch (C3: 1024
+    segments; C2: 64; C5: a 16-segment slice — the fp32 pixel stem costs ~0.25
+    s per segment on the CPU), plus a 1-thread figure on a 64-segment slice (8
+    for C5).  Learner env-steps/s on the CPU is close to batch-size independent
+    at these sizes; each sample is stated."""
+    from oracle import ppo_ref as R
+    from surreal_amd import synthetic
+    from tests.helpers import oracle_batch
+    D, A = dims['D'], dims['A']
+    T = lc.algo.n_step
+
+    def make(B):
+        c = copy.deepcopy(lc)
+        c.replay.batch_size = B
+        ref = R.PPOLearnerRef(c, D, A, pixel=dims.get('pixel'))
+        bs = [oracle_batch(synthetic.ppo_batch(B, T, D, A, seed=i, rnn_hidden=dims['rnn_hidden'],
+                                                pixel=dims.get('pixel'))) for i in range(2)]
+        return ref, bs
+    threads = host_threads()
+    B_all = {'c5': 16}.get(name, dims['B_global'])
+    torch.set_num_threads(threads)
+    ref, bs = make(B_all)
+    med, n = _time_oracle(ref, bs, budget_s)
+    B_one = 8 if name == 'c5' else min(64, B_all)
+    torch.set_num_threads(1)
+    ref1, bs1 = make(B_one)
+    med1, n1 = _time_oracle(ref1, bs1, one_thread_budget_s, max_calls=20)
+    torch.set_num_threads(threads)
+    return {'value': round(B_all * T / med, 1), 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
+            'cpu_model': cpu_model(), 'os_cpu_count': os.cpu_count(),
             'sample': f'oracle PPOLearnerRef.learn() (torch CPU fp32, {threads} threads) on a '
-                      f'{B}-segment x {T}-step batch of the {name.upper()} workload, {len(times)} '
-                      f'timed calls after 1 warm-up (~{budget_s:.0f} s), median {med * 1e3:.1f} ms'}
+                      f'{B_all}-segment x {T}-step batch of the {name.upper()} workload, {n} timed '
+                      f'calls after 1 warm-up (~{budget_s:.0f} s budget), median {med * 1e3:.1f} ms',
+            'value_1thread': round(B_one * T / med1, 1),
+            'sample_1thread': f'same learn() on 1 thread, {B_one}-segment slice, {n1} timed calls, '
+                              f'median {med1 * 1e3:.1f} ms'}
 
 
 DDPG_METRIC = 'DDPG learner env-steps/sec (replay sample + n-step target + critic/actor update)'
@@ -229,11 +342,8 @@ def run_ddpg(args):
     torch.cuda.synchronize()
     L.kernel_timing(False)
     kt = L.kernel_timing_report()
-    kernels = {n: {'launches_per_step': round(c / n_inst, 2), 'avg_ms': round(ms / c, 5),
-                   'ms_per_step': round(ms / n_inst, 4),
-                   'tflops': round(fl / (ms * 1e-3) / 1e12, 3)}
-               for n, (c, ms, fl) in kt.items()}
-    dom = max(kt, key=lambda n: kt[n][1])
+    kernels = kernel_table(kt, n_inst)
+    dom = mfma_dominant(kt)
     c, ms_k, fl = kt[dom]
     ach = fl / (ms_k * 1e-3) / 1e12
     out = {
@@ -269,7 +379,7 @@ def cpu_baseline_ddpg(lc, rows, D, A, B, budget_s=12.0):
     random.randint index draws over the same replay rows, timed per step."""
     import random
     from oracle import ddpg_ref as R
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
     ref = R.DDPGLearnerRef(lc, D, A)
     table = torch.from_numpy(rows)
@@ -290,6 +400,7 @@ def cpu_baseline_ddpg(lc, rows, D, A, B, budget_s=12.0):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {'value': round(B / med, 1), 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
+            'cpu_model': cpu_model(), 'os_cpu_count': os.cpu_count(),
             'sample': f'oracle DDPGLearnerRef.optimize() (torch CPU fp32, {threads} threads) + '
                       f'random.randint sampling, batch {B} of the C4 workload, {len(times)} timed '
                       f'steps after 1 warm-up (~{budget_s:.0f} s), median {med * 1e3:.2f} ms'}
@@ -328,8 +439,18 @@ def main():
     ap.add_argument('--config', choices=['c2', 'c3', 'c4', 'c5'], default='c3')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
+    ap.add_argument('--scaling', choices=['strong', 'weak'], default=None,
+                    help='strong (default for c3/c5): the workload\'s global batch split over '
+                         'the ranks; weak (c2, c4): the per-GPU batch fixed')
     args = ap.parse_args()
 
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        return spawn_ranks(args.gpus)
+    if os.environ.get('SMI_BENCH_PROBE') == '1':     # launch-path test (tests/test_cpu_bench.py)
+        print(json.dumps({'rank': int(os.environ.get('RANK', '0')),
+                          'world': int(os.environ.get('WORLD_SIZE', '1')),
+                          'local_rank': int(os.environ.get('LOCAL_RANK', '0'))}), flush=True)
+        return 0
     if args.config == 'c4':
         return run_ddpg(args)
     dist, world, rank, dev = init_dist()
@@ -337,6 +458,11 @@ def main():
     from surreal_amd import synthetic
     from surreal_amd.learner import PPOLearner, TorchDistAllReduce
     lc, ec, dims = make_config(args.config)
+    scaling = args.scaling or ('weak' if args.config == 'c2' else 'strong')
+    if scaling == 'strong':
+        if dims['B_global'] % world:
+            raise SystemExit(f'global batch {dims["B_global"]} does not split over {world} ranks')
+        lc.replay.batch_size = dims['B_global'] // world
     B, T = lc.replay.batch_size, lc.algo.n_step
     D, A = dims['D'], dims['A']
     dp = TorchDistAllReduce() if dist is not None else None
@@ -371,6 +497,8 @@ def main():
     # stream, and per-phase torch events -> roofline / kernels / phases
     n_inst = min(args.steps, 5)
     learner.kernel_events = {}
+    if dp is not None:
+        dp.timing = []
     L.kernel_timing(True)
     for k in range(n_inst):
         learner.learn(pool[k % len(pool)])
@@ -378,18 +506,28 @@ def main():
     L.kernel_timing(False)
     ev = learner.kernel_events
     learner.kernel_events = None
+    allreduce = None
+    if dp is not None:
+        # per-rank time inside the stream-ordered all-reduces (max over ranks)
+        ar_ms = sum(s_.elapsed_time(e_) for s_, e_, _ in dp.timing) / n_inst
+        ar_n = len(dp.timing) / n_inst
+        ar_b = sum(b_ for _, _, b_ in dp.timing) / n_inst
+        dp.timing = None
+        t = torch.tensor([ar_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        allreduce = {'ms_per_step_max_over_ranks': round(float(t.item()), 4),
+                     'calls_per_step': ar_n, 'bytes_per_step': int(ar_b),
+                     'backend': dist.get_backend()}
 
     # per-kernel (MFMA engine) classes from the library's own events, and the
     # learner-level launches/phases from torch events on the same stream
     kt = L.kernel_timing_report()
-    kernels = {n: {'launches_per_step': round(c / n_inst, 2), 'avg_ms': round(ms / c, 5),
-                   'ms_per_step': round(ms / n_inst, 4),
-                   'tflops': round(fl / (ms * 1e-3) / 1e12, 3)}
-               for n, (c, ms, fl) in kt.items()}
+    kernels = kernel_table(kt, n_inst)
     phases = {n: round(float(np.sum([s.elapsed_time(e) for s, e in v])) / n_inst, 4)
               for n, v in ev.items()}
-    if kt:
-        dom = max(kt, key=lambda n: kt[n][1])
+    rhbm = roofline_hbm(kt, n_inst)
+    if mfma_dominant(kt):
+        dom = mfma_dominant(kt)
         c, ms, fl = kt[dom]
         ach = fl / (ms * 1e-3) / 1e12
         traffic, tsrc = pmc_traffic(args.config, dom)
@@ -421,21 +559,23 @@ def main():
                 'avg_ms': round(kdur[dom], 5), 'algorithmic_flops_per_launch': int(fl)}
     ms = elapsed / args.steps * 1e3
     value = world * B * T * args.steps / elapsed
+    split = (f'{dims["B_global"]} segments split over {world} GPU(s) ({B} per GPU)'
+             if scaling == 'strong' else f'{B} segments per GPU')
     if args.config == 'c5':
         wl = ('C5: C3 (LSTM 100, horizon 5, heads 300x200, n_step 25, adapt, z-filter, 10/10 '
               'epochs, obs 42, act 8) + pixel stem: camera0 3x84x84 uint8 -> conv 16@8s4 -> '
-              '32@4s2 -> FC 256; 128 segments per GPU (1024 over 8 GPUs)')
+              '32@4s2 -> FC 256; ' + split)
     elif args.config == 'c3':
         wl = ('C3: synthetic PPO learner batch, reference PPO defaults (LSTM 100, horizon 5, heads '
               '300x200, n_step 25, adapt, z-filter, 10/10 epochs), SawyerLift state dims (obs 42, '
-              'act 8), 1024 segments per GPU')
+              'act 8), ' + split)
     else:
         wl = ('C2: synthetic PPO learner batch, HalfCheetah dims (obs 17, act 6), 64x64 MLP, '
               '64 segments x n_step 50 per GPU, adapt mode, z-filter, 10/10 epochs')
     out = {
         'metric': METRIC, 'value': round(value, 1), 'unit': 'env-steps/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 4),
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'higher_is_better': True, 'scaling': scaling, 'vs_baseline': None, 'dtype': 'f32',
         'data': 'synthetic (seeded, SURVEY §8(d)); random-init weights of the named architecture',
         'config': {'workload': wl, 'segments_per_gpu': B, 'n_step': T,
                    'env_steps_per_learn_per_gpu': B * T, 'global_segments': world * B,
@@ -445,8 +585,13 @@ def main():
         'kernels': kernels,
         'phase_ms_per_step': phases,
     }
+    if rhbm is not None:
+        out['roofline_hbm'] = rhbm
+    if allreduce is not None:
+        out['allreduce'] = allreduce
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(args.config, lc, dims, args.cpu_budget)
+        out['cpu_baseline'] = cpu_baseline(args.config, make_config(args.config)[0], dims,
+                                           args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -454,4 +599,4 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main() or 0)

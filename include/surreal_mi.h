@@ -43,9 +43,10 @@ int64_t smi_workspace_bytes(void);
 int     smi_set_workspace(void* dev_ptr, int64_t bytes);
 
 /* Measurement only (not part of the reference API): per-launch HIP-event
- * timing of the MFMA kernels, by class.  smi_kernel_timing(1) starts a fresh
- * record, (0) stops; smi_kernel_timing_report(cls, out4) -> {launches, total
- * ms, total algorithmic flops, 0}. */
+ * timing of the MFMA kernels and of the HBM-bound streaming kernels of the
+ * RNN learner phases, by class.  smi_kernel_timing(1) starts a fresh record,
+ * (0) stops; smi_kernel_timing_report(cls, out4) -> {launches, total ms, total
+ * algorithmic work, 0}: flops for classes 0-7, bytes for classes 8-13. */
 #define SMI_KT_GEMM_FWD    0
 #define SMI_KT_GEMM_DX     1
 #define SMI_KT_GEMM_DW     2
@@ -54,6 +55,12 @@ int     smi_set_workspace(void* dev_ptr, int64_t bytes);
 #define SMI_KT_LSTM_BWD    5
 #define SMI_KT_CNN_FWD     6
 #define SMI_KT_CNN_BWD     7
+#define SMI_KT_GAE         8    /* windowed GAE (bytes)                         */
+#define SMI_KT_POLICY_STATS 9   /* policy loss / KL statistics rows (bytes)     */
+#define SMI_KT_POLICY_GRAD 10   /* policy loss gradient rows (bytes)            */
+#define SMI_KT_VALUE_ROWS  11   /* value loss rows (bytes)                      */
+#define SMI_KT_ADAM        12   /* grad-norm partials + Adam (bytes)            */
+#define SMI_KT_ZF_TMAJOR   13   /* ZFilter apply into the time-major stem input */
 int smi_kernel_timing(int on);
 int smi_kernel_timing_report(int cls, double* out4);
 

@@ -93,7 +93,10 @@ RNN_PH_GAE, RNN_PH_PREP, RNN_PH_POLICY_FWD, RNN_PH_POLICY_BWD, RNN_PH_POLICY_APP
     RNN_PH_VALUE_GRAD, RNN_PH_VALUE_APPLY, RNN_PH_ZSTATS, RNN_PH_ZAPPLY, RNN_PH_POLICY_DECIDE = range(10)
 RNN_PSTAT = 16
 KT_NAMES = ['gemm_fwd', 'gemm_dx', 'gemm_dw', 'gemm_splitk_reduce', 'lstm_fwd', 'lstm_bwd',
-            'cnn_fwd', 'cnn_bwd']
+            'cnn_fwd', 'cnn_bwd',
+            # HBM-bound streaming classes: their work unit is algorithmic BYTES
+            'gae', 'policy_rows_stats', 'policy_rows_grad', 'value_rows', 'adam', 'zf_tmajor']
+KT_BYTES = set(KT_NAMES[8:])
 
 
 def kernel_timing(on):

@@ -49,7 +49,29 @@ struct GemmArgs {
   float* part;                    // split-K partials [gridDim.z][M][N] (nullptr: no split)
   const int* skip;                // device flag: nonzero -> no-op (early stop)
   int avec, bvec;                 // 16-byte operand loads (set by gemm_launch)
+  // EPI_DW with a two-source B (the LSTM's [x_t | h_{t-1}], one launch for the
+  // W_ih and W_hh gradients): B2 != null makes columns n >= split_col read
+  // B2[k*b2_rs + n - split_col] and land in C2 (ld ldc2); columns c1_real <= n
+  // < split_col are padding (never stored); bias_out2 receives a copy of the
+  // bias column (b_ih and b_hh have the same gradient).
+  const float* B2; int64_t b2_rs; int split_col, c1_real;
+  float* C2; int64_t ldc2; float* bias_out2;
 };
+
+// where output (m, n) of a weight gradient goes (bias column, the second
+// destination of a two-source B, padding)
+__device__ __forceinline__ void dw_put(const GemmArgs& g, int m, int n, float v) {
+  if (n == g.ones_col) {
+    g.bias_out[m] = g.accumulate ? g.bias_out[m] + v : v;
+    if (g.bias_out2) g.bias_out2[m] = g.accumulate ? g.bias_out2[m] + v : v;
+    return;
+  }
+  float* dst;
+  if (g.B2 && n >= g.split_col) dst = g.C2 + (int64_t)m * g.ldc2 + (n - g.split_col);
+  else if (g.B2 && n >= g.c1_real) return;                   // padding column
+  else dst = g.C + (int64_t)m * g.ldc + n;
+  *dst = g.accumulate ? *dst + v : v;
+}
 
 // Operand loader: one 64 (rows) x 32 (k) tile, 2048 elements, 8 per thread
 // (scalar) or 2 float4 per thread (VEC: along the contiguous dimension, when
@@ -303,12 +325,11 @@ gemm_kernel(GemmArgs g) {
 // flight), then the 4 lane sums are combined in LDS in a fixed order
 // (deterministic, no atomics).
 __global__ void __launch_bounds__(kWG)
-gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, float* C,
-                          int64_t ldc, int ones_col, float* bias_out, int accumulate,
-                          const int* skip, const float* bias, int act, const float* mask,
-                          int64_t ldm) {
-  if (skip && skip[0] != 0) return;
+gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, GemmArgs g, const float* bias,
+                          int act, const float* mask) {
+  if (g.skip && g.skip[0] != 0) return;
   __shared__ float red[4][64];
+  const int M = g.M, N = g.N;
   const int64_t MN = (int64_t)M * N;
   const int el = threadIdx.x & 63, zl = threadIdx.x >> 6;
   const int64_t e = (int64_t)blockIdx.x * 64 + el;
@@ -330,13 +351,8 @@ gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, f
   if (bias) s += bias[n];                       // split-K forward epilogue
   if (act == ACT_RELU) s = s > 0.f ? s : 0.f;
   else if (act == ACT_TANH) s = tanhf(s);
-  if (mask && !(mask[(int64_t)m * ldm + n] > 0.f)) s = 0.f;   // split-K input gradient
-  if (n == ones_col) {
-    bias_out[m] = accumulate ? bias_out[m] + s : s;
-  } else {
-    float* dst = C + (int64_t)m * ldc + n;
-    *dst = accumulate ? *dst + s : s;
-  }
+  if (mask && !(mask[(int64_t)m * g.ldm + n] > 0.f)) s = 0.f;   // split-K input gradient
+  dw_put(g, m, n, s);
 }
 
 // Small-K forward (K <= 64: the LSTM input projection x W_ih^T over the
@@ -634,6 +650,12 @@ __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m
   const bool ok = r < ke;
   const float* Ar = ok ? g.A + (int64_t)r * g.a_cs : g_dwd_zero;
   const float* Br = ok ? g.B + (int64_t)r * g.b_rs : g_dwd_zero;
+  // second source (columns >= split_col): its row base, shifted so that column
+  // cb reads Br2 + cb (rows past the slab read the zero row at offset cb - split)
+  const float* Br2 = g.B2 ? (ok ? g.B2 + (int64_t)r * g.b2_rs - g.split_col
+                                : g_dwd_zero - g.split_col)
+                          : Br;
+  const int split = g.B2 ? g.split_col : 0x7fffffff;
   const float* one = ok ? g_dwd_one : g_dwd_zero;
   if constexpr (MT == 4 && VA) {
     const int c = min(m0 + 4 * li, g.M - 4);
@@ -647,14 +669,16 @@ __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m
   for (int h = 0; h < NB / 4; ++h) {
     const int cb = n0 + 64 * h + 4 * li;
     if constexpr (VB) {
-      const float* src = cb < bdata ? Br + cb : (cb == g.ones_col ? one : g_dwd_zero);
+      const float* src = cb < bdata ? (cb >= split ? Br2 : Br) + cb
+                                    : (cb == g.ones_col ? one : g_dwd_zero);
       const float4 x = *reinterpret_cast<const float4*>(src);
       bv[4 * h] = x.x; bv[4 * h + 1] = x.y; bv[4 * h + 2] = x.z; bv[4 * h + 3] = x.w;
     } else {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int c = cb + t;
-        bv[4 * h + t] = *(c < bdata ? Br + c : (c == g.ones_col ? one : g_dwd_zero));
+        bv[4 * h + t] = *(c < bdata ? (c >= split ? Br2 : Br) + c
+                                    : (c == g.ones_col ? one : g_dwd_zero));
       }
     }
   }
@@ -664,13 +688,9 @@ __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m
 // every WV-th 4-row step of the slab, so a SIMD interleaves two waves' loads
 // and MFMAs; the waves' sums meet in LDS in a fixed tree order)
 template <int MT, int NT, bool VA, bool VB, int WV>
-__global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWD_OCC : 1)
-gemm_dwd_kernel(GemmArgs g) {
-  if (g.skip && g.skip[0] != 0) return;
-  extern __shared__ float4 dwd_red[];            // 2 x [MT*NT][64] float4
+__device__ __forceinline__ void dwd_tile(const GemmArgs& g, const TileIdx ti, float4* dwd_red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const TileIdx ti = gemm_tile_index();
   const int m0 = ti.mt * 16 * MT, n0 = ti.nt * 16 * NT;
   const int kb = ti.z * g.kchunk;
   const int ke = min(g.K, kb + g.kchunk);
@@ -764,18 +784,98 @@ gemm_dwd_kernel(GemmArgs g) {
           const int n = nb + t;
           if (n >= g.N) continue;
           const float v = acc[a][4 * h + t][i];
-          if (g.part) {
-            g.part[((int64_t)ti.z * g.M + m) * g.N + n] = v;
-          } else if (n == g.ones_col) {
-            g.bias_out[m] = g.accumulate ? g.bias_out[m] + v : v;
-          } else {
-            float* dst = g.C + (int64_t)m * g.ldc + n;
-            *dst = g.accumulate ? *dst + v : v;
-          }
+          if (g.part) g.part[((int64_t)ti.z * g.M + m) * g.N + n] = v;
+          else dw_put(g, m, n, v);
         }
       }
     }
 }
+
+template <int MT, int NT, bool VA, bool VB, int WV>
+__global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWD_OCC : 1)
+gemm_dwd_kernel(GemmArgs g) {
+  if (g.skip && g.skip[0] != 0) return;
+  extern __shared__ float4 dwd_red[];            // 2 x [MT*NT][64] float4
+  dwd_tile<MT, NT, VA, VB, WV>(g, gemm_tile_index(), dwd_red);
+}
+
+// Grouped weight gradients: every dW GEMM of one backward phase (the head's
+// three layers and the LSTM's fused W_ih | W_hh) in ONE launch.  Workgroups are
+// dealt to GEMMs by a prefix over their (tiles x slabs); slab lengths are
+// balanced so every workgroup reduces about the same number of rows; each GEMM
+// writes its own split-K partials, and one grouped reducer finishes them all.
+// One launch and one reduce per phase instead of a launch + reduce per layer
+// (and no side stream): the ~20 us fixed cost of a dW launch is paid once.
+constexpr int kDwGroupMax = 6;
+struct DwGroup {
+  GemmArgs g[kDwGroupMax];
+  int wg0[kDwGroupMax + 1];      // workgroup prefix
+  int rb0[kDwGroupMax + 1];      // reducer-block prefix
+  int gm[kDwGroupMax], gn[kDwGroupMax], S[kDwGroupMax];
+  int vec[kDwGroupMax];          // 2*VA + VB
+  int n;
+};
+
+template <int WV>
+__global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWD_OCC : 1)
+gemm_dwd_group_kernel(DwGroup G) {
+  extern __shared__ float4 dwd_red[];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  int w = orig;
+  if (nwg > 8) {                                  // XCD-contiguous runs (gemm_tile_index)
+    const int x = orig & 7, q = nwg >> 3, r = nwg & 7;
+    w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
+  }
+  int gi = 0;
+  while (gi + 1 < G.n && w >= G.wg0[gi + 1]) ++gi;
+  const GemmArgs& g = G.g[gi];
+  if (g.skip && g.skip[0] != 0) return;
+  const int local = w - G.wg0[gi], gn = G.gn[gi], gm = G.gm[gi];
+  TileIdx ti;
+  ti.nt = local % gn;
+  ti.mt = (local / gn) % gm;
+  ti.z = local / (gn * gm);
+  switch (G.vec[gi]) {
+    case 3: dwd_tile<4, 8, true, true, WV>(g, ti, dwd_red); break;
+    case 2: dwd_tile<4, 8, true, false, WV>(g, ti, dwd_red); break;
+    case 1: dwd_tile<4, 8, false, true, WV>(g, ti, dwd_red); break;
+    default: dwd_tile<4, 8, false, false, WV>(g, ti, dwd_red); break;
+  }
+}
+
+// the partials of every GEMM of a group, each element summed over its slabs in
+// the fixed order of gemm_splitk_reduce_kernel
+__global__ void __launch_bounds__(kWG)
+gemm_group_reduce_kernel(DwGroup G) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < G.n && b >= G.rb0[gi + 1]) ++gi;
+  const GemmArgs& g = G.g[gi];
+  if (g.skip && g.skip[0] != 0) return;
+  const int S = G.S[gi];
+  const float* __restrict__ part = g.part;
+  const int64_t MN = (int64_t)g.M * g.N;
+  const int el = threadIdx.x & 63, zl = threadIdx.x >> 6;
+  const int64_t e = (int64_t)(b - G.rb0[gi]) * 64 + el;
+  const int64_t ec = e < MN ? e : MN - 1;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int z = zl;
+  for (; z + 12 < S; z += 16) {
+    s0 += part[(int64_t)z * MN + ec];
+    s1 += part[(int64_t)(z + 4) * MN + ec];
+    s2 += part[(int64_t)(z + 8) * MN + ec];
+    s3 += part[(int64_t)(z + 12) * MN + ec];
+  }
+  for (; z < S; z += 4) s0 += part[(int64_t)z * MN + ec];
+  red[zl][el] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (zl != 0 || e >= MN) return;
+  const float v = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+  const int m = (int)(e / g.N), n = (int)(e - (int64_t)m * g.N);
+  dw_put(g, m, n, v);
+}
+
 
 // Row-panel GEMM for the learner's tall activations (rows >> N, K small):
 //   EPI_FWD: Y = act(X W^T + b)        EPI_DX: dX = (dY W) * [mask > 0]
@@ -962,7 +1062,8 @@ static int dwd_launch(GemmArgs g, hipStream_t st) {
   const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
   const int MT = g.M > 32 ? 4 : 1, NT = g.N > 64 ? 8 : 4;
   const bool va = MT == 4 && al16(g.A) && g.M % 4 == 0 && g.a_cs % 4 == 0;
-  const bool vb = al16(g.B) && bdata >= 4 && bdata % 4 == 0 && g.b_rs % 4 == 0;
+  const bool vb = al16(g.B) && bdata >= 4 && bdata % 4 == 0 && g.b_rs % 4 == 0 &&
+                  (!g.B2 || (al16(g.B2) && g.b2_rs % 4 == 0 && g.split_col % 4 == 0));
   const int gm = (g.M + 16 * MT - 1) / (16 * MT), gn = (g.N + 16 * NT - 1) / (16 * NT);
   const int tiles = gm * gn;
   static int target = 0;
@@ -1001,12 +1102,113 @@ static int dwd_launch(GemmArgs g, hipStream_t st) {
     else if (NT == 8) dwd_dispatch<1, 8, 4>(g, grid, false, vb, st);
     else dwd_dispatch<1, 4, 4>(g, grid, false, vb, st);
   }
-  const int nreal = g.ones_col >= 0 ? g.N - 1 : g.N;
+  const int nreal = (g.ones_col >= 0 ? g.N - 1 : g.N) -
+                    (g.B2 ? g.split_col - g.c1_real : 0);      // padding columns do no work
   ktime_end(kslot, KT_GEMM_DW,
             2.0 * g.M * (double)nreal * g.K + (g.ones_col >= 0 ? (double)g.M * g.K : 0.0), st);
   const int rc = check_launch("gemm_dwd_kernel");
   if (rc || S == 1) return rc;
   return splitk_reduce(g, S, EPI_DW, st);
+}
+
+// ---- grouped weight gradients (gemm_dwd_group_kernel) ----------------------
+static DwGroup g_grp;
+static bool g_grp_on = false;
+static double g_grp_flops = 0.0;
+
+int dw_group_begin() {
+  g_grp_on = true;
+  g_grp.n = 0;
+  g_grp_flops = 0.0;
+  return SMI_OK;
+}
+
+static bool dw_group_add(const GemmArgs& g) {
+  if (!g_grp_on || g_grp.n >= kDwGroupMax) return false;
+  auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
+  const bool va = al16(g.A) && g.M >= 4 && g.M % 4 == 0 && g.a_cs % 4 == 0;
+  const bool vb = al16(g.B) && bdata >= 4 && bdata % 4 == 0 && g.b_rs % 4 == 0 &&
+                  (!g.B2 || (al16(g.B2) && g.b2_rs % 4 == 0 && g.split_col % 4 == 0));
+  const int i = g_grp.n++;
+  g_grp.g[i] = g;
+  g_grp.vec[i] = (va ? 2 : 0) + (vb ? 1 : 0);
+  const int nreal = (g.ones_col >= 0 ? g.N - 1 : g.N) - (g.B2 ? g.split_col - g.c1_real : 0);
+  g_grp_flops += 2.0 * g.M * (double)nreal * g.K + (g.ones_col >= 0 ? (double)g.M * g.K : 0.0);
+  return true;
+}
+
+// target workgroups of a grouped launch (SMI_DWD_GROUP_TARGET; tuning knob)
+static int dw_group_target() {
+  static int t = 0;
+  if (!t) {
+    // measured at C3 (bench, one MI355X): 256 -> 4.44 ms of dW per learn, 512 ->
+    // 3.71, 768 -> 3.17, 1024 -> 2.83 (45 TF/s), 1536 -> 3.32, 3072 -> 4.43
+    const char* e = getenv("SMI_DWD_GROUP_TARGET");
+    t = e ? atoi(e) : 1024;
+    if (t < 64) t = 64;
+  }
+  return t;
+}
+
+int dw_group_flush(hipStream_t st) {
+  g_grp_on = false;
+  DwGroup& G = g_grp;
+  if (G.n == 0) return SMI_OK;
+  constexpr int MT = 4, NT = 8;
+  const int rs = 4 * dwd_waves() * DWD_P;           // rows per prefetch window
+  double work = 0.0;                                 // sum of tiles x rows
+  int64_t tiles[kDwGroupMax];
+  for (int i = 0; i < G.n; ++i) {
+    const GemmArgs& g = G.g[i];
+    G.gm[i] = (g.M + 16 * MT - 1) / (16 * MT);
+    G.gn[i] = (g.N + 16 * NT - 1) / (16 * NT);
+    tiles[i] = (int64_t)G.gm[i] * G.gn[i];
+    work += (double)tiles[i] * g.K;
+  }
+  const int64_t cap = smi_workspace_floats();
+  int64_t rows = (int64_t)(work / dw_group_target()) + 1;
+  rows = (rows + rs - 1) / rs * rs;
+  if (rows < 2 * rs) rows = 2 * rs;                 // >= 8 MFMA steps per wave
+  int64_t need = 0;
+  for (int pass = 0; pass < 8; ++pass) {            // grow the slabs until the partials fit
+    need = 0;
+    for (int i = 0; i < G.n; ++i) {
+      const GemmArgs& g = G.g[i];
+      const int64_t kc = rows < g.K ? rows : ((int64_t)g.K + rs - 1) / rs * rs;
+      const int S = (int)((g.K + kc - 1) / kc);
+      need += (int64_t)S * g.M * g.N;
+    }
+    if (need <= cap) break;
+    rows *= 2;
+  }
+  float* base = workspace_f32(need);
+  if (!base) return set_error(SMI_E_ARG, "gemm: workspace too small for the grouped dW partials");
+  int64_t off = 0;
+  G.wg0[0] = 0;
+  G.rb0[0] = 0;
+  for (int i = 0; i < G.n; ++i) {
+    GemmArgs& g = G.g[i];
+    const int64_t kc = rows < g.K ? rows : ((int64_t)g.K + rs - 1) / rs * rs;
+    g.kchunk = (int)kc;
+    G.S[i] = (int)((g.K + kc - 1) / kc);
+    g.part = base + off;
+    off += (int64_t)G.S[i] * g.M * g.N;
+    G.wg0[i + 1] = G.wg0[i] + (int)(tiles[i] * G.S[i]);
+    G.rb0[i + 1] = G.rb0[i] + (int)(((int64_t)g.M * g.N + 63) / 64);
+  }
+  const int kslot = ktime_begin(st);
+  const size_t lds = (size_t)2 * MT * NT * 64 * sizeof(float4);
+  if (dwd_waves() == 8)
+    hipLaunchKernelGGL(gemm_dwd_group_kernel<8>, dim3(G.wg0[G.n]), dim3(512), lds, st, G);
+  else
+    hipLaunchKernelGGL(gemm_dwd_group_kernel<4>, dim3(G.wg0[G.n]), dim3(256), lds, st, G);
+  ktime_end(kslot, KT_GEMM_DW, g_grp_flops, st);
+  RC_CHECK(check_launch("gemm_dwd_group_kernel"));
+  const int rslot = ktime_begin(st);
+  hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(G.rb0[G.n]), dim3(kWG), 0, st, G);
+  ktime_end(rslot, KT_GEMM_REDUCE, (double)need, st);
+  return check_launch("gemm_group_reduce_kernel");
 }
 
 static int use_panel() {
@@ -1178,7 +1380,7 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (epi != EPI_DW && panel_ok(epi, g)) return panel_launch(epi, g, st);
   if (epi == EPI_DW && use_dwd() && g.a_rs == 1 && g.b_cs == 1 && g.K >= 1 &&
       (g.ones_col >= 0 ? g.ones_col : g.N) >= 1 && g.M <= 512 && g.N <= 512)
-    return dwd_launch(g, st);
+    return dw_group_add(g) ? SMI_OK : dwd_launch(g, st);
   const bool ak = g.a_cs == 1;         // A contiguous along k
   const bool bk = g.b_rs == 1;         // B contiguous along k (rows n)
   auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -1248,10 +1450,9 @@ static int splitk_reduce(const GemmArgs& g, int S, int epi, hipStream_t st) {
   const int64_t MN = (int64_t)g.M * g.N;
   const int rg = (int)((MN + 63) / 64);
   const bool fwd = epi == EPI_FWD;
-  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, g.part, S, g.M, g.N,
-                     g.C, g.ldc, g.ones_col, g.bias_out, g.accumulate, g.skip,
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, g.part, S, g,
                      fwd ? g.bias : nullptr, fwd ? g.act : ACT_NONE,
-                     epi == EPI_DX ? g.mask : nullptr, g.ldm);
+                     epi == EPI_DX ? g.mask : nullptr);
   ktime_end(rslot, KT_GEMM_REDUCE, (double)S * MN, st);
   return check_launch("gemm_splitk_reduce_kernel");
 }
@@ -1261,8 +1462,10 @@ int launch_slab_reduce(const float* part, int S, int64_t n, float* out, hipStrea
                        const int* skip) {
   if (n < 1 || S < 1) return SMI_OK;
   const int rg = (int)((n + 63) / 64);
-  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, part, S, 1, (int)n, out,
-                     n, -1, nullptr, 0, skip, nullptr, ACT_NONE, nullptr, 0);
+  GemmArgs g{};
+  g.M = 1; g.N = (int)n; g.C = out; g.ldc = n; g.ones_col = -1; g.skip = skip;
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(kWG), 0, st, part, S, g, nullptr,
+                     ACT_NONE, nullptr);
   return check_launch("gemm_splitk_reduce_kernel");
 }
 
@@ -1288,6 +1491,29 @@ int launch_linear_bwd_dx(const float* dY, int64_t ldg, int M, int N, const float
   g.B = W; g.b_rs = ldw; g.b_cs = 1;        // B(k=n', n=k') = W[n'][k']
   g.C = dX; g.ldc = lddx; g.mask = mask; g.ldm = ldm; g.ones_col = -1; g.skip = skip;
   return gemm_launch(EPI_DX, g, st);
+}
+
+// weight gradients of two layers fed by the same dY over [X1 | X2] (the LSTM:
+// W_ih over x_t, W_hh over h_{t-1}, one bias gradient shared by b_ih / b_hh)
+// in ONE launch: dY read once, one split-K reduce.  X1 has K1 real columns and
+// row stride ldx1 (a multiple of 4 >= K1: the padding columns are computed and
+// dropped so both sources load as 16-byte vectors).
+int launch_linear_bwd_dw2(const float* dY, int64_t ldg, int M, int N, const float* X1,
+                          int64_t ldx1, int K1, const float* X2, int64_t ldx2, int K2,
+                          float* dW1, int64_t ld1, float* dW2, int64_t ld2, float* db1,
+                          float* db2, hipStream_t st, const int* skip) {
+  const int K1p = (int)ldx1;
+  if (K1p < K1 || K1p % 4) return set_error(SMI_E_ARG, "bwd_dw2: ldx1 must be a multiple of 4 >= K1");
+  GemmArgs g{};
+  g.M = N; g.N = K1p + K2 + 1; g.K = M;
+  g.A = dY; g.a_rs = 1; g.a_cs = ldg;
+  g.B = X1; g.b_rs = ldx1; g.b_cs = 1;
+  g.B2 = X2; g.b2_rs = ldx2; g.split_col = K1p; g.c1_real = K1;
+  g.C = dW1; g.ldc = ld1; g.C2 = dW2; g.ldc2 = ld2;
+  g.ones_col = K1p + K2; g.bias_out = db1; g.bias_out2 = db2; g.skip = skip;
+  if (!(g.a_rs == 1 && g.b_cs == 1 && use_dwd() && g.M <= 512 && g.N <= 512))
+    return set_error(SMI_E_ARG, "bwd_dw2: shape not supported");
+  return dw_group_add(g) ? SMI_OK : dwd_launch(g, st);
 }
 
 int launch_linear_bwd_dw(const float* dY, int64_t ldg, int M, int N, const float* X, int64_t ldx,

@@ -48,6 +48,9 @@ struct RnnDims {
   int B, T, Hz, E, S1, D, H, G4, A, h1, h2, c1, c2;
   int F, Din;                         // pixel features (0: no CNN stem), LSTM input D + F
   int Hin;                            // head input width: H (LSTM) or Din (H == 0: MLP policy)
+  int ldx;                            // row stride of the stem input Xz / Xr: Din rounded up to
+                                      // 4 (16-byte rows; the padding columns stay zero)
+  int Hld;                            // row stride of the head input: H, or ldx (MLP policy)
   int64_t NE, NG;
   int64_t nA_head, nC_head, nL, nCnn, nS;   // parameter counts; stem = [lstm | cnn]
   MlpLayout LA, LC;
@@ -65,6 +68,8 @@ __host__ __device__ inline RnnDims rnn_dims(int B, int T, int Hz, int D, int H, 
   d.A = A; d.h1 = h1; d.h2 = h2; d.c1 = c1; d.c2 = c2;
   d.NE = (int64_t)d.E * B; d.NG = (int64_t)d.S1 * B;
   d.Hin = H > 0 ? H : d.Din;
+  d.ldx = (d.Din + 3) & ~3;
+  d.Hld = H > 0 ? H : d.ldx;
   d.LA = mlp_layout(d.Hin, h1, h2, A, 1);
   d.LC = mlp_layout(d.Hin, c1, c2, 1, 0);
   d.nA_head = d.LA.fcount; d.nC_head = d.LC.fcount;
@@ -96,8 +101,8 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   int64_t o = 0;
   auto take = [&](int64_t n) { float* r = p ? p + o : nullptr; o += al64(n); return r; };
   const int hmax1 = d.h1 > d.c1 ? d.h1 : d.c1, hmax2 = d.h2 > d.c2 ? d.h2 : d.c2;
-  s.Xz = take(d.NG * d.Din);
-  s.Xr = take(d.NE * d.Din);
+  s.Xz = take(d.NG * d.ldx);
+  s.Xr = take(d.NE * d.ldx);
   s.xproj = take(d.NG * d.G4);
   s.hbuf = take((int64_t)(d.S1 + 1) * d.B * d.H);
   s.cbuf = take((int64_t)(d.E + 1) * d.B * d.H);
@@ -713,11 +718,11 @@ static LstmP lstm_params(const float* p, int D, int H) {
 static int lstm_forward(const RnnDims& d, const LstmP& l, const float* X, int S, const float* h0,
                         const float* c0, const RnnScratch& s, float* cbuf, float* gates,
                         hipStream_t st, const int* skip) {
-  const int rf = launch_lstm_fwd_x(X, d.Din, d.Din, l.Wih, l.bih, l.Whh, l.bhh, h0, c0, S, d.B,
+  const int rf = launch_lstm_fwd_x(X, d.ldx, d.Din, l.Wih, l.bih, l.Whh, l.bhh, h0, c0, S, d.B,
                                   d.H, s.hbuf, cbuf, gates, st, skip);
   if (rf != SMI_E_NOFIT) return rf;
   const int64_t rows = (int64_t)S * d.B;
-  RC(launch_linear_fwd(X, d.Din, (int)rows, d.Din, l.Wih, d.Din, l.bih, d.G4, ACT_NONE, s.xproj,
+  RC(launch_linear_fwd(X, d.ldx, (int)rows, d.Din, l.Wih, d.Din, l.bih, d.G4, ACT_NONE, s.xproj,
                        d.G4, st, skip));
   return launch_lstm_fwd(s.xproj, l.Whh, l.bhh, h0, c0, S, d.B, d.H, s.hbuf, cbuf, gates, st,
                          skip);
@@ -732,11 +737,17 @@ static int lstm_backward(const RnnDims& d, const LstmP& l, float* G, const RnnSc
   float* gbih = gWhh + (int64_t)4 * d.H * d.H;
   float* gbhh = gbih + d.G4;
   const int M = (int)d.NE;
-  RC(launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.Xz, d.Din, d.Din, gWih, d.Din, gbih, 0, st,
-                          skip));
-  // h_{t-1} rows: hbuf[0..E-1] (hbuf[0] = h0)
-  return launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.hbuf, d.H, d.H, gWhh, d.H, gbhh, 0, st,
-                              skip);
+  static const int fused = [] { const char* e = getenv("SMI_LSTM_DW2"); return e ? atoi(e) : 1; }();
+  if (!fused) {     // A/B: the two launches over Xz and hbuf
+    RC(launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.Xz, d.ldx, d.Din, gWih, d.Din, gbih, 0, st,
+                            skip));
+    return launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.hbuf, d.H, d.H, gWhh, d.H, gbhh, 0, st,
+                                skip);
+  }
+  // W_ih over x_t (Xz rows), W_hh over h_{t-1} (hbuf[0..E-1], hbuf[0] = h0) and
+  // the shared bias gradient in ONE launch over [x_t | h_{t-1}]
+  return launch_linear_bwd_dw2(s.dgates, d.G4, M, d.G4, s.Xz, d.ldx, d.Din, s.hbuf, d.H, d.H,
+                               gWih, d.Din, gWhh, d.H, gbih, gbhh, st, skip);
 }
 
 static PixRows pix_rows(const smi_ppo_rnn_args& a, const RnnDims& d) {
@@ -750,7 +761,7 @@ static int cnn_features(const smi_ppo_rnn_args& a, const RnnDims& d, const float
                         const int* skip) {
   if (d.F == 0) return SMI_OK;
   return cnn_forward(cnn, pix_rows(a, d), d.G.C, d.G.H, d.G.W, d.F, (int64_t)S * d.B, A1, s.A2,
-                     X + d.D, d.Din, st, skip);
+                     X + d.D, d.ldx, st, skip);
 }
 
 // CNN backward from dF = dL/d(features) * relu'(features) in s.dF
@@ -766,7 +777,7 @@ static int cnn_grad(const smi_ppo_rnn_args& a, const RnnDims& d, const LstmP& l,
                     float* Gc, const RnnScratch& s, hipStream_t st, const int* skip) {
   if (d.F == 0) return SMI_OK;
   RC(launch_linear_bwd_dx(s.dgates, d.G4, (int)d.NE, d.G4, l.Wih + d.D, d.Din, d.F, s.Xz + d.D,
-                          d.Din, s.dF, d.F, st, skip));
+                          d.ldx, s.dF, d.F, st, skip));
   return cnn_bwd_from_dF(a, d, cnn, Gc, s, st, skip);
 }
 
@@ -783,14 +794,14 @@ static int stem_backward_chain(const smi_ppo_rnn_args& a, const RnnDims& d, cons
                                int64_t n_head, hipStream_t st, const int* skip, SideStream* side) {
   const float* X = head_in(d, s, s.Xz);
   if (d.H > 0) {
-    RC(head_bwd(hd, s.dOUT, X, d.Hin, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, 0, d.H, nullptr, 0,
+    RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, 0, d.H, nullptr, 0,
                 s.dh, st, skip, side));
     RC(lstm_backward(d, lm, G + n_head, s, st, skip));
     return cnn_grad(a, d, lm, cnn, G + n_head + d.nL, s, st, skip);
   }
   // MLP policy: the first head layer's input gradient over the CNN columns only
-  RC(head_bwd(hd, s.dOUT, X, d.Hin, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, d.D, d.F, s.Xz + d.D,
-              d.Din, s.dF, st, skip, side));
+  RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, d.D, d.F, s.Xz + d.D,
+              d.ldx, s.dF, st, skip, side));
   if (d.F == 0) return SMI_OK;
   return cnn_bwd_from_dF(a, d, cnn, G + n_head, s, st, skip);
 }
@@ -798,6 +809,16 @@ static int stem_backward_chain(const smi_ppo_rnn_args& a, const RnnDims& d, cons
 static int stem_backward(const smi_ppo_rnn_args& a, const RnnDims& d, const Head& hd,
                          const LstmP& lm, const float* cnn, float* G, const RnnScratch& s,
                          int64_t n_head, hipStream_t st, const int* skip) {
+  // default: every weight gradient of the phase (head layers + LSTM) queued
+  // and run as one grouped launch after the input-gradient chain and BPTT
+  // (SMI_DW_GROUP=0: per-layer launches with the head's on the side stream)
+  static const int grouped = [] { const char* e = getenv("SMI_DW_GROUP"); return e ? atoi(e) : 1; }();
+  if (grouped) {
+    dw_group_begin();
+    const int rc = stem_backward_chain(a, d, hd, lm, cnn, G, s, n_head, st, skip, nullptr);
+    const int rf = dw_group_flush(st);     // always flush: nothing stays queued after an error
+    return rc ? rc : rf;
+  }
   SideStream* side = side_stream();
   const int rc = stem_backward_chain(a, d, hd, lm, cnn, G, s, n_head, st, skip, side);
   if (side) {   // join even on error, so no side work outlives the phase
@@ -847,19 +868,24 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_GAE: {
       hipLaunchKernelGGL(rnn_init_kernel, dim3(1), dim3(64), 0, st, s.ci, s.cf);
       RC(check_launch("rnn_init_kernel"));
+      int kt = ktime_begin(st);
       hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NG * d.D)), dim3(kWG), zlds, st, a.obs,
                          a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum, a.zf_sumsq,
-                         a.zf_count, a.zf_eps, s.Xz, d.Din);
+                         a.zf_count, a.zf_eps, s.Xz, d.ldx);
+      ktime_end(kt, KT_ZF_TMAJOR, 8.0 * (double)d.NG * d.D, st);      // read x, write z(x)
       RC(check_launch("zf_tmajor_kernel"));
       RC(cnn_features(a, d, cnn, d.S1, s.Xz, nullptr, s, st, nullptr));
       if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.S1, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
-      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hin, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
+      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
       hipLaunchKernelGGL(tmajor_to_bmajor_kernel, dim3(grid_of(d.NG)), dim3(kWG), 0, st, s.OUT,
                          d.S1, d.B, s.values);
       RC(check_launch("tmajor_to_bmajor_kernel"));
       int np = 0;
+      kt = ktime_begin(st);
       RC(launch_gae_windows(s.values, nullptr, a.rewards, a.dones, d.B, d.T, d.Hz, a.gamma_tab,
                             a.lam_tab, a.gamma, a.gamma_H, s.adv, s.ret, s.gaepart, &np, st));
+      // r, d (8 B) + V (4 (T+1)/T B) per env-step, adv + ret (8 B) per window
+      ktime_end(kt, KT_GAE, (double)d.B * (8.0 * d.T + 4.0 * d.S1 + 8.0 * d.E), st);
       hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.gaepart, np, 2,
                          a.moments, nullptr);
       RC(check_launch("reduce_partials_kernel"));
@@ -871,7 +897,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       if (a.use_zf || d.F > 0) {   // the reference model's own z-filter / CNN stem
         hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NE * d.D)), dim3(kWG), zlds, st, a.obs,
                            a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
-                           a.rzf_count, a.zf_eps, s.Xr, d.Din);
+                           a.rzf_count, a.zf_eps, s.Xr, d.ldx);
         RC(check_launch("zf_tmajor_kernel"));
         RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, s, st, nullptr));
         X = s.Xr;
@@ -884,16 +910,19 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       const LstmP lr = lstm_params(a.ref_lstm, d.Din, d.H);
       if (d.H > 0) RC(lstm_forward(d, lr, X, d.E, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
       const Head ref{a.ref_actor, d.LA, d.Hin, d.h1, d.h2, d.A, 1};
-      return head_fwd(ref, head_in(d, s, X), d.Hin, d.NE, s.HA1, s.HA2, s.refmu, st,
+      return head_fwd(ref, head_in(d, s, X), d.Hld, d.NE, s.HA1, s.HA2, s.refmu, st,
                       nullptr);
     }
     case SMI_RNN_PH_POLICY_FWD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, stop));
       if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, stop));
-      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hin, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
+      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE);
+      const int kt = ktime_begin(st);
       hipLaunchKernelGGL(policy_rows_stats_kernel, dim3(nb), dim3(kWG), 0, st, p);
+      // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
+      ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
       RC(check_launch("policy_rows_stats_kernel"));
       hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, PS_N,
                          a.pstat, stop);
@@ -909,7 +938,10 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_POLICY_BWD: {
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE);
+      const int kt = ktime_begin(st);
       hipLaunchKernelGGL(policy_rows_grad_kernel, dim3(nb), dim3(kWG), 0, st, p);
+      // per row: mu, refmu, actions, behave (5A) + adv read, dz (A) written
+      ktime_end(kt, KT_POLICY_GRAD, 4.0 * (double)d.NE * (6 * d.A + 1), st);
       RC(check_launch("policy_rows_grad_kernel"));
       RC(stem_backward(a, d, actor, lm, cnn, gA, s, d.nA_head, st, stop));
       hipLaunchKernelGGL(logvar_grad_kernel, dim3(1), dim3(kWG), 0, st, s.lvpart, nb, d.A,
@@ -919,6 +951,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_POLICY_APPLY: {
       const int64_t n = d.nA_head + d.nS;
       const int g = grid_of(n, 1024);
+      const int kt = ktime_begin(st);
       hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gA, n, s.part, stop,
                          a.actor_step, s.ci + CI_RUNS);
       RC(check_launch("sumsq_part_kernel"));
@@ -927,16 +960,20 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                        a.clip_actor_grad ? a.actor_max_norm : 0.f, s.part, g, stop,
                        a.clip_actor_grad ? a.stats + SMI_ST_GRAD_NORM_ACTOR : nullptr, nullptr};
       hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(kWG), 0, st, aa);
+      // grad-norm pass (g: 4 B) + Adam (p, g, m, v read 16 B; p, m, v written 12 B)
+      ktime_end(kt, KT_ADAM, 32.0 * (double)n, st);
       return check_launch("adam_split_kernel");
     }
     case SMI_RNN_PH_VALUE_GRAD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
       if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, nullptr));
-      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hin, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
+      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
       const int nb = rnn_nblk(d.NE);
       const bool last = e == a.epoch_baseline - 1;
+      const int kt = ktime_begin(st);
       hipLaunchKernelGGL(value_rows_kernel, dim3(nb), dim3(kWG), 0, st, s.OUT, s.ret, d.B, d.E,
                          (float)(2.0 / (double)NEg), s.dOUT, last ? s.part : nullptr);
+      ktime_end(kt, KT_VALUE_ROWS, 12.0 * (double)d.NE, st);     // V, R read, dV written
       RC(check_launch("value_rows_kernel"));
       if (last) {
         hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, 5,
@@ -948,6 +985,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_VALUE_APPLY: {
       const int64_t n = d.nC_head + d.nS;
       const int g = grid_of(n, 1024);
+      const int kt = ktime_begin(st);
       hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gC, n, s.part, nullptr,
                          a.critic_step, nullptr);
       RC(check_launch("sumsq_part_kernel"));
@@ -957,6 +995,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                        nullptr, a.clip_critic_grad ? a.stats + SMI_ST_GRAD_NORM_CRITIC : nullptr,
                        nullptr};
       hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(kWG), 0, st, aa);
+      ktime_end(kt, KT_ADAM, 32.0 * (double)n, st);
       return check_launch("adam_split_kernel");
     }
     case SMI_RNN_PH_ZSTATS: {

@@ -12,8 +12,12 @@ int set_error(int code, const char* msg);
 // Optional per-launch HIP-event timing of the MFMA kernels (smi_kernel_timing):
 // each launch records (class, algorithmic flops, start/end events) on its own
 // stream.  Off by default; bench.py turns it on over its timed region.
+// Classes up to KT_CNN_BWD count algorithmic flops; the HBM-bound streaming
+// classes after them count algorithmic bytes (SURVEY §8(d) per-unit figures).
 enum { KT_GEMM_FWD = 0, KT_GEMM_DX, KT_GEMM_DW, KT_GEMM_REDUCE, KT_LSTM_FWD, KT_LSTM_BWD,
-       KT_CNN_FWD, KT_CNN_BWD, KT_COUNT };
+       KT_CNN_FWD, KT_CNN_BWD,
+       KT_GAE, KT_POLICY_STATS, KT_POLICY_GRAD, KT_VALUE_ROWS, KT_ADAM, KT_ZF_TMAJOR,
+       KT_COUNT };
 bool ktime_on();
 int ktime_begin(hipStream_t st);                       // returns a slot, -1 when off/full
 void ktime_end(int slot, int cls, double flops, hipStream_t st);
@@ -32,6 +36,15 @@ int launch_linear_bwd_dx(const float* dY, int64_t ldg, int M, int N, const float
 int launch_linear_bwd_dw(const float* dY, int64_t ldg, int M, int N, const float* X, int64_t ldx,
                          int K, float* dW, int64_t lddw, float* db, int accumulate,
                          hipStream_t st, const int* skip = nullptr);
+int launch_linear_bwd_dw2(const float* dY, int64_t ldg, int M, int N, const float* X1,
+                          int64_t ldx1, int K1, const float* X2, int64_t ldx2, int K2,
+                          float* dW1, int64_t ld1, float* dW2, int64_t ld2, float* db1,
+                          float* db2, hipStream_t st, const int* skip = nullptr);
+// grouped weight gradients: between dw_group_begin() and dw_group_flush(st) the
+// eligible launch_linear_bwd_dw / _dw2 calls are queued (their operands must
+// stay unchanged until the flush) and then run as ONE launch + ONE reduce
+int dw_group_begin();
+int dw_group_flush(hipStream_t st);
 int check_launch(const char* what);
 
 #define RC_CHECK(x) do { const int rc_ = (x); if (rc_) return rc_; } while (0)

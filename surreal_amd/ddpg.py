@@ -177,7 +177,8 @@ class DDPGLearner(object):
         passes its own `replay.batch_size` rows; every gradient is averaged over
         the ranks before clip + Adam, which equals the reference's mean loss on
         the concatenated global batch (equal shards).  Initial weights are
-        seed-identical, so parameters stay replicated."""
+        broadcast from rank 0 (learner.replicate_from_rank0), so parameters stay
+        replicated whatever seed each rank passes."""
         L.require_gpu()
         self.dp = dp if dp is not None and dp.world_size > 1 else None
         self.learner_config = lc = learner_config if isinstance(learner_config, Config) else Config(learner_config)
@@ -223,6 +224,11 @@ class DDPGLearner(object):
                                     device=self.device, generator=gen)
             self.model2 = mk2()
             self.model_target2 = mk2()
+        from .learner import replicate_from_rank0
+        flats = [self.model.actor.flat, self.model.critic.flat]
+        if self.use_double_critic:
+            flats.append(self.model2.critic.flat)
+        replicate_from_rank0(self.dp, flats)
         self._hard_update()
         dev = self.device
         self.opt = {}

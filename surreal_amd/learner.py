@@ -72,10 +72,41 @@ class TorchDistAllReduce(object):
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        # optional: a list receiving (start, end, bytes) event pairs of every
+        # all-reduce, recorded on the caller's stream (bench.py instrumentation)
+        self.timing = None
 
     def allreduce_(self, t):
+        if self.timing is not None and t.is_cuda:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group)
+            e.record()
+            self.timing.append((s, e, t.numel() * t.element_size()))
+            return t
         self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group)
         return t
+
+    def broadcast_(self, t, src=0):
+        """Rank src's tensor on every rank (replica initialisation)."""
+        self._dist.broadcast(t, src=self._dist.get_global_rank(self.group, src)
+                             if self.group is not None else src, group=self.group)
+        return t
+
+
+def replicate_from_rank0(dp, tensors):
+    """Broadcast initial parameters / filter state from rank 0 so the replicas
+    start identical whatever seed each rank passed ("identical
+    init is broadcast at start"), then check it: an all-reduced checksum of
+    every tensor must equal world_size x the local one."""
+    if dp is None or getattr(dp, 'world_size', 1) <= 1 or not hasattr(dp, 'broadcast_'):
+        return
+    for t in tensors:
+        dp.broadcast_(t)
+    sums = torch.stack([t.detach().double().sum() for t in tensors])
+    tot = dp.allreduce_(sums.clone())
+    if not torch.allclose(tot, sums * dp.world_size, rtol=1e-12, atol=1e-30):
+        raise RuntimeError('data-parallel replicas differ after the initial broadcast')
 
 
 _RNN_PHASE_NAMES = {0: 'rnn_gae', 1: 'rnn_prep', 2: 'rnn_policy_fwd', 3: 'rnn_policy_bwd',
@@ -164,6 +195,7 @@ class PPOLearner(object):
                               self.use_z_filter, self.if_pixel_input, algo.rnn, self.device, gen)
         self.model = mk()
         self.ref_target_model = mk()
+        replicate_from_rank0(dp, self._replicated_state())
         self.ref_target_model.update_target_params(self.model)
 
         net = algo.network
@@ -214,6 +246,16 @@ class PPOLearner(object):
         # optional export of the advantages as the policy epochs use them (and
         # the RNN window returns) into self._bufs['adv_used'] / ['ret_used']
         self.export_advantages = False
+
+    def _replicated_state(self):
+        """parameters and filter buffers every data-parallel replica must share"""
+        m = self.model
+        out = [m.actor.flat, m.critic.flat]
+        if m.stem_flat.numel():
+            out.append(m.stem_flat)
+        if self.use_z_filter:
+            out += [m.z_filter.running_sum, m.z_filter.running_sumsq, m.z_filter.count]
+        return out
 
     def _ev(self, name):
         """Context for recording a (start, end) event pair around one launch."""
