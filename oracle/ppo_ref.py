@@ -260,6 +260,28 @@ class PPOModelRef(nn.Module):
     def forward_critic(self, x, cells=None):                # ppo_net.py:284-315
         return self.critic(self._features(x, cells))
 
+    def forward_actor_expose_cells(self, x, cells=None):    # ppo_net.py:317-352
+        """one agent step: x (1, D) [or a (low, pixel) pair]; with the LSTM
+        the stem input is viewed (1, 1, -1) and the new (h, c) returned"""
+        pix = None
+        if self.pixel is not None:
+            x, pix = x
+        parts = []
+        if x is not None:
+            parts.append(self.z_filter.forward(x) if self.use_z_filter else x)
+        if pix is not None:
+            img = pix.reshape(-1, *pix.shape[-3:])
+            dt = self.actor.log_var.dtype
+            img = img / 255.0 if dt == torch.float32 else img.to(dt) / 255.0
+            parts.append(self.cnn_stem(img))
+        x = parts[0] if len(parts) == 1 else torch.cat(parts, -1)
+        if self.rnn:
+            x = x.view(1, 1, -1)
+            x, cells = self.rnn_stem(x, cells)
+            cells = (cells[0].detach(), cells[1].detach())
+            x = x.contiguous().view(-1, self.rnn_stem.hidden_size)
+        return self.actor(x), cells
+
     def update_target_params(self, net):                    # ppo_net.py:226-242
         self.actor.load_state_dict(net.actor.state_dict())
         self.critic.load_state_dict(net.critic.state_dict())

@@ -1,0 +1,176 @@
+"""Batched actor inference on the MI355X kernels.
+
+The reference runs one actor process per environment, each calling act() on
+ONE observation at a time (surreal/agent/ppo_agent.py:103-151,
+ddpg_agent.py:153-182).  Here N agents share one GPU model: act() takes the N
+agents' observations, stages them in one H2D copy, runs the policy forward for
+all N rows (ZFilter -> [CNN] -> one LSTM step from each agent's own cells ->
+actor MLP, on the same HIP kernels as the learner), copies the N policies back
+in one D2H, and samples in numpy in agent order — so the action of agent i is
+exactly what the i-th of N sequential reference agents sharing numpy's global
+RNG would draw.  The returned action infos keep the reference's per-agent
+format: onetime [h, c] (rnn_layer, hidden) cells before the step, persistent
+[pd] (2A,).
+
+Parameters come from the learner's modules (load_module_dict) or from a
+published numpy dict (load_numpy: ModuleDict.load, distributed/module_dict.py:47-63).
+"""
+import numpy as np
+import torch
+
+from . import _lib as L
+from .config import Config
+from .model import PPOModel
+
+
+def _np_state_to_torch(sd):
+    """ModuleDict.load: every array cast to float32 (np_cast) and wrapped."""
+    return {k: torch.from_numpy(np.asarray(v, dtype=np.float32)) for k, v in sd.items()}
+
+
+class PPOAgentBatch(object):
+    """N PPO actors (agent_mode 'training' | 'eval_stochastic' | 'eval_deterministic')."""
+
+    def __init__(self, learner_config, env_config, n_agents, agent_mode='training', device=None,
+                 seed=0):
+        L.require_gpu()
+        lc = learner_config if isinstance(learner_config, Config) else Config(learner_config)
+        ec = env_config if isinstance(env_config, Config) else Config(env_config)
+        self.n = int(n_agents)
+        self.agent_mode = agent_mode
+        self.action_dim = ec.action_spec['dim'][0]
+        self.device = torch.device(device) if device is not None else torch.device('cuda')
+        algo = lc.algo
+        self.rnn = algo.rnn if algo.rnn.if_rnn_policy else None
+        self.model = PPOModel(ec.obs_spec, self.action_dim, lc.model, True, algo.consts.init_log_sig,
+                              algo.use_z_filter, bool(ec.get('pixel_input', False)), algo.rnn,
+                              self.device, torch.Generator().manual_seed(seed))
+        log_sig_range = algo.consts.log_sig_range
+        # per-agent log-sigma exploration noise, drawn as each reference agent
+        # draws it at construction (ppo_agent.py:56-60)
+        self.noise = np.zeros(self.n)
+        if agent_mode == 'training':
+            self.noise = np.array([np.random.uniform(low=-log_sig_range, high=log_sig_range)
+                                   for _ in range(self.n)])
+        self.cells = None
+        if self.rnn is not None:
+            L_, H = self.rnn.rnn_layer, self.rnn.rnn_hidden
+            self.cells = (torch.zeros(L_, self.n, H, device=self.device),
+                          torch.zeros(L_, self.n, H, device=self.device))
+
+    def load_module_dict(self, module_dict):
+        self.model.load_state_dict(module_dict['ppo'].state_dict())
+
+    def load_numpy(self, numpy_dict):
+        self.model.load_state_dict(_np_state_to_torch(numpy_dict['ppo']))
+
+    def reset(self, agents=None):
+        """ppo_agent.py:166-180 for the given agent indices (all by default)."""
+        if self.cells is not None:
+            idx = slice(None) if agents is None else list(agents)
+            self.cells[0][:, idx] = 0
+            self.cells[1][:, idx] = 0
+
+    def act(self, obs):
+        """obs: {modality: {key: array (N, ...)}} for the N agents.
+        Returns (actions (N, A) float64, [action_info per agent]) in training
+        mode (actions only otherwise), like N reference act() calls."""
+        A = self.action_dim
+        dev_obs = {}
+        for mod, d in obs.items():
+            dev_obs[mod] = {}
+            for k, v in d.items():
+                arr = np.asarray(v)
+                dt = torch.uint8 if mod == 'pixel' else torch.float32
+                t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.uint8 if mod == 'pixel'
+                                                          else np.float32))
+                dev_obs[mod][k] = t.to(self.device, non_blocking=False).to(dt)
+        if self.cells is not None:
+            h_prev = self.cells[0].transpose(0, 1).cpu().numpy()     # (N, L, H)
+            c_prev = self.cells[1].transpose(0, 1).cpu().numpy()
+            x = self.model._stem_input(dev_obs)                       # (N, D [+F])
+            out, cells = self.model.rnn_stem(x.reshape(self.n, 1, -1).contiguous(), self.cells)
+            self.cells = cells
+            pd = self.model.actor(out.reshape(self.n, -1))
+        else:
+            pd = self.model.forward_actor(dev_obs)
+        pd = pd.cpu().numpy()                                        # one D2H
+        pd[:, A:] *= np.exp(self.noise)[:, None]          # float64 product, stored fp32 (as the reference)
+        if self.agent_mode != 'eval_deterministic':
+            act = np.random.randn(self.n, A) * pd[:, A:] + pd[:, :A]  # DiagGauss.sample, agent order
+        else:
+            act = pd[:, :A].copy()                                    # DiagGauss.maxprob
+        np.clip(act, -1, 1, out=act)
+        if self.agent_mode != 'training':
+            return act
+        infos = []
+        for i in range(self.n):
+            one = [h_prev[i], c_prev[i]] if self.cells is not None else []
+            infos.append([one, [pd[i].copy()]])
+        return act, infos
+
+
+class DDPGAgentBatch(object):
+    """N DDPG actors with their own exploration noise processes
+    (ddpg_agent.py:103-182; action_noise.py:9-40)."""
+
+    def __init__(self, learner_config, env_config, n_agents, agent_mode='training', device=None,
+                 seed=0, agent_ids=None, num_agents=None):
+        """agent_ids / num_agents: the reference agents' ids and env_config.num_agents,
+        which set each agent's exploration sigma (ddpg_agent.py:78-83: max_sigma / 3
+        for a single agent, else max_sigma * id / num_agents)."""
+        from .ddpg import DDPGModel
+        L.require_gpu()
+        lc = learner_config if isinstance(learner_config, Config) else Config(learner_config)
+        ec = env_config if isinstance(env_config, Config) else Config(env_config)
+        self.n = int(n_agents)
+        self.agent_mode = agent_mode
+        self.action_dim = ec.action_spec['dim'][0]
+        self.device = torch.device(device) if device is not None else torch.device('cuda')
+        self.model = DDPGModel(ec.obs_spec, self.action_dim, lc.model.use_layernorm,
+                               lc.model.actor_fc_hidden_sizes, lc.model.critic_fc_hidden_sizes,
+                               device=self.device, generator=torch.Generator().manual_seed(seed))
+        exp = lc.algo.exploration
+        if exp.get('param_noise_type') is not None:
+            raise NotImplementedError('surreal_amd: DDPG parameter-space noise is not built')
+        if exp.noise_type not in ('normal', 'ou_noise'):
+            raise ValueError('Noise type {} undefined.'.format(exp.noise_type))
+        self.noise_type = exp.noise_type
+        ids = np.arange(self.n) if agent_ids is None else np.asarray(agent_ids)
+        total = self.n if num_agents is None else int(num_agents)
+        self.sigma = (np.full(self.n, exp.max_sigma / 3.0) if total == 1
+                      else exp.max_sigma * (ids.astype(np.float64) / total))
+        self.theta = exp.theta
+        self.dt = exp.dt
+        self.x_prev = np.zeros((self.n, self.action_dim))
+
+    def load_module_dict(self, module_dict):
+        self.model.load_state_dict(module_dict['ddpg'].state_dict())
+
+    def load_numpy(self, numpy_dict):
+        self.model.load_state_dict(_np_state_to_torch(numpy_dict['ddpg']))
+
+    def reset(self, agents=None):
+        idx = slice(None) if agents is None else list(agents)
+        self.x_prev[idx] = 0.0
+
+    def _noise(self):
+        A = self.action_dim
+        if self.noise_type == 'normal':                  # NormalActionNoise, per agent in order
+            mu = np.zeros((self.n, A))
+            return np.random.normal(mu, np.ones((self.n, A)) * self.sigma[:, None])
+        # OrnsteinUhlenbeckActionNoise (mu = 0), per agent in order
+        x = self.x_prev + self.theta * (np.zeros((self.n, A)) - self.x_prev) * self.dt + \
+            (self.sigma[:, None] * np.sqrt(self.dt)) * np.random.normal(size=(self.n, A))
+        self.x_prev = x
+        return x
+
+    def act(self, obs):
+        """obs: (N, D) low-dim observations (or {'low_dim': {key: (N, D)}})."""
+        if isinstance(obs, dict):
+            obs = obs['low_dim'][list(obs['low_dim'])[0]]
+        x = torch.from_numpy(np.ascontiguousarray(obs, dtype=np.float32)).to(self.device)
+        a = self.model.forward_actor(x).cpu().numpy().clip(-1, 1)
+        if self.agent_mode != 'eval_deterministic':
+            a += self._noise()
+        return a.clip(-1, 1)

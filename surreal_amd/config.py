@@ -155,6 +155,14 @@ DDPG_DEFAULT_LEARNER_CONFIG = Config({
             'use_double_critic': False,
             'target_update': {'type': 'hard', 'interval': 500},
         },
+        # agent-side exploration (ddpg_configs.py:63-86); parameter noise is not built
+        'exploration': {
+            'param_noise_type': None,
+            'noise_type': 'normal',
+            'max_sigma': 1.0,
+            'theta': 0.15,
+            'dt': 1e-3,
+        },
     },
     'replay': {'batch_size': 512, 'memory_size': int(1000000 / 3),
                'sampling_start_size': 3000, 'replay_shards': 3},

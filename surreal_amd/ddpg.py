@@ -170,7 +170,7 @@ class DDPGLearner(object):
     """ddpg.py:12-440 on MI355X (low-dim, no layernorm)."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
-                 device=None, seed=0, use_graph=False, dp=None):
+                 device=None, seed=0, use_graph=False, dp=None, checkpoint_full_state=False):
         """dp: None (one GPU) or a data-parallel group exposing `world_size`,
         `rank` and `allreduce_(tensor)` (in-place SUM, stream-ordered), e.g.
         learner.TorchDistAllReduce() over RCCL (SURVEY §8(e) DDPG row).  Each rank
@@ -180,6 +180,7 @@ class DDPGLearner(object):
         broadcast from rank 0 (learner.replicate_from_rank0), so parameters stay
         replicated whatever seed each rank passes."""
         L.require_gpu()
+        self.checkpoint_full_state = bool(checkpoint_full_state)
         self.dp = dp if dp is not None and dp.world_size > 1 else None
         self.learner_config = lc = learner_config if isinstance(learner_config, Config) else Config(learner_config)
         self.env_config = ec = env_config if isinstance(env_config, Config) else Config(env_config)
@@ -484,11 +485,32 @@ class DDPGLearner(object):
     def module_dict(self):
         return {'ddpg': self.model}
 
-    def checkpoint_attributes(self):
+    def checkpoint_attributes(self):                                     # ddpg.py:383-387
+        """Reference list (+ the TD3 twin critics, which the reference omits);
+        checkpoint_full_state adds the Adam moments / steps and the hard-update
+        counter for a bit-identical continuation."""
         attrs = ['current_iteration', 'model', 'model_target']
         if self.use_double_critic:
             attrs += ['model2', 'model_target2']
+        if self.checkpoint_full_state:
+            attrs += ['optimizer_state_host']
         return attrs
+
+    @property
+    def optimizer_state_host(self):
+        out = {name: {k: o[k].detach().cpu().clone() for k in ('m', 'v', 'step', 'lr')}
+               for name, o in self.opt.items()}
+        out['target_update_counter'] = getattr(self, 'target_update_counter', 0)
+        return out
+
+    @optimizer_state_host.setter
+    def optimizer_state_host(self, d):
+        with torch.no_grad():
+            for name, o in self.opt.items():
+                for k in ('m', 'v', 'step', 'lr'):
+                    o[k].copy_(torch.as_tensor(d[name][k]).to(o[k].device))
+        if self.target_update_type == 'hard':
+            self.target_update_counter = d['target_update_counter']
 
     def _prefetcher_preprocess(self, batch):
         from .aggregator import FrameStackPreprocessor, SSARAggregator

@@ -119,14 +119,20 @@ class PPOLearner(object):
     publish_parameter/checkpoint_attributes/preprocess/_prefetcher_preprocess."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
-                 publisher=None, device=None, seed=0, dp=None):
+                 publisher=None, device=None, seed=0, dp=None, checkpoint_full_state=False):
         """dp: None (one GPU) or a data-parallel group exposing `world_size` and
         `allreduce_(tensor)` (in-place SUM, stream-ordered), e.g.
         TorchDistAllReduce() over RCCL.  Each rank passes its own shard of
         `replay.batch_size` segments; the update equals the reference's on the
-        concatenated global batch."""
+        concatenated global batch.
+        checkpoint_full_state: checkpoint_attributes() also lists the Adam
+        moments / step counters and the adaptive state (beta, clip epsilon, KL
+        record, experience counter), so a restored learner continues
+        bit-identically.  The reference checkpoints neither (ppo.py:668-678);
+        off by default, which restores exactly what the reference restores."""
         L.require_gpu()
         self.dp = dp
+        self.checkpoint_full_state = bool(checkpoint_full_state)
         self.learner_config = lc = _as_config(learner_config)
         self.env_config = ec = _as_config(env_config)
         self.session_config = _as_config(session_config)
@@ -277,7 +283,13 @@ class PPOLearner(object):
         return _Ctx()
 
     # ------------------------------------------------------------ helpers
+    def _hyper_values(self):
+        lr_a = self.actor_lr_scheduler.get_lr()[0] if hasattr(self, 'actor_lr_scheduler') else self.lr_actor
+        lr_c = self.critic_lr_scheduler.get_lr()[0] if hasattr(self, 'critic_lr_scheduler') else self.lr_critic
+        return (self.clip_epsilon, self.beta, lr_a, lr_c)
+
     def _write_hyper(self):
+        self._hyper_key = self._hyper_values()
         h = np.zeros(L.HYP_COUNT, dtype=np.float32)
         h[L.HYP_CLIP_EPS] = self.clip_epsilon
         h[L.HYP_BETA] = self.beta
@@ -573,6 +585,8 @@ class PPOLearner(object):
         """learn() as a generator of the buffers a data-parallel learner must
         all-reduce (SUM) between its launches; yields nothing when dp is None."""
         self.current_iteration += 1
+        if self._hyper_values() != self._hyper_key:       # e.g. schedulers restored from a checkpoint
+            self._write_hyper()
         batch = self._preprocess_batch_ppo(batch)
         yield from self._optimize(batch['obs'], batch['actions'], batch['rewards'],
                                   batch['obs_next'], batch['persistent_infos'],
@@ -623,9 +637,17 @@ class PPOLearner(object):
         return {'ppo': self.model}
 
     def publish_parameter(self, iteration, message=''):       # ppo.py:623-635
+        """Publish once `exp_interval` experiences were learned since the last
+        publish.  `publisher` may be a publish.DeviceParameterPublisher (an
+        asynchronous snapshot: D2D on the learner stream, D2H on a side stream,
+        serialization on a worker thread) or any callable(iteration, message,
+        module_dict)."""
         if self.exp_counter >= self.learner_config.parameter_publish.exp_interval:
             if self.publisher is not None:
-                self.publisher(iteration, message, self.module_dict())
+                if hasattr(self.publisher, 'snapshot'):
+                    self.publisher.snapshot(iteration, message)
+                else:
+                    self.publisher(iteration, message, self.module_dict())
             self._post_publish()
 
     def _post_publish(self):                                  # ppo.py:637-666
@@ -657,8 +679,49 @@ class PPOLearner(object):
         self._write_hyper()
 
     def checkpoint_attributes(self):                          # ppo.py:668-678
-        return ['model', 'ref_target_model', 'actor_lr_scheduler', 'critic_lr_scheduler',
-                'current_iteration']
+        """Attribute names for the reference Checkpoint (utils/checkpoint.py:
+        234-246: state_dict() of nn.Modules, the object itself otherwise).
+        `model` / `ref_target_model` are nn.Modules (compact state_dicts of the
+        flat device buffers), the LR schedulers plain picklable objects."""
+        attrs = ['model', 'ref_target_model', 'actor_lr_scheduler', 'critic_lr_scheduler',
+                 'current_iteration']
+        if self.checkpoint_full_state:
+            attrs += ['optimizer_state_host', 'adaptive_state']
+        return attrs
+
+    @property
+    def optimizer_state_host(self):
+        """Adam moments and step counters as host tensors (checkpointable)."""
+        return {k: v.detach().cpu().clone() for k, v in self.optimizer_state().items()}
+
+    @optimizer_state_host.setter
+    def optimizer_state_host(self, d):
+        with torch.no_grad():
+            for k, v in self.optimizer_state().items():
+                v.copy_(torch.as_tensor(d[k]).to(v.device))
+
+    @property
+    def adaptive_state(self):
+        """Host-side adaptive hyper-parameters and the device KL record."""
+        n = min(int(self.kl_count.item()), self.kl_capacity)
+        out = {'beta': self.beta, 'clip_epsilon': self.clip_epsilon, 'exp_counter': self.exp_counter,
+               'global_step': self.global_step, 'kl_record': self.kl_record_buf[:n].cpu().clone(),
+               'kl_count': self.kl_count.cpu().clone()}
+        if self.use_r_filter:
+            out['reward_filter'] = {k: v.cpu().clone() for k, v in self.reward_filter.state_dict().items()}
+        return out
+
+    @adaptive_state.setter
+    def adaptive_state(self, d):
+        self.beta, self.clip_epsilon = d['beta'], d['clip_epsilon']
+        self.exp_counter, self.global_step = d['exp_counter'], d['global_step']
+        with torch.no_grad():
+            rec = torch.as_tensor(d['kl_record'])
+            self.kl_record_buf[:rec.numel()].copy_(rec.to(self.device))
+            self.kl_count.copy_(torch.as_tensor(d['kl_count']).to(self.device))
+        if self.use_r_filter and 'reward_filter' in d:
+            self.reward_filter.load_state_dict(d['reward_filter'])
+        self._write_hyper()
 
     def preprocess(self, batch):                              # learner/base.py:321-330
         return batch

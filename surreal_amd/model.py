@@ -25,7 +25,24 @@ def mlp_param_count(d_in, h1, h2, d_out, with_log_var):
     return h1 * d_in + h1 + h2 * h1 + h2 + d_out * h2 + d_out + (d_out if with_log_var else 0)
 
 
-class _LinearView(nn.Module):
+class _FlatViews(nn.Module):
+    """Parameters that are views of a flat device buffer: state_dict() returns
+    compact copies (each tensor its own storage), so pickling a state_dict —
+    the reference Checkpoint (utils/checkpoint.py:234-246) and ModuleDict.dumps
+    (distributed/module_dict.py:22-35) both do — does not drag the whole flat
+    buffer along with every view.  load_state_dict() copies in place, into the
+    flat buffer."""
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        if not keep_vars:
+            for name in self._parameters:
+                key = prefix + name
+                if key in destination:
+                    destination[key] = destination[key].clone()
+
+
+class _LinearView(_FlatViews):
     """Holds weight/bias Parameters that are views of a flat buffer."""
 
     def __init__(self, flat, off, d_in, d_out):
@@ -46,7 +63,7 @@ class _LinearView(nn.Module):
             self.bias.copy_(b)
 
 
-class _FlatMLP(nn.Module):
+class _FlatMLP(_FlatViews):
     """Linear-ReLU-Linear-ReLU-Linear[-Tanh] over one flat device buffer."""
 
     def __init__(self, d_in, h1, h2, d_out, out_tanh, with_log_var, device, init_log_sig=0.0,
@@ -135,7 +152,7 @@ class PPO_CriticNetwork(_FlatMLP):
         return out
 
 
-class LSTMStem(nn.Module):
+class LSTMStem(_FlatViews):
     """nn.LSTM(input_size, hidden_size, 1, batch_first=True) of PPOModel
     (ppo_net.py:143-152) over ONE flat device buffer in the C-ABI LSTM layout
     [W_ih (4H, in) | W_hh (4H, H) | b_ih (4H) | b_hh (4H)] (torch's parameter
@@ -197,7 +214,7 @@ class LSTMStem(nn.Module):
         return out, (hbuf[S].unsqueeze(0).clone(), cbuf[S].unsqueeze(0).clone())
 
 
-class _ParamView(nn.Module):
+class _ParamView(_FlatViews):
     """weight/bias Parameters (torch Conv2d / Linear shapes) viewing a flat buffer."""
 
     def __init__(self, flat, off, wshape, nbias):

@@ -1,0 +1,176 @@
+"""Parameter publishing from the learner.
+
+The reference publishes by `ModuleDict(module_dict).dumps()`: every module's
+state_dict() moved to host numpy (`state_dict[key].cpu().numpy()`), the
+{name: {key: ndarray}} dict serialized and sent with {'time', 'iteration',
+'message', 'hash'} (surreal/distributed/module_dict.py:22-35,
+parameter_server.py:40-55).  Agents consume it with ModuleDict.load, so the
+state_dict keys and shapes are the wire format.
+
+MI355X side: the learner's parameters live in a handful of flat device
+buffers (model.py), so a snapshot is a few device-to-device copies into a
+snapshot arena, enqueued on the learner's stream right after the last
+learn() (stream-ordered: no host wait), followed by ONE device-to-host copy of
+the arena into pinned memory on a side stream.  The next learn() is enqueued
+immediately and overlaps the D2H; its parameter updates cannot race the copy
+because the copy reads the arena, not the parameters.  A background thread
+waits for the copy and hands the numpy dict — views of the pinned arena
+reshaped to the state_dict shapes, copied out — to the sink.
+"""
+import base64
+import hashlib
+import pickle
+import queue
+import threading
+import time
+
+import numpy as np
+import torch
+
+
+def binary_hash(binary):
+    """surreal/utils/serializer.py:55-65: 16-char hash of the serialized bytes."""
+    return base64.b64encode(hashlib.md5(binary).digest())[:16].decode('ascii').replace('/', '_')
+
+
+class _Layout(object):
+    """state_dict keys -> (storage index, byte offset, shape, dtype) over the
+    distinct device storages the tensors live in (the flat buffers)."""
+
+    def __init__(self, module_dict):
+        self.keys = []            # (module name, key, storage idx, byte offset, shape, np dtype)
+        self.storages = []        # (uint8 device view of the whole storage, arena offset, nbytes)
+        index = {}
+        off = 0
+        for name, m in module_dict.items():
+            for key, t in m.state_dict(keep_vars=True).items():
+                t = t.detach()
+                if not t.is_cuda or not t.is_contiguous():
+                    raise ValueError(f'{name}.{key}: parameters must be contiguous device tensors')
+                st = t.untyped_storage()
+                sid = st.data_ptr()
+                if sid not in index:
+                    nbytes = st.nbytes()
+                    view = torch.empty(0, dtype=torch.uint8, device=t.device).set_(st, 0, (nbytes,))
+                    index[sid] = len(self.storages)
+                    self.storages.append((view, off, nbytes))
+                    off += (nbytes + 255) // 256 * 256
+                i = index[sid]
+                boff = self.storages[i][1] + t.storage_offset() * t.element_size()
+                self.keys.append((name, key, boff, tuple(t.shape),
+                                  torch.empty(0, dtype=t.dtype).numpy().dtype))
+        self.nbytes = max(off, 256)
+
+
+class Snapshot(object):
+    """One published parameter set; numpy_dict() waits for its D2H copy."""
+
+    def __init__(self, layout, host, event, iteration, message, slot=None):
+        self._layout, self._host, self._event, self._slot = layout, host, event, slot
+        self.iteration, self.message = iteration, message
+        self.time = time.time()
+
+    def ready(self):
+        return self._event.query()
+
+    def numpy_dict(self):
+        """{module name: {state_dict key: ndarray}} as ModuleDict.dumps builds it
+        (copies, so the pinned slot can be reused)."""
+        self._event.synchronize()
+        raw = self._host.numpy()
+        out = {}
+        for name, key, boff, shape, dt in self._layout.keys:
+            n = int(np.prod(shape)) * dt.itemsize
+            out.setdefault(name, {})[key] = raw[boff:boff + n].view(dt).reshape(shape).copy()
+        return out
+
+
+class DeviceParameterPublisher(object):
+    """ParameterPublisher.publish (parameter_server.py:40-55) for the MI355X
+    learner: snapshot() is asynchronous; a worker thread serializes the numpy
+    dict and calls sink(binary, info) in publish order.
+
+    module_dict: {name: nn.Module} (learner.module_dict()).
+    sink: callable(binary, info) — e.g. a ZMQ socket's send; None keeps the
+          last published (binary, info) in `self.last` (tests, offline use).
+    serializer: the reference uses pyarrow's pa.serialize (removed from
+          current pyarrow) with pickle as its commented alternative
+          (utils/serializer.py:8-24); pickle is the default here.
+    """
+
+    def __init__(self, module_dict, sink=None, serializer=pickle.dumps, slots=2):
+        self.layout = _Layout(module_dict)
+        dev = self.layout.storages[0][0].device
+        self.device = dev
+        self.sink = sink
+        self.serializer = serializer
+        self.side = torch.cuda.Stream(device=dev)
+        self.slots = [{'dev': torch.empty(self.layout.nbytes, dtype=torch.uint8, device=dev),
+                       'host': torch.empty(self.layout.nbytes, dtype=torch.uint8).pin_memory(),
+                       'free': threading.Event()} for _ in range(slots)]
+        for sl in self.slots:
+            sl['free'].set()
+        self.next = 0
+        self.last = None
+        self.published = 0
+        self._q = queue.Queue()
+        self._err = None
+        self._worker = threading.Thread(target=self._run, daemon=True)
+        self._worker.start()
+
+    def snapshot(self, iteration=0, message=''):
+        """Enqueue the parameter snapshot on the current (learner) stream and its
+        D2H on the side stream; returns a Snapshot without waiting."""
+        if self._err is not None:
+            raise RuntimeError('parameter publisher worker failed') from self._err
+        slot = self.slots[self.next]
+        self.next = (self.next + 1) % len(self.slots)
+        slot['free'].wait()                   # the worker has copied this slot's last snapshot out
+        slot['free'].clear()
+        cur = torch.cuda.current_stream(self.device)
+        for view, off, nbytes in self.layout.storages:        # D2D, stream-ordered after learn()
+            slot['dev'][off:off + nbytes].copy_(view, non_blocking=True)
+        taken = torch.cuda.Event()
+        taken.record(cur)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(taken)
+            slot['host'].copy_(slot['dev'], non_blocking=True)   # ONE D2H, off the learner stream
+            done = torch.cuda.Event()
+            done.record(self.side)
+        snap = Snapshot(self.layout, slot['host'], done, iteration, message, slot)
+        # neither half of the slot is rewritten before the worker has copied the
+        # host half out (slot['free'], set after the D2H completed and was read)
+        self._q.put(snap)
+        return snap
+
+    def _run(self):
+        while True:
+            snap = self._q.get()
+            if snap is None:
+                return
+            try:
+                nd = snap.numpy_dict()
+                snap._slot['free'].set()
+                binary = self.serializer(nd)
+                info = {'time': snap.time, 'iteration': snap.iteration, 'message': snap.message,
+                        'hash': binary_hash(binary)}
+                if self.sink is not None:
+                    self.sink(binary, info)
+                self.last = (binary, info)
+                self.published += 1
+            except Exception as e:           # surfaced on the next snapshot() / flush()
+                self._err = e
+                snap._slot['free'].set()
+            finally:
+                self._q.task_done()
+
+    def flush(self):
+        """Wait until every snapshot taken so far has reached the sink."""
+        self._q.join()
+        if self._err is not None:
+            raise RuntimeError('parameter publisher worker failed') from self._err
+
+    def close(self):
+        self.flush()
+        self._q.put(None)
+        self._worker.join(timeout=10)

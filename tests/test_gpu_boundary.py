@@ -1,0 +1,262 @@
+"""The learner's boundary beyond learn(): checkpoint / restore, parameter
+publishing and batched actor inference.
+
+* Checkpoint: the reference Checkpoint pickles state_dict() of nn.Module
+  attributes and the objects themselves otherwise, and restores with
+  load_state_dict / setattr (surreal/utils/checkpoint.py:115-123,234-246),
+  over learner.checkpoint_attributes() (ppo.py:668-678, ddpg.py:383-387).
+  With the reference attribute list a restored learner has the reference's
+  restored state (parameters, schedulers, iteration; fresh Adam); with
+  checkpoint_full_state it continues bit-identically.
+* Publishing: ModuleDict.dumps semantics (module_dict.py:22-35) — the
+  published numpy dict equals the parameters at snapshot time bit for bit
+  while the next learn() already runs, and loads into an agent
+  (ModuleDict.load, module_dict.py:47-63).
+* Batched actors: PPOAgentBatch / DDPGAgentBatch vs N sequential reference
+  agents (oracle/agent_ref.py restating ppo_agent.py:103-151,
+  ddpg_agent.py:153-182) drawing from numpy's global RNG in agent order.
+"""
+import copy
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import agent_ref as AR
+from oracle import ddpg_ref as DR
+from oracle import ppo_ref as R
+from surreal_amd import synthetic
+from surreal_amd.agent import DDPGAgentBatch, PPOAgentBatch
+from surreal_amd.config import DDPG_DEFAULT_LEARNER_CONFIG, gym_env_config
+from surreal_amd.ddpg import DDPGLearner
+from surreal_amd.learner import PPOLearner
+from surreal_amd.publish import DeviceParameterPublisher
+from tests.helpers import env_config, load_lstm_flat, max_rel_err, ppo_config
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def ref_checkpoint_save(obj):                     # utils/checkpoint.py:234-246
+    data = {}
+    for a in obj.checkpoint_attributes():
+        v = getattr(obj, a)
+        data[a] = v.state_dict() if isinstance(v, (torch.nn.Module, torch.optim.Optimizer)) else v
+    return pickle.dumps(data)
+
+
+def ref_checkpoint_restore(obj, blob):            # utils/checkpoint.py:115-123
+    data = pickle.loads(blob)
+    for a in obj.checkpoint_attributes():
+        v = getattr(obj, a)
+        if isinstance(v, (torch.nn.Module, torch.optim.Optimizer)):
+            v.load_state_dict(data[a])
+        else:
+            setattr(obj, a, data[a])
+
+
+def _state(learner):
+    m, rm = learner.model, learner.ref_target_model
+    out = [m.actor.flat, m.critic.flat, m.stem_flat, rm.actor.flat, rm.critic.flat, rm.stem_flat]
+    if learner.use_z_filter:
+        out += [m.z_filter.running_sum, m.z_filter.running_sumsq, m.z_filter.count]
+    return [t.detach().clone() for t in out]
+
+
+def _same(a, b):
+    return all(torch.equal(x, y) for x, y in zip(a, b))
+
+
+def _ppo_setup(rnn):
+    if rnn:
+        lc = ppo_config(B=8, T=6, mode='adapt', use_z_filter=True, hidden=(32, 24), lam=1.0,
+                        epochs=(3, 3), rnn=True, rnn_hidden=16, horizon=2)
+        D, A, Hd = 9, 3, 16
+    else:
+        lc = ppo_config(B=16, T=8, mode='clip', use_z_filter=True, epochs=(3, 3))
+        D, A, Hd = 17, 6, None
+    lc.parameter_publish.exp_interval = 2 * lc.replay.batch_size
+    return lc, D, A, Hd
+
+
+@pytest.mark.parametrize('rnn', [False, True])
+def test_ppo_checkpoint_reference_and_full_state(rnn):
+    lc, D, A, Hd = _ppo_setup(rnn)
+    B, T = lc.replay.batch_size, lc.algo.n_step
+    batches = [synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=s, rnn_hidden=Hd), DEV)
+               for s in range(4)]
+    # full state: the restored learner continues bit-identically
+    l1 = PPOLearner(lc, env_config(D, A), seed=1, checkpoint_full_state=True)
+    for b in batches[:2]:
+        l1.learn(b)
+    l1.publish_parameter(2)                     # moves beta / the target model / the schedulers
+    blob = ref_checkpoint_save(l1)
+    n_param_bytes = sum(t.numel() * 4 for t in _state(l1))
+    assert len(blob) < 3 * n_param_bytes + 200000, (len(blob), n_param_bytes)   # compact state_dicts
+    l2 = PPOLearner(lc, env_config(D, A), seed=2, checkpoint_full_state=True)
+    assert not _same(_state(l1), _state(l2))
+    ref_checkpoint_restore(l2, blob)
+    assert _same(_state(l1), _state(l2))
+    assert l2.current_iteration == l1.current_iteration and l2.beta == l1.beta
+    for b in batches[2:]:
+        l1.learn(b)
+        l2.learn(b)
+        assert _same(_state(l1), _state(l2))
+        assert l1.last_stats() == l2.last_stats()
+    # reference attribute list: parameters / schedulers / iteration restored,
+    # fresh optimizer state; two restores continue identically
+    lr_ = PPOLearner(lc, env_config(D, A), seed=1)
+    for b in batches[:2]:
+        lr_.learn(b)
+    assert lr_.checkpoint_attributes() == ['model', 'ref_target_model', 'actor_lr_scheduler',
+                                           'critic_lr_scheduler', 'current_iteration']
+    blob_r = ref_checkpoint_save(lr_)
+    l3 = PPOLearner(lc, env_config(D, A), seed=3)
+    l4 = PPOLearner(lc, env_config(D, A), seed=4)
+    for ll in (l3, l4):
+        ref_checkpoint_restore(ll, blob_r)
+        assert _same(_state(lr_), _state(ll))
+        assert float(ll.actor_m.abs().sum()) == 0.0 and int(ll.actor_step.item()) == 0
+    l3.learn(batches[2])
+    l4.learn(batches[2])
+    assert _same(_state(l3), _state(l4))
+
+
+def test_ddpg_checkpoint_full_state():
+    lc = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
+    lc.replay.batch_size = 64
+    lc.algo.network.target_update = {'type': 'hard', 'interval': 2}
+    ec = gym_env_config(17, 6)
+    bs = [synthetic.to_device(synthetic.ddpg_batch(64, 17, 6, seed=s), DEV) for s in range(5)]
+    l1 = DDPGLearner(lc, ec, seed=1, checkpoint_full_state=True)
+    for b in bs[:3]:
+        l1.learn(b)
+    blob = ref_checkpoint_save(l1)
+    l2 = DDPGLearner(lc, ec, seed=2, checkpoint_full_state=True)
+    ref_checkpoint_restore(l2, blob)
+    for b in bs[3:]:
+        l1.learn(b)
+        l2.learn(b)
+    for a, b in ((l1.model.actor.flat, l2.model.actor.flat), (l1.model.critic.flat, l2.model.critic.flat),
+                 (l1.model_target.actor.flat, l2.model_target.actor.flat)):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('rnn', [False, True])
+def test_publish_snapshot_overlaps_next_learn(rnn):
+    lc, D, A, Hd = _ppo_setup(rnn)
+    B, T = lc.replay.batch_size, lc.algo.n_step
+    got = []
+    learner = PPOLearner(lc, env_config(D, A), seed=1)
+    pub = DeviceParameterPublisher(learner.module_dict(), sink=lambda b, i: got.append((b, i)))
+    learner.publisher = pub
+    batches = [synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=s, rnn_hidden=Hd), DEV)
+               for s in range(6)]
+    expected = []
+    for it, b in enumerate(batches):
+        learner.learn(b)
+        if learner.exp_counter >= lc.parameter_publish.exp_interval:
+            sd = {k: v.detach().clone() for k, v in learner.model.state_dict().items()}
+            expected.append((it, sd))
+        learner.publish_parameter(it)           # snapshot is enqueued; the next learn() follows at once
+    pub.flush()
+    assert len(expected) == 3
+    assert [i['iteration'] for _, i in got] == [it for it, _ in expected]
+    for (binary, info), (it, sd) in zip(got, expected):
+        nd = pickle.loads(binary)['ppo']
+        assert sorted(nd) == sorted(sd)
+        for k, v in sd.items():
+            assert nd[k].dtype == np.float32 and nd[k].shape == tuple(v.shape)
+            assert np.array_equal(nd[k], v.cpu().numpy()), k
+        assert len(info['hash']) == 16
+    # the published dict loads into a batched agent (ModuleDict.load)
+    agents = PPOAgentBatch(lc, env_config(D, A), 3, agent_mode='eval_deterministic', seed=9)
+    agents.load_numpy(pickle.loads(got[-1][0]))
+    for k, v in agents.model.state_dict().items():
+        assert np.array_equal(v.cpu().numpy(), pickle.loads(got[-1][0])['ppo'][k])
+    pub.close()
+
+
+@pytest.mark.parametrize('rnn,mode', [(True, 'training'), (False, 'training'),
+                                      (True, 'eval_deterministic')])
+def test_ppo_agent_batch_matches_sequential_reference_agents(rnn, mode):
+    lc, D, A, Hd = _ppo_setup(rnn)
+    lc.algo.consts.log_sig_range = 0.3
+    N, steps = 5, 4
+    ec = env_config(D, A)
+    np.random.seed(11)
+    agents = PPOAgentBatch(lc, ec, N, agent_mode=mode, seed=3)
+    zf = agents.model.z_filter
+    with torch.no_grad():                   # a non-trivial observation filter
+        zf.running_sum.add_(0.5)
+        zf.running_sumsq.add_(2.0)
+        zf.count.add_(3.0)
+    # N reference agents with the same weights, constructed in agent order from
+    # the same numpy seed (their log-sigma noise draws, ppo_agent.py:56-60)
+    np.random.seed(11)
+    hid = list(lc.model.actor_fc_hidden_sizes)
+    refs = []
+    for i in range(N):
+        ref_model = R.PPOModelRef(D, A, hid, hid, -1.0, True, rnn=rnn, rnn_hidden=Hd or 100)
+        ref_model.actor.load_flat(agents.model.actor.flat.cpu())
+        ref_model.critic.load_flat(agents.model.critic.flat.cpu())
+        if rnn:
+            load_lstm_flat(ref_model.rnn_stem, agents.model.rnn_stem.flat.cpu())
+        with torch.no_grad():
+            ref_model.z_filter.running_sum.copy_(zf.running_sum.cpu())
+            ref_model.z_filter.running_sumsq.copy_(zf.running_sumsq.cpu())
+            ref_model.z_filter.count.copy_(zf.count.cpu())
+        refs.append(AR.PPOAgentRef(ref_model, A, rnn_hidden=Hd, agent_mode=mode, log_sig_range=0.3))
+    assert np.array_equal(agents.noise, np.array([float(r.noise) for r in refs]))
+    rs = np.random.RandomState(5)
+    for step in range(steps):
+        obs = rs.randn(N, D)
+        state = np.random.get_state()
+        out = agents.act({'low_dim': {'flat_inputs': obs}})
+        np.random.set_state(state)
+        ref_out = [refs[i].act(obs[i]) for i in range(N)]
+        acts = out[0] if mode == 'training' else out
+        ref_acts = np.stack([o[0] for o in ref_out])
+        assert acts.shape == (N, A)
+        assert max_rel_err(acts, ref_acts) < 1e-5, (step, acts, ref_acts)
+        if mode == 'training':
+            for i in range(N):
+                info, rinfo = out[1][i], ref_out[i][1]
+                assert max_rel_err(info[1][0], rinfo[1][0]) < 1e-5
+                assert len(info[0]) == len(rinfo[0])
+                for a, b in zip(info[0], rinfo[0]):
+                    assert a.shape == b.shape and max_rel_err(a, b) < 1e-5
+        if step == 1:
+            agents.reset([1, 3])
+            refs[1].reset()
+            refs[3].reset()
+
+
+@pytest.mark.parametrize('noise', ['normal', 'ou_noise'])
+def test_ddpg_agent_batch_matches_sequential_reference_agents(noise):
+    lc = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
+    lc.algo.exploration.noise_type = noise
+    D, A, N = 17, 6, 4
+    ec = gym_env_config(D, A)
+    agents = DDPGAgentBatch(lc, ec, N, seed=2)
+    refs = []
+    for i in range(N):
+        actor = DR.ActorX(D, A, lc.model.actor_fc_hidden_sizes)
+        DR.load_flat(actor.params(), agents.model.actor.flat.cpu())
+        sigma = lc.algo.exploration.max_sigma * (float(i) / N)
+        nz = (AR.NormalActionNoiseRef(np.zeros(A), np.ones(A) * sigma) if noise == 'normal' else
+              AR.OUNoiseRef(np.zeros(A), sigma, lc.algo.exploration.theta, lc.algo.exploration.dt))
+        refs.append(AR.DDPGAgentRef(actor, nz))
+    rs = np.random.RandomState(3)
+    np.random.seed(7)
+    for step in range(5):
+        obs = rs.randn(N, D)
+        state = np.random.get_state()
+        a = agents.act(obs)
+        np.random.set_state(state)
+        ra = np.stack([refs[i].act(obs[i]) for i in range(N)])
+        assert a.shape == (N, A)
+        # actions live in [-1, 1]: judge against that scale (floor 1e-2), not
+        # against the largest entry of a small OU-noise step
+        assert max_rel_err(a, ra, floor=1e-2) < 1e-5, (step, a, ra)
