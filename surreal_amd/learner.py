@@ -330,8 +330,19 @@ class PPOLearner(object):
         return Config(batch) if not isinstance(batch, Config) else batch
 
     def _optimize(self, obs, actions, rewards, obs_next, persistent_infos, onetime_infos, dones):
-        """ppo.py:487-586 (low-dim model; LSTM stem via _optimize_rnn)."""
-        if self.if_rnn_policy or self.if_pixel_input:      # phase path (LSTM and/or CNN stem)
+        """ppo.py:487-586.  The low-dim MLP model runs the single-CU epoch kernels
+        when the batch and both networks fit one CU's LDS (B <= 256); an LSTM or
+        CNN stem, or a larger low-dim batch (ppo.py:408-418 takes any batch), runs
+        the multi-workgroup phase sequence of _optimize_rnn (one window of n_step
+        per trajectory without the LSTM)."""
+        c_h1, c_h2 = self.learner_config.model.critic_fc_hidden_sizes
+        a_h1, a_h2 = self.learner_config.model.actor_fc_hidden_sizes
+        phases = self.if_rnn_policy or self.if_pixel_input
+        if not phases:
+            B_, T_, D_ = self._low_dim(obs).shape
+            lds = L.lib().smi_ppo_fused_lds_bytes(B_, D_, a_h1, a_h2, self.action_dim, c_h1, c_h2)
+            phases = B_ > 256 or lds > 160 * 1024
+        if phases:
             yield from self._optimize_rnn(obs, actions, rewards, obs_next, persistent_infos,
                                           onetime_infos, dones)
             return
@@ -349,13 +360,11 @@ class PPOLearner(object):
         m, rm = self.model, self.ref_target_model
         zf = m.z_filter if self.use_z_filter else None
         rzf = rm.z_filter if self.use_z_filter else None
-        c_h1, c_h2 = self.learner_config.model.critic_fc_hidden_sizes
-        a_h1, a_h2 = self.learner_config.model.actor_fc_hidden_sizes
         values = self._buf('values', (B, T + 1))
         adv_raw = self._buf('adv_raw', (B,))
         ret = self._buf('ret', (B,))
         zp = (lambda t: L.ptr(t) if zf is not None else None)
-        # --- GAE over the critic (ppo.py:355-418)
+        # --- GAE over the critic (ppo.py:355-418) -- the fused path
         with self._ev('critic_gae_kernel'):
             L.call('smi_ppo_critic_gae', L.ptr(m.critic.flat), D, c_h1, c_h2, 1 if zf else 0,
                    zp(zf.running_sum if zf else None), zp(zf.running_sumsq if zf else None),
@@ -364,10 +373,6 @@ class PPOLearner(object):
                    L.ptr(self.gamma_tab), L.ptr(self.lam_tab), float(self.gamma),
                    float(self.gamma ** self.n_step), L.ptr(values), L.ptr(adv_raw), L.ptr(ret), st)
         # --- epochs (ppo.py:505-576)
-        lds = L.lib().smi_ppo_fused_lds_bytes(B, D, a_h1, a_h2, A, c_h1, c_h2)
-        if B > 256 or lds > 160 * 1024:
-            raise NotImplementedError('batch/model too large for the single-CU epoch kernels; '
-                                      'the multi-CU epoch path is not built yet')
         a = self._args
         dp = self.dp
         a.B_global = B * (dp.world_size if dp is not None else 1)

@@ -231,8 +231,8 @@ def pinned_run(lc, D, A, iters=1, pixel=None, seed=0, rnn_hidden=None, source='s
             as_good_as_fp32(f'{k}@{it}', [s[k]], [[x[k]] for x in svs], [s64[k]], report,
                             rtol=RTOL_STAT, factor=STAT_FACTOR)
         # advantages as the epochs use them, raw advantages, returns (per segment)
-        rnn = learner.if_rnn_policy or learner.if_pixel_input
-        seg = lambda name: [v.per_segment(getattr(v.ref, name).numpy()) for v in vs]  # noqa: E731
+        rnn = 'ret_used' in learner._bufs          # the phase path exports (B, E) windows
+        seg =lambda name: [v.per_segment(getattr(v.ref, name).numpy()) for v in vs]  # noqa: E731
         as_good_as_fp32(f'adv@{it}', learner._bufs['adv_used'].cpu(), seg('last_adv'),
                         r64.last_adv, report)
         if rnn:
@@ -262,6 +262,14 @@ def test_pinned_c2(mode):
     # BASELINE configs[1]: HalfCheetah dims, 64x64 MLP, 64 segments x n_step 50
     lc = ppo_config(B=64, T=50, mode=mode, use_z_filter=True)
     pinned_run(lc, 17, 6, iters=2)
+
+
+@pytest.mark.parametrize('mode', ['clip', 'adapt'])
+def test_pinned_mlp_large_batch_phase_path(mode):
+    # low-dim MLP policy with B > 256: the multi-workgroup phase sequence
+    # (ppo.py:408-418 takes any batch; the single-CU kernels stop at 256)
+    lc = ppo_config(B=1024, T=50, mode=mode, use_z_filter=True)
+    pinned_run(lc, 17, 6, iters=2, seed=4)
 
 
 def test_pinned_c2_early_stop():
