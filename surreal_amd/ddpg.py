@@ -238,12 +238,20 @@ class DDPGLearner(object):
         if self.use_double_critic:                      # critic_optim2 (ddpg.py:163-168)
             groups.append(('critic2', self.model2.critic.flat, net.lr_critic,
                            net.critic_regularization))
+        # gradient buffers packed for the data-parallel exchange: [critic | critic2]
+        # (independent, one all-reduce) and [actor | 12 statistics] (one more)
+        nc = self.model.critic.flat.numel()
+        na = self.model.actor.flat.numel()
+        self._critic_pack = torch.zeros(nc * (2 if self.use_double_critic else 1), device=dev)
+        self._actor_pack = torch.zeros(na + 12, device=dev)
+        packs = {'critic': self._critic_pack[:nc], 'critic2': self._critic_pack[nc:],
+                 'actor': self._actor_pack[:na]}
         for name, flat, lr, wd in groups:
             self.opt[name] = {'m': torch.zeros_like(flat), 'v': torch.zeros_like(flat),
                               'step': torch.zeros(1, dtype=torch.int32, device=dev),
                               'lr': torch.tensor([lr], dtype=torch.float32, device=dev),
-                              'wd': float(wd), 'g': torch.zeros_like(flat)}
-        self.stats_buf = torch.zeros(12, dtype=torch.float32, device=dev)
+                              'wd': float(wd), 'g': packs[name]}
+        self.stats_buf = self._actor_pack[na:]
         self._bufs = {}
         self.kernel_events = None
         # hipGraph replay of the update (learn() -> _optimize_graphed); the TD3
@@ -269,7 +277,6 @@ class DDPGLearner(object):
 
     def _adam(self, name, flat, clip_value, st):
         o = self.opt[name]
-        self._dp_mean_(o['g'])
         L.call('smi_adam_clip', _p(flat), _p(o['g']), _p(o['m']), _p(o['v']), flat.numel(),
                _p(o['step']), _p(o['lr']), 0.9, 0.999, 1e-8, o['wd'], 0.0, float(clip_value),
                None, None, st)
@@ -327,9 +334,10 @@ class DDPGLearner(object):
         L.call('smi_mse_grad', _p(q), 1, _p(y), B, _p(dq), _p(self.stats_buf[1:2]), st)
         g = self.opt['critic']['g']
         self._critic_backward(net, crit, obs, B, dq, 'c', g, st, need_obs_grad=True)
-        self._adam('critic', crit.flat,
-                   self.critic_gradient_clip_value if self.clip_critic_gradient else 0.0, st)
+        cclip = self.critic_gradient_clip_value if self.clip_critic_gradient else 0.0
         if self.use_double_critic:                      # second critic (ddpg.py:312-320)
+            # its gradient does not depend on the first critic's step: both are
+            # computed first and averaged over the ranks in one exchange
             crit2 = self.model2.critic
             q_2 = net.critic_fwd(crit2, obs, actions, B, store='q2c')
             dq_2 = net.buf('dq_2', (B, 1))
@@ -337,11 +345,13 @@ class DDPGLearner(object):
             L.call('smi_mse_grad', _p(q_2), 1, _p(y), B, _p(dq_2), _p(self.stats_buf[1:2]), st)
             self._critic_backward(net, crit2, obs, B, dq_2, 'q2c', self.opt['critic2']['g'], st,
                                   need_obs_grad=True)
-            self._adam('critic2', crit2.flat,
-                       self.critic_gradient_clip_value if self.clip_critic_gradient else 0.0, st)
             L.call('smi_ddpg_stats', _p(actions), actions.stride(0), self.action_dim, _p(rewards),
                    rewards.stride(0) if rewards.dim() == 2 else 1, _p(y), _p(q_2), 1, B,
                    _p(self.stats_buf[8:12]), st)         # [.., .., .., Q_policy2]
+        self._dp_mean_(self._critic_pack)
+        self._adam('critic', crit.flat, cclip, st)
+        if self.use_double_critic:
+            self._adam('critic2', self.model2.critic.flat, cclip, st)
         # actor update with the updated critic (ddpg.py:323-333)
         act = self.model.actor
         a = net.actor_fwd(obs, B, store='a')
@@ -350,12 +360,13 @@ class DDPGLearner(object):
         L.call('smi_neg_mean_grad', _p(q2), 1, B, _p(dq2), _p(self.stats_buf[0:1]), st)
         dA = self._critic_backward(net, crit, obs, B, dq2, 'c2', None, st, need_obs_grad=False)
         self._actor_backward(net, act, obs, B, dA, self.opt['actor']['g'], st)
-        self._adam('actor', act.flat,
-                   self.actor_gradient_clip_value if self.clip_actor_gradient else 0.0, st)
-        # statistics (ddpg.py:335-345)
+        # statistics (ddpg.py:335-345); shard means -> global means together with
+        # the actor gradient (one exchange)
         L.call('smi_ddpg_stats', _p(actions), actions.stride(0), A, _p(rewards), rs, _p(y), _p(q), 1,
                B, _p(self.stats_buf[2:6]), st)
-        self._dp_mean_(self.stats_buf)                  # shard means -> global means
+        self._dp_mean_(self._actor_pack)
+        self._adam('actor', act.flat,
+                   self.actor_gradient_clip_value if self.clip_actor_gradient else 0.0, st)
         if target_update:
             self._target_update()
 

@@ -90,8 +90,11 @@ class UniformReplay(object):
         """Bulk ring insert of packed rows (same slot sequence as repeated insert)."""
         rows = torch.as_tensor(rows, dtype=torch.float32)
         n = rows.shape[0]
-        slots = (self._next_idx + np.arange(n)) % self.memory_size
-        self.table[torch.as_tensor(slots, device=self.device)] = rows.to(self.device)
+        # more rows than slots: only the last memory_size survive a sequence of
+        # single inserts; scatter just those (no duplicate slot indices)
+        skip = max(0, n - self.memory_size)
+        slots = (self._next_idx + np.arange(skip, n)) % self.memory_size
+        self.table[torch.as_tensor(slots, device=self.device)] = rows[skip:].to(self.device)
         self._len = min(self.memory_size, self._len + n)
         self._next_idx = int((self._next_idx + n) % self.memory_size)
 

@@ -1,5 +1,8 @@
-"""World-size-2 gloo test (CPU) of the DDPG data-parallel decomposition that
-DDPGLearner(dp=...) implements (SURVEY §8(e) DDPG row): each rank holds half
+"""World-size-2 gloo test (CPU) of the MATH of the DDPG data-parallel
+decomposition that DDPGLearner(dp=...) implements (SURVEY §8(e) DDPG row).  It
+runs a torch restatement of the rank-local step, not the product's HIP learner
+(no GPU here); tests/test_gpu_ddpg_dp.py runs DDPGLearner(dp=...) itself,
+with and without gradient clipping.  Each rank holds half
 of the batch, computes the reference's mean-loss gradients on it, averages
 them over the ranks (through the product's TorchDistAllReduce) before
 clip_grad_value + Adam, and draws the TD3 smoothing noise for the global batch

@@ -181,6 +181,27 @@ def test_replay_sample_feeds_learner_with_cpython_indices():
     assert np.isfinite(list(learner.last_stats().values())).all()
 
 
+def test_replay_bulk_insert_wraps_like_single_inserts():
+    """uniform_replay.py:36-41: insert() appends until memory_size, then
+    overwrites the oldest slot; a bulk insert of more rows than slots keeps the
+    last memory_size rows in the same slots as repeated single inserts."""
+    from surreal_amd.replay import UniformReplay
+    D, A = 5, 2
+    lc = _cfg(8)
+    lc.replay.memory_size = 7
+    ec = gym_env_config(D, A)
+    bulk = UniformReplay(lc, ec, seed=1)
+    single = UniformReplay(lc, ec, seed=1)
+    rs = np.random.RandomState(3)
+    for n in (3, 18, 1, 9):
+        rows = rs.randn(n, bulk.width).astype(np.float32)
+        bulk.insert_rows(rows)
+        for r in rows:
+            single.insert_rows(r[None])
+        assert torch.equal(bulk.table.cpu(), single.table.cpu()), n
+        assert len(bulk) == len(single) and bulk._next_idx == single._next_idx
+
+
 @pytest.mark.parametrize('target', ['hard', 'soft'])
 def test_ddpg_graph_replay_bit_exact(target):
     """hipGraph replay of the update (use_graph=True) runs the same launch

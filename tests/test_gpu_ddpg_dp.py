@@ -21,16 +21,19 @@ pytestmark = pytest.mark.gpu
 B_LOC, D, A = 256, 17, 6
 
 
-def _cfg(target, td3):
+def _cfg(target, td3, clip=False):
     from tests.test_gpu_ddpg import _cfg as base
-    lc = base(B_LOC, target, False)
+    lc = base(B_LOC, target, clip)
+    if clip:                       # small enough that clip_grad_value_ acts on the averaged gradient
+        lc.algo.network.critic_gradient_value_clip = 0.02
+        lc.algo.network.actor_gradient_value_clip = 0.005
     if td3:
         lc.algo.network.use_double_critic = True
         lc.algo.network.use_action_regularization = True
     return lc
 
 
-def _worker(rank, world, port, target, td3, outdir):
+def _worker(rank, world, port, target, td3, clip, outdir):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     import torch.distributed as dist
@@ -40,7 +43,7 @@ def _worker(rank, world, port, target, td3, outdir):
     from surreal_amd.config import gym_env_config
     from surreal_amd.ddpg import DDPGLearner
     from surreal_amd.learner import TorchDistAllReduce
-    learner = DDPGLearner(_cfg(target, td3), gym_env_config(D, A), seed=2, device='cuda:0',
+    learner = DDPGLearner(_cfg(target, td3, clip), gym_env_config(D, A), seed=2, device='cuda:0',
                           dp=TorchDistAllReduce())
     init = {'actor': learner.model.actor.flat.cpu(), 'critic': learner.model.critic.flat.cpu()}
     if td3:
@@ -60,16 +63,17 @@ def _worker(rank, world, port, target, td3, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('target,td3', [('hard', False), ('soft', True)])
-def test_two_process_ddpg_dp_matches_oracle(target, td3):
+@pytest.mark.parametrize('target,td3,clip', [('hard', False, False), ('soft', True, False),
+                                             ('hard', False, True), ('soft', True, True)])
+def test_two_process_ddpg_dp_matches_oracle(target, td3, clip):
     from oracle import ddpg_ref as R
     from surreal_amd import synthetic
     from tests.test_gpu_ppo import _compare_params
     world = 2
     with tempfile.TemporaryDirectory() as outdir:
-        mp.spawn(_worker, args=(world, _free_port(), target, td3, outdir), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), target, td3, clip, outdir), nprocs=world, join=True)
         out = [torch.load(os.path.join(outdir, f'rank{r}.pt'), weights_only=True) for r in range(world)]
-    lc = _cfg(target, td3)
+    lc = _cfg(target, td3, clip)
     lc.replay.batch_size = B_LOC * world
     ref = R.DDPGLearnerRef(lc, D, A)
     R.load_flat(ref.actor.params(), out[0]['init']['actor'])
