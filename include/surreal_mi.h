@@ -110,6 +110,19 @@ int smi_reward_filter(float* rewards, int64_t n, float reward_scale, int mode,
                       float* running_sum, float* running_sumsq, float* count,
                       float eps, void* stream);
 
+/* RewardFilter under data parallelism (one process per GPU; the reference has
+ * one learner, reward_filter.py:33-42 over the whole batch).  _partial scales
+ * (and, if forward != 0, whitens with the pre-update stats) like
+ * smi_reward_filter, but leaves the filter untouched and writes this rank's
+ * {sum(r), sum(r*r), n} (fp64) to sums3[3].  After a SUM all-reduce of sums3
+ * over the ranks, _commit applies the reference update with the global sums:
+ * count += n, running_sum += sum, running_sumsq = sum of squares. */
+int smi_reward_filter_partial(float* rewards, int64_t n, float reward_scale, int forward,
+                              const float* running_sum, const float* running_sumsq,
+                              const float* count, float eps, double* sums3, void* stream);
+int smi_reward_filter_commit(const double* sums3, float* running_sum, float* running_sumsq,
+                             float* count, void* stream);
+
 /* ---------------------------------------------------------- DiagGauss ops */
 /* Replaces DiagGauss.loglikelihood / likelihood / kl / entropy
  * (surreal/model/ppo_net.py:29-72).  prob rows are [mean(A) | std(A)].

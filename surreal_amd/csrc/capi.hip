@@ -65,8 +65,9 @@ int launch_zfilter_apply(const float*, float*, int64_t, int, const float*, const
                          const float*, float, hipStream_t);
 int launch_colstats(const float*, int64_t, int, int64_t, int, float*, float*, float*,
                     hipStream_t);
-int launch_reward_filter(float*, int64_t, float, int, float*, float*, float*, float,
+int launch_reward_filter(float*, int64_t, float, int, float*, float*, float*, float, double*,
                          hipStream_t);
+int launch_reward_filter_commit(const double*, float*, float*, float*, hipStream_t);
 int launch_diag_gauss(const float*, const float*, const float*, int64_t, int, float*, float*,
                       float*, float*, hipStream_t);
 int launch_mlp_forward(const float*, int, int, int, int, int, int, const float*, int64_t,
@@ -179,8 +180,23 @@ int smi_reward_filter(float* rewards, int64_t n, float reward_scale, int mode, f
                       float* rsq, float* cnt, float eps, void* stream) {
   REQUIRE(rewards && n >= 0 && mode >= 0 && mode <= 3, "reward_filter: bad args");
   REQUIRE(mode == 0 || (rs && rsq && cnt), "reward_filter: filter buffers required");
-  return launch_reward_filter(rewards, n, reward_scale, mode, rs, rsq, cnt, eps,
+  return launch_reward_filter(rewards, n, reward_scale, mode, rs, rsq, cnt, eps, nullptr,
                               SMI_STREAM(stream));
+}
+
+int smi_reward_filter_partial(float* rewards, int64_t n, float reward_scale, int forward,
+                              const float* rs, const float* rsq, const float* cnt, float eps,
+                              double* sums3, void* stream) {
+  REQUIRE(rewards && n >= 0 && sums3 && rs && rsq && cnt, "reward_filter_partial: bad args");
+  return launch_reward_filter(rewards, n, reward_scale, (forward ? 1 : 0) | 4,
+                              const_cast<float*>(rs), const_cast<float*>(rsq),
+                              const_cast<float*>(cnt), eps, sums3, SMI_STREAM(stream));
+}
+
+int smi_reward_filter_commit(const double* sums3, float* rs, float* rsq, float* cnt,
+                             void* stream) {
+  REQUIRE(sums3 && rs && rsq && cnt, "reward_filter_commit: bad args");
+  return launch_reward_filter_commit(sums3, rs, rsq, cnt, SMI_STREAM(stream));
 }
 
 int smi_diag_gauss(const float* actions, const float* prob0, const float* prob1, int64_t rows,

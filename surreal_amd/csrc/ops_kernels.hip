@@ -156,9 +156,13 @@ colstats_small_kernel(const float* __restrict__ x, int64_t rows, int dim, int64_
 //      with the running stats from BEFORE this call's update (reward_filter.py:44-56)
 //   2: update   — count += n, running_sum += sum(r), running_sumsq = sum(r*r)
 //      (the reference's '=' instead of '+=' at reward_filter.py:42 is kept)
+//   4: partial  — instead of updating, write {sum(r), sum(r*r), n} (fp64) to
+//      out3: a data-parallel learner all-reduces them and commits the global
+//      sums with reward_filter_commit_kernel, so every rank's filter equals
+//      the one a single process would hold after the global batch
 __global__ void __launch_bounds__(kWG)
 reward_filter_kernel(float* __restrict__ r, int64_t n, float scale, int mode,
-                     float* rsum, float* rsumsq, float* rcount, float eps) {
+                     float* rsum, float* rsumsq, float* rcount, float eps, double* out3) {
   __shared__ double scr[kNW];
   float mean = 0.f, sd = 1.f;
   if (mode & 1) {
@@ -180,14 +184,28 @@ reward_filter_kernel(float* __restrict__ r, int64_t n, float scale, int mode,
       r[i] = x;
     }
   }
-  if (mode & 2) {
+  if (mode & 6) {
     const double t1 = block_sum_d(a1, scr);
     const double t2 = block_sum_d(a2, scr);
     if (threadIdx.x == 0) {
-      rcount[0] = rcount[0] + (float)n;
-      rsum[0] = rsum[0] + (float)t1;
-      rsumsq[0] = (float)t2;
+      if (mode & 4) {
+        out3[0] = t1; out3[1] = t2; out3[2] = (double)n;
+      } else {
+        rcount[0] = rcount[0] + (float)n;
+        rsum[0] = rsum[0] + (float)t1;
+        rsumsq[0] = (float)t2;
+      }
     }
+  }
+}
+
+// the update of mode 2 from (all-reduced) sums {sum, sumsq, n}
+__global__ void reward_filter_commit_kernel(const double* __restrict__ s3, float* rsum,
+                                            float* rsumsq, float* rcount) {
+  if (threadIdx.x == 0) {
+    rcount[0] = rcount[0] + (float)s3[2];
+    rsum[0] = rsum[0] + (float)s3[0];
+    rsumsq[0] = (float)s3[1];
   }
 }
 
@@ -620,10 +638,15 @@ int launch_colstats(const float* x, int64_t rows, int dim, int64_t stride, int m
 }
 
 int launch_reward_filter(float* r, int64_t n, float scale, int use, float* s, float* sq,
-                         float* c, float eps, hipStream_t st) {
+                         float* c, float eps, double* out3, hipStream_t st) {
   hipLaunchKernelGGL(reward_filter_kernel, dim3(1), dim3(kWG), 0, st, r, n, scale, use, s, sq,
-                     c, eps);
+                     c, eps, out3);
   return check_launch("reward_filter_kernel");
+}
+
+int launch_reward_filter_commit(const double* s3, float* s, float* sq, float* c, hipStream_t st) {
+  hipLaunchKernelGGL(reward_filter_commit_kernel, dim3(1), dim3(64), 0, st, s3, s, sq, c);
+  return check_launch("reward_filter_commit_kernel");
 }
 
 int launch_diag_gauss(const float* a, const float* p0, const float* p1, int64_t rows, int A,

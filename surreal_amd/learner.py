@@ -187,9 +187,6 @@ class PPOLearner(object):
             raise NotImplementedError('surreal_amd: the LSTM policy supports rnn_layer == 1 '
                                       '(the reference default)')
         self.if_pixel_input = bool(ec.get('pixel_input', False))
-        if dp is not None and self.use_r_filter:
-            raise NotImplementedError('surreal_amd: RewardFilter under data parallelism needs a '
-                                      'global reward all-reduce (not built yet)')
 
         anneal = algo.network.anneal
         num_updates = int(anneal.frames_to_anneal / lc.parameter_publish.exp_interval)
@@ -315,13 +312,18 @@ class PPOLearner(object):
         return parts[0] if len(parts) == 1 else torch.cat(parts, -1)
 
     # ------------------------------------------------------- reference API
-    def _preprocess_batch_ppo(self, batch):                 # ppo.py:420-484
+    def _preprocess_batch_ppo(self, batch, rf_sums=None):   # ppo.py:420-484
+        """rf_sums (data parallel): the RewardFilter whitens with its current
+        stats and writes this rank's {sum, sumsq, n} there instead of updating;
+        the caller all-reduces them and commits (RewardFilter.commit_)."""
         if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
             batch = self._arena.stage(batch)          # one pinned buffer, one H2D
         else:
             batch = dict(batch)
         rewards = batch['rewards'].to(torch.float32).contiguous().clone()   # filtered in place
-        if self.use_r_filter:
+        if self.use_r_filter and rf_sums is not None:
+            self.reward_filter.scale_forward_partial_(rewards, self.reward_scale, rf_sums)
+        elif self.use_r_filter:
             self.reward_filter.scale_forward_update_(rewards, self.reward_scale)
         elif self.reward_scale != 1.0:
             L.call('smi_reward_filter', L.ptr(rewards), rewards.numel(), float(self.reward_scale),
@@ -592,7 +594,15 @@ class PPOLearner(object):
         self.current_iteration += 1
         if self._hyper_values() != self._hyper_key:       # e.g. schedulers restored from a checkpoint
             self._write_hyper()
-        batch = self._preprocess_batch_ppo(batch)
+        if self.dp is not None and self.use_r_filter:
+            # global reward statistics: one 3-double all-reduce (reward_filter.py:33-42
+            # over the global batch, as one learner would see it)
+            rf = self._buf('rf_sums', (3,), torch.float64)
+            batch = self._preprocess_batch_ppo(batch, rf_sums=rf)
+            yield rf
+            self.reward_filter.commit_(rf)
+        else:
+            batch = self._preprocess_batch_ppo(batch)
         yield from self._optimize(batch['obs'], batch['actions'], batch['rewards'],
                                   batch['obs_next'], batch['persistent_infos'],
                                   batch['onetime_infos'], batch['dones'])

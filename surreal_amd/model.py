@@ -353,6 +353,19 @@ class RewardFilter(nn.Module):
         self._run(rewards, scale, 3)
         return rewards
 
+    def scale_forward_partial_(self, rewards, scale, sums3):
+        """Data parallel: rewards*scale and whitening as scale_forward_update_,
+        the update deferred: this rank's {sum, sumsq, n} (fp64) go to sums3."""
+        L.call('smi_reward_filter_partial', L.ptr(rewards), rewards.numel(), float(scale), 1,
+               L.ptr(self.running_sum), L.ptr(self.running_sumsq), L.ptr(self.count),
+               float(self.eps), L.ptr(sums3), L.stream(rewards.device))
+        return rewards
+
+    def commit_(self, sums3):
+        """the reference update (reward_filter.py:33-42) from all-reduced sums"""
+        L.call('smi_reward_filter_commit', L.ptr(sums3), L.ptr(self.running_sum),
+               L.ptr(self.running_sumsq), L.ptr(self.count), L.stream(sums3.device))
+
     def reward_mean(self):
         return (self.running_sum / self.count).item()
 

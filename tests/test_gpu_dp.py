@@ -58,13 +58,17 @@ def _lockstep(learners, shards):
         nphase += 1
 
 
-@pytest.mark.parametrize('mode,world,B_loc', [('clip', 2, 32), ('adapt', 2, 32), ('adapt', 4, 16),
-                                              ('clip', 3, 7)])
-def test_dp_equals_global_batch(mode, world, B_loc):
+@pytest.mark.parametrize('mode,world,B_loc,rf', [('clip', 2, 32, False), ('adapt', 2, 32, False),
+                                                 ('adapt', 4, 16, False), ('clip', 3, 7, False),
+                                                 ('adapt', 2, 32, True), ('clip', 3, 7, True)])
+def test_dp_equals_global_batch(mode, world, B_loc, rf):
+    # rf: RewardFilter on (reward_scale 2): each rank whitens with the shared
+    # pre-update stats and the update uses the all-reduced global sums
     T, D, A = 12, 17, 6
-    lc = ppo_config(B=B_loc, T=T, mode=mode, use_z_filter=True)
+    kw = dict(use_r_filter=True, reward_scale=2.0) if rf else {}
+    lc = ppo_config(B=B_loc, T=T, mode=mode, use_z_filter=True, **kw)
     learners = [PPOLearner(lc, env_config(D, A), seed=21, dp=_Group(world)) for _ in range(world)]
-    lcg = ppo_config(B=B_loc * world, T=T, mode=mode, use_z_filter=True)
+    lcg = ppo_config(B=B_loc * world, T=T, mode=mode, use_z_filter=True, **kw)
     ref = R.PPOLearnerRef(lcg, D, A)
     copy_weights_to_oracle(learners[0], ref)
     report = {}
@@ -73,7 +77,7 @@ def test_dp_equals_global_batch(mode, world, B_loc):
         dev = synthetic.to_device(batch, 'cuda')
         shards = [_shard(dev, r * B_loc, (r + 1) * B_loc) for r in range(world)]
         nphase = _lockstep(learners, shards)
-        assert nphase == 1 + max(11, 10) + 1          # moments, epochs, z-filter
+        assert nphase == int(rf) + 1 + max(11, 10) + 1   # [reward sums,] moments, epochs, z-filter
         rstats = ref.learn(oracle_batch(batch))
         stats = learners[0].last_stats()
         assert stats['epochs_run'] == rstats['epochs_run']
@@ -89,6 +93,12 @@ def test_dp_equals_global_batch(mode, world, B_loc):
             assert torch.equal(l.model.actor.flat, learners[0].model.actor.flat)
             assert torch.equal(l.model.critic.flat, learners[0].model.critic.flat)
             assert torch.equal(l.model.z_filter.running_sum, learners[0].model.z_filter.running_sum)
+        if rf:
+            rfl, rfr = learners[0].reward_filter, ref.reward_filter
+            for b in ('running_sum', 'running_sumsq', 'count'):
+                got, exp = float(getattr(rfl, b).item()), float(getattr(rfr, b).item())
+                assert abs(got - exp) <= 1e-5 * abs(exp) + 1e-6, (it, b, got, exp)
+                assert all(torch.equal(getattr(l.reward_filter, b), getattr(rfl, b)) for l in learners)
         zf, rzf = learners[0].model.z_filter, ref.model.z_filter
         assert max_rel_err(zf.running_sum.cpu(), rzf.running_sum) < 1e-5
         assert float(zf.count.item()) == float(rzf.count.item())
