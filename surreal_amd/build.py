@@ -39,7 +39,9 @@ VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             # dW-kernel experiments (tools/dwd_exp.sh)
             'p8': ['-DSMI_DWD_P=8'], 'p6': ['-DSMI_DWD_P=6'], 'occ1': ['-DSMI_DWD_OCC=1'],
             # LSTM activation A/B (the pre-round-2 cancelling tanh)
-            'oldtanh': ['-DSMI_OLD_TANH']}
+            'oldtanh': ['-DSMI_OLD_TANH'],
+            # dW: the checked loop everywhere (A/B of the unchecked full-slab loop)
+            'nofast': ['-DSMI_DWD_FAST=0']}
 
 
 def lib_path(variant=None):

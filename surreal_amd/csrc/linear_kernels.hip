@@ -684,6 +684,83 @@ __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m
   }
 }
 
+// Unchecked streaming loop over a slab whose rows are all valid (every slab
+// but possibly the last: slab lengths are multiples of the prefetch window)
+// with 16-byte operands: the lane's operand addresses are formed once and
+// advanced by RS rows per step, so a step is its loads and MFMAs only — no
+// per-step 64-bit row products, clamps, zero-row selects or exec-masked
+// branches (the checked loop spends ~40 VALU/SALU ops per step on them).
+// The last DWD_P steps are peeled without loads (no reads past the slab).
+// Same MFMA chains in the same order as the checked loop: bit-identical.
+#ifndef SMI_DWD_FAST
+#define SMI_DWD_FAST 1
+#endif
+__device__ __forceinline__ bool use_dwd_fast() { return SMI_DWD_FAST != 0; }
+
+template <int MT, int NT, int NB, int RS>
+__device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nsteps, int m0, int n0,
+                                              int bdata, f32x4 (&acc)[MT][NT]) {
+  static_assert(MT == 4, "fast dW loop: 4 m sub-tiles (float4 A loads)");
+  constexpr int NH = NB / 4;
+  const int li = threadIdx.x & 15;
+  const float* pa = g.A + (int64_t)rw * g.a_cs + min(m0 + 4 * li, g.M - 4);
+  const int64_t sa = (int64_t)RS * g.a_cs;
+  const float* pb[NH];
+  int64_t sb[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int cb = n0 + 64 * h + 4 * li;
+    if (cb < bdata) {
+      if (g.B2 && cb >= g.split_col) {
+        pb[h] = g.B2 + (int64_t)rw * g.b2_rs + (cb - g.split_col);
+        sb[h] = (int64_t)RS * g.b2_rs;
+      } else {
+        pb[h] = g.B + (int64_t)rw * g.b_rs + cb;
+        sb[h] = (int64_t)RS * g.b_rs;
+      }
+    } else {
+      pb[h] = cb == g.ones_col ? g_dwd_one : g_dwd_zero;
+      sb[h] = 0;
+    }
+  }
+  float4 av[DWD_P], bv[DWD_P][NH];
+  auto load = [&](int p) {
+    av[p] = *reinterpret_cast<const float4*>(pa);
+    pa += sa;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      bv[p][h] = *reinterpret_cast<const float4*>(pb[h]);
+      pb[h] += sb[h];
+    }
+  };
+  auto step = [&](int p) {
+    const float a4[4] = {av[p].x, av[p].y, av[p].z, av[p].w};
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float4 q = bv[p][b >> 2];
+      const float bb = (b & 3) == 0 ? q.x : (b & 3) == 1 ? q.y : (b & 3) == 2 ? q.z : q.w;
+#pragma unroll
+      for (int a = 0; a < MT; ++a) acc[a][b] = mfma4(a4[a], bb, acc[a][b]);
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < DWD_P; ++p) load(p);
+  // sched_barrier pins each refill right behind the MFMAs of the step it
+  // replaces: without it the scheduler sinks all DWD_P refills to the end of
+  // the unrolled body and the next iteration waits on them (vmcnt(9..0)), i.e.
+  // no prefetch distance at all
+  for (int s0 = DWD_P; s0 < nsteps; s0 += DWD_P) {
+#pragma unroll
+    for (int p = 0; p < DWD_P; ++p) {
+      step(p);
+      load(p);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < DWD_P; ++p) step(p);
+}
+
 // WV waves per workgroup (4: one per SIMD; 8: two per SIMD, each wave takes
 // every WV-th 4-row step of the slab, so a SIMD interleaves two waves' loads
 // and MFMAs; the waves' sums meet in LDS in a fixed tree order)
@@ -723,11 +800,30 @@ __device__ __forceinline__ void dwd_tile(const GemmArgs& g, const TileIdx ti, fl
 #pragma unroll
           for (int a = 0; a < MT; ++a) acc[a][b] = mfma4(av[p][a], bv[p][b], acc[a][b]);
         dwd_load<MT, NT, VA, VB, NB>(g, rw + RS * (s0 + p + DWD_P), ke, m0, n0, bdata, av[p], bv[p]);
+        __builtin_amdgcn_sched_barrier(0);     // keep the refill here (see dwd_main_fast)
       }
     }
   };
-  if (NT == 8 && n0 + 64 >= g.N) mainloop(std::integral_constant<int, (NT > 4 ? 4 : NT)>{});
-  else mainloop(std::integral_constant<int, NT>{});
+  // full slabs of 16-byte operands take the unchecked streaming loop
+  bool fast = false;
+  if constexpr (VA && VB && MT == 4)
+    fast = use_dwd_fast() && nsteps >= DWD_P && nsteps % DWD_P == 0 && kb + nsteps * RS <= ke;
+  constexpr int NBH = NT > 4 ? 4 : NT;
+  if (NT == 8 && n0 + 64 >= g.N) {
+    if constexpr (VA && VB && MT == 4) {
+      if (fast) dwd_main_fast<MT, NT, NBH, RS>(g, rw, nsteps, m0, n0, bdata, acc);
+      else mainloop(std::integral_constant<int, NBH>{});
+    } else {
+      mainloop(std::integral_constant<int, NBH>{});
+    }
+  } else {
+    if constexpr (VA && VB && MT == 4) {
+      if (fast) dwd_main_fast<MT, NT, NT, RS>(g, rw, nsteps, m0, n0, bdata, acc);
+      else mainloop(std::integral_constant<int, NT>{});
+    } else {
+      mainloop(std::integral_constant<int, NT>{});
+    }
+  }
   // combine the waves in a fixed tree: at stride h, waves [h, 2h) add into
   // waves [0, h), two at a time through the two LDS buffers (WV = 4 gives
   // (w0 + w2) + (w1 + w3))

@@ -71,6 +71,13 @@ def test_dp_equals_global_batch(mode, world, B_loc, rf):
     lcg = ppo_config(B=B_loc * world, T=T, mode=mode, use_z_filter=True, **kw)
     ref = R.PPOLearnerRef(lcg, D, A)
     copy_weights_to_oracle(learners[0], ref)
+    if rf:
+        # whitened rewards carry the filter's fp32 rounding (rank sums in fp64,
+        # the reference's one fp32 sum): after 10 + 10 Adam epochs the learner
+        # is compared with the fp64 oracle against the fp32 envelope
+        # (test_gpu_parity_pinned.py), the bar every learn() parity test uses
+        from tests.test_gpu_parity_pinned import _envelope, as_good_as_fp32, print_report
+        r64, vs = _envelope(learners[0], lcg, D, A, None, n_ulp=4)
     report = {}
     for it in range(2):
         batch = synthetic.ppo_batch(B_loc * world, T, D, A, seed=300 + it)
@@ -81,6 +88,24 @@ def test_dp_equals_global_batch(mode, world, B_loc, rf):
         rstats = ref.learn(oracle_batch(batch))
         stats = learners[0].last_stats()
         assert stats['epochs_run'] == rstats['epochs_run']
+        if rf:
+            ob = oracle_batch(batch)
+            r64.learn(ob)
+            for k, v in enumerate(vs):
+                v.learn(ob, 300 + it)
+            rep = {}
+            for name, got, ref_of in (('actor', learners[0].model.actor.flat, lambda r: r.model.actor.flat()),
+                                      ('critic', learners[0].model.critic.flat, lambda r: r.model.critic.flat())):
+                as_good_as_fp32(f'{name}@{it}', got.cpu(), [ref_of(v.ref) for v in vs], ref_of(r64), rep)
+            for b in ('running_sum', 'running_sumsq', 'count'):
+                got, exp = float(getattr(learners[0].reward_filter, b).item()), float(getattr(r64.reward_filter, b).item())
+                assert abs(got - exp) <= 1e-6 * abs(exp) + 1e-6, (it, b, got, exp)
+                assert all(torch.equal(getattr(l.reward_filter, b), getattr(learners[0].reward_filter, b))
+                           for l in learners)
+            print_report(rep)
+            for l in learners[1:]:
+                assert torch.equal(l.model.actor.flat, learners[0].model.actor.flat)
+            continue
         for k in ('_surr_loss', '_pol_kl', '_entropy', '_val_loss', '_avg_return_targ',
                   '_avg_behave_likelihood', '_avg_is_weight', '_ref_behave_diff',
                   'grad_norm_actor', 'grad_norm_critic', '_val_explained_var'):
@@ -93,12 +118,6 @@ def test_dp_equals_global_batch(mode, world, B_loc, rf):
             assert torch.equal(l.model.actor.flat, learners[0].model.actor.flat)
             assert torch.equal(l.model.critic.flat, learners[0].model.critic.flat)
             assert torch.equal(l.model.z_filter.running_sum, learners[0].model.z_filter.running_sum)
-        if rf:
-            rfl, rfr = learners[0].reward_filter, ref.reward_filter
-            for b in ('running_sum', 'running_sumsq', 'count'):
-                got, exp = float(getattr(rfl, b).item()), float(getattr(rfr, b).item())
-                assert abs(got - exp) <= 1e-5 * abs(exp) + 1e-6, (it, b, got, exp)
-                assert all(torch.equal(getattr(l.reward_filter, b), getattr(rfl, b)) for l in learners)
         zf, rzf = learners[0].model.z_filter, ref.model.z_filter
         assert max_rel_err(zf.running_sum.cpu(), rzf.running_sum) < 1e-5
         assert float(zf.count.item()) == float(rzf.count.item())
