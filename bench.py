@@ -100,14 +100,14 @@ def spawn_ranks(n):
 
 # kernel class (smi_kernel_timing) -> kernel-name patterns of its launches
 CLASS_KERNELS = {
-    'gemm_dw': ('gemm_dwd_kernel', 'gemm_dw128_kernel', 'gemm_kernel<2,'),
+    'gemm_dw': ('gemm_dwd_kernel', 'gemm_dwd_group_kernel', 'gemm_dw128_kernel', 'gemm_kernel<2,'),
     'gemm_fwd': ('gemm_panel_kernel<0,', 'gemm_kernel<0,', 'gemm_smallk_fwd_kernel'),
     'gemm_dx': ('gemm_panel_kernel<1,', 'gemm_kernel<1,', 'dx_smallk_kernel'),
     'lstm_fwd': ('lstm_fwd',), 'lstm_bwd': ('lstm_bwd',),
     'cnn_fwd': ('cnn_fwd_kernel',), 'cnn_bwd': ('cnn_bwd_kernel',),
 }
-PMC_TRAFFIC = {'c3': 'profiles/r01/pmc_traffic_c3_final5.json',
-               'c5': 'profiles/r01/pmc_traffic_c5_final5.json'}
+PMC_TRAFFIC = {'c3': 'profiles/r02/pmc_traffic_c3_r2.json',
+               'c5': 'profiles/r02/pmc_traffic_c5_r2.json'}
 
 
 def pmc_traffic(config, cls):
@@ -439,6 +439,9 @@ def main():
     ap.add_argument('--config', choices=['c2', 'c3', 'c4', 'c5'], default='c3')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
+    ap.add_argument('--local-segments', type=int, default=None,
+                    help='segments per rank (overrides --scaling): e.g. 128 runs on one GPU '
+                         'the share one rank of an 8-GPU strong-scaling C3 job computes')
     ap.add_argument('--scaling', choices=['strong', 'weak'], default=None,
                     help='strong (default for c3/c5): the workload\'s global batch split over '
                          'the ranks; weak (c2, c4): the per-GPU batch fixed')
@@ -463,6 +466,9 @@ def main():
         if dims['B_global'] % world:
             raise SystemExit(f'global batch {dims["B_global"]} does not split over {world} ranks')
         lc.replay.batch_size = dims['B_global'] // world
+    if args.local_segments:
+        lc.replay.batch_size = args.local_segments
+        scaling = 'weak'
     B, T = lc.replay.batch_size, lc.algo.n_step
     D, A = dims['D'], dims['A']
     dp = TorchDistAllReduce() if dist is not None else None

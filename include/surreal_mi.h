@@ -508,6 +508,21 @@ int smi_tanh_backward(const float* dy, int64_t ldg, const float* y, int64_t ldy,
 /* dst[r][0:cols] = src[r][0:cols] (strided) — the action block of torch.cat((h, a), 1) */
 int smi_copy_cols(const float* src, int64_t lds, int64_t rows, int cols, float* dst,
                   int64_t ldd, void* stream);
+/* LayerNorm blocks of the DDPG networks with use_layernorm=True (builders.py:
+ * 41-48, 65-75: Linear -> ReLU -> L.LayerNorm(1)); L.LayerNorm(1) is taken as
+ * torch.nn.LayerNorm(n) over the last dimension (biased variance, eps inside
+ * the square root, affine), n <= 1024.  forward: y = (x - mean) rstd gamma +
+ * beta per row, mean / rstd [rows] saved for the backward.  backward: dx from
+ * dy (relu_input != 0: zero where x <= 0, the ReLU before the norm), and
+ * dgamma = sum_rows dy xhat, dbeta = sum_rows dy (overwritten; fixed order). */
+int smi_layernorm_forward(const float* x, int64_t ldx, int64_t rows, int n, const float* gamma,
+                          const float* beta, float eps, float* y, int64_t ldy, float* mean,
+                          float* rstd, void* stream);
+int smi_layernorm_backward(const float* dy, int64_t ldg, const float* x, int64_t ldx,
+                           const float* mean, const float* rstd, const float* gamma, int64_t rows,
+                           int n, int relu_input, float* dx, int64_t lddx, float* dgamma,
+                           float* dbeta, void* stream);
+
 /* target <- tau*src + (1-tau)*target (soft target update, ddpg.py:409-417) */
 int smi_soft_update(float* target, const float* src, int64_t n, float tau, void* stream);
 /* action_norm, rewards, Q_target, Q_policy means of ddpg.py:335-345 -> stats4 */

@@ -68,6 +68,11 @@ int launch_colstats(const float*, int64_t, int, int64_t, int, float*, float*, fl
 int launch_reward_filter(float*, int64_t, float, int, float*, float*, float*, float, double*,
                          hipStream_t);
 int launch_reward_filter_commit(const double*, float*, float*, float*, hipStream_t);
+int launch_layernorm_fwd(const float*, int64_t, int64_t, int, const float*, const float*, float,
+                         float*, int64_t, float*, float*, hipStream_t);
+int launch_layernorm_bwd(const float*, int64_t, const float*, int64_t, const float*, const float*,
+                         const float*, int64_t, int, int, float*, int64_t, float*, float*,
+                         hipStream_t);
 int launch_diag_gauss(const float*, const float*, const float*, int64_t, int, float*, float*,
                       float*, float*, hipStream_t);
 int launch_mlp_forward(const float*, int, int, int, int, int, int, const float*, int64_t,
@@ -359,6 +364,24 @@ int smi_tanh_backward(const float* dy, int64_t ldg, const float* y, int64_t ldy,
   REQUIRE(dy && y && dz && rows >= 0 && cols > 0, "tanh_backward: bad args");
   if (rows == 0) return SMI_OK;
   return launch_tanh_backward(dy, ldg, y, ldy, rows, cols, dz, ldz, SMI_STREAM(stream));
+}
+
+int smi_layernorm_forward(const float* x, int64_t ldx, int64_t rows, int n, const float* gamma,
+                          const float* beta, float eps, float* y, int64_t ldy, float* mean,
+                          float* rstd, void* stream) {
+  REQUIRE(x && gamma && beta && y && mean && rstd && rows >= 0, "layernorm_forward: bad args");
+  return launch_layernorm_fwd(x, ldx, rows, n, gamma, beta, eps, y, ldy, mean, rstd,
+                              SMI_STREAM(stream));
+}
+
+int smi_layernorm_backward(const float* dy, int64_t ldg, const float* x, int64_t ldx,
+                           const float* mean, const float* rstd, const float* gamma, int64_t rows,
+                           int n, int relu_input, float* dx, int64_t lddx, float* dgamma,
+                           float* dbeta, void* stream) {
+  REQUIRE(dy && x && mean && rstd && gamma && dx && dgamma && dbeta && rows >= 0,
+          "layernorm_backward: bad args");
+  return launch_layernorm_bwd(dy, ldg, x, ldx, mean, rstd, gamma, rows, n, relu_input, dx, lddx,
+                              dgamma, dbeta, SMI_STREAM(stream));
 }
 
 int smi_copy_cols(const float* src, int64_t lds, int64_t rows, int cols, float* dst, int64_t ldd,

@@ -8,6 +8,9 @@
 //   copy_cols       write the action block of the critic's concat input
 //   soft_update     target <- tau * src + (1 - tau) * target
 //   ddpg_stats      action_norm, rewards, Q_target, Q_policy means (ddpg.py:335-345)
+//   layernorm       the use_layernorm=True blocks of ActorNetworkX / CriticNetworkX
+//                   (builders.py:41-48,65-75: Linear -> ReLU -> L.LayerNorm(1)),
+//                   forward and backward (dx through the ReLU, dgamma, dbeta)
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
 
@@ -101,6 +104,123 @@ static int grid_of(int64_t n) {
   return (int)(g < 2048 ? g : 2048);
 }
 
+// ---------------------------------------------------------------- LayerNorm
+// torchx's L.LayerNorm(1) normalises the last dimension; it is taken here as
+// torch.nn.LayerNorm(n): biased variance, eps inside the square root, affine
+// gamma / beta (torchx is not available: parity unpinned).
+// One wave per row (n <= 64 * LN_MAXV), the row held in registers: mean, then
+// the centred second moment (two passes over registers, no cancellation).
+constexpr int LN_MAXV = 16;
+
+__global__ void __launch_bounds__(kWG)
+layernorm_fwd_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int n,
+                     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                     float* __restrict__ y, int64_t ldy, float* __restrict__ mean,
+                     float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + r * ldx;
+  float v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < n ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mu = wave_sum(s) / (float)n;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    const float d = v[i] - mu;
+    q += c < n ? d * d : 0.f;
+  }
+  const float rs = 1.f / sqrtf(wave_sum(q) / (float)n + eps);
+  float* yr = y + r * ldy;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n) yr[c] = (v[i] - mu) * rs * gamma[c] + beta[c];
+  }
+  if (lane == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
+// dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma, xhat = (x - mu) rstd,
+// then through the ReLU that produced x (relu != 0: dx = 0 where x <= 0);
+// per-block partials of dgamma = sum dy xhat and dbeta = sum dy ([nblk][2][n]),
+// the block's waves combined in a fixed order
+__global__ void __launch_bounds__(kWG)
+layernorm_bwd_kernel(const float* __restrict__ dy, int64_t ldg, const float* __restrict__ x,
+                     int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
+                     const float* __restrict__ gamma, int64_t rows, int n, int relu,
+                     float* __restrict__ dx, int64_t lddx, float* __restrict__ part) {
+  __shared__ float red[kWG / 64][2][64 * LN_MAXV];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dg[LN_MAXV], db[LN_MAXV];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) dg[i] = db[i] = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * (kWG / 64) + wave; r < rows;
+       r += (int64_t)gridDim.x * (kWG / 64)) {
+    const float mu = mean[r], rs = rstd[r];
+    float xh[LN_MAXV], g[LN_MAXV];
+    bool keep[LN_MAXV];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      const bool ok = c < n;
+      const float xv = ok ? x[r * ldx + c] : 0.f;
+      const float d = ok ? dy[r * ldg + c] : 0.f;
+      xh[i] = ok ? (xv - mu) * rs : 0.f;
+      g[i] = ok ? d * gamma[c] : 0.f;
+      a += g[i];
+      b += g[i] * xh[i];
+      dg[i] += d * xh[i];
+      db[i] += d;
+      keep[i] = !relu || xv > 0.f;
+    }
+    const float am = wave_sum(a) / (float)n, bm = wave_sum(b) / (float)n;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < n) dx[r * lddx + c] = keep[i] ? rs * (g[i] - am - xh[i] * bm) : 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    red[wave][0][lane + 64 * i] = dg[i];
+    red[wave][1][lane + 64 * i] = db[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < n; c += kWG) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < kWG / 64; ++w) {
+      sg += red[w][0][c];
+      sb += red[w][1][c];
+    }
+    part[((int64_t)blockIdx.x * 2) * n + c] = sg;
+    part[((int64_t)blockIdx.x * 2 + 1) * n + c] = sb;
+  }
+}
+
+// dgamma / dbeta: block partials summed in block order
+__global__ void __launch_bounds__(kWG)
+layernorm_param_grad_kernel(const float* __restrict__ part, int nb, int n, float* dgamma,
+                            float* dbeta) {
+  const int c = blockIdx.x * kWG + threadIdx.x;
+  if (c >= 2 * n) return;
+  const int which = c / n, col = c - which * n;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[((int64_t)b * 2 + which) * n + col];
+  (which ? dbeta : dgamma)[col] = s;
+}
+
 int launch_mse_grad(const float* q, int64_t qs, const float* y, int64_t n, float* dq, float* loss,
                     hipStream_t st) {
   hipLaunchKernelGGL(mse_grad_kernel, dim3(1), dim3(kWG), 0, st, q, qs, y, n, dq, loss);
@@ -133,6 +253,35 @@ int launch_ddpg_stats(const float* a, int64_t lda, int A, const float* r, int64_
   hipLaunchKernelGGL(ddpg_stats_kernel, dim3(1), dim3(kWG), 0, st, a, lda, A, r, rs, y, q, qs, n,
                      stats);
   return check_launch("ddpg_stats_kernel");
+}
+
+int launch_layernorm_fwd(const float* x, int64_t ldx, int64_t rows, int n, const float* gamma,
+                         const float* beta, float eps, float* y, int64_t ldy, float* mean,
+                         float* rstd, hipStream_t st) {
+  if (n < 1 || n > 64 * LN_MAXV) return set_error(SMI_E_ARG, "layernorm: width must be in [1, 1024]");
+  if (rows <= 0) return SMI_OK;
+  const int64_t g = (rows + kWG / 64 - 1) / (kWG / 64);
+  hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((unsigned)g), dim3(kWG), 0, st, x, ldx, rows, n,
+                     gamma, beta, eps, y, ldy, mean, rstd);
+  return check_launch("layernorm_fwd_kernel");
+}
+
+int launch_layernorm_bwd(const float* dy, int64_t ldg, const float* x, int64_t ldx,
+                         const float* mean, const float* rstd, const float* gamma, int64_t rows,
+                         int n, int relu, float* dx, int64_t lddx, float* dgamma, float* dbeta,
+                         hipStream_t st) {
+  if (n < 1 || n > 64 * LN_MAXV) return set_error(SMI_E_ARG, "layernorm: width must be in [1, 1024]");
+  int64_t nb = (rows + kWG / 64 - 1) / (kWG / 64);
+  if (nb > 256) nb = 256;
+  if (nb < 1) nb = 1;
+  float* part = workspace_f32(nb * 2 * n);
+  if (!part) return set_error(SMI_E_ARG, "layernorm: workspace unavailable");
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3((unsigned)nb), dim3(kWG), 0, st, dy, ldg, x, ldx,
+                     mean, rstd, gamma, rows, n, relu, dx, lddx, part);
+  RC_CHECK(check_launch("layernorm_bwd_kernel"));
+  hipLaunchKernelGGL(layernorm_param_grad_kernel, dim3((2 * n + kWG - 1) / kWG), dim3(kWG), 0, st,
+                     part, (int)nb, n, dgamma, dbeta);
+  return check_launch("layernorm_param_grad_kernel");
 }
 
 }  // namespace smi

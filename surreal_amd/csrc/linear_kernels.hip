@@ -700,10 +700,11 @@ __device__ __forceinline__ bool use_dwd_fast() { return SMI_DWD_FAST != 0; }
 template <int MT, int NT, int NB, int RS>
 __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nsteps, int m0, int n0,
                                               int bdata, f32x4 (&acc)[MT][NT]) {
-  static_assert(MT == 4, "fast dW loop: 4 m sub-tiles (float4 A loads)");
+  static_assert(MT == 4 || MT == 1, "fast dW loop: 4 m sub-tiles (float4 A) or 1 (scalar A)");
   constexpr int NH = NB / 4;
   const int li = threadIdx.x & 15;
-  const float* pa = g.A + (int64_t)rw * g.a_cs + min(m0 + 4 * li, g.M - 4);
+  const float* pa = g.A + (int64_t)rw * g.a_cs + (MT == 4 ? min(m0 + 4 * li, g.M - 4)
+                                                          : min(m0 + li, g.M - 1));
   const int64_t sa = (int64_t)RS * g.a_cs;
   const float* pb[NH];
   int64_t sb[NH];
@@ -725,7 +726,8 @@ __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nst
   }
   float4 av[DWD_P], bv[DWD_P][NH];
   auto load = [&](int p) {
-    av[p] = *reinterpret_cast<const float4*>(pa);
+    if constexpr (MT == 4) av[p] = *reinterpret_cast<const float4*>(pa);
+    else av[p].x = *pa;
     pa += sa;
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
@@ -805,19 +807,21 @@ __device__ __forceinline__ void dwd_tile(const GemmArgs& g, const TileIdx ti, fl
     }
   };
   // full slabs of 16-byte operands take the unchecked streaming loop
+  // (MT == 1: scalar A loads, no A alignment needed)
+  constexpr bool kFast = VB && ((VA && MT == 4) || MT == 1);
   bool fast = false;
-  if constexpr (VA && VB && MT == 4)
+  if constexpr (kFast)
     fast = use_dwd_fast() && nsteps >= DWD_P && nsteps % DWD_P == 0 && kb + nsteps * RS <= ke;
   constexpr int NBH = NT > 4 ? 4 : NT;
   if (NT == 8 && n0 + 64 >= g.N) {
-    if constexpr (VA && VB && MT == 4) {
+    if constexpr (kFast) {
       if (fast) dwd_main_fast<MT, NT, NBH, RS>(g, rw, nsteps, m0, n0, bdata, acc);
       else mainloop(std::integral_constant<int, NBH>{});
     } else {
       mainloop(std::integral_constant<int, NBH>{});
     }
   } else {
-    if constexpr (VA && VB && MT == 4) {
+    if constexpr (kFast) {
       if (fast) dwd_main_fast<MT, NT, NT, RS>(g, rw, nsteps, m0, n0, bdata, acc);
       else mainloop(std::integral_constant<int, NT>{});
     } else {
@@ -909,6 +913,7 @@ struct DwGroup {
   int rb0[kDwGroupMax + 1];      // reducer-block prefix
   int gm[kDwGroupMax], gn[kDwGroupMax], S[kDwGroupMax];
   int vec[kDwGroupMax];          // 2*VA + VB
+  int narrow[kDwGroupMax];       // last m-tile is a 16-wide tail (M % 64 in 1..16)
   int n;
 };
 
@@ -931,6 +936,14 @@ gemm_dwd_group_kernel(DwGroup G) {
   ti.nt = local % gn;
   ti.mt = (local / gn) % gm;
   ti.z = local / (gn * gm);
+  if (G.narrow[gi] && ti.mt == gm - 1) {
+    // a tail of <= 16 gradient rows (M 8 / 200 / 400 at C3) on one 16-wide
+    // m sub-tile instead of a 64-wide tile that is >= 75 % padding
+    ti.mt *= 4;                                   // m0 = 16 * mt = 64 * (gm - 1)
+    if (G.vec[gi] & 1) dwd_tile<1, 8, false, true, WV>(g, ti, dwd_red);
+    else dwd_tile<1, 8, false, false, WV>(g, ti, dwd_red);
+    return;
+  }
   switch (G.vec[gi]) {
     case 3: dwd_tile<4, 8, true, true, WV>(g, ti, dwd_red); break;
     case 2: dwd_tile<4, 8, true, false, WV>(g, ti, dwd_red); break;
@@ -1247,6 +1260,16 @@ static int dw_group_target() {
   return t;
 }
 
+// narrow 16-wide tail tiles in grouped launches (SMI_DWD_NARROW=0: off; A/B knob)
+static int use_dwd_narrow() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("SMI_DWD_NARROW");
+    u = (e && e[0] == '0') ? 0 : 1;
+  }
+  return u;
+}
+
 int dw_group_flush(hipStream_t st) {
   g_grp_on = false;
   DwGroup& G = g_grp;
@@ -1257,6 +1280,8 @@ int dw_group_flush(hipStream_t st) {
   int64_t tiles[kDwGroupMax];
   for (int i = 0; i < G.n; ++i) {
     const GemmArgs& g = G.g[i];
+    const int tail = g.M % (16 * MT);
+    G.narrow[i] = use_dwd_narrow() && tail > 0 && tail <= 16;
     G.gm[i] = (g.M + 16 * MT - 1) / (16 * MT);
     G.gn[i] = (g.N + 16 * NT - 1) / (16 * NT);
     tiles[i] = (int64_t)G.gm[i] * G.gn[i];

@@ -825,18 +825,22 @@ lstm_bwd_r4_kernel(LstmBwdArgs a) {
       f32x4 acc[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // dgates operand reads LQ float4 ahead (as in the forward's h loop)
+      constexpr int NQ = KW / 4, LQ = 4;
       const float4* dr = reinterpret_cast<const float4*>(dG + (lane & 3) * G4P + k0);
+      float4 q[LQ];
 #pragma unroll
-      for (int k8 = 0; k8 < KW / 8; ++k8) {
-        const float4 u = dr[2 * k8], v = dr[2 * k8 + 1];
-        acc[0] = mfma4x64(u.x, w[8 * k8 + 0], acc[0]);
-        acc[1] = mfma4x64(u.y, w[8 * k8 + 1], acc[1]);
-        acc[2] = mfma4x64(u.z, w[8 * k8 + 2], acc[2]);
-        acc[3] = mfma4x64(u.w, w[8 * k8 + 3], acc[3]);
-        acc[4] = mfma4x64(v.x, w[8 * k8 + 4], acc[4]);
-        acc[5] = mfma4x64(v.y, w[8 * k8 + 5], acc[5]);
-        acc[6] = mfma4x64(v.z, w[8 * k8 + 6], acc[6]);
-        acc[7] = mfma4x64(v.w, w[8 * k8 + 7], acc[7]);
+      for (int j = 0; j < LQ && j < NQ; ++j) q[j] = dr[j];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const float4 u = q[j % LQ];
+        if (j + LQ < NQ) q[j % LQ] = dr[j + LQ];
+        const int a0 = (j & 1) * 4;
+        acc[a0 + 0] = mfma4x64(u.x, w[4 * j + 0], acc[a0 + 0]);
+        acc[a0 + 1] = mfma4x64(u.y, w[4 * j + 1], acc[a0 + 1]);
+        acc[a0 + 2] = mfma4x64(u.z, w[4 * j + 2], acc[a0 + 2]);
+        acc[a0 + 3] = mfma4x64(u.w, w[4 * j + 3], acc[a0 + 3]);
+        __builtin_amdgcn_sched_barrier(0);
       }
       const f32x4 sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
                         ((acc[4] + acc[5]) + (acc[6] + acc[7]));

@@ -90,10 +90,14 @@ struct RnnScratch {
 
 static inline int64_t al64(int64_t n) { return (n + 63) & ~(int64_t)63; }
 
-__host__ __device__ inline int rnn_nblk(int64_t rows) {
-  const int64_t b = (rows + kWG - 1) / kWG;
+__host__ __device__ inline int rnn_nblk(int64_t rows, int nt = kWG) {
+  const int64_t b = (rows + nt - 1) / nt;
   return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
 }
+// per-row loss kernels (a thread per row, ~100 dependent VALU / transcendental
+// ops each): one-wave blocks so the rows of a C3 batch (21504) spread over
+// 336 CUs' worth of blocks instead of 84 four-wave blocks
+constexpr int kRowNT = 64;
 
 static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   RnnScratch s{};
@@ -249,13 +253,14 @@ adv_export_kernel(PolRowArgs a, float* __restrict__ adv_out, float* __restrict__
 
 // forward statistics of the policy over the E*B rows (ppo.py:203-224,
 // 262-284, 553-575)
-__global__ void __launch_bounds__(kWG)
+template <int NT>
+__global__ void __launch_bounds__(NT)
 policy_rows_stats_kernel(PolRowArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   __shared__ float sig[32], lsig[32], rsig[32];
-  __shared__ double scr[kNW][PS_N];
+  __shared__ double scr[NT / 64][PS_N];
   const int A = a.A;
-  for (int j = threadIdx.x; j < A; j += kWG) {
+  for (int j = threadIdx.x; j < A; j += NT) {
     sig[j] = expf(a.lv[j]);                 // builders.py:127 std = exp(log_var)
     lsig[j] = logf(sig[j]);                 // std0.log() of ppo_net.py:40
     rsig[j] = expf(a.ref_lv[j]);
@@ -266,7 +271,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
 #pragma unroll
   for (int k = 0; k < PS_N; ++k) acc[k] = 0.0;
   const int64_t N = (int64_t)a.E * a.B;
-  for (int64_t n = (int64_t)blockIdx.x * kWG + threadIdx.x; n < N; n += (int64_t)gridDim.x * kWG) {
+  for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
     const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
     const float* m = a.mu + n * A;
     const float* rm = a.refmu + n * A;
@@ -303,7 +308,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
   if (threadIdx.x < PS_N) {
     double t = 0.0;
 #pragma unroll
-    for (int w = 0; w < kNW; ++w) t += scr[w][threadIdx.x];
+    for (int w = 0; w < NT / 64; ++w) t += scr[w][threadIdx.x];
     a.part[(int64_t)blockIdx.x * PS_N + threadIdx.x] = t;
   }
 }
@@ -312,13 +317,14 @@ policy_rows_stats_kernel(PolRowArgs a) {
 // block partials of d loss / d log_var (ppo_net.py:29-72, ppo.py:209-217,
 // 267-277): surrogate weight cf[CF_SURRW] (1/N), KL weight cf[CF_KLCOEF] (adapt:
 // (beta + 2 eta relu(kl - 2kt)) / N, clip: 0)
-__global__ void __launch_bounds__(kWG)
+template <int NT>
+__global__ void __launch_bounds__(NT)
 policy_rows_grad_kernel(PolRowArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   __shared__ float sig[32], lsig[32], rsig[32];
-  __shared__ float gls[kWG / 64][32];
+  __shared__ float gls[NT / 64][32];
   const int A = a.A;
-  for (int j = threadIdx.x; j < A; j += kWG) {
+  for (int j = threadIdx.x; j < A; j += NT) {
     sig[j] = expf(a.lv[j]);
     lsig[j] = logf(sig[j]);
     rsig[j] = expf(a.ref_lv[j]);
@@ -329,7 +335,7 @@ policy_rows_grad_kernel(PolRowArgs a) {
   float glv[32];
   for (int j = 0; j < A; ++j) glv[j] = 0.f;
   const int64_t N = (int64_t)a.E * a.B;
-  for (int64_t n = (int64_t)blockIdx.x * kWG + threadIdx.x; n < N; n += (int64_t)gridDim.x * kWG) {
+  for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
     const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
     const float* m = a.mu + n * A;
     const float* rm = a.refmu + n * A;
@@ -376,9 +382,9 @@ policy_rows_grad_kernel(PolRowArgs a) {
     if (lane == 0) gls[wave][j] = s;
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < A; j += kWG) {
+  for (int j = threadIdx.x; j < A; j += NT) {
     float s = 0.f;
-    for (int w = 0; w < kWG / 64; ++w) s += gls[w][j];
+    for (int w = 0; w < NT / 64; ++w) s += gls[w][j];
     a.lvpart[(int64_t)blockIdx.x * A + j] = s;
   }
 }
@@ -456,13 +462,14 @@ __global__ void policy_decide_kernel(DecideArgs a) {
 
 // value loss rows: V (time-major [NE]) vs ret [B][E]; dV = 2 (V - R) / N and,
 // in the last epoch, the sums of ppo.py:324-331
-__global__ void __launch_bounds__(kWG)
+template <int NT>
+__global__ void __launch_bounds__(NT)
 value_rows_kernel(const float* __restrict__ V, const float* __restrict__ ret, int B, int E,
                   float invN2, float* __restrict__ dV, double* part) {
-  __shared__ double scr[kNW];
+  __shared__ double scr[NT / 64];
   double se = 0.0, d1 = 0.0, d2 = 0.0, r1 = 0.0, r2 = 0.0;
   const int64_t N = (int64_t)E * B;
-  for (int64_t n = (int64_t)blockIdx.x * kWG + threadIdx.x; n < N; n += (int64_t)gridDim.x * kWG) {
+  for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
     const int t = (int)(n / B), b = (int)(n - (int64_t)t * B);
     const float r = ret[(int64_t)b * E + t];
     const float v = V[n];
@@ -478,7 +485,7 @@ value_rows_kernel(const float* __restrict__ V, const float* __restrict__ ret, in
   if (!part) return;
   const double s[5] = {se, d1, d2, r1, r2};
   for (int k = 0; k < 5; ++k) {
-    const double t = block_sum_d(s[k], scr);
+    const double t = block_sum_d<NT>(s[k], scr);
     if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 5 + k] = t;
   }
 }
@@ -918,9 +925,9 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, stop));
       RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
       PolRowArgs p = pol_rows(a, d, s);
-      const int nb = rnn_nblk(d.NE);
+      const int nb = rnn_nblk(d.NE, kRowNT);
       const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(policy_rows_stats_kernel, dim3(nb), dim3(kWG), 0, st, p);
+      hipLaunchKernelGGL(policy_rows_stats_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, p);
       // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
       ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
       RC(check_launch("policy_rows_stats_kernel"));
@@ -937,9 +944,9 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     }
     case SMI_RNN_PH_POLICY_BWD: {
       PolRowArgs p = pol_rows(a, d, s);
-      const int nb = rnn_nblk(d.NE);
+      const int nb = rnn_nblk(d.NE, kRowNT);
       const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(policy_rows_grad_kernel, dim3(nb), dim3(kWG), 0, st, p);
+      hipLaunchKernelGGL(policy_rows_grad_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, p);
       // per row: mu, refmu, actions, behave (5A) + adv read, dz (A) written
       ktime_end(kt, KT_POLICY_GRAD, 4.0 * (double)d.NE * (6 * d.A + 1), st);
       RC(check_launch("policy_rows_grad_kernel"));
@@ -968,10 +975,10 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
       if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, nullptr));
       RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
-      const int nb = rnn_nblk(d.NE);
+      const int nb = rnn_nblk(d.NE, kRowNT);
       const bool last = e == a.epoch_baseline - 1;
       const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(value_rows_kernel, dim3(nb), dim3(kWG), 0, st, s.OUT, s.ret, d.B, d.E,
+      hipLaunchKernelGGL(value_rows_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, s.OUT, s.ret, d.B, d.E,
                          (float)(2.0 / (double)NEg), s.dOUT, last ? s.part : nullptr);
       ktime_end(kt, KT_VALUE_ROWS, 12.0 * (double)d.NE, st);     // V, R read, dV written
       RC(check_launch("value_rows_kernel"));
