@@ -1,7 +1,8 @@
 """ORACLE (test infrastructure only — see oracle/__init__.py).
 
-fp32 CPU restatement of the DDPG learner step (low-dim observations, no
-layernorm — the reference default, ddpg_configs.py:21):
+fp32 CPU restatement of the DDPG learner step (low-dim observations; the
+use_layernorm blocks of builders.py:41-48,65-75 — off by default,
+ddpg_configs.py:21 — with torchx's L.LayerNorm(1) taken as nn.LayerNorm(n)):
   ActorNetworkX / CriticNetworkX   surreal/model/model_builders/builders.py:35-84
   DDPGModel.forward                surreal/model/ddpg_net.py:86-93
   DDPGLearner._optimize            surreal/learner/ddpg.py:244-352 (incl. the TD3 options:
@@ -18,36 +19,61 @@ import torch.nn as nn
 
 
 class ActorX(nn.Module):
-    """Linear-ReLU-Linear-ReLU-Linear-Tanh (builders.py:35-56)."""
+    """Linear-ReLU[-LN]-Linear-ReLU[-LN]-Linear-Tanh (builders.py:35-56)."""
 
-    def __init__(self, d_in, d_act, hidden):
+    def __init__(self, d_in, d_act, hidden, ln=False):
         super().__init__()
         self.l1 = nn.Linear(d_in, hidden[0])
         self.l2 = nn.Linear(hidden[0], hidden[1])
         self.l3 = nn.Linear(hidden[1], d_act)
+        self.ln = ln
+        if ln:
+            self.n1, self.n2 = nn.LayerNorm(hidden[0]), nn.LayerNorm(hidden[1])
 
     def forward(self, x):
-        return torch.tanh(self.l3(torch.relu(self.l2(torch.relu(self.l1(x))))))
+        h = torch.relu(self.l1(x))
+        if self.ln:
+            h = self.n1(h)
+        h = torch.relu(self.l2(h))
+        if self.ln:
+            h = self.n2(h)
+        return torch.tanh(self.l3(h))
 
     def params(self):
-        return [self.l1.weight, self.l1.bias, self.l2.weight, self.l2.bias, self.l3.weight, self.l3.bias]
+        out = [self.l1.weight, self.l1.bias]
+        out += [self.n1.weight, self.n1.bias] if self.ln else []
+        out += [self.l2.weight, self.l2.bias]
+        out += [self.n2.weight, self.n2.bias] if self.ln else []
+        return out + [self.l3.weight, self.l3.bias]
 
 
 class CriticX(nn.Module):
-    """obs -> Linear-ReLU ; cat(h, a) -> Linear-ReLU-Linear (builders.py:58-84)."""
+    """obs -> Linear-ReLU[-LN] ; cat(h, a) -> Linear-ReLU[-LN]-Linear (builders.py:58-84)."""
 
-    def __init__(self, d_in, d_act, hidden):
+    def __init__(self, d_in, d_act, hidden, ln=False):
         super().__init__()
         self.lo = nn.Linear(d_in, hidden[0])
         self.lc = nn.Linear(hidden[0] + d_act, hidden[1])
         self.lq = nn.Linear(hidden[1], 1)
+        self.ln = ln
+        if ln:
+            self.no, self.nc = nn.LayerNorm(hidden[0]), nn.LayerNorm(hidden[1])
 
     def forward(self, obs, act):
         h = torch.relu(self.lo(obs))
-        return self.lq(torch.relu(self.lc(torch.cat((h, act), 1))))
+        if self.ln:
+            h = self.no(h)
+        h = torch.relu(self.lc(torch.cat((h, act), 1)))
+        if self.ln:
+            h = self.nc(h)
+        return self.lq(h)
 
     def params(self):
-        return [self.lo.weight, self.lo.bias, self.lc.weight, self.lc.bias, self.lq.weight, self.lq.bias]
+        out = [self.lo.weight, self.lo.bias]
+        out += [self.no.weight, self.no.bias] if self.ln else []
+        out += [self.lc.weight, self.lc.bias]
+        out += [self.nc.weight, self.nc.bias] if self.ln else []
+        return out + [self.lq.weight, self.lq.bias]
 
 
 def flat_of(params):
@@ -71,13 +97,14 @@ class DDPGLearnerRef:
         self.n_step = lc['algo']['n_step']
         self.batch_size = lc['replay']['batch_size']
         ah, ch = lc['model']['actor_fc_hidden_sizes'], lc['model']['critic_fc_hidden_sizes']
-        self.actor, self.critic = ActorX(obs_dim, act_dim, ah), CriticX(obs_dim, act_dim, ch)
-        self.actor_t, self.critic_t = ActorX(obs_dim, act_dim, ah), CriticX(obs_dim, act_dim, ch)
+        ln = bool(lc['model'].get('use_layernorm', False))
+        self.actor, self.critic = ActorX(obs_dim, act_dim, ah, ln), CriticX(obs_dim, act_dim, ch, ln)
+        self.actor_t, self.critic_t = ActorX(obs_dim, act_dim, ah, ln), CriticX(obs_dim, act_dim, ch, ln)
         self.double = bool(net.get('use_double_critic', False))
         self.action_reg = bool(net.get('use_action_regularization', False))
         self.act_dim = act_dim
         if self.double:
-            self.critic2, self.critic2_t = CriticX(obs_dim, act_dim, ch), CriticX(obs_dim, act_dim, ch)
+            self.critic2, self.critic2_t = CriticX(obs_dim, act_dim, ch, ln), CriticX(obs_dim, act_dim, ch, ln)
         self.hard_update()
         self.clip_actor = net['clip_actor_gradient']
         self.actor_clip_value = net['actor_gradient_value_clip']

@@ -6,12 +6,14 @@ One DDPG learn() (ddpg.py:244-352, batch 512, actor 17-300-200-6, critic
 target actor + target critic forward, n-step target, critic forward, MSE
 gradient, critic backward, Adam; actor forward, critic forward with the
 updated critic, -mean(Q) gradient, backward through the critic's action block
-and the actor, Adam; target update; statistics.  Layernorm (off by default,
-ddpg_configs.py:21) and pixel inputs are not built.
+and the actor, Adam; target update; statistics.  With use_layernorm
+(off by default, ddpg_configs.py:21) every hidden ReLU is followed by a
+LayerNorm block (smi_layernorm_*); pixel inputs are not built.
 
-Parameter layouts (flat, torch (out, in) order):
-  actor : W1[h1][D] b1 W2[h2][h1] b2 W3[A][h2] b3
-  critic: Wo[c1][D] bo Wc[c2][c1+A] bc Wq[1][c2] bq
+Parameter layouts (flat, torch (out, in) order; [g b] = LayerNorm weight / bias
+with use_layernorm):
+  actor : W1[h1][D] b1 [g1 b1'] W2[h2][h1] b2 [g2 b2'] W3[A][h2] b3
+  critic: Wo[c1][D] bo [go bo'] Wc[c2][c1+A] bc [gc bc'] Wq[1][c2] bq
 """
 import math
 
@@ -21,50 +23,90 @@ import torch.nn as nn
 
 from . import _lib as L
 from .config import Config, ConfigError
-from .model import _LinearView
+from .model import _FlatViews, _LinearView
 
 RELU, TANH, NONE = 1, 2, 0
 
 
-class _FlatNet(nn.Module):
-    def __init__(self, shapes, device, generator=None):
+class _LayerNormView(_FlatViews):
+    """weight / bias of one LayerNorm block (torch.nn.LayerNorm(n) init: ones,
+    zeros) as views of the network's flat buffer."""
+
+    def __init__(self, flat, off, n):
         super().__init__()
-        n = sum(o * i + o for (i, o) in shapes)
+        self.n = n
+        self.weight = nn.Parameter(flat[off:off + n])
+        self.bias = nn.Parameter(flat[off + n:off + 2 * n])
+        with torch.no_grad():
+            self.weight.fill_(1.0)
+            self.bias.zero_()
+        self.end = off + 2 * n
+
+
+class _FlatNet(nn.Module):
+    """Linear (spec (d_in, d_out)) and LayerNorm (spec ('ln', n)) blocks over one
+    flat fp32 buffer, in the torch Sequential parameter order."""
+
+    def __init__(self, specs, device, generator=None):
+        super().__init__()
+        n = sum(2 * sp[1] if sp[0] == 'ln' else sp[1] * sp[0] + sp[1] for sp in specs)
         flat = torch.zeros(n, dtype=torch.float32, device=device)
         self.__dict__['flat'] = flat
-        self.layers = []
+        self.layers, self.norms = [], []
         off = 0
-        for (i, o) in shapes:
-            lin = _LinearView(flat, off, i, o)
-            lin.reset_parameters(generator)
-            off = lin.end
-            self.layers.append(lin)
+        for sp in specs:
+            if sp[0] == 'ln':
+                ln = _LayerNormView(flat, off, sp[1])
+                off = ln.end
+                self.norms.append(ln)
+            else:
+                lin = _LinearView(flat, off, sp[0], sp[1])
+                lin.reset_parameters(generator)
+                off = lin.end
+                self.layers.append(lin)
 
     def wb(self, k):
         lin = self.layers[k]
         return lin.weight, lin.bias
 
+    def off(self, p):
+        """offset of a parameter view in the flat buffer (= in a gradient image)"""
+        return (p.data_ptr() - self.flat.data_ptr()) // 4
+
 
 class ActorNetworkX(_FlatNet):
-    """builders.py:35-56 (use_layernorm=False)."""
+    """builders.py:35-56: Linear-ReLU[-LayerNorm]-Linear-ReLU[-LayerNorm]-Linear-Tanh."""
 
-    def __init__(self, D_in, D_act, hidden_sizes=(300, 200), device=None, generator=None):
-        shapes = [(D_in, hidden_sizes[0]), (hidden_sizes[0], hidden_sizes[1]), (hidden_sizes[1], D_act)]
-        super().__init__(shapes, device, generator)
-        self.model = nn.Sequential(self.layers[0], nn.ReLU(), self.layers[1], nn.ReLU(),
-                                   self.layers[2], nn.Tanh())
-        self.dims = (D_in, hidden_sizes[0], hidden_sizes[1], D_act)
+    def __init__(self, D_in, D_act, hidden_sizes=(300, 200), device=None, generator=None,
+                 use_layernorm=False):
+        h1, h2 = hidden_sizes
+        ln = bool(use_layernorm)
+        specs = [(D_in, h1)] + ([('ln', h1)] if ln else []) + [(h1, h2)] + \
+            ([('ln', h2)] if ln else []) + [(h2, D_act)]
+        super().__init__(specs, device, generator)
+        self.use_layernorm = ln
+        l0, l1, l2 = self.layers
+        mods = [l0, nn.ReLU()] + ([self.norms[0]] if ln else []) + [l1, nn.ReLU()] + \
+            ([self.norms[1]] if ln else []) + [l2, nn.Tanh()]
+        self.model = nn.Sequential(*mods)
+        self.dims = (D_in, h1, h2, D_act)
 
 
 class CriticNetworkX(_FlatNet):
-    """builders.py:58-84 (use_layernorm=False)."""
+    """builders.py:58-84: obs -> Linear-ReLU[-LayerNorm]; cat(h, a) ->
+    Linear-ReLU[-LayerNorm]-Linear."""
 
-    def __init__(self, D_in, D_act, hidden_sizes=(400, 300), device=None, generator=None):
+    def __init__(self, D_in, D_act, hidden_sizes=(400, 300), device=None, generator=None,
+                 use_layernorm=False):
         c1, c2 = hidden_sizes
-        shapes = [(D_in, c1), (c1 + D_act, c2), (c2, 1)]
-        super().__init__(shapes, device, generator)
-        self.model_obs = nn.Sequential(self.layers[0], nn.ReLU())
-        self.model_concat = nn.Sequential(self.layers[1], nn.ReLU(), self.layers[2])
+        ln = bool(use_layernorm)
+        specs = [(D_in, c1)] + ([('ln', c1)] if ln else []) + [(c1 + D_act, c2)] + \
+            ([('ln', c2)] if ln else []) + [(c2, 1)]
+        super().__init__(specs, device, generator)
+        self.use_layernorm = ln
+        l0, l1, l2 = self.layers
+        self.model_obs = nn.Sequential(*([l0, nn.ReLU()] + ([self.norms[0]] if ln else [])))
+        self.model_concat = nn.Sequential(*([l1, nn.ReLU()] + ([self.norms[1]] if ln else []) + [l2]))
         self.dims = (D_in, c1, c2, D_act)
 
 
@@ -79,15 +121,15 @@ class DDPGModel(nn.Module):
         L.require_gpu()
         if 'pixel' in obs_spec:
             raise NotImplementedError('surreal_amd: DDPG pixel inputs are SURVEY §8(f) rank 1')
-        if use_layernorm:
-            raise NotImplementedError('surreal_amd: DDPG layernorm is not built')
         self.device = torch.device(device) if device is not None else torch.device('cuda')
         self.action_dim = action_dim
         self.input_dim = int(obs_spec['low_dim']['flat_inputs'][0])
+        self.use_layernorm = bool(use_layernorm)
         self.actor = None if critic_only else ActorNetworkX(
-            self.input_dim, action_dim, actor_fc_hidden_sizes, self.device, generator)
+            self.input_dim, action_dim, actor_fc_hidden_sizes, self.device, generator,
+            use_layernorm)
         self.critic = CriticNetworkX(self.input_dim, action_dim, critic_fc_hidden_sizes,
-                                     self.device, generator)
+                                     self.device, generator, use_layernorm)
 
     def get_actor_parameters(self):
         return self.actor.parameters()
@@ -139,6 +181,26 @@ class _Net(object):
         L.call('smi_linear_forward', _p(x), ldx, rows, k, _p(w), ldw, _p(b), n, act, _p(y), ldy,
                self.st)
 
+    def norm(self, net, j, x, rows, y, ldy, tag):
+        """LayerNorm block j over x [rows][n] (post-ReLU) into y; mean / rstd kept
+        under tag for the backward"""
+        ln = net.norms[j]
+        mu, rs = self.buf(tag + '_mu', (rows,)), self.buf(tag + '_rs', (rows,))
+        L.call('smi_layernorm_forward', _p(x), x.stride(0), rows, ln.n, _p(ln.weight), _p(ln.bias),
+               1e-5, _p(y), ldy, _p(mu), _p(rs), self.st)
+
+    def norm_bwd(self, net, j, dy, x, rows, dx, g, tag):
+        """backward of LayerNorm block j (and of the ReLU before it) from dy;
+        dgamma / dbeta into the gradient image g (None: input gradient only)"""
+        ln = net.norms[j]
+        if g is None:
+            dg, db = self.buf('ln_dg', (ln.n,)), self.buf('ln_db', (ln.n,))
+        else:
+            dg, db = g[net.off(ln.weight):], g[net.off(ln.bias):]
+        L.call('smi_layernorm_backward', _p(dy), dy.stride(0), _p(x), x.stride(0),
+               _p(self.bufs[tag + '_mu']), _p(self.bufs[tag + '_rs']), _p(ln.weight), rows, ln.n, 1,
+               _p(dx), dx.stride(0), _p(dg), _p(db), self.st)
+
     def actor_fwd(self, obs, rows, store='a', actor=None):
         actor = actor if actor is not None else self.m.actor
         D, h1, h2, A = actor.dims
@@ -148,8 +210,16 @@ class _Net(object):
         out = self.buf(pre + '_act', (rows, A))
         (w1, b1), (w2, b2), (w3, b3) = actor.wb(0), actor.wb(1), actor.wb(2)
         self.lin(obs, obs.stride(0), rows, D, w1, D, b1, h1, RELU, H1, h1)
-        self.lin(H1, h1, rows, h1, w2, h1, b2, h2, RELU, H2, h2)
-        self.lin(H2, h2, rows, h2, w3, h2, b3, A, TANH, out, A)
+        X1 = H1
+        if actor.use_layernorm:
+            X1 = self.buf(pre + '_n1', (rows, h1))
+            self.norm(actor, 0, H1, rows, X1, h1, pre + '_ln1')
+        self.lin(X1, h1, rows, h1, w2, h1, b2, h2, RELU, H2, h2)
+        X2 = H2
+        if actor.use_layernorm:
+            X2 = self.buf(pre + '_n2', (rows, h2))
+            self.norm(actor, 1, H2, rows, X2, h2, pre + '_ln2')
+        self.lin(X2, h2, rows, h2, w3, h2, b3, A, TANH, out, A)
         return out if store else out.clone()
 
     def critic_fwd(self, critic, obs, act, rows, store):
@@ -159,15 +229,24 @@ class _Net(object):
         H2 = self.buf(pre + '_h2', (rows, c2))
         Q = self.buf(pre + '_q', (rows, 1))
         (wo, bo), (wc, bc), (wq, bq) = critic.wb(0), critic.wb(1), critic.wb(2)
-        self.lin(obs, obs.stride(0), rows, D, wo, D, bo, c1, RELU, CAT, c1 + A)
+        if critic.use_layernorm:
+            H1 = self.buf(pre + '_h1', (rows, c1))
+            self.lin(obs, obs.stride(0), rows, D, wo, D, bo, c1, RELU, H1, c1)
+            self.norm(critic, 0, H1, rows, CAT, c1 + A, pre + '_ln1')
+        else:
+            self.lin(obs, obs.stride(0), rows, D, wo, D, bo, c1, RELU, CAT, c1 + A)
         L.call('smi_copy_cols', _p(act), act.stride(0), rows, A, _p(CAT[:, c1:]), c1 + A, self.st)
         self.lin(CAT, c1 + A, rows, c1 + A, wc, c1 + A, bc, c2, RELU, H2, c2)
-        self.lin(H2, c2, rows, c2, wq, c2, bq, 1, NONE, Q, 1)
+        X2 = H2
+        if critic.use_layernorm:
+            X2 = self.buf(pre + '_n2', (rows, c2))
+            self.norm(critic, 1, H2, rows, X2, c2, pre + '_ln2')
+        self.lin(X2, c2, rows, c2, wq, c2, bq, 1, NONE, Q, 1)
         return Q if store else Q.clone()
 
 
 class DDPGLearner(object):
-    """ddpg.py:12-440 on MI355X (low-dim, no layernorm)."""
+    """ddpg.py:12-440 on MI355X (low-dim observations; optional layernorm)."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
                  device=None, seed=0, use_graph=False, dp=None, checkpoint_full_state=False):
@@ -374,27 +453,36 @@ class DDPGLearner(object):
         """Backward through CriticNetworkX.  With g: weight grads into g (flat).
         Always returns d loss / d action (B, A) when g is None."""
         D, c1, c2, A = crit.dims
+        ln = crit.use_layernorm
         CAT = net.bufs[pre + '_cat']
         H2 = net.bufs[pre + '_h2']
+        X2 = net.bufs[pre + '_n2'] if ln else H2               # input of the Q layer
         (wo, bo), (wc, bc), (wq, bq) = crit.wb(0), crit.wb(1), crit.wb(2)
         dH2 = net.buf('dH2', (B, c2))
-        L.call('smi_linear_backward_input', _p(dq), 1, B, 1, _p(wq), c2, c2, _p(H2), c2, _p(dH2),
-               c2, st)
+        if ln:      # d/d(norm output), then through the norm and the ReLU
+            dN2 = net.buf('dN2', (B, c2))
+            L.call('smi_linear_backward_input', _p(dq), 1, B, 1, _p(wq), c2, c2, None, 0, _p(dN2),
+                   c2, st)
+            net.norm_bwd(crit, 1, dN2, H2, B, dH2, g, pre + '_ln2')
+        else:
+            L.call('smi_linear_backward_input', _p(dq), 1, B, 1, _p(wq), c2, c2, _p(H2), c2,
+                   _p(dH2), c2, st)
         if g is not None:
-            off_bo = c1 * D
-            off_wc = off_bo + c1
-            off_bc = off_wc + c2 * (c1 + A)
-            off_wq = off_bc + c2
-            off_bq = off_wq + c2
-            L.call('smi_linear_backward_weight', _p(dq), 1, B, 1, _p(H2), c2, c2, _p(g[off_wq:]), c2,
-                   _p(g[off_bq:]), 0, st)
+            L.call('smi_linear_backward_weight', _p(dq), 1, B, 1, _p(X2), c2, c2,
+                   _p(g[crit.off(wq):]), c2, _p(g[crit.off(bq):]), 0, st)
             L.call('smi_linear_backward_weight', _p(dH2), c2, B, c2, _p(CAT), c1 + A, c1 + A,
-                   _p(g[off_wc:]), c1 + A, _p(g[off_bc:]), 0, st)
+                   _p(g[crit.off(wc):]), c1 + A, _p(g[crit.off(bc):]), 0, st)
             dH1 = net.buf('dH1c', (B, c1))
-            L.call('smi_linear_backward_input', _p(dH2), c2, B, c2, _p(wc), c1 + A, c1, _p(CAT),
-                   c1 + A, _p(dH1), c1, st)
+            if ln:
+                dN1 = net.buf('dN1c', (B, c1))
+                L.call('smi_linear_backward_input', _p(dH2), c2, B, c2, _p(wc), c1 + A, c1, None, 0,
+                       _p(dN1), c1, st)
+                net.norm_bwd(crit, 0, dN1, net.bufs[pre + '_h1'], B, dH1, g, pre + '_ln1')
+            else:
+                L.call('smi_linear_backward_input', _p(dH2), c2, B, c2, _p(wc), c1 + A, c1, _p(CAT),
+                       c1 + A, _p(dH1), c1, st)
             L.call('smi_linear_backward_weight', _p(dH1), c1, B, c1, _p(obs), obs.stride(0), D,
-                   _p(g[0:]), D, _p(g[off_bo:]), 0, st)
+                   _p(g[crit.off(wo):]), D, _p(g[crit.off(bo):]), 0, st)
             return None
         dA = net.buf('dA', (B, A))
         L.call('smi_linear_backward_input', _p(dH2), c2, B, c2, _p(wc[:, c1:]), c1 + A, A, None, 0,
@@ -403,26 +491,37 @@ class DDPGLearner(object):
 
     def _actor_backward(self, net, act, obs, B, dA, g, st):
         D, h1, h2, A = act.dims
+        ln = act.use_layernorm
         H1, H2, out = net.bufs['a_h1'], net.bufs['a_h2'], net.bufs['a_act']
+        X1 = net.bufs['a_n1'] if ln else H1                     # inputs of layers 2 and 3
+        X2 = net.bufs['a_n2'] if ln else H2
         (w1, b1), (w2, b2), (w3, b3) = act.wb(0), act.wb(1), act.wb(2)
         dZ = net.buf('dZ3', (B, A))
         L.call('smi_tanh_backward', _p(dA), A, _p(out), A, B, A, _p(dZ), A, st)
-        off_b1 = h1 * D
-        off_w2 = off_b1 + h1
-        off_b2 = off_w2 + h2 * h1
-        off_w3 = off_b2 + h2
-        off_b3 = off_w3 + A * h2
-        L.call('smi_linear_backward_weight', _p(dZ), A, B, A, _p(H2), h2, h2, _p(g[off_w3:]), h2,
-               _p(g[off_b3:]), 0, st)
+        L.call('smi_linear_backward_weight', _p(dZ), A, B, A, _p(X2), h2, h2, _p(g[act.off(w3):]), h2,
+               _p(g[act.off(b3):]), 0, st)
         dH2 = net.buf('dH2a', (B, h2))
-        L.call('smi_linear_backward_input', _p(dZ), A, B, A, _p(w3), h2, h2, _p(H2), h2, _p(dH2), h2, st)
-        L.call('smi_linear_backward_weight', _p(dH2), h2, B, h2, _p(H1), h1, h1, _p(g[off_w2:]), h1,
-               _p(g[off_b2:]), 0, st)
+        if ln:
+            dN2 = net.buf('dN2a', (B, h2))
+            L.call('smi_linear_backward_input', _p(dZ), A, B, A, _p(w3), h2, h2, None, 0, _p(dN2), h2,
+                   st)
+            net.norm_bwd(act, 1, dN2, H2, B, dH2, g, 'a_ln2')
+        else:
+            L.call('smi_linear_backward_input', _p(dZ), A, B, A, _p(w3), h2, h2, _p(H2), h2, _p(dH2),
+                   h2, st)
+        L.call('smi_linear_backward_weight', _p(dH2), h2, B, h2, _p(X1), h1, h1, _p(g[act.off(w2):]), h1,
+               _p(g[act.off(b2):]), 0, st)
         dH1 = net.buf('dH1a', (B, h1))
-        L.call('smi_linear_backward_input', _p(dH2), h2, B, h2, _p(w2), h1, h1, _p(H1), h1, _p(dH1),
-               h1, st)
-        L.call('smi_linear_backward_weight', _p(dH1), h1, B, h1, _p(obs), obs.stride(0), D, _p(g[0:]),
-               D, _p(g[off_b1:]), 0, st)
+        if ln:
+            dN1 = net.buf('dN1a', (B, h1))
+            L.call('smi_linear_backward_input', _p(dH2), h2, B, h2, _p(w2), h1, h1, None, 0, _p(dN1),
+                   h1, st)
+            net.norm_bwd(act, 0, dN1, H1, B, dH1, g, 'a_ln1')
+        else:
+            L.call('smi_linear_backward_input', _p(dH2), h2, B, h2, _p(w2), h1, h1, _p(H1), h1,
+                   _p(dH1), h1, st)
+        L.call('smi_linear_backward_weight', _p(dH1), h1, B, h1, _p(obs), obs.stride(0), D,
+               _p(g[act.off(w1):]), D, _p(g[act.off(b1):]), 0, st)
 
     def _target_update(self):                                            # ddpg.py:403-428
         st = L.stream(self.device)

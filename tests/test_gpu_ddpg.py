@@ -19,9 +19,10 @@ from tests.test_gpu_ppo import _compare_params
 pytestmark = pytest.mark.gpu
 
 
-def _cfg(B=512, target='hard', clip_critic=False):
+def _cfg(B=512, target='hard', clip_critic=False, layernorm=False):
     lc = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
     lc.replay.batch_size = B
+    lc.model.use_layernorm = layernorm
     lc.algo.network.clip_critic_gradient = clip_critic
     if target == 'soft':
         lc.algo.network.target_update = {'type': 'soft', 'tau': 1e-3}
@@ -94,10 +95,49 @@ def test_linear_ops_vs_torch(rows, k, n):
     _fp32_as_good_as_torch(db.cpu(), 2 * dy.sum(0), 2 * dy.double().sum(0), sl, 2 * mb)
 
 
-@pytest.mark.parametrize('target,clip_critic', [('hard', False), ('soft', True)])
-def test_ddpg_learn_matches_oracle(target, clip_critic):
+@pytest.mark.parametrize('rows,n', [(512, 300), (512, 400), (70, 200), (3, 37), (1, 1024)])
+def test_layernorm_kernels_vs_torch(rows, n):
+    """smi_layernorm_forward / _backward (ReLU before the norm) against
+    torch.nn.functional.layer_norm in fp64 autograd, at 2x the error of torch's
+    own fp32 CPU layer_norm (or 1e-6 of scale)."""
+    g = torch.Generator().manual_seed(rows * 7 + n)
+    z = torch.randn(rows, n, generator=g, dtype=torch.float64)
+    x = torch.relu(z)
+    gamma = 1 + 0.1 * torch.randn(n, generator=g, dtype=torch.float64)
+    beta = 0.1 * torch.randn(n, generator=g, dtype=torch.float64)
+    dy = torch.randn(rows, n, generator=g, dtype=torch.float64)
+
+    def ref(dtype):
+        xx = x.to(dtype).clone().requires_grad_(True)
+        gg, bb = gamma.to(dtype).clone().requires_grad_(True), beta.to(dtype).clone().requires_grad_(True)
+        y = torch.nn.functional.layer_norm(xx, (n,), gg, bb, 1e-5)
+        y.backward(dy.to(dtype))
+        dx = xx.grad * (x > 0).to(dtype)                      # through the ReLU
+        return [t.detach().double() for t in (y, dx, gg.grad, bb.grad)]
+    r64, r32 = ref(torch.float64), ref(torch.float32)
+    dev = 'cuda'
+    xd, gd, bd, dyd = (t.float().to(dev) for t in (x, gamma, beta, dy))
+    y, mu, rs = torch.empty(rows, n, device=dev), torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    dx, dg, db = torch.empty(rows, n, device=dev), torch.empty(n, device=dev), torch.empty(n, device=dev)
+    st = L.stream(torch.device(dev))
+    L.call('smi_layernorm_forward', L.ptr(xd), n, rows, n, L.ptr(gd), L.ptr(bd), 1e-5, L.ptr(y), n,
+           L.ptr(mu), L.ptr(rs), st)
+    L.call('smi_layernorm_backward', L.ptr(dyd), n, L.ptr(xd), n, L.ptr(mu), L.ptr(rs), L.ptr(gd), rows,
+           n, 1, L.ptr(dx), n, L.ptr(dg), L.ptr(db), st)
+    torch.cuda.synchronize()
+    for name, got, a, b in zip(('y', 'dx', 'dgamma', 'dbeta'), (y, dx, dg, db), r32, r64):
+        got = got.double().cpu()
+        scale = float(b.abs().max())
+        e_gpu, e_cpu = float((got - b).abs().max()), float((a - b).abs().max())
+        assert e_gpu <= 2 * e_cpu + 1e-6 * scale, (name, e_gpu, e_cpu, scale)
+    assert torch.allclose(mu.double().cpu(), x.mean(1), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('target,clip_critic,layernorm', [('hard', False, False), ('soft', True, False),
+                                                          ('hard', False, True), ('soft', True, True)])
+def test_ddpg_learn_matches_oracle(target, clip_critic, layernorm):
     B, D, A = 512, 17, 6
-    lc = _cfg(B, target, clip_critic)
+    lc = _cfg(B, target, clip_critic, layernorm)
     learner = DDPGLearner(lc, gym_env_config(D, A), seed=2)
     ref = R.DDPGLearnerRef(lc, D, A)
     _sync_weights(learner, ref)
