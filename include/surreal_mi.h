@@ -347,7 +347,7 @@ int smi_ppo_epoch_apply(const smi_ppo_args* args, int epoch, void* stream);
 typedef struct smi_ppo_rnn_args {
   /* dims (local batch) */
   int B, T, horizon;                 /* segments on this rank, n_step, horizon */
-  int obs_dim, rnn_hidden;           /* D, H (one LSTM layer).  H == 0: no LSTM — the heads
+  int obs_dim, rnn_hidden;           /* D, H (rnn_layer LSTM layers).  H == 0: no LSTM — the heads
                                         read the stem input [zfilter(low) | cnn] directly
                                         (the non-RNN pixel model); then horizon == T (one
                                         window: ppo.py:408-418) and only step 0 of each
@@ -364,8 +364,8 @@ typedef struct smi_ppo_rnn_args {
   const float* rewards;    /* [B][T]      */
   const float* dones;      /* [B][T]      */
   const float* behave;     /* [B][T][2A]  */
-  const float* h0;         /* [B][H]  onetime_infos[0] (layer 0) */
-  const float* c0;         /* [B][H]  onetime_infos[1]           */
+  const float* h0;         /* [L][B][H]  onetime_infos[0] layer-major */
+  const float* c0;         /* [L][B][H]  onetime_infos[1]              */
   /* parameters */
   float* lstm; float* actor; float* critic;
   const float* ref_lstm; const float* ref_actor;
@@ -404,15 +404,20 @@ typedef struct smi_ppo_rnn_args {
      policy epochs use them (normalised over all B_global*E windows when
      norm_adv, ppo.py:402-405) and the returns, both [B][E] batch-major */
   float* adv_out; float* ret_out;
+  /* nn.LSTM num_layers (rnn_layer, ppo_net.py:146-149), 1..3 (0 = 1).  h0 / c0
+     are then [rnn_layer][B][H] (onetime_infos[i].transpose(0, 1), ppo.py:508-509)
+     and `lstm` / `ref_lstm` hold the layers one after another, each in
+     nn.LSTM's order [W_ih | W_hh | b_ih | b_hh] (layer k >= 1: W_ih is 4H x H) */
+  int rnn_layer;
 } smi_ppo_rnn_args;
 
 #define SMI_RNN_PSTAT 16
 int64_t smi_ppo_rnn_scratch_bytes(int B, int T, int horizon, int obs_dim, int rnn_hidden,
                                   int h1, int h2, int act_dim, int critic_h1, int critic_h2,
-                                  int pix_c, int pix_h, int pix_w, int cnn_feat);
+                                  int pix_c, int pix_h, int pix_w, int cnn_feat, int rnn_layer);
 int64_t smi_ppo_rnn_xbuf_floats(int obs_dim, int rnn_hidden, int h1, int h2, int act_dim,
                                 int critic_h1, int critic_h2, int pix_c, int pix_h, int pix_w,
-                                int cnn_feat);
+                                int cnn_feat, int rnn_layer);
 int64_t smi_lstm_param_count(int in_dim, int hidden);
 int smi_ppo_rnn_phase(const smi_ppo_rnn_args* args, int phase, int epoch, void* stream);
 

@@ -86,6 +86,7 @@ class RNNArgs(ctypes.Structure):
         ('pix_c', c_int), ('pix_h', c_int), ('pix_w', c_int), ('cnn_feat', c_int),
         ('pixels', P), ('pixels_next', P),
         ('adv_out', P), ('ret_out', P),
+        ('rnn_layer', c_int),
     ]
 
 
@@ -165,8 +166,8 @@ _SIGS = {
     'smi_lstm_param_count': (c_i64, [c_int, c_int]),
     'smi_kernel_timing': (c_int, [c_int]),
     'smi_kernel_timing_report': (c_int, [c_int, P]),
-    'smi_ppo_rnn_scratch_bytes': (c_i64, [c_int] * 14),
-    'smi_ppo_rnn_xbuf_floats': (c_i64, [c_int] * 11),
+    'smi_ppo_rnn_scratch_bytes': (c_i64, [c_int] * 15),
+    'smi_ppo_rnn_xbuf_floats': (c_i64, [c_int] * 12),
     'smi_cnn_param_count': (c_i64, [c_int] * 4),
     'smi_cnn_scratch_bytes': (c_i64, [c_i64] + [c_int] * 4),
     'smi_cnn_forward': (c_int, [P, P, P, c_i64, c_i64, c_i64] + [c_int] * 4 + [P, P, P, c_i64, P]),

@@ -444,19 +444,22 @@ int64_t smi_lstm_param_count(int in_dim, int hidden) {
 
 int64_t smi_ppo_rnn_scratch_bytes(int B, int T, int horizon, int obs_dim, int rnn_hidden, int h1,
                                   int h2, int act_dim, int critic_h1, int critic_h2, int pix_c,
-                                  int pix_h, int pix_w, int cnn_feat) {
-  return ppo_rnn_scratch_bytes(B, T, horizon, obs_dim, rnn_hidden, h1, h2, act_dim, critic_h1,
-                               critic_h2, pix_c, pix_h, pix_w, cnn_feat);
+                                  int pix_h, int pix_w, int cnn_feat, int rnn_layer) {
+  return ppo_rnn_scratch_bytes(B, T, horizon, obs_dim, rnn_hidden, rnn_layer, h1, h2, act_dim,
+                               critic_h1, critic_h2, pix_c, pix_h, pix_w, cnn_feat);
 }
 
 int64_t smi_cnn_param_count(int C, int H, int W, int F) { return cnn_geom(C, H, W, F).total; }
 
 int64_t smi_ppo_rnn_xbuf_floats(int obs_dim, int rnn_hidden, int h1, int h2, int act_dim,
                                 int critic_h1, int critic_h2, int pix_c, int pix_h, int pix_w,
-                                int cnn_feat) {
+                                int cnn_feat, int rnn_layer) {
   const int F = cnn_feat > 0 ? cnn_feat : 0;
   const int hin = rnn_hidden > 0 ? rnn_hidden : obs_dim + F;     // 0: MLP policy on the stem
-  const int64_t ns = (rnn_hidden > 0 ? smi_lstm_param_count(obs_dim + F, rnn_hidden) : 0) +
+  const int nl = rnn_layer > 1 ? rnn_layer : 1;
+  const int64_t ns = (rnn_hidden > 0 ? smi_lstm_param_count(obs_dim + F, rnn_hidden) +
+                                           (nl - 1) * smi_lstm_param_count(rnn_hidden, rnn_hidden)
+                                     : 0) +
                      (F > 0 ? smi_cnn_param_count(pix_c, pix_h, pix_w, F) : 0);
   return mlp_layout(hin, h1, h2, act_dim, 1).fcount +
          mlp_layout(hin, critic_h1, critic_h2, 1, 0).fcount + 2 * ns;
@@ -495,6 +498,8 @@ int smi_cnn_backward(const float* params, const uint8_t* pix, const uint8_t* pix
 
 int smi_ppo_rnn_phase(const smi_ppo_rnn_args* a, int phase, int epoch, void* stream) {
   REQUIRE(a, "ppo_rnn: null args");
+  REQUIRE(a->rnn_layer >= 0 && a->rnn_layer <= 3 && (a->rnn_layer <= 1 || a->rnn_hidden > 0),
+          "ppo_rnn: rnn_layer must be in [1, 3] (0 = 1)");
   REQUIRE(a->B >= 1 && a->T >= 1 && a->horizon >= 1 && a->horizon <= a->T, "ppo_rnn: bad B/T/horizon");
   REQUIRE(a->obs_dim >= (a->cnn_feat > 0 ? 0 : 1) && a->obs_dim <= 128,
           "ppo_rnn: obs_dim must be in [1, 128] ([0, 128] with a pixel stem)");

@@ -46,6 +46,8 @@ enum { CF_KLCOEF = 0, CF_SURRW, CF_COUNT = 8 };
 
 struct RnnDims {
   int B, T, Hz, E, S1, D, H, G4, A, h1, h2, c1, c2;
+  int L;                              // LSTM layers (nn.LSTM num_layers = rnn_layer)
+  int64_t nL0, nLk;                   // parameters of layer 0 / of each layer above it
   int F, Din;                         // pixel features (0: no CNN stem), LSTM input D + F
   int Hin;                            // head input width: H (LSTM) or Din (H == 0: MLP policy)
   int ldx;                            // row stride of the stem input Xz / Xr: Din rounded up to
@@ -59,8 +61,9 @@ struct RnnDims {
 
 __host__ __device__ inline RnnDims rnn_dims(int B, int T, int Hz, int D, int H, int h1, int h2,
                                             int A, int c1, int c2, int pc = 0, int ph = 0,
-                                            int pw = 0, int F = 0) {
+                                            int pw = 0, int F = 0, int L = 1) {
   RnnDims d;
+  d.L = L > 1 ? L : 1;
   d.F = F > 0 ? F : 0; d.Din = D + d.F;
   d.G = cnn_geom(pc, ph, pw, d.F);
   d.nCnn = d.F > 0 ? d.G.total : 0;
@@ -73,7 +76,11 @@ __host__ __device__ inline RnnDims rnn_dims(int B, int T, int Hz, int D, int H, 
   d.LA = mlp_layout(d.Hin, h1, h2, A, 1);
   d.LC = mlp_layout(d.Hin, c1, c2, 1, 0);
   d.nA_head = d.LA.fcount; d.nC_head = d.LC.fcount;
-  d.nL = H > 0 ? (int64_t)4 * H * d.Din + (int64_t)4 * H * H + 8 * (int64_t)H : 0;
+  // nn.LSTM parameter order per layer: W_ih, W_hh, b_ih, b_hh (layer k >= 1 reads
+  // layer k-1's h, so its W_ih is 4H x H)
+  d.nL0 = H > 0 ? (int64_t)4 * H * d.Din + (int64_t)4 * H * H + 8 * (int64_t)H : 0;
+  d.nLk = H > 0 ? (int64_t)8 * H * H + 8 * (int64_t)H : 0;
+  d.nL = d.nL0 + (d.L - 1) * d.nLk;
   d.nS = d.nL + d.nCnn;
   return d;
 }
@@ -108,9 +115,9 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   s.Xz = take(d.NG * d.ldx);
   s.Xr = take(d.NE * d.ldx);
   s.xproj = take(d.NG * d.G4);
-  s.hbuf = take((int64_t)(d.S1 + 1) * d.B * d.H);
-  s.cbuf = take((int64_t)(d.E + 1) * d.B * d.H);
-  s.gates = take(d.NE * d.G4);
+  s.hbuf = take((int64_t)d.L * (d.S1 + 1) * d.B * d.H);     // per layer (see hbuf_of)
+  s.cbuf = take((int64_t)d.L * (d.E + 1) * d.B * d.H);
+  s.gates = take((int64_t)d.L * d.NE * d.G4);
   s.HA1 = take(d.NG * hmax1);
   s.HA2 = take(d.NG * hmax2);
   s.OUT = take(d.NG * (d.A > 1 ? d.A : 1));
@@ -118,7 +125,7 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   s.dH1 = take(d.NE * hmax1);
   s.dH2 = take(d.NE * hmax2);
   s.dh = take(d.NE * d.H);
-  s.dgates = take(d.NE * d.G4);
+  s.dgates = take((int64_t)d.L * d.NE * d.G4);
   s.values = take((int64_t)d.B * d.S1);
   s.adv = take(d.NE);
   s.ret = take(d.NE);
@@ -711,6 +718,20 @@ static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx,
                               dxn, st, skip);
 }
 
+// per-layer regions of the LSTM buffers
+static float* hbuf_of(const RnnDims& d, const RnnScratch& s, int l) {
+  return s.hbuf + (int64_t)l * (d.S1 + 1) * d.B * d.H;
+}
+static float* cbuf_of(const RnnDims& d, const RnnScratch& s, int l) {
+  return s.cbuf + (int64_t)l * (d.E + 1) * d.B * d.H;
+}
+static float* gates_of(const RnnDims& d, const RnnScratch& s, int l) {
+  return s.gates + (int64_t)l * d.NE * d.G4;
+}
+static float* dgates_of(const RnnDims& d, const RnnScratch& s, int l) {
+  return s.dgates + (int64_t)l * d.NE * d.G4;
+}
+
 struct LstmP { const float *Wih, *Whh, *bih, *bhh; };
 static LstmP lstm_params(const float* p, int D, int H) {
   LstmP l;
@@ -720,41 +741,78 @@ static LstmP lstm_params(const float* p, int D, int H) {
   l.bhh = l.bih + 4 * H;
   return l;
 }
-
-// LSTM over S steps from (h0, c0): xproj GEMM + recurrence
-static int lstm_forward(const RnnDims& d, const LstmP& l, const float* X, int S, const float* h0,
-                        const float* c0, const RnnScratch& s, float* cbuf, float* gates,
-                        hipStream_t st, const int* skip) {
-  const int rf = launch_lstm_fwd_x(X, d.ldx, d.Din, l.Wih, l.bih, l.Whh, l.bhh, h0, c0, S, d.B,
-                                  d.H, s.hbuf, cbuf, gates, st, skip);
-  if (rf != SMI_E_NOFIT) return rf;
-  const int64_t rows = (int64_t)S * d.B;
-  RC(launch_linear_fwd(X, d.ldx, (int)rows, d.Din, l.Wih, d.Din, l.bih, d.G4, ACT_NONE, s.xproj,
-                       d.G4, st, skip));
-  return launch_lstm_fwd(s.xproj, l.Whh, l.bhh, h0, c0, S, d.B, d.H, s.hbuf, cbuf, gates, st,
-                         skip);
+// layer l of a stem buffer [layer 0 (in Din) | layer 1 (in H) | ...]
+static LstmP lstm_layer(const RnnDims& d, const float* p, int l) {
+  return l == 0 ? lstm_params(p, d.Din, d.H)
+                : lstm_params(p + d.nL0 + (int64_t)(l - 1) * d.nLk, d.H, d.H);
 }
 
-// gradients of the LSTM parameters (flat layout) from dh [E][B][H]
-static int lstm_backward(const RnnDims& d, const LstmP& l, float* G, const RnnScratch& s,
+// the stacked LSTM over S steps from (h0, c0) ([L][B][H] each): layer 0 reads X
+// (fused input projection when it fits, else xproj GEMM + recurrence), layer
+// l >= 1 reads layer l-1's outputs hbuf_l-1[1..S]; keep: store the cell states
+// and gate activations of every layer for a backward
+static int lstm_forward(const RnnDims& d, const float* P, const float* X, int S, const float* h0,
+                        const float* c0, const RnnScratch& s, bool keep, hipStream_t st,
+                        const int* skip) {
+  const int64_t BH = (int64_t)d.B * d.H;
+  for (int l = 0; l < d.L; ++l) {
+    const LstmP lp = lstm_layer(d, P, l);
+    const float* Xl = l == 0 ? X : hbuf_of(d, s, l - 1) + BH;
+    const int64_t ldx = l == 0 ? d.ldx : d.H;
+    const int din = l == 0 ? d.Din : d.H;
+    float* hb = hbuf_of(d, s, l);
+    float* cb = keep ? cbuf_of(d, s, l) : nullptr;
+    float* gt = keep ? gates_of(d, s, l) : nullptr;
+    const int rf = launch_lstm_fwd_x(Xl, ldx, din, lp.Wih, lp.bih, lp.Whh, lp.bhh, h0 + l * BH,
+                                     c0 + l * BH, S, d.B, d.H, hb, cb, gt, st, skip);
+    if (rf == SMI_E_NOFIT) {
+      const int64_t rows = (int64_t)S * d.B;
+      RC(launch_linear_fwd(Xl, ldx, (int)rows, din, lp.Wih, din, lp.bih, d.G4, ACT_NONE, s.xproj,
+                           d.G4, st, skip));
+      RC(launch_lstm_fwd(s.xproj, lp.Whh, lp.bhh, h0 + l * BH, c0 + l * BH, S, d.B, d.H, hb, cb, gt,
+                         st, skip));
+    } else if (rf) {
+      return rf;
+    }
+  }
+  return SMI_OK;
+}
+
+// gradients of the stacked LSTM's parameters (flat layout) from dh [E][B][H] at
+// the top layer's outputs: BPTT layer by layer downwards, each layer's input
+// gradient dgates_l W_ih_l (no activation between layers) the dh of the layer
+// below; the weight gradients over [x_t | h_{t-1}] join the phase's dW group
+static int lstm_backward(const RnnDims& d, const float* P, float* G, const RnnScratch& s,
                          hipStream_t st, const int* skip) {
-  RC(launch_lstm_bwd(s.dh, s.gates, s.cbuf, l.Whh, d.E, d.B, d.H, s.dgates, st, skip));
-  float* gWih = G;
-  float* gWhh = G + (int64_t)4 * d.H * d.Din;
-  float* gbih = gWhh + (int64_t)4 * d.H * d.H;
-  float* gbhh = gbih + d.G4;
+  const int64_t BH = (int64_t)d.B * d.H;
   const int M = (int)d.NE;
   static const int fused = [] { const char* e = getenv("SMI_LSTM_DW2"); return e ? atoi(e) : 1; }();
-  if (!fused) {     // A/B: the two launches over Xz and hbuf
-    RC(launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.Xz, d.ldx, d.Din, gWih, d.Din, gbih, 0, st,
-                            skip));
-    return launch_linear_bwd_dw(s.dgates, d.G4, M, d.G4, s.hbuf, d.H, d.H, gWhh, d.H, gbhh, 0, st,
-                                skip);
+  for (int l = d.L - 1; l >= 0; --l) {
+    const LstmP lp = lstm_layer(d, P, l);
+    float* dg = dgates_of(d, s, l);
+    float* hb = hbuf_of(d, s, l);
+    RC(launch_lstm_bwd(s.dh, gates_of(d, s, l), cbuf_of(d, s, l), lp.Whh, d.E, d.B, d.H, dg, st,
+                       skip));
+    const int din = l == 0 ? d.Din : d.H;
+    const float* Xl = l == 0 ? s.Xz : hbuf_of(d, s, l - 1) + BH;
+    const int64_t ldx = l == 0 ? d.ldx : d.H;
+    float* gWih = G + (l == 0 ? 0 : d.nL0 + (int64_t)(l - 1) * d.nLk);
+    float* gWhh = gWih + (int64_t)4 * d.H * din;
+    float* gbih = gWhh + (int64_t)4 * d.H * d.H;
+    float* gbhh = gbih + d.G4;
+    if (!fused) {     // A/B: the two launches over the layer input and hbuf
+      RC(launch_linear_bwd_dw(dg, d.G4, M, d.G4, Xl, ldx, din, gWih, din, gbih, 0, st, skip));
+      RC(launch_linear_bwd_dw(dg, d.G4, M, d.G4, hb, d.H, d.H, gWhh, d.H, gbhh, 0, st, skip));
+    } else {
+      // W_ih over x_t, W_hh over h_{t-1} (hbuf[0..E-1], hbuf[0] = h0) and the
+      // shared bias gradient in ONE launch over [x_t | h_{t-1}]
+      RC(launch_linear_bwd_dw2(dg, d.G4, M, d.G4, Xl, ldx, din, hb, d.H, d.H, gWih, din, gWhh,
+                               d.H, gbih, gbhh, st, skip));
+    }
+    if (l > 0)        // dh of layer l-1's outputs (steps 1..E) = dgates_l W_ih_l
+      RC(launch_linear_bwd_dx(dg, d.G4, M, d.G4, lp.Wih, d.H, d.H, nullptr, 0, s.dh, d.H, st, skip));
   }
-  // W_ih over x_t (Xz rows), W_hh over h_{t-1} (hbuf[0..E-1], hbuf[0] = h0) and
-  // the shared bias gradient in ONE launch over [x_t | h_{t-1}]
-  return launch_linear_bwd_dw2(s.dgates, d.G4, M, d.G4, s.Xz, d.ldx, d.Din, s.hbuf, d.H, d.H,
-                               gWih, d.Din, gWhh, d.H, gbih, gbhh, st, skip);
+  return SMI_OK;
 }
 
 static PixRows pix_rows(const smi_ppo_rnn_args& a, const RnnDims& d) {
@@ -783,15 +841,15 @@ static int cnn_bwd_from_dF(const smi_ppo_rnn_args& a, const RnnDims& d, const fl
 static int cnn_grad(const smi_ppo_rnn_args& a, const RnnDims& d, const LstmP& l, const float* cnn,
                     float* Gc, const RnnScratch& s, hipStream_t st, const int* skip) {
   if (d.F == 0) return SMI_OK;
-  RC(launch_linear_bwd_dx(s.dgates, d.G4, (int)d.NE, d.G4, l.Wih + d.D, d.Din, d.F, s.Xz + d.D,
-                          d.ldx, s.dF, d.F, st, skip));
+  RC(launch_linear_bwd_dx(dgates_of(d, s, 0), d.G4, (int)d.NE, d.G4, l.Wih + d.D, d.Din, d.F,
+                          s.Xz + d.D, d.ldx, s.dF, d.F, st, skip));
   return cnn_bwd_from_dF(a, d, cnn, Gc, s, st, skip);
 }
 
 // the policy / value features the heads read: LSTM outputs hbuf[1..] ([S][B][H])
 // or, without the LSTM (MLP policy), the stem input itself ([S][B][Din])
 static const float* head_in(const RnnDims& d, const RnnScratch& s, const float* X) {
-  return d.H > 0 ? s.hbuf + (int64_t)d.B * d.H : X;
+  return d.H > 0 ? hbuf_of(d, s, d.L - 1) + (int64_t)d.B * d.H : X;
 }
 
 // backward of one head into G (+ the stem below it): LSTM BPTT and/or CNN,
@@ -803,7 +861,7 @@ static int stem_backward_chain(const smi_ppo_rnn_args& a, const RnnDims& d, cons
   if (d.H > 0) {
     RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, 0, d.H, nullptr, 0,
                 s.dh, st, skip, side));
-    RC(lstm_backward(d, lm, G + n_head, s, st, skip));
+    RC(lstm_backward(d, a.lstm, G + n_head, s, st, skip));
     return cnn_grad(a, d, lm, cnn, G + n_head + d.nL, s, st, skip);
   }
   // MLP policy: the first head layer's input gradient over the CNN columns only
@@ -840,9 +898,9 @@ static float c_entropy_of(int A) {
   return (float)(0.5 * log(2.0 * 3.141592653589793 * 2.718281828459045) * (double)A);
 }
 
-int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int h1, int h2, int A, int c1,
+int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int L, int h1, int h2, int A, int c1,
                               int c2, int pc, int ph, int pw, int F) {
-  return 4 * rnn_scratch(rnn_dims(B, T, Hz, D, H, h1, h2, A, c1, c2, pc, ph, pw, F), nullptr)
+  return 4 * rnn_scratch(rnn_dims(B, T, Hz, D, H, h1, h2, A, c1, c2, pc, ph, pw, F, L), nullptr)
                  .total_floats;
 }
 
@@ -859,7 +917,8 @@ static PolRowArgs pol_rows(const smi_ppo_rnn_args& a, const RnnDims& d, const Rn
 
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
   const RnnDims d = rnn_dims(a.B, a.T, a.horizon, a.obs_dim, a.rnn_hidden, a.h1, a.h2, a.act_dim,
-                             a.critic_h1, a.critic_h2, a.pix_c, a.pix_h, a.pix_w, a.cnn_feat);
+                             a.critic_h1, a.critic_h2, a.pix_c, a.pix_h, a.pix_w, a.cnn_feat,
+                             a.rnn_layer);
   const RnnScratch s = rnn_scratch(d, a.scratch);
   if (s.total_floats * 4 > a.scratch_bytes) return set_error(SMI_E_ARG, "ppo_rnn: scratch too small");
   const int* stop = s.ci + CI_STOP;
@@ -882,7 +941,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       ktime_end(kt, KT_ZF_TMAJOR, 8.0 * (double)d.NG * d.D, st);      // read x, write z(x)
       RC(check_launch("zf_tmajor_kernel"));
       RC(cnn_features(a, d, cnn, d.S1, s.Xz, nullptr, s, st, nullptr));
-      if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.S1, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
+      if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.S1, a.h0, a.c0, s, false, st, nullptr));
       RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
       hipLaunchKernelGGL(tmajor_to_bmajor_kernel, dim3(grid_of(d.NG)), dim3(kWG), 0, st, s.OUT,
                          d.S1, d.B, s.values);
@@ -914,15 +973,14 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                            pol_rows(a, d, s), a.adv_out, a.ret_out);
         RC(check_launch("adv_export_kernel"));
       }
-      const LstmP lr = lstm_params(a.ref_lstm, d.Din, d.H);
-      if (d.H > 0) RC(lstm_forward(d, lr, X, d.E, a.h0, a.c0, s, nullptr, nullptr, st, nullptr));
+      if (d.H > 0) RC(lstm_forward(d, a.ref_lstm, X, d.E, a.h0, a.c0, s, false, st, nullptr));
       const Head ref{a.ref_actor, d.LA, d.Hin, d.h1, d.h2, d.A, 1};
       return head_fwd(ref, head_in(d, s, X), d.Hld, d.NE, s.HA1, s.HA2, s.refmu, st,
                       nullptr);
     }
     case SMI_RNN_PH_POLICY_FWD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, stop));
-      if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, stop));
+      if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, stop));
       RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE, kRowNT);
@@ -973,7 +1031,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     }
     case SMI_RNN_PH_VALUE_GRAD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
-      if (d.H > 0) RC(lstm_forward(d, lm, s.Xz, d.E, a.h0, a.c0, s, s.cbuf, s.gates, st, nullptr));
+      if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, nullptr));
       RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
       const int nb = rnn_nblk(d.NE, kRowNT);
       const bool last = e == a.epoch_baseline - 1;

@@ -128,7 +128,7 @@ int64_t ppo_xbuf_floats(int D, int H1, int H2, int A, int cH1, int cH2, int mode
 int launch_ppo_epoch_grad(const smi_ppo_args* args, int epoch, hipStream_t stream);
 int launch_ppo_epoch_apply(const smi_ppo_args* args, int epoch, hipStream_t stream);
 
-int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int h1, int h2, int A, int c1,
+int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int L, int h1, int h2, int A, int c1,
                               int c2, int pc, int ph, int pw, int F);
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st);
 int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,

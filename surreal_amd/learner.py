@@ -183,9 +183,9 @@ class PPOLearner(object):
             self.beta = self.beta_init
         else:
             raise ConfigError('ppo_mode must be clip or adapt')
-        if self.if_rnn_policy and algo.rnn.get('rnn_layer', 1) != 1:
-            raise NotImplementedError('surreal_amd: the LSTM policy supports rnn_layer == 1 '
-                                      '(the reference default)')
+        self.rnn_layer = int(algo.rnn.get('rnn_layer', 1)) if self.if_rnn_policy else 1
+        if not 1 <= self.rnn_layer <= 3:
+            raise NotImplementedError('surreal_amd: the LSTM policy supports rnn_layer 1..3')
         self.if_pixel_input = bool(ec.get('pixel_input', False))
 
         anneal = algo.network.anneal
@@ -482,8 +482,10 @@ class PPOLearner(object):
             if onetime_infos is None or len(onetime_infos) < 2:
                 raise ValueError('RNN policy: onetime_infos must hold the (h, c) LSTM cells')
             Hd = self.learner_config.algo.rnn.rnn_hidden
-            h0 = onetime_infos[0].reshape(B, -1, Hd)[:, 0, :].contiguous()   # (B, L, H) -> layer 0
-            c0 = onetime_infos[1].reshape(B, -1, Hd)[:, 0, :].contiguous()
+            # (B, L, H) -> (L, B, H), as ppo.py:508-509 transposes them
+            NL = self.rnn_layer
+            h0 = onetime_infos[0].reshape(B, NL, Hd).transpose(0, 1).contiguous()
+            c0 = onetime_infos[1].reshape(B, NL, Hd).transpose(0, 1).contiguous()
         else:                       # MLP policy over the pixel stem (ppo.py:532-535: step 0)
             Hd, h0, c0 = 0, None, None
         pds = persistent_infos[-1].contiguous()
@@ -500,9 +502,10 @@ class PPOLearner(object):
         pc, ph, pw = self.obs_spec['pixel']['camera0'] if pix is not None else (0, 0, 0)
         F = int(self.learner_config.model.cnn_feature_dim) if pix is not None else 0
         nbytes = lib.smi_ppo_rnn_scratch_bytes(B, T, H, D, Hd, a_h1, a_h2, A, c_h1, c_h2,
-                                               pc, ph, pw, F)
+                                               pc, ph, pw, F, self.rnn_layer)
         scratch = self._buf('rnn_scratch', (nbytes // 4,))
-        nx = lib.smi_ppo_rnn_xbuf_floats(D, Hd, a_h1, a_h2, A, c_h1, c_h2, pc, ph, pw, F)
+        nx = lib.smi_ppo_rnn_xbuf_floats(D, Hd, a_h1, a_h2, A, c_h1, c_h2, pc, ph, pw, F,
+                                         self.rnn_layer)
         xbuf = self._buf('rnn_xbuf', (nx,))
         moments = self._buf('rnn_moments', (3,), torch.float64)
         pstat = self._buf('rnn_pstat', (L.RNN_PSTAT,), torch.float64)
@@ -524,6 +527,7 @@ class PPOLearner(object):
         a.obs_next = xn.data_ptr() if xn is not None else None
         a.actions = actions.data_ptr()
         a.pix_c, a.pix_h, a.pix_w, a.cnn_feat = pc, ph, pw, F
+        a.rnn_layer = self.rnn_layer
         a.pixels = pix.data_ptr() if pix is not None else None
         a.pixels_next = pixn.data_ptr() if pixn is not None else None
         a.rewards, a.dones, a.behave = rewards.data_ptr(), dones.data_ptr(), pds.data_ptr()

@@ -152,66 +152,90 @@ class PPO_CriticNetwork(_FlatMLP):
         return out
 
 
+def lstm_param_count(input_size, hidden_size, num_layers=1):
+    """floats of a stacked LSTM in the C-ABI layout (layer k >= 1 reads hidden_size)"""
+    lib = L.lib()
+    return int(lib.smi_lstm_param_count(input_size, hidden_size)) + \
+        (num_layers - 1) * int(lib.smi_lstm_param_count(hidden_size, hidden_size))
+
+
 class LSTMStem(_FlatViews):
-    """nn.LSTM(input_size, hidden_size, 1, batch_first=True) of PPOModel
-    (ppo_net.py:143-152) over ONE flat device buffer in the C-ABI LSTM layout
-    [W_ih (4H, in) | W_hh (4H, H) | b_ih (4H) | b_hh (4H)] (torch's parameter
-    order and gate order i, f, g, o).  The Parameters are views named and shaped
-    like torch's (weight_ih_l0, weight_hh_l0, bias_ih_l0, bias_hh_l0), so
-    state_dict() matches nn.LSTM's.  forward() runs the x-projection GEMM and the
+    """nn.LSTM(input_size, hidden_size, num_layers, batch_first=True) of PPOModel
+    (ppo_net.py:143-152) over ONE flat device buffer in the C-ABI LSTM layout:
+    per layer [W_ih (4H, in) | W_hh (4H, H) | b_ih (4H) | b_hh (4H)] (torch's
+    parameter order and gate order i, f, g, o; layer k >= 1 has in = H), layers
+    one after another.  The Parameters are views named and shaped like torch's
+    (weight_ih_l{k}, weight_hh_l{k}, bias_ih_l{k}, bias_hh_l{k}), so state_dict()
+    matches nn.LSTM's.  forward() runs, per layer, the x-projection GEMM and the
     persistent LSTM sequence kernel; inputs are batch_first (B, S, in)."""
 
     def __init__(self, input_size, hidden_size, num_layers=1, batch_first=True, device=None,
                  generator=None, flat=None):
         super().__init__()
-        if num_layers != 1:
-            raise NotImplementedError('surreal_amd: LSTM stem supports rnn_layer == 1 '
-                                      '(the reference default, ppo_configs.py)')
+        if not 1 <= num_layers <= 3:
+            raise NotImplementedError('surreal_amd: LSTM stem supports rnn_layer 1..3')
         if not batch_first:
             raise NotImplementedError('surreal_amd: the reference builds the LSTM batch_first')
         self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
-        H, D = hidden_size, input_size
-        n = int(L.lib().smi_lstm_param_count(D, H))
+        H = hidden_size
+        n = lstm_param_count(input_size, H, num_layers)
         if flat is None:
             flat = torch.zeros(n, dtype=torch.float32, device=device)
         assert flat.numel() == n
         o = 0
-        self.weight_ih_l0 = nn.Parameter(flat[o:o + 4 * H * D].view(4 * H, D)); o += 4 * H * D
-        self.weight_hh_l0 = nn.Parameter(flat[o:o + 4 * H * H].view(4 * H, H)); o += 4 * H * H
-        self.bias_ih_l0 = nn.Parameter(flat[o:o + 4 * H]); o += 4 * H
-        self.bias_hh_l0 = nn.Parameter(flat[o:o + 4 * H]); o += 4 * H
+        for k in range(num_layers):
+            D = input_size if k == 0 else H
+            setattr(self, f'weight_ih_l{k}', nn.Parameter(flat[o:o + 4 * H * D].view(4 * H, D)))
+            o += 4 * H * D
+            setattr(self, f'weight_hh_l{k}', nn.Parameter(flat[o:o + 4 * H * H].view(4 * H, H)))
+            o += 4 * H * H
+            setattr(self, f'bias_ih_l{k}', nn.Parameter(flat[o:o + 4 * H]))
+            o += 4 * H
+            setattr(self, f'bias_hh_l{k}', nn.Parameter(flat[o:o + 4 * H]))
+            o += 4 * H
         self.__dict__['flat'] = flat
         self.reset_parameters(generator)
+
+    def layer_params(self, k):
+        return tuple(getattr(self, f'{n}_l{k}') for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh'))
 
     def reset_parameters(self, generator=None):
         # torch.nn.LSTM default init: every parameter U(-1/sqrt(H), 1/sqrt(H))
         k = 1.0 / math.sqrt(self.hidden_size)
         with torch.no_grad():
-            for p in (self.weight_ih_l0, self.weight_hh_l0, self.bias_ih_l0, self.bias_hh_l0):
-                p.copy_(torch.empty(p.shape).uniform_(-k, k, generator=generator))
+            for layer in range(self.num_layers):
+                for p in self.layer_params(layer):
+                    p.copy_(torch.empty(p.shape).uniform_(-k, k, generator=generator))
 
     def forward(self, x, cells=None):
-        """x (B, S, in) -> (out (B, S, H), (h_n, c_n) each (1, B, H))."""
-        B, S, D = x.shape
-        H = self.hidden_size
+        """x (B, S, in) -> (out (B, S, H), (h_n, c_n) each (num_layers, B, H))."""
+        B, S, _ = x.shape
+        H, NL = self.hidden_size, self.num_layers
         dev = self.flat.device
         st = L.stream(dev)
-        xt = x.transpose(0, 1).contiguous()                       # time-major (S, B, D)
-        xproj = torch.empty(S, B, 4 * H, dtype=torch.float32, device=dev)
-        L.call('smi_linear_forward', L.ptr(xt), D, S * B, D, L.ptr(self.weight_ih_l0), D,
-               L.ptr(self.bias_ih_l0), 4 * H, 0, L.ptr(xproj), 4 * H, st)
         if cells is None:
-            h0 = torch.zeros(B, H, device=dev)
-            c0 = torch.zeros(B, H, device=dev)
+            h0 = torch.zeros(NL, B, H, device=dev)
+            c0 = torch.zeros(NL, B, H, device=dev)
         else:
-            h0 = cells[0].reshape(B, H).contiguous()
-            c0 = cells[1].reshape(B, H).contiguous()
-        hbuf = torch.empty(S + 1, B, H, dtype=torch.float32, device=dev)
-        cbuf = torch.empty(S + 1, B, H, dtype=torch.float32, device=dev)
-        L.call('smi_lstm_forward', L.ptr(xproj), L.ptr(self.weight_hh_l0), L.ptr(self.bias_hh_l0),
-               L.ptr(h0), L.ptr(c0), S, B, H, L.ptr(hbuf), L.ptr(cbuf), None, st)
-        out = hbuf[1:].transpose(0, 1).contiguous()
-        return out, (hbuf[S].unsqueeze(0).clone(), cbuf[S].unsqueeze(0).clone())
+            h0 = cells[0].reshape(NL, B, H).contiguous()
+            c0 = cells[1].reshape(NL, B, H).contiguous()
+        inp = x.transpose(0, 1).contiguous()                      # time-major (S, B, in)
+        hn, cn = [], []
+        for k in range(NL):
+            w_ih, w_hh, b_ih, b_hh = self.layer_params(k)
+            D = inp.shape[-1]
+            xproj = torch.empty(S, B, 4 * H, dtype=torch.float32, device=dev)
+            L.call('smi_linear_forward', L.ptr(inp), D, S * B, D, L.ptr(w_ih), D, L.ptr(b_ih), 4 * H, 0,
+                   L.ptr(xproj), 4 * H, st)
+            hbuf = torch.empty(S + 1, B, H, dtype=torch.float32, device=dev)
+            cbuf = torch.empty(S + 1, B, H, dtype=torch.float32, device=dev)
+            L.call('smi_lstm_forward', L.ptr(xproj), L.ptr(w_hh), L.ptr(b_hh), L.ptr(h0[k]),
+                   L.ptr(c0[k]), S, B, H, L.ptr(hbuf), L.ptr(cbuf), None, st)
+            hn.append(hbuf[S].clone())
+            cn.append(cbuf[S].clone())
+            inp = hbuf[1:]                                        # (S, B, H), contiguous
+        out = inp.transpose(0, 1).contiguous()
+        return out, (torch.stack(hn), torch.stack(cn))
 
 
 class _ParamView(_FlatViews):
@@ -423,7 +447,7 @@ class DiagGauss(object):
 class PPOModel(nn.Module):
     """ppo_net.py:94-375 (low-dimensional observations).
 
-    The LSTM stem (if_rnn_policy, rnn_layer 1) is the HIP LSTMStem and the pixel
+    The LSTM stem (if_rnn_policy, rnn_layer 1..3) is the HIP LSTMStem and the pixel
     stem (if_pixel_input) the HIP CNNStemNetwork on obs['pixel']['camera0']
     (uint8).  With both, their parameters share one flat `stem_flat` buffer
     [lstm | cnn] (the layout smi_ppo_rnn_phase and the optimizers use).
@@ -459,7 +483,8 @@ class PPOModel(nn.Module):
             n_cnn = int(L.lib().smi_cnn_param_count(C, H, W, F))
         n_rnn = 0
         if self.if_rnn:
-            n_rnn = int(L.lib().smi_lstm_param_count(d_in, self.rnn_config['rnn_hidden']))
+            n_rnn = lstm_param_count(d_in, self.rnn_config['rnn_hidden'],
+                                     self.rnn_config.get('rnn_layer', 1))
         stem = torch.zeros(n_rnn + n_cnn, dtype=torch.float32, device=self.device)
         if if_pixel_input:                                  # ppo_net.py:137-141
             self.cnn_stem = CNNStemNetwork(obs_spec['pixel']['camera0'], F, device=self.device,

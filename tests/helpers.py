@@ -10,7 +10,7 @@ from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, Config, gym_env_confi
 def ppo_config(B=64, T=50, mode='clip', use_z_filter=True, hidden=(64, 64), lam=0.95,
                gamma=0.99, epochs=(10, 10), norm_adv=True, use_r_filter=False, reward_scale=1.0,
                kl_target=0.02, lr=(3e-4, 3e-4), wd=(0.0, 0.0), rnn=False, rnn_hidden=100,
-               horizon=5, critic_hidden=None, cnn_feat=256):
+               horizon=5, critic_hidden=None, cnn_feat=256, rnn_layer=1):
     lc = copy.deepcopy(PPO_DEFAULT_LEARNER_CONFIG)
     lc.model.actor_fc_hidden_sizes = list(hidden)
     lc.model.critic_fc_hidden_sizes = list(critic_hidden if critic_hidden is not None else hidden)
@@ -24,7 +24,7 @@ def ppo_config(B=64, T=50, mode='clip', use_z_filter=True, hidden=(64, 64), lam=
     lc.algo.advantage.reward_scale = reward_scale
     lc.algo.rnn.if_rnn_policy = bool(rnn)
     lc.algo.rnn.rnn_hidden = rnn_hidden
-    lc.algo.rnn.rnn_layer = 1
+    lc.algo.rnn.rnn_layer = rnn_layer
     lc.algo.rnn.horizon = horizon
     lc.algo.consts.epoch_policy = epochs[0]
     lc.algo.consts.epoch_baseline = epochs[1]
@@ -64,10 +64,11 @@ def copy_weights_to_oracle(learner, ref):
 
 
 def load_lstm_flat(lstm, flat):
-    """C-ABI LSTM layout [W_ih | W_hh | b_ih | b_hh] -> a torch nn.LSTM (1 layer)."""
+    """C-ABI LSTM layout (per layer [W_ih | W_hh | b_ih | b_hh]) -> a torch nn.LSTM
+    (nn.LSTM.parameters() has exactly that order)."""
     o = 0
     with torch.no_grad():
-        for p in (lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0):
+        for p in lstm.parameters():
             n = p.numel()
             p.copy_(flat[o:o + n].reshape(p.shape))
             o += n
@@ -89,8 +90,7 @@ def seq_flat(module):
 
 
 def lstm_flat(lstm):
-    return torch.cat([p.detach().reshape(-1) for p in
-                      (lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0)])
+    return torch.cat([p.detach().reshape(-1) for p in lstm.parameters()])
 
 
 def oracle_batch(batch):

@@ -14,12 +14,15 @@ For every tensor and statistic:
 
     max|GPU - fp64| <= 2 * max_variants max|variant - fp64| + SLACK * scale
 
-with scale = max|fp64| (|fp64| for a scalar), SLACK = 1e-6, and the number of
+with scale = max|fp64| (|fp64| for a scalar; for the explained variance
+max(|ev|, |1 - ev|), the magnitude of the variance ratio it is one minus),
+SLACK = 1e-6, and the number of
 policy epochs run equal in all executions.  A scalar statistic (last_stats())
 passes within 3x the envelope, or within the north_star's fixed fp32
 tolerance, 1e-5 relative: after 10 epochs a statistic is ONE draw from the
 chaotic spread, and 9 envelope draws bound a single draw less tightly than
-the max over the 1e5 entries of a parameter tensor does.  (Measured at
+the max over the 1e5 entries of a parameter tensor does — so a statistic's
+envelope is pooled over the run's learn() calls.  (Measured at
 C3 adapt: the envelope of a post-training statistic is set by the perturbed
 fp64 executions; the fp32 summation orders sit 10-100x closer to fp64.)
 
@@ -74,14 +77,17 @@ STAT_KEYS = ('_surr_loss', '_entropy', '_pol_kl', '_val_loss', '_avg_return_targ
              'grad_norm_critic', '_avg_log_sig', '_val_explained_var')
 
 
-def as_good_as_fp32(name, got, variants, r64, report, slack=SLACK, rtol=None, factor=2.0):
-    """max|got - r64| <= factor * max_k max|variants[k] - r64| + slack * max|r64|
-    (or, when rtol is given, <= rtol * max|r64|: the north_star's fixed fp32
-    tolerance, used for scalar statistics)."""
+def as_good_as_fp32(name, got, variants, r64, report, slack=SLACK, rtol=None, factor=2.0,
+                    scale=None):
+    """max|got - r64| <= factor * max_k max|variants[k] - r64| + slack * scale
+    (or, when rtol is given, <= rtol * scale: the north_star's fixed fp32
+    tolerance, used for scalar statistics); scale = max|r64| unless given."""
     got, r64 = (np.asarray(t, dtype=np.float64).reshape(-1) for t in (got, r64))
     variants = [np.asarray(t, dtype=np.float64).reshape(-1) for t in variants]
     assert all(got.shape == r64.shape == r.shape for r in variants), (name, got.shape, r64.shape)
-    scale = max(float(np.abs(r64).max()) if r64.size else 0.0, 1e-30)
+    if scale is None:
+        scale = float(np.abs(r64).max()) if r64.size else 0.0
+    scale = max(scale, 1e-30)
     e_gpu = float(np.abs(got - r64).max()) if r64.size else 0.0
     e_env = max(float(np.abs(r - r64).max()) for r in variants) if r64.size else 0.0
     ok = e_gpu <= factor * e_env + slack * scale or (rtol is not None and e_gpu <= rtol * scale)
@@ -213,12 +219,13 @@ def pinned_run(lc, D, A, iters=1, pixel=None, seed=0, rnn_hidden=None, source='s
     learner.export_advantages = True
     r64, vs = _envelope(learner, lc, D, A, pixel, n_ulp, orders)
     report = {}
+    stat_rec = {}
     for it in range(iters):
         if source == 'host':
             batch = _host_batch(learner, B, T, D, A, seed * 100 + it, rnn_hidden, pixel)
         else:
             batch = synthetic.ppo_batch(B, T, D, A, seed=seed * 100 + it, rnn_hidden=rnn_hidden,
-                                        pixel=pixel)
+                                        pixel=pixel, rnn_layers=lc.algo.rnn.rnn_layer)
         ob = oracle_batch(batch)
         s64, svs = _run_oracles(r64, vs, ob, seed * 100 + it)
         learner.learn(batch if source == 'host' else synthetic.to_device(batch, DEV))
@@ -227,8 +234,14 @@ def pinned_run(lc, D, A, iters=1, pixel=None, seed=0, rnn_hidden=None, source='s
         assert len(set(runs)) == 1, (it, runs)
         keys = STAT_KEYS + (('_clip_surr_loss',) if lc.algo.ppo_mode == 'clip' else ('_kl_loss_adapt',))
         for k in keys:
-            as_good_as_fp32(f'{k}@{it}', [s[k]], [[x[k]] for x in svs], [s64[k]], report,
-                            rtol=RTOL_STAT, factor=STAT_FACTOR)
+            # explained variance 1 - var(R - V)/var(R) (ppo.py:324-331) is a
+            # difference from 1: its error is that of the variance ratio, so its
+            # scale is the ratio's magnitude (near-zero values would otherwise be
+            # held to a relative bar they cannot carry)
+            sc = max(abs(s64[k]), abs(1.0 - s64[k])) if k == '_val_explained_var' else abs(s64[k])
+            sc = max(sc, 1e-30)
+            stat_rec.setdefault(k, []).append(
+                (it, abs(s[k] - s64[k]) / sc, max(abs(x[k] - s64[k]) for x in svs) / sc))
         # advantages as the epochs use them, raw advantages, returns (per segment)
         rnn = 'ret_used' in learner._bufs          # the phase path exports (B, E) windows
         seg =lambda name: [v.per_segment(getattr(v.ref, name).numpy()) for v in vs]  # noqa: E731
@@ -252,6 +265,17 @@ def pinned_run(lc, D, A, iters=1, pixel=None, seed=0, rnn_hidden=None, source='s
                 as_good_as_fp32(f'zf_{b}@{it}', getattr(zf, b).cpu(),
                                 [getattr(v.ref.model.z_filter, b) for v in vs], getattr(z64, b), report)
             assert float(zf.count.item()) == float(vs[0].ref.model.z_filter.count.item())
+    # scalar statistics: one draw each per learn(); their envelope is pooled over
+    # the run's learn() calls (the fp32 spread of a statistic is a property of
+    # the configuration — e.g. the post-update KL is quadratic in mean
+    # differences of ~1e-2 and moves ~1e-5..1e-4 relative per fp32 draw)
+    for k, rec in stat_rec.items():
+        env = max(r[2] for r in rec)
+        for it, e_gpu, e_env in rec:
+            ok = e_gpu <= STAT_FACTOR * env + SLACK or e_gpu <= RTOL_STAT
+            report[f'{k}@{it}'] = (e_gpu, env, ok)
+            if not ok:
+                report.setdefault('_fail', []).append(f'{k}@{it}')
     print_report(report)
     return report
 
@@ -343,6 +367,19 @@ def test_pinned_c5_full_batch():
     lc.model.cnn_feature_dim = 256
     pinned_run(lc, 42, 8, iters=1, pixel=(3, 84, 84), rnn_hidden=100, seed=4, n_ulp=3,
                orders=('given', 'reversed'))
+
+
+@pytest.mark.parametrize('layers,Hd', [(2, 100), (3, 24)])
+def test_pinned_stacked_lstm(layers, Hd):
+    # nn.LSTM(num_layers = rnn_layer) (ppo_net.py:146-149): layer 0 on the fused
+    # input projection, layers >= 1 on the x-projection GEMM + recurrence, BPTT
+    # layer by layer with the inter-layer input gradient dgates W_ih
+    lc = ppo_config(B=64, T=10, mode='adapt', use_z_filter=True, hidden=(64, 64), lam=1.0,
+                    epochs=(3, 3), rnn=True, rnn_hidden=Hd, horizon=3, rnn_layer=layers)
+    # a cheap case: 16 perturbed executions make the envelope a better estimate
+    # of the fp32 spread of the post-update KL (quadratic in mean differences
+    # of ~1e-2, so one fp32 draw moves it ~1e-5..1e-4 relative)
+    pinned_run(lc, 42, 8, iters=2, rnn_hidden=Hd, seed=8 + layers, n_ulp=16)
 
 
 # ------------------------------------------------ host numpy input path (a2/a18)
