@@ -17,6 +17,8 @@ bench)
   done
   timeout -k 10 300 python -u bench.py --config c3 --local-segments 128 --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_c3_local128.json 2> $OUT/bench_c3_local128.err || exit 1
   timeout -k 10 300 python -u bench.py --config c5 --local-segments 128 --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_c5_local128.json 2> $OUT/bench_c5_local128.err || exit 1
+  # streaming kernels at > 256 MB working sets inside learn(): 65536 segments
+  timeout -k 10 300 python -u bench.py --config c3 --local-segments 65536 --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench_c3_local65536.json 2> $OUT/bench_c3_local65536.err || exit 1
   SMI_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_c3_dp2_gloo.json 2> $OUT/bench_c3_dp2_gloo.err || exit 1
   cut -c1-300 $OUT/bench_c3_local128.json ;;
 prof)
