@@ -98,8 +98,10 @@ struct RnnScratch {
 static inline int64_t al64(int64_t n) { return (n + 63) & ~(int64_t)63; }
 
 __host__ __device__ inline int rnn_nblk(int64_t rows, int nt = kWG) {
+  // at most 1024 four-wave blocks' worth of waves (4096 one-wave blocks)
+  const int64_t cap = (int64_t)1024 * kWG / nt;
   const int64_t b = (rows + nt - 1) / nt;
-  return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
+  return (int)(b < cap ? (b < 1 ? 1 : b) : cap);
 }
 // per-row loss kernels (a thread per row, ~100 dependent VALU / transcendental
 // ops each): one-wave blocks so the rows of a C3 batch (21504) spread over
@@ -130,7 +132,7 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   s.adv = take(d.NE);
   s.ret = take(d.NE);
   s.refmu = take(d.NE * d.A);
-  s.lvpart = take((int64_t)1024 * d.A);
+  s.lvpart = take((int64_t)4096 * d.A);
   const bool px = d.F > 0;
   s.A1 = take(px ? d.NE * 16 * d.G.P1 : 0);
   s.A2 = take(px ? d.NG * d.G.flat : 0);
@@ -193,27 +195,6 @@ reduce_partials_kernel(const double* __restrict__ part, int nb, int w, double* o
   }
 }
 
-__device__ inline float dg_row_loglik(const float* act, const float* mu, const float* sd,
-                                      const float* logsd, int A, float c_ll) {
-  float s = 0.f, l = 0.f;
-  for (int j = 0; j < A; ++j) {
-    const float u = (act[j] - mu[j]) / sd[j];
-    s += u * u;
-    l += logsd[j];
-  }
-  return (-0.5f * s - c_ll) - l;
-}
-__device__ inline float dg_row_kl(const float* mu0, const float* sd0, const float* mu1,
-                                  const float* sd1, int A) {
-  float s1 = 0.f, s2 = 0.f;
-  for (int j = 0; j < A; ++j) {
-    s1 += logf(sd1[j] / sd0[j]);
-    const float d = mu0[j] - mu1[j];
-    s2 += (sd0[j] * sd0[j] + d * d) / (2.f * (sd1[j] * sd1[j]));
-  }
-  return (s1 + s2) - 0.5f * (float)A;
-}
-
 struct PolRowArgs {
   int B, T, E, A, mode;
   const float* mu;        // [NE][A] learner means (tanh applied)
@@ -258,21 +239,83 @@ adv_export_kernel(PolRowArgs a, float* __restrict__ adv_out, float* __restrict__
   }
 }
 
+// Row access of the per-row loss kernels.  AT > 0: the action width is a
+// compile-time constant (the benched A = 8 and HalfCheetah's 6), so a row's
+// values live in registers (fully unrolled loops) and rows of 4k floats move
+// as float4 (16-byte aligned: row offsets are multiples of 4A bytes); AT == 0:
+// any A <= 32 through runtime loops.
+template <int AT>
+__device__ __forceinline__ void ld_row(float* dst, const float* __restrict__ src, int A) {
+  if constexpr (AT > 0 && AT % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < AT / 4; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(src)[q];
+      dst[4 * q] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
+    }
+  } else if constexpr (AT > 0) {
+#pragma unroll
+    for (int j = 0; j < AT; ++j) dst[j] = src[j];
+  } else {
+    for (int j = 0; j < A; ++j) dst[j] = src[j];
+  }
+}
+template <int AT>
+__device__ __forceinline__ void st_row(float* __restrict__ dst, const float* src, int A) {
+  if constexpr (AT > 0 && AT % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < AT / 4; ++q)
+      reinterpret_cast<float4*>(dst)[q] = float4{src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]};
+  } else if constexpr (AT > 0) {
+#pragma unroll
+    for (int j = 0; j < AT; ++j) dst[j] = src[j];
+  } else {
+    for (int j = 0; j < A; ++j) dst[j] = src[j];
+  }
+}
+template <int AT>
+__device__ __forceinline__ float row_loglik(const float* act, const float* mu, const float* sd,
+                                            const float* logsd, int A, float c_ll) {
+  float s = 0.f, l = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    const float u = (act[j] - mu[j]) / sd[j];
+    s += u * u;
+    l += logsd[j];
+  }
+  return (-0.5f * s - c_ll) - l;
+}
+template <int AT>
+__device__ __forceinline__ float row_kl(const float* mu0, const float* sd0, const float* mu1,
+                                        const float* sd1, int A) {
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    s1 += logf(sd1[j] / sd0[j]);
+    const float d = mu0[j] - mu1[j];
+    s2 += (sd0[j] * sd0[j] + d * d) / (2.f * (sd1[j] * sd1[j]));
+  }
+  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
+}
+
 // forward statistics of the policy over the E*B rows (ppo.py:203-224,
 // 262-284, 553-575)
-template <int NT>
+template <int NT, int AT>
 __global__ void __launch_bounds__(NT)
 policy_rows_stats_kernel(PolRowArgs a) {
   if (a.skip && a.skip[0] != 0) return;
-  __shared__ float sig[32], lsig[32], rsig[32];
+  constexpr int AM = AT > 0 ? AT : 32;
+  __shared__ float ssig[32], slsig[32], srsig[32];
   __shared__ double scr[NT / 64][PS_N];
-  const int A = a.A;
+  const int A = AT > 0 ? AT : a.A;
   for (int j = threadIdx.x; j < A; j += NT) {
-    sig[j] = expf(a.lv[j]);                 // builders.py:127 std = exp(log_var)
-    lsig[j] = logf(sig[j]);                 // std0.log() of ppo_net.py:40
-    rsig[j] = expf(a.ref_lv[j]);
+    ssig[j] = expf(a.lv[j]);                 // builders.py:127 std = exp(log_var)
+    slsig[j] = logf(ssig[j]);                // std0.log() of ppo_net.py:40
+    srsig[j] = expf(a.ref_lv[j]);
   }
   __syncthreads();
+  float sig[AM], lsig[AM], rsig[AM];
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) { sig[j] = ssig[j]; lsig[j] = slsig[j]; rsig[j] = srsig[j]; }
   const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   double acc[PS_N];
 #pragma unroll
@@ -280,16 +323,19 @@ policy_rows_stats_kernel(PolRowArgs a) {
   const int64_t N = (int64_t)a.E * a.B;
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
     const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
-    const float* m = a.mu + n * A;
-    const float* rm = a.refmu + n * A;
-    const float* ac = a.actions + ((int64_t)b * a.T + t) * A;
+    float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM];
+    ld_row<AT>(m, a.mu + n * A, A);
+    ld_row<AT>(rm, a.refmu + n * A, A);
+    ld_row<AT>(ac, a.actions + ((int64_t)b * a.T + t) * A, A);
     const float* bp = a.behave + ((int64_t)b * a.T + t) * 2 * A;
+    ld_row<AT>(bmu, bp, A);
+    ld_row<AT>(bsd, bp + A, A);
     const float av = norm_adv_of(a, a.adv[(int64_t)b * a.E + t]);
-    const float lp = fmaxf(expf(dg_row_loglik(ac, m, sig, lsig, A, a.c_ll)), 1e-5f);
-    float blsd[32];
-    for (int j = 0; j < A; ++j) blsd[j] = logf(bp[A + j]);
-    const float bl = fmaxf(expf(dg_row_loglik(ac, bp, bp + A, blsd, A, a.c_ll)), 1e-5f);
-    acc[PS_KL] += (double)dg_row_kl(rm, rsig, m, sig, A);
+    const float lp = fmaxf(expf(row_loglik<AT>(ac, m, sig, lsig, A, a.c_ll)), 1e-5f);
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) blsd[j] = logf(bsd[j]);
+    const float bl = fmaxf(expf(row_loglik<AT>(ac, bmu, bsd, blsd, A, a.c_ll)), 1e-5f);
+    acc[PS_KL] += (double)row_kl<AT>(rm, rsig, m, sig, A);
     if (a.mode == 0) {
       const float ratio = lp / bl;
       const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
@@ -301,7 +347,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
     }
     acc[PS_ISW] += (double)(lp / (bl + 1e-4f));
     acc[PS_BL] += (double)bl;
-    acc[PS_RBD] += (double)dg_row_kl(rm, rsig, bp, bp + A, A);
+    acc[PS_RBD] += (double)row_kl<AT>(rm, rsig, bmu, bsd, A);
     acc[PS_RET] += (double)a.ret[(int64_t)b * a.E + t];
   }
   // all PS_N sums at once: wave butterflies, one barrier, fixed wave order
@@ -324,37 +370,45 @@ policy_rows_stats_kernel(PolRowArgs a) {
 // block partials of d loss / d log_var (ppo_net.py:29-72, ppo.py:209-217,
 // 267-277): surrogate weight cf[CF_SURRW] (1/N), KL weight cf[CF_KLCOEF] (adapt:
 // (beta + 2 eta relu(kl - 2kt)) / N, clip: 0)
-template <int NT>
+template <int NT, int AT>
 __global__ void __launch_bounds__(NT)
 policy_rows_grad_kernel(PolRowArgs a) {
   if (a.skip && a.skip[0] != 0) return;
-  __shared__ float sig[32], lsig[32], rsig[32];
+  constexpr int AM = AT > 0 ? AT : 32;
+  __shared__ float ssig[32], slsig[32], srsig[32];
   __shared__ float gls[NT / 64][32];
-  const int A = a.A;
+  const int A = AT > 0 ? AT : a.A;
   for (int j = threadIdx.x; j < A; j += NT) {
-    sig[j] = expf(a.lv[j]);
-    lsig[j] = logf(sig[j]);
-    rsig[j] = expf(a.ref_lv[j]);
+    ssig[j] = expf(a.lv[j]);
+    slsig[j] = logf(ssig[j]);
+    srsig[j] = expf(a.ref_lv[j]);
   }
   __syncthreads();
+  float sig[AM], lsig[AM], rsig[AM];
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) { sig[j] = ssig[j]; lsig[j] = slsig[j]; rsig[j] = srsig[j]; }
   const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   const float wsurr = a.cf[CF_SURRW], wkl = a.cf[CF_KLCOEF];
-  float glv[32];
-  for (int j = 0; j < A; ++j) glv[j] = 0.f;
+  float glv[AM];
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
   const int64_t N = (int64_t)a.E * a.B;
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
     const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
-    const float* m = a.mu + n * A;
-    const float* rm = a.refmu + n * A;
-    const float* ac = a.actions + ((int64_t)b * a.T + t) * A;
+    float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM], dz[AM];
+    ld_row<AT>(m, a.mu + n * A, A);
+    ld_row<AT>(rm, a.refmu + n * A, A);
+    ld_row<AT>(ac, a.actions + ((int64_t)b * a.T + t) * A, A);
     const float* bp = a.behave + ((int64_t)b * a.T + t) * 2 * A;
+    ld_row<AT>(bmu, bp, A);
+    ld_row<AT>(bsd, bp + A, A);
     const float av = norm_adv_of(a, a.adv[(int64_t)b * a.E + t]);
-    const float ll = dg_row_loglik(ac, m, sig, lsig, A, a.c_ll);
+    const float ll = row_loglik<AT>(ac, m, sig, lsig, A, a.c_ll);
     const float ex = expf(ll);
     const float lp = fmaxf(ex, 1e-5f);
-    float blsd[32];
-    for (int j = 0; j < A; ++j) blsd[j] = logf(bp[A + j]);
-    const float bl = fmaxf(expf(dg_row_loglik(ac, bp, bp + A, blsd, A, a.c_ll)), 1e-5f);
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) blsd[j] = logf(bsd[j]);
+    const float bl = fmaxf(expf(row_loglik<AT>(ac, bmu, bsd, blsd, A, a.c_ll)), 1e-5f);
     float g_lp;
     if (a.mode == 0) {
       const float ratio = lp / bl;
@@ -367,8 +421,8 @@ policy_rows_grad_kernel(PolRowArgs a) {
       g_lp = (-wsurr * av) / fmaxf(bl, 1e-2f);
     }
     const float g_ll = (ex >= 1e-5f) ? g_lp * ex : 0.f;    // clamp + exp backward
-    float* dz = a.dz + n * A;
-    for (int j = 0; j < A; ++j) {
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
       const float s1 = sig[j];
       const float u = (ac[j] - m[j]) / s1;
       float gmu = g_ll * (u / s1);
@@ -381,10 +435,12 @@ policy_rows_grad_kernel(PolRowArgs a) {
       glv[j] += gsd;
       dz[j] = gmu * (1.f - m[j] * m[j]);                    // tanh backward
     }
+    st_row<AT>(a.dz + n * A, dz, A);
   }
   // block partials of sum_rows d/dstd (times std at the reduction: d/dlog_var)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int j = 0; j < A; ++j) {
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
     const float s = wave_sum(glv[j]);
     if (lane == 0) gls[wave][j] = s;
   }
@@ -985,7 +1041,17 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE, kRowNT);
       const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(policy_rows_stats_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, p);
+      switch (d.A) {   // compile-time action widths 1..8 (registers); others generic
+        case 1: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 1>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 2: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 2>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 3: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 3>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 4: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 4>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 5: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 5>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 6: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 6>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 7: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 7>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 8: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 8>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        default: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 0>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+      }
       // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
       ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
       RC(check_launch("policy_rows_stats_kernel"));
@@ -1004,7 +1070,17 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE, kRowNT);
       const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(policy_rows_grad_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, p);
+      switch (d.A) {   // compile-time action widths 1..8 (registers); others generic
+        case 1: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 1>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 2: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 2>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 3: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 3>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 4: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 4>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 5: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 5>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 6: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 6>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 7: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 7>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        case 8: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 8>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        default: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 0>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+      }
       // per row: mu, refmu, actions, behave (5A) + adv read, dz (A) written
       ktime_end(kt, KT_POLICY_GRAD, 4.0 * (double)d.NE * (6 * d.A + 1), st);
       RC(check_launch("policy_rows_grad_kernel"));

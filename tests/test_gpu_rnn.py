@@ -148,10 +148,14 @@ def test_rnn_learn_small_matches_oracle(mode):
 
 
 def test_rnn_learn_no_zfilter_early_stop():
-    # large lr: the KL early stop (ppo.py:556) fires on device
-    rep = _run_rnn('adapt', B=16, T=6, H=2, D=7, A=3, Hd=16, hidden=(16, 24), zf=False,
-                   lr=(3e-2, 1e-3), kl_target=0.002)
-    print('rnn early-stop parity:', rep)
+    # large lr: the KL early stop (ppo.py:556) fires on device.  At lr 3e-2 every
+    # Adam step is a large move, so a one-rounding difference in a row's loss
+    # gradient flips LSTM entries in any two fp32 implementations: parity is
+    # held to the fp32 envelope (test_gpu_parity_pinned.py), which also requires
+    # the same number of policy epochs in every execution
+    from tests.test_gpu_parity_pinned import pinned_run
+    lc = _rnn_cfg('adapt', 16, 6, 2, 16, (16, 24), zf=False, lr=(3e-2, 1e-3), kl_target=0.002)
+    pinned_run(lc, 7, 3, iters=2, rnn_hidden=16, seed=0)
 
 
 @pytest.mark.parametrize('mode', ['adapt', 'clip'])
