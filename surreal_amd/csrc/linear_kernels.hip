@@ -661,12 +661,6 @@ __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m
     const int c = min(m0 + 4 * li, g.M - 4);
     const float4 x = *reinterpret_cast<const float4*>(Ar + c);
     av[0] = x.x; av[1] = x.y; av[2] = x.z; av[3] = x.w;
-  } else if constexpr (MT == 8 && VA) {
-    const int c = min(m0 + 8 * li, g.M - 8);
-    const float4 x = *reinterpret_cast<const float4*>(Ar + c);
-    const float4 y = *reinterpret_cast<const float4*>(Ar + c + 4);
-    av[0] = x.x; av[1] = x.y; av[2] = x.z; av[3] = x.w;
-    av[4] = y.x; av[5] = y.y; av[6] = y.z; av[7] = y.w;
   } else {
 #pragma unroll
     for (int t = 0; t < MT; ++t) av[t] = Ar[min(m0 + MT * li + t, g.M - 1)];
@@ -706,10 +700,10 @@ __device__ __forceinline__ bool use_dwd_fast() { return SMI_DWD_FAST != 0; }
 template <int MT, int NT, int NB, int RS>
 __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nsteps, int m0, int n0,
                                               int bdata, f32x4 (&acc)[MT][NT]) {
-  static_assert(MT == 8 || MT == 4 || MT == 1, "fast dW loop: 8 / 4 m sub-tiles (float4 A) or 1");
-  constexpr int NH = NB / 4, AQ = MT >= 4 ? MT / 4 : 1;
+  static_assert(MT == 4 || MT == 1, "fast dW loop: 4 m sub-tiles (float4 A) or 1 (scalar A)");
+  constexpr int NH = NB / 4;
   const int li = threadIdx.x & 15;
-  const float* pa = g.A + (int64_t)rw * g.a_cs + (MT >= 4 ? min(m0 + MT * li, g.M - MT)
+  const float* pa = g.A + (int64_t)rw * g.a_cs + (MT == 4 ? min(m0 + 4 * li, g.M - 4)
                                                           : min(m0 + li, g.M - 1));
   const int64_t sa = (int64_t)RS * g.a_cs;
   const float* pb[NH];
@@ -730,14 +724,10 @@ __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nst
       sb[h] = 0;
     }
   }
-  float4 av[DWD_P][AQ], bv[DWD_P][NH];
+  float4 av[DWD_P], bv[DWD_P][NH];
   auto load = [&](int p) {
-    if constexpr (MT >= 4) {
-#pragma unroll
-      for (int q = 0; q < AQ; ++q) av[p][q] = reinterpret_cast<const float4*>(pa)[q];
-    } else {
-      av[p][0].x = *pa;
-    }
+    if constexpr (MT == 4) av[p] = *reinterpret_cast<const float4*>(pa);
+    else av[p].x = *pa;
     pa += sa;
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
@@ -746,12 +736,7 @@ __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nst
     }
   };
   auto step = [&](int p) {
-    float a4[4 * AQ];
-#pragma unroll
-    for (int q = 0; q < AQ; ++q) {
-      a4[4 * q] = av[p][q].x; a4[4 * q + 1] = av[p][q].y;
-      a4[4 * q + 2] = av[p][q].z; a4[4 * q + 3] = av[p][q].w;
-    }
+    const float a4[4] = {av[p].x, av[p].y, av[p].z, av[p].w};
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const float4 q = bv[p][b >> 2];
@@ -823,7 +808,7 @@ __device__ __forceinline__ void dwd_tile(const GemmArgs& g, const TileIdx ti, fl
   };
   // full slabs of 16-byte operands take the unchecked streaming loop
   // (MT == 1: scalar A loads, no A alignment needed)
-  constexpr bool kFast = VB && ((VA && (MT == 4 || MT == 8)) || MT == 1);
+  constexpr bool kFast = VB && ((VA && MT == 4) || MT == 1);
   bool fast = false;
   if constexpr (kFast)
     fast = use_dwd_fast() && nsteps >= DWD_P && nsteps % DWD_P == 0 && kb + nsteps * RS <= ke;
@@ -964,42 +949,6 @@ gemm_dwd_group_kernel(DwGroup G) {
     case 2: dwd_tile<4, 8, true, false, WV>(g, ti, dwd_red); break;
     case 1: dwd_tile<4, 8, false, true, WV>(g, ti, dwd_red); break;
     default: dwd_tile<4, 8, false, false, WV>(g, ti, dwd_red); break;
-  }
-}
-
-// Wide variant (SMI_DWD_WIDE=1, A/B knob): 128 x 128 tiles per wave (8 x 8
-// MFMA sub-tiles, accumulators in AGPRs, one wave per SIMD): 16 operand floats
-// per 4-row step for 64 MFMAs instead of 12 for 32, i.e. 1.5x the MACs per
-// byte streamed.  Remainder tiles: <= 16 rows on a 16-wide tile, <= 64 on a
-// 64-wide one (narrow[] = 1 / 2).  Used when every GEMM of the group has
-// 16-byte operands.
-template <int WV>
-__global__ void __launch_bounds__(64 * WV, 1)
-gemm_dwd_group_wide_kernel(DwGroup G) {
-  extern __shared__ float4 dwd_red[];
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  int w = orig;
-  if (nwg > 8) {
-    const int x = orig & 7, q = nwg >> 3, r = nwg & 7;
-    w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
-  }
-  int gi = 0;
-  while (gi + 1 < G.n && w >= G.wg0[gi + 1]) ++gi;
-  const GemmArgs& g = G.g[gi];
-  if (g.skip && g.skip[0] != 0) return;
-  const int local = w - G.wg0[gi], gn = G.gn[gi], gm = G.gm[gi];
-  TileIdx ti;
-  ti.nt = local % gn;
-  ti.mt = (local / gn) % gm;
-  ti.z = local / (gn * gm);
-  if (ti.mt == gm - 1 && G.narrow[gi] == 1) {
-    ti.mt *= 8;                                    // m0 = 16 * mt = 128 * (gm - 1)
-    dwd_tile<1, 8, false, true, WV>(g, ti, dwd_red);
-  } else if (ti.mt == gm - 1 && G.narrow[gi] == 2) {
-    ti.mt *= 2;                                    // m0 = 64 * mt
-    dwd_tile<4, 8, true, true, WV>(g, ti, dwd_red);
-  } else {
-    dwd_tile<8, 8, true, true, WV>(g, ti, dwd_red);
   }
 }
 
@@ -1321,50 +1270,25 @@ static int use_dwd_narrow() {
   return u;
 }
 
-// wide 128 x 128 grouped dW tiles (SMI_DWD_WIDE=1; A/B knob) and their
-// workgroup target (SMI_DWD_WIDE_TARGET)
-static int use_dwd_wide() {
-  static int u = -1;
-  if (u < 0) {
-    const char* e = getenv("SMI_DWD_WIDE");
-    u = (e && e[0] == '1') ? 1 : 0;
-  }
-  return u;
-}
-static int dw_wide_target() {
-  static int t = 0;
-  if (!t) {
-    const char* e = getenv("SMI_DWD_WIDE_TARGET");
-    t = e ? atoi(e) : 512;
-    if (t < 64) t = 64;
-  }
-  return t;
-}
-
 int dw_group_flush(hipStream_t st) {
   g_grp_on = false;
   DwGroup& G = g_grp;
   if (G.n == 0) return SMI_OK;
-  bool wide = use_dwd_wide() && dwd_waves() == 4;
-  for (int i = 0; i < G.n; ++i) wide = wide && G.vec[i] == 3;
-  const int MT = wide ? 8 : 4, NT = 8;
+  constexpr int MT = 4, NT = 8;
   const int rs = 4 * dwd_waves() * DWD_P;           // rows per prefetch window
   double work = 0.0;                                 // sum of tiles x rows
   int64_t tiles[kDwGroupMax];
   for (int i = 0; i < G.n; ++i) {
     const GemmArgs& g = G.g[i];
     const int tail = g.M % (16 * MT);
-    if (wide)
-      G.narrow[i] = tail == 0 ? 0 : tail <= 16 ? 1 : tail <= 64 ? 2 : 0;
-    else
-      G.narrow[i] = use_dwd_narrow() && tail > 0 && tail <= 16;
+    G.narrow[i] = use_dwd_narrow() && tail > 0 && tail <= 16;
     G.gm[i] = (g.M + 16 * MT - 1) / (16 * MT);
     G.gn[i] = (g.N + 16 * NT - 1) / (16 * NT);
     tiles[i] = (int64_t)G.gm[i] * G.gn[i];
     work += (double)tiles[i] * g.K;
   }
   const int64_t cap = smi_workspace_floats();
-  int64_t rows = (int64_t)(work / (wide ? dw_wide_target() : dw_group_target())) + 1;
+  int64_t rows = (int64_t)(work / dw_group_target()) + 1;
   rows = (rows + rs - 1) / rs * rs;
   if (rows < 2 * rs) rows = 2 * rs;                 // >= 8 MFMA steps per wave
   int64_t need = 0;
@@ -1396,19 +1320,10 @@ int dw_group_flush(hipStream_t st) {
   }
   const int kslot = ktime_begin(st);
   const size_t lds = (size_t)2 * MT * NT * 64 * sizeof(float4);
-  if (wide) {
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_dwd_group_wide_kernel<4>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr = true;
-    }
-    hipLaunchKernelGGL(gemm_dwd_group_wide_kernel<4>, dim3(G.wg0[G.n]), dim3(256), lds, st, G);
-  } else if (dwd_waves() == 8) {
+  if (dwd_waves() == 8)
     hipLaunchKernelGGL(gemm_dwd_group_kernel<8>, dim3(G.wg0[G.n]), dim3(512), lds, st, G);
-  } else {
+  else
     hipLaunchKernelGGL(gemm_dwd_group_kernel<4>, dim3(G.wg0[G.n]), dim3(256), lds, st, G);
-  }
   ktime_end(kslot, KT_GEMM_DW, g_grp_flops, st);
   RC_CHECK(check_launch("gemm_dwd_group_kernel"));
   const int rslot = ktime_begin(st);
