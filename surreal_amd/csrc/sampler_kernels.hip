@@ -209,24 +209,31 @@ __device__ __forceinline__ void gather_body(const V* __restrict__ table, I cols,
 __global__ void __launch_bounds__(kWG)
 gather_rows_kernel(const float* __restrict__ table, int64_t cols, const int64_t* __restrict__ idx,
                    int64_t batch, float* __restrict__ out) {
-  const bool v4 = (cols & 3) == 0 &&
-                  ((reinterpret_cast<uintptr_t>(table) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
-  const int64_t c = v4 ? cols >> 2 : cols;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(table) | reinterpret_cast<uintptr_t>(out);
+  const bool v4 = (cols & 3) == 0 && (al & 15) == 0;
+  // even widths (the DDPG row [s | a | r | s' | d] of HalfCheetah is 42 floats)
+  // move as 8-byte elements
+  const bool v2 = !v4 && (cols & 1) == 0 && (al & 7) == 0;
+  const int64_t c = v4 ? cols >> 2 : v2 ? cols >> 1 : cols;
   const int64_t total = batch * c;
   if (total < ((int64_t)1 << 31)) {
     if (v4) gather_body<float4, uint32_t>(reinterpret_cast<const float4*>(table), (uint32_t)c, idx,
                                           (uint32_t)total, reinterpret_cast<float4*>(out));
+    else if (v2) gather_body<float2, uint32_t>(reinterpret_cast<const float2*>(table), (uint32_t)c,
+                                               idx, (uint32_t)total, reinterpret_cast<float2*>(out));
     else gather_body<float, uint32_t>(table, (uint32_t)c, idx, (uint32_t)total, out);
   } else {
     if (v4) gather_body<float4, int64_t>(reinterpret_cast<const float4*>(table), c, idx, total,
                                          reinterpret_cast<float4*>(out));
+    else if (v2) gather_body<float2, int64_t>(reinterpret_cast<const float2*>(table), c, idx, total,
+                                              reinterpret_cast<float2*>(out));
     else gather_body<float, int64_t>(table, c, idx, total, out);
   }
 }
 
 int launch_gather_rows(const float* table, int64_t cols, const int64_t* idx, int64_t batch,
                        float* out, hipStream_t s) {
-  const int64_t work = batch * ((cols & 3) == 0 ? cols / 4 : cols);
+  const int64_t work = batch * ((cols & 3) == 0 ? cols / 4 : (cols & 1) == 0 ? cols / 2 : cols);
   if (work <= 0) return SMI_OK;
   int64_t g = (work + kWG - 1) / kWG;
   g = (g + 3) / 4;

@@ -20,6 +20,8 @@ bench)
   # streaming kernels at > 256 MB working sets inside learn(): 65536 segments
   timeout -k 10 300 python -u bench.py --config c3 --local-segments 65536 --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench_c3_local65536.json 2> $OUT/bench_c3_local65536.err || exit 1
   SMI_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_c3_dp2_gloo.json 2> $OUT/bench_c3_dp2_gloo.err || exit 1
+  timeout -k 10 300 python -u tools/bench_hbm.py --iters 20 > $OUT/hbm_sweep.jsonl 2> $OUT/hbm_sweep.err || exit 1
+  cut -c1-200 $OUT/hbm_sweep.jsonl
   cut -c1-300 $OUT/bench_c3_local128.json ;;
 prof)
   for c in c3 c5; do
