@@ -1356,7 +1356,13 @@ static void panel_dispatch(const GemmArgs& g, dim3 grid, int ntw, hipStream_t st
 // tall forward / input-gradient GEMMs with 16-byte operands: gemm_panel_kernel
 static bool panel_ok(int epi, const GemmArgs& g) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  if (!use_panel() || g.M < 2048 || g.N > 640 || g.K > 1024 || g.K < 1) return false;
+  // below panel_min_rows the row panels cannot fill the GPU and their serial K
+  // loop is the latency: the tiled kernel with split-K takes those
+  static const int panel_min_rows = [] {
+    const char* e = getenv("SMI_PANEL_MIN_ROWS");
+    return e ? atoi(e) : 2048;
+  }();
+  if (!use_panel() || g.M < panel_min_rows || g.N > 640 || g.K > 1024 || g.K < 1) return false;
   if (g.a_cs != 1 || g.a_rs % 4 || g.K % 4 || !al16(g.A) || !al16(g.B)) return false;
   if (epi == EPI_FWD) return g.b_rs == 1 && g.b_cs % 4 == 0;
   // input gradients: the transposing LDS stage costs more than it saves below

@@ -16,6 +16,7 @@ bench)
     cut -c1-300 $OUT/bench_$c.json
   done
   timeout -k 10 300 python -u bench.py --config c3 --local-segments 128 --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_c3_local128.json 2> $OUT/bench_c3_local128.err || exit 1
+  SMI_PANEL_MIN_ROWS=4096 timeout -k 10 300 python -u bench.py --config c3 --local-segments 128 --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_c3_local128_nopanel.json 2> $OUT/bench_c3_local128_nopanel.err || exit 1
   timeout -k 10 300 python -u bench.py --config c5 --local-segments 128 --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_c5_local128.json 2> $OUT/bench_c5_local128.err || exit 1
   # streaming kernels at > 256 MB working sets inside learn(): 65536 segments
   timeout -k 10 300 python -u bench.py --config c3 --local-segments 65536 --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench_c3_local65536.json 2> $OUT/bench_c3_local65536.err || exit 1
