@@ -555,24 +555,7 @@ adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restric
   const float4* g4 = reinterpret_cast<const float4*>(g);
   float4* m4 = reinterpret_cast<float4*>(m);
   float4* v4 = reinterpret_cast<float4*>(v);
-  // two independent float4 groups per iteration: 8 loads in flight per thread
   int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  for (; i + stride < n4; i += 2 * stride) {
-    float4 pp[2], mm[2], vv[2], gg[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      pp[u] = p4[i + u * stride]; mm[u] = m4[i + u * stride];
-      vv[u] = v4[i + u * stride]; gg[u] = g4[i + u * stride];
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      adam_elem(pp[u].x, gg[u].x, mm[u].x, vv[u].x, k);
-      adam_elem(pp[u].y, gg[u].y, mm[u].y, vv[u].y, k);
-      adam_elem(pp[u].z, gg[u].z, mm[u].z, vv[u].z, k);
-      adam_elem(pp[u].w, gg[u].w, mm[u].w, vv[u].w, k);
-      p4[i + u * stride] = pp[u]; m4[i + u * stride] = mm[u]; v4[i + u * stride] = vv[u];
-    }
-  }
   for (; i < n4; i += stride) {
     float4 pp = p4[i], mm = m4[i], vv = v4[i];
     const float4 gg = g4[i];
