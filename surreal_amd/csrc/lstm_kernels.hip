@@ -781,39 +781,32 @@ lstm_bwd_r4_kernel(LstmBwdArgs a) {
   const bool cok = cell && cgr < B;
   const int64_t grc = cgr < B ? cgr : B - 1;
   const int cug = cunit >> 6, cl = cunit & 63;
-  // the cell inputs of step t (gate activations, c_t, c_{t-1}, dh_t) are
-  // fetched two steps ahead into two register sets used alternately (the loop
-  // is unrolled by two so each set is a fixed register group): the loads of a
-  // set have two MFMA phases to land instead of one
-  struct CellIn { float g[4], c, cp, dh; };
-  CellIn s0{{0.f, 0.f, 0.f, 0.f}, 0.f, 0.f, 0.f}, s1{{0.f, 0.f, 0.f, 0.f}, 0.f, 0.f, 0.f};
-  auto fetch = [&](CellIn& x, int t) {
+  float pg[4], pc = 0.f, pcp = 0.f, pdh = 0.f;
+  auto fetch = [&](int t) {
     const float* gp = a.gates + ((int64_t)t * B + grc) * G4 + cunit;
-    x.g[0] = gp[0]; x.g[1] = gp[H]; x.g[2] = gp[2 * H]; x.g[3] = gp[3 * H];
-    x.c = a.cbuf[(int64_t)(t + 1) * BH + grc * H + cunit];
-    x.cp = a.cbuf[(int64_t)t * BH + grc * H + cunit];
-    x.dh = a.dh[(int64_t)t * BH + grc * H + cunit];
+    pg[0] = gp[0]; pg[1] = gp[H]; pg[2] = gp[2 * H]; pg[3] = gp[3 * H];
+    pc = a.cbuf[(int64_t)(t + 1) * BH + grc * H + cunit];
+    pcp = a.cbuf[(int64_t)t * BH + grc * H + cunit];
+    pdh = a.dh[(int64_t)t * BH + grc * H + cunit];
   };
-  if (cell && a.S > 0) fetch(s0, a.S - 1);
-  if (cell && a.S > 1) fetch(s1, a.S - 2);
+  if (cell && a.S > 0) fetch(a.S - 1);
   float dcreg = 0.f;
   __syncthreads();
   LSTM_T0();
-  // one step; false after the last (t == 0) cell update
-  auto step = [&](CellIn& x, int t) -> bool {
+  for (int t = a.S - 1; t >= 0; --t) {
     if (cell) {
       float dhr = 0.f;
       if (t < a.S - 1) {
         for (int p = 0; p < WPG; ++p) dhr += red[cug * WPG + p][crow][cl];
       }
-      const float ig = x.g[0], fg = x.g[1], cg = x.g[2], og = x.g[3];
-      const float dh = x.dh + dhr;
-      const float tc = ftanh(x.c);
+      const float ig = pg[0], fg = pg[1], cg = pg[2], og = pg[3];
+      const float dh = pdh + dhr;
+      const float tc = ftanh(pc);
       const float dc = dh * og * (1.f - tc * tc) + dcreg;
       const float d_o = (dh * tc) * (og * (1.f - og));
       const float d_i = (dc * cg) * (ig * (1.f - ig));
       const float d_g = (dc * ig) * (1.f - cg * cg);
-      const float d_f = (dc * x.cp) * (fg * (1.f - fg));
+      const float d_f = (dc * pcp) * (fg * (1.f - fg));
       dcreg = cok ? dc * fg : 0.f;
       float* l = dG + crow * G4P + cunit;
       l[0] = cok ? d_i : 0.f; l[H] = cok ? d_f : 0.f;
@@ -822,12 +815,12 @@ lstm_bwd_r4_kernel(LstmBwdArgs a) {
         float* o = a.dgates + ((int64_t)t * B + cgr) * G4 + cunit;
         o[0] = d_i; o[H] = d_f; o[2 * H] = d_g; o[3 * H] = d_o;
       }
-      if (t > 1) fetch(x, t - 2);
+      if (t > 0) fetch(t - 1);
     }
     LSTM_TICK(3);
     __syncthreads();
     LSTM_TICK(4);
-    if (t == 0) return false;
+    if (t == 0) break;
     if (wave < NU * WPG) {
       f32x4 acc[8];
 #pragma unroll
@@ -856,11 +849,6 @@ lstm_bwd_r4_kernel(LstmBwdArgs a) {
     }
     LSTM_TICK(5);
     __syncthreads();
-    return true;
-  };
-  for (int t = a.S - 1; t >= 0; t -= 2) {
-    if (!step(s0, t) || t == 0) break;
-    if (!step(s1, t - 1)) break;
   }
 }
 
