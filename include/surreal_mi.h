@@ -318,6 +318,8 @@ int smi_ppo_epoch_apply(const smi_ppo_args* args, int epoch, void* stream);
  *   PREP             (reference-policy forward)
  *   POLICY_FWD(e)    e = 0..epoch_policy: forward + loss sums -> all-reduce pstat
  *   POLICY_DECIDE(e) KL early stop / adapt coefficient / statistics from pstat
+ *                    (with B_global == B, one rank, POLICY_FWD already decides
+ *                    in the same launch as its reduction and this phase is a no-op)
  *   POLICY_BWD(e)    e < epoch_policy: backward -> all-reduce actor grads
  *                    (xbuf[0 : nA], nA = actor params + lstm params)
  *   POLICY_APPLY(e)  clip_grad_norm_ + Adam over [actor | lstm]

@@ -473,8 +473,7 @@ struct DecideArgs {
   const float* hyper; const float* lv; int A; float c_ent;
   int* ci; float* cf; float* stats;
 };
-__global__ void policy_decide_kernel(DecideArgs a) {
-  if (threadIdx.x != 0) return;
+__device__ void policy_decide_body(const DecideArgs& a) {
   if (a.ci[CI_STOP]) return;
   const double n = (double)a.N;
   const float kl = (float)(a.ps[PS_KL] / n);
@@ -521,6 +520,28 @@ __global__ void policy_decide_kernel(DecideArgs a) {
     a.stats[SMI_ST_POL_KL] = kl;
     a.cf[CF_KLCOEF] = (float)(coef / n);
   }
+}
+
+__global__ void policy_decide_kernel(DecideArgs a) {
+  if (threadIdx.x != 0) return;
+  policy_decide_body(a);
+}
+
+// single rank (no exchange between the two): the pstat reduction and the
+// decision in one launch — one wave per sum, then thread 0 decides
+__global__ void __launch_bounds__(kWG)
+reduce_decide_kernel(const double* __restrict__ part, int nb, DecideArgs a, const int* skip) {
+  if (skip && skip[0] != 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* out = const_cast<double*>(a.ps);
+  for (int j = wave; j < PS_N; j += kNW) {
+    double t = 0.0;
+    for (int i = lane; i < nb; i += 64) t += part[(int64_t)i * PS_N + j];
+    t = wave_sum_d(t);
+    if (lane == 0) out[j] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) policy_decide_body(a);
 }
 
 // value loss rows: V (time-major [NE]) vs ret [B][E]; dV = 2 (V - R) / N and,
@@ -1055,11 +1076,19 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
       ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
       RC(check_launch("policy_rows_stats_kernel"));
+      if (a.B_global == a.B) {         // one rank: nothing to exchange before the decision
+        DecideArgs da{a.pstat, e, a.epoch_policy, a.mode,
+                      a.kl_target, a.kl_cutoff_coeff, NEg, a.hyper, a.actor + d.LA.flv, d.A,
+                      c_entropy_of(d.A), s.ci, s.cf, a.stats};
+        hipLaunchKernelGGL(reduce_decide_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, da, stop);
+        return check_launch("reduce_decide_kernel");
+      }
       hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, PS_N,
                          a.pstat, stop);
       return check_launch("reduce_partials_kernel");
     }
     case SMI_RNN_PH_POLICY_DECIDE: {   // after the pstat all-reduce
+      if (a.B_global == a.B) return SMI_OK;     // decided by POLICY_FWD's reduce_decide_kernel
       DecideArgs da{a.pstat, e, a.epoch_policy, a.mode,
                     a.kl_target, a.kl_cutoff_coeff, NEg, a.hyper, a.actor + d.LA.flv, d.A,
                     c_entropy_of(d.A), s.ci, s.cf, a.stats};
