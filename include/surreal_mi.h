@@ -501,6 +501,14 @@ int smi_linear_backward_input(const float* dy, int64_t ldg, int rows, int out_di
 int smi_linear_backward_weight(const float* dy, int64_t ldg, int rows, int out_dim,
                                const float* x, int64_t ldx, int in_dim, float* dw, int64_t lddw,
                                float* db, int accumulate, void* stream);
+/* Grouped weight gradients: smi_linear_backward_weight calls between
+ * smi_dw_group_begin() and smi_dw_group_flush(stream) (row-major operands,
+ * outputs <= 512 x 512, at most 6 per group) are queued and run as ONE launch
+ * (workgroups dealt over every GEMM's tiles x split-K slabs) plus one
+ * fixed-order reduce at the flush; the caller keeps their dY / X buffers
+ * unchanged until then.  Calls that do not qualify launch immediately. */
+int smi_dw_group_begin(void);
+int smi_dw_group_flush(void* stream);
 
 /* ------------------------------------------------------- DDPG loss pieces */
 /* critic loss nn.MSELoss()(Q, y) (ddpg.py:306): loss = mean((Q-y)^2), dQ = 2(Q-y)/n */

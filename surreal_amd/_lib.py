@@ -128,6 +128,8 @@ _SIGS = {
     'smi_reward_filter': (c_int, [P, c_i64, c_f32, c_int, P, P, P, c_f32, P]),
     'smi_reward_filter_partial': (c_int, [P, c_i64, c_f32, c_int, P, P, P, c_f32, P, P]),
     'smi_reward_filter_commit': (c_int, [P, P, P, P, P]),
+    'smi_dw_group_begin': (c_int, []),
+    'smi_dw_group_flush': (c_int, [P]),
     'smi_layernorm_forward': (c_int, [P, c_i64, c_i64, c_int, P, P, c_f32, P, c_i64, P, P, P]),
     'smi_layernorm_backward': (c_int, [P, c_i64, P, c_i64, P, P, P, c_i64, c_int, c_int, P, c_i64,
                                        P, P, P]),

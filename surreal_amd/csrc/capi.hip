@@ -338,6 +338,10 @@ int smi_linear_backward_input(const float* dy, int64_t ldg, int rows, int out_di
                               SMI_STREAM(stream));
 }
 
+int smi_dw_group_begin(void) { return dw_group_begin(); }
+
+int smi_dw_group_flush(void* stream) { return dw_group_flush(SMI_STREAM(stream)); }
+
 int smi_linear_backward_weight(const float* dy, int64_t ldg, int rows, int out_dim, const float* x,
                                int64_t ldx, int in_dim, float* dw, int64_t lddw, float* db,
                                int accumulate, void* stream) {

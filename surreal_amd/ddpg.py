@@ -16,6 +16,7 @@ with use_layernorm):
   critic: Wo[c1][D] bo [go bo'] Wc[c2][c1+A] bc [gc bc'] Wq[1][c2] bq
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -24,6 +25,9 @@ import torch.nn as nn
 from . import _lib as L
 from .config import Config, ConfigError
 from .model import _FlatViews, _LinearView
+
+# group each backward's weight-gradient GEMMs into one launch (SMI_DDPG_DW_GROUP=0: A/B off)
+_DW_GROUP = os.environ.get('SMI_DDPG_DW_GROUP', '1') != '0'
 
 RELU, TANH, NONE = 1, 2, 0
 
@@ -450,8 +454,18 @@ class DDPGLearner(object):
             self._target_update()
 
     def _critic_backward(self, net, crit, obs, B, dq, pre, g, st, need_obs_grad):
-        """Backward through CriticNetworkX.  With g: weight grads into g (flat).
+        """Backward through CriticNetworkX.  With g: weight grads into g (flat),
+        the three weight-gradient GEMMs as one grouped launch (smi_dw_group_*).
         Always returns d loss / d action (B, A) when g is None."""
+        if g is None or not _DW_GROUP:
+            return self._critic_backward_body(net, crit, obs, B, dq, pre, g, st)
+        L.call('smi_dw_group_begin')
+        try:
+            return self._critic_backward_body(net, crit, obs, B, dq, pre, g, st)
+        finally:
+            L.call('smi_dw_group_flush', st)   # always flush: nothing stays queued
+
+    def _critic_backward_body(self, net, crit, obs, B, dq, pre, g, st):
         D, c1, c2, A = crit.dims
         ln = crit.use_layernorm
         CAT = net.bufs[pre + '_cat']
@@ -490,6 +504,17 @@ class DDPGLearner(object):
         return dA
 
     def _actor_backward(self, net, act, obs, B, dA, g, st):
+        """Backward through ActorNetworkX into g; its three weight-gradient
+        GEMMs as one grouped launch (smi_dw_group_*)."""
+        if not _DW_GROUP:
+            return self._actor_backward_body(net, act, obs, B, dA, g, st)
+        L.call('smi_dw_group_begin')
+        try:
+            self._actor_backward_body(net, act, obs, B, dA, g, st)
+        finally:
+            L.call('smi_dw_group_flush', st)
+
+    def _actor_backward_body(self, net, act, obs, B, dA, g, st):
         D, h1, h2, A = act.dims
         ln = act.use_layernorm
         H1, H2, out = net.bufs['a_h1'], net.bufs['a_h2'], net.bufs['a_act']
