@@ -95,6 +95,36 @@ def test_linear_ops_vs_torch(rows, k, n):
     _fp32_as_good_as_torch(db.cpu(), 2 * dy.sum(0), 2 * dy.double().sum(0), sl, 2 * mb)
 
 
+def test_dw_group_vs_torch():
+    """smi_dw_group_begin / _flush: weight gradients queued between them run as
+    one grouped launch at the flush.  Mixed group: the DDPG layer shapes, an
+    accumulating call, one output too large to group (launches at once), and
+    more calls than a group holds (the overflow launches at once)."""
+    L.ensure_workspace(torch.device('cuda'))
+    shapes = [(512, 17, 400, 0), (512, 406, 300, 1), (512, 301, 1, 0), (512, 17, 300, 0),
+              (512, 300, 600, 0), (512, 300, 200, 0), (512, 201, 6, 1), (4099, 64, 33, 0)]
+    g = torch.Generator().manual_seed(11)
+    st = L.stream()
+    cases = []
+    for rows, k, n, acc in shapes:
+        x, dy = torch.randn(rows, k, generator=g), torch.randn(rows, n, generator=g)
+        w0, b0 = torch.randn(n, k, generator=g), torch.randn(n, generator=g)
+        dev = [t.cuda() for t in (x, dy, w0, b0)]
+        cases.append((rows, k, n, acc, x, dy, w0, b0, dev))
+    L.call('smi_dw_group_begin')
+    for rows, k, n, acc, x, dy, w0, b0, (xd, dyd, dw, db) in cases:
+        L.call('smi_linear_backward_weight', L.ptr(dyd), n, rows, n, L.ptr(xd), k, k, L.ptr(dw), k,
+               L.ptr(db), acc, st)
+    L.call('smi_dw_group_flush', st)
+    for rows, k, n, acc, x, dy, w0, b0, (xd, dyd, dw, db) in cases:
+        mw = float((dy.abs().t() @ x.abs()).max()) + acc * float(w0.abs().max())
+        mb = float(dy.abs().sum(0).max()) + acc * float(b0.abs().max())
+        _fp32_as_good_as_torch(dw.cpu(), acc * w0 + dy.t() @ x,
+                               acc * w0.double() + dy.double().t() @ x.double(), 1e-6, mw)
+        _fp32_as_good_as_torch(db.cpu(), acc * b0 + dy.sum(0), acc * b0.double() + dy.double().sum(0),
+                               1e-6, mb)
+
+
 @pytest.mark.parametrize('rows,n', [(512, 300), (512, 400), (70, 200), (3, 37), (1, 1024)])
 def test_layernorm_kernels_vs_torch(rows, n):
     """smi_layernorm_forward / _backward (ReLU before the norm) against
