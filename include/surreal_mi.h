@@ -37,10 +37,26 @@ int         smi_version(void);
 const char* smi_last_error(void);
 
 /* Device scratch for the multi-workgroup reductions (ZFilter column partials,
- * Adam norm partials).  The caller allocates smi_workspace_bytes() of device
- * memory once and registers it; launches that need it are stream-ordered. */
+ * Adam norm partials, split-K GEMM partials).  The caller allocates
+ * smi_workspace_bytes() of device memory and registers it.
+ *
+ * Re-entrancy (SURVEY §8(b) Threading: the reference issues DDPG preprocess
+ * GPU work from the prefetch thread while learn() runs, data_fetcher.py:47-58).
+ * Kernels themselves are stateless; the only host state a launch consults is
+ * (a) the workspace its partials go to and (b) the queue of a grouped weight-
+ * gradient launch.  (b) is thread-local (smi_dw_group_begin/flush bracket a
+ * call sequence on one thread).  (a) belongs to an smi_context: each object
+ * that launches work (a learner, an agent batch) owns one context with its
+ * own workspace and makes it current on the calling thread before its calls;
+ * launches then use the calling thread's current context, so two objects on
+ * two streams (or two threads) never share partial buffers.  With no current
+ * context a thread uses the default workspace of smi_set_workspace. */
 int64_t smi_workspace_bytes(void);
 int     smi_set_workspace(void* dev_ptr, int64_t bytes);
+typedef struct smi_context smi_context;
+smi_context* smi_context_create(void* workspace, int64_t bytes);   /* NULL on bad args */
+int          smi_context_make_current(smi_context* ctx);            /* this thread; NULL = default */
+int          smi_context_destroy(smi_context* ctx);
 
 /* Measurement only (not part of the reference API): per-launch HIP-event
  * timing of the MFMA kernels and of the HBM-bound streaming kernels of the

@@ -90,8 +90,15 @@ def load_flat(params, f):
 
 
 class DDPGLearnerRef:
-    def __init__(self, lc, obs_dim, act_dim, seed=0):
+    """dtype=torch.float64 runs the same step in double precision (the
+    parity tests' "truth"); noise_perm (a row permutation or None) reorders
+    the TD3 smoothing noise rows as the batch rows were reordered, so a
+    row-permuted execution draws the same noise per transition."""
+
+    def __init__(self, lc, obs_dim, act_dim, seed=0, dtype=torch.float32):
         torch.manual_seed(seed)
+        self.dtype = dtype
+        self.noise_perm = None
         net = lc['algo']['network']
         self.gamma = lc['algo']['gamma']
         self.n_step = lc['algo']['n_step']
@@ -105,6 +112,8 @@ class DDPGLearnerRef:
         self.act_dim = act_dim
         if self.double:
             self.critic2, self.critic2_t = CriticX(obs_dim, act_dim, ch, ln), CriticX(obs_dim, act_dim, ch, ln)
+        for m in self.nets():
+            m.to(dtype)
         self.hard_update()
         self.clip_actor = net['clip_actor_gradient']
         self.actor_clip_value = net['actor_gradient_value_clip']
@@ -123,6 +132,10 @@ class DDPGLearnerRef:
         self.interval = tu.get('interval', 500)
         self.counter = 0
 
+    def nets(self):
+        out = [self.actor, self.critic, self.actor_t, self.critic_t]
+        return out + ([self.critic2, self.critic2_t] if self.double else [])
+
     def hard_update(self):
         self.actor_t.load_state_dict(self.actor.state_dict())
         self.critic_t.load_state_dict(self.critic.state_dict())
@@ -130,6 +143,9 @@ class DDPGLearnerRef:
             self.critic2_t.load_state_dict(self.critic2.state_dict())
 
     def optimize(self, obs, actions, rewards, obs_next, done):          # ddpg.py:244-352
+        cv = lambda t: t if (isinstance(t, torch.Tensor) and t.dtype == self.dtype) \
+            else torch.as_tensor(t, dtype=torch.float32).to(self.dtype)  # noqa: E731
+        obs, actions, rewards, obs_next, done = (cv(t) for t in (obs, actions, rewards, obs_next, done))
         assert actions.max().item() <= 1.0 and actions.min().item() >= -1.0
         with torch.no_grad():
             a_t = self.actor_t(obs_next)
@@ -137,7 +153,9 @@ class DDPGLearnerRef:
             if self.action_reg:
                 noise = np.clip(np.random.normal(0, 0.2, size=(self.batch_size, self.act_dim)),
                                 -0.5, 0.5)
-                a_t = (a_t + torch.tensor(noise, dtype=torch.float32)).clamp(-1, 1)
+                if self.noise_perm is not None:
+                    noise = noise[self.noise_perm]
+                a_t = (a_t + torch.tensor(noise, dtype=torch.float32).to(self.dtype)).clamp(-1, 1)
             y = rewards + pow(self.gamma, self.n_step) * q_t * (1.0 - done)
             if self.double:
                 q_t2 = self.critic2_t(obs_next, a_t)

@@ -119,6 +119,9 @@ _SIGS = {
     'smi_last_error': (ctypes.c_char_p, []),
     'smi_workspace_bytes': (c_i64, []),
     'smi_set_workspace': (c_int, [P, c_i64]),
+    'smi_context_create': (P, [P, c_i64]),
+    'smi_context_make_current': (c_int, [P]),
+    'smi_context_destroy': (c_int, [P]),
     'smi_mlp_param_count': (c_i64, [c_int, c_int, c_int, c_int, c_int]),
     'smi_ppo_fused_lds_bytes': (c_i64, [c_int] * 7),
     'smi_ppo_fused_max_params': (c_i64, []),
@@ -242,6 +245,31 @@ def ensure_workspace(device):
         _workspaces[key] = ws
         check(lib().smi_set_workspace(ctypes.c_void_p(ws.data_ptr()), nbytes), 'smi_set_workspace')
     return _workspaces[key]
+
+
+class Context(object):
+    """An smi_context (include/surreal_mi.h, re-entrancy): its own device
+    workspace for the split-K / reduction partials of the launches its owner
+    enqueues.  Every object that launches work (learner, agent batch) owns
+    one and calls make_current() before its library calls, so objects on
+    different streams or threads never share partial buffers."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        nbytes = lib().smi_workspace_bytes()
+        self.ws = torch.zeros(nbytes // 4, dtype=torch.float32, device=self.device)
+        self.handle = lib().smi_context_create(ctypes.c_void_p(self.ws.data_ptr()), nbytes)
+        if not self.handle:
+            check(-1, 'smi_context_create')
+
+    def make_current(self):
+        check(lib().smi_context_make_current(ctypes.c_void_p(self.handle)), 'smi_context_make_current')
+
+    def __del__(self):
+        h, self.handle = getattr(self, 'handle', None), None
+        if h and _lib is not None:
+            _lib.smi_context_make_current(None)
+            _lib.smi_context_destroy(ctypes.c_void_p(h))
 
 
 def require_gpu():

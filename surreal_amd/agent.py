@@ -40,6 +40,7 @@ class PPOAgentBatch(object):
         self.agent_mode = agent_mode
         self.action_dim = ec.action_spec['dim'][0]
         self.device = torch.device(device) if device is not None else torch.device('cuda')
+        self._ctx = L.Context(self.device)      # own workspace (re-entrancy)
         algo = lc.algo
         self.rnn = algo.rnn if algo.rnn.if_rnn_policy else None
         self.model = PPOModel(ec.obs_spec, self.action_dim, lc.model, True, algo.consts.init_log_sig,
@@ -75,6 +76,7 @@ class PPOAgentBatch(object):
         """obs: {modality: {key: array (N, ...)}} for the N agents.
         Returns (actions (N, A) float64, [action_info per agent]) in training
         mode (actions only otherwise), like N reference act() calls."""
+        self._ctx.make_current()
         A = self.action_dim
         dev_obs = {}
         for mod, d in obs.items():
@@ -127,6 +129,7 @@ class DDPGAgentBatch(object):
         self.agent_mode = agent_mode
         self.action_dim = ec.action_spec['dim'][0]
         self.device = torch.device(device) if device is not None else torch.device('cuda')
+        self._ctx = L.Context(self.device)      # own workspace (re-entrancy)
         self.model = DDPGModel(ec.obs_spec, self.action_dim, lc.model.use_layernorm,
                                lc.model.actor_fc_hidden_sizes, lc.model.critic_fc_hidden_sizes,
                                device=self.device, generator=torch.Generator().manual_seed(seed))
@@ -167,6 +170,7 @@ class DDPGAgentBatch(object):
 
     def act(self, obs):
         """obs: (N, D) low-dim observations (or {'low_dim': {key: (N, D)}})."""
+        self._ctx.make_current()
         if isinstance(obs, dict):
             obs = obs['low_dim'][list(obs['low_dim'])[0]]
         x = torch.from_numpy(np.ascontiguousarray(obs, dtype=np.float32)).to(self.device)

@@ -3,6 +3,7 @@
 // error message for smi_last_error().
 #include <stdio.h>
 #include <string.h>
+#include <atomic>
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
 
@@ -25,17 +26,20 @@ int check_launch(const char* what) {
 }
 
 // ------------------------------------------------------------ kernel timing
+// process-wide record (measurement only): slots are claimed atomically, so
+// launches from several threads may record at once
 static bool g_kt = false;
 static const int kKtCap = 16384;
 static hipEvent_t* g_kt_ev = nullptr;        // [2 * kKtCap]
-static int g_kt_n = 0;
+static std::atomic<int> g_kt_n{0};
 struct KtRec { int cls; double flops; };
 static KtRec g_kt_rec[kKtCap];
 
 bool ktime_on() { return g_kt; }
 int ktime_begin(hipStream_t st) {
-  if (!g_kt || g_kt_n >= kKtCap) return -1;
-  const int slot = g_kt_n++;
+  if (!g_kt) return -1;
+  const int slot = g_kt_n.fetch_add(1);
+  if (slot >= kKtCap) return -1;
   (void)hipEventRecord(g_kt_ev[2 * slot], st);
   return slot;
 }
@@ -46,18 +50,25 @@ void ktime_end(int slot, int cls, double flops, hipStream_t st) {
   (void)hipEventRecord(g_kt_ev[2 * slot + 1], st);
 }
 
-// caller-registered device workspace (smi_set_workspace)
-// Two halves: slot 0 for launches on the caller's stream, slot 1 for the
-// side stream the RNN phases overlap weight-gradient GEMMs on (ppo_rnn.hip).
-static void* g_ws = nullptr;
-static int64_t g_ws_bytes = 0;
-static int g_ws_slot = 0;
-int workspace_slot(int slot) { const int old = g_ws_slot; g_ws_slot = slot; return old; }
-int64_t smi_workspace_floats() { return g_ws ? g_ws_bytes / 8 : 0; }
+// ---------------------------------------------------------- workspace contexts
+// A context = one caller-owned device workspace.  The calling thread's current
+// context (smi_context_make_current) serves every workspace request of the
+// launches that thread enqueues; without one, the default context
+// (smi_set_workspace) does.
+}  // namespace smi
+struct smi_context { void* ws; int64_t bytes; };
+namespace smi {
+static smi_context g_default_ctx{nullptr, 0};
+static thread_local smi_context* t_ctx = nullptr;
+static smi_context* cur_ctx() { return t_ctx ? t_ctx : &g_default_ctx; }
+int64_t smi_workspace_floats() {
+  const smi_context* c = cur_ctx();
+  return c->ws ? c->bytes / 4 : 0;
+}
 float* workspace_f32(int64_t nfloats) {
-  const int64_t half = g_ws_bytes / 8;
-  if (!g_ws || nfloats > half) return nullptr;
-  return static_cast<float*>(g_ws) + (g_ws_slot ? half : 0);
+  const smi_context* c = cur_ctx();
+  if (!c->ws || nfloats > c->bytes / 4) return nullptr;
+  return static_cast<float*>(c->ws);
 }
 
 // declared in the other translation units
@@ -114,8 +125,29 @@ const char* smi_last_error(void) { return g_err; }
 /* Registers the device scratch used by the multi-workgroup reductions
  * (colstats partials, Adam norm partials).  Not part of the reference API. */
 int smi_set_workspace(void* dev_ptr, int64_t bytes) {
-  g_ws = dev_ptr;
-  g_ws_bytes = bytes;
+  REQUIRE(dev_ptr && bytes > 0, "set_workspace: bad args");
+  g_default_ctx.ws = dev_ptr;
+  g_default_ctx.bytes = bytes;
+  return SMI_OK;
+}
+
+smi_context* smi_context_create(void* workspace, int64_t bytes) {
+  if (!workspace || bytes <= 0) {
+    set_error(SMI_E_ARG, "context_create: bad args");
+    return nullptr;
+  }
+  return new smi_context{workspace, bytes};
+}
+
+int smi_context_make_current(smi_context* ctx) {
+  t_ctx = ctx;
+  return SMI_OK;
+}
+
+int smi_context_destroy(smi_context* ctx) {
+  REQUIRE(ctx, "context_destroy: null context");
+  if (t_ctx == ctx) t_ctx = nullptr;
+  delete ctx;
   return SMI_OK;
 }
 int64_t smi_workspace_bytes(void) { return (int64_t)128 << 20; }
@@ -130,7 +162,7 @@ int smi_kernel_timing(int on) {
       if (hipEventCreate(&g_kt_ev[i]) != hipSuccess) return set_error(SMI_E_LAUNCH, "hipEventCreate");
   }
   g_kt = on != 0;
-  if (on) g_kt_n = 0;
+  if (on) g_kt_n.store(0);
   return SMI_OK;
 }
 /* out4 = {launches, total ms, total algorithmic flops, 0} of class cls
@@ -138,7 +170,8 @@ int smi_kernel_timing(int on) {
 int smi_kernel_timing_report(int cls, double* out4) {
   if (!out4 || cls < 0 || cls >= KT_COUNT) return set_error(SMI_E_ARG, "kernel_timing_report: bad args");
   double n = 0, ms = 0, fl = 0;
-  for (int i = 0; i < g_kt_n; ++i) {
+  const int nrec = g_kt_n.load() < kKtCap ? g_kt_n.load() : kKtCap;
+  for (int i = 0; i < nrec; ++i) {
     if (g_kt_rec[i].cls != cls) continue;
     if (hipEventSynchronize(g_kt_ev[2 * i + 1]) != hipSuccess) return set_error(SMI_E_LAUNCH, "event sync");
     float t = 0.f;

@@ -1221,9 +1221,10 @@ static int dwd_launch(GemmArgs g, hipStream_t st) {
 }
 
 // ---- grouped weight gradients (gemm_dwd_group_kernel) ----------------------
-static DwGroup g_grp;
-static bool g_grp_on = false;
-static double g_grp_flops = 0.0;
+// the queue of the calling thread (begin ... flush bracket one call sequence)
+static thread_local DwGroup g_grp;
+static thread_local bool g_grp_on = false;
+static thread_local double g_grp_flops = 0.0;
 
 int dw_group_begin() {
   g_grp_on = true;

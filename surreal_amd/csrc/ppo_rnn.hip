@@ -727,69 +727,27 @@ static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, fl
                            h.tanh_out ? ACT_TANH : ACT_NONE, Y, h.out, st, skip);
 }
 
-// Side stream for the heads' weight-gradient GEMMs: they only feed the Adam
-// step, so in the backward phases they run beside the critical chain (the
-// input gradients -> LSTM BPTT -> W_ih / W_hh / CNN gradients) and are joined
-// before the phase returns.  Split-K partials of side launches use workspace
-// slot 1.  SMI_SIDE_STREAM=0 keeps everything on the caller's stream.
-struct SideStream { hipStream_t st; hipEvent_t fork, join; };
-static SideStream* side_stream() {
-  static int enabled = -1;
-  if (enabled < 0) {
-    const char* e = getenv("SMI_SIDE_STREAM");
-    enabled = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (!enabled) return nullptr;
-  static SideStream ss[64];
-  static bool made[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!made[dev]) {
-    if (hipStreamCreateWithFlags(&ss[dev].st, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&ss[dev].fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&ss[dev].join, hipEventDisableTiming) != hipSuccess) return nullptr;
-    made[dev] = true;
-  }
-  return &ss[dev];
-}
-
-// make `to` wait for the work enqueued on `from` so far
-static int stream_after(hipStream_t to, hipStream_t from, hipEvent_t ev) {
-  if (hipEventRecord(ev, from) != hipSuccess || hipStreamWaitEvent(to, ev, 0) != hipSuccess)
-    return set_error(SMI_E_LAUNCH, "ppo_rnn: side-stream event");
-  return SMI_OK;
-}
-
-// one weight-gradient GEMM of a head: on the side stream (slot 1) after the
-// main stream's work so far, or inline
-static int head_dw(SideStream* side, const float* dY, int n, int M, const float* X, int64_t ldx,
-                   int k, float* gW, float* gb, hipStream_t st, const int* skip) {
-  if (!side) return launch_linear_bwd_dw(dY, n, M, n, X, ldx, k, gW, k, gb, 0, st, skip);
-  RC(stream_after(side->st, st, side->fork));
-  const int prev = workspace_slot(1);
-  const int rc = launch_linear_bwd_dw(dY, n, M, n, X, ldx, k, gW, k, gb, 0, side->st, skip);
-  workspace_slot(prev);
-  return rc;
-}
-
 // backward from dZ (gradient at the last layer's pre-activation) into the flat
 // gradient image G (same layout as P); input-gradient columns [dx0, dx0+dxn)
 // to dXout ([rows][dxn], masked by dxmask > 0 when given; dxn == 0: none).
-// With a side stream the weight gradients are left running on it: the caller
-// joins (stream_after(st, side->st, side->join)) before G is read.
+// Inside a dW group (stem_backward) the weight gradients are queued and run
+// as one grouped launch at the flush.
 static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx, int64_t rows,
                     const float* HA1, const float* HA2, float* dH1, float* dH2, float* G,
                     int dx0, int dxn, const float* dxmask, int64_t ldm, float* dXout,
-                    hipStream_t st, const int* skip, SideStream* side) {
+                    hipStream_t st, const int* skip) {
   const int M = (int)rows;
   const MlpLayout& L = h.L;
-  RC(head_dw(side, dZ, h.out, M, HA2, h.h2, h.h2, G + L.fW3, G + L.fb3, st, skip));
+  RC(launch_linear_bwd_dw(dZ, h.out, M, h.out, HA2, h.h2, h.h2, G + L.fW3, h.h2, G + L.fb3, 0, st,
+                          skip));
   RC(launch_linear_bwd_dx(dZ, h.out, M, h.out, h.P + L.fW3, h.h2, h.h2, HA2, h.h2, dH2, h.h2, st,
                           skip));
-  RC(head_dw(side, dH2, h.h2, M, HA1, h.h1, h.h1, G + L.fW2, G + L.fb2, st, skip));
+  RC(launch_linear_bwd_dw(dH2, h.h2, M, h.h2, HA1, h.h1, h.h1, G + L.fW2, h.h1, G + L.fb2, 0, st,
+                          skip));
   RC(launch_linear_bwd_dx(dH2, h.h2, M, h.h2, h.P + L.fW2, h.h1, h.h1, HA1, h.h1, dH1, h.h1, st,
                           skip));
-  RC(head_dw(side, dH1, h.h1, M, X, ldx, h.in, G + L.fW1, G + L.fb1, st, skip));
+  RC(launch_linear_bwd_dw(dH1, h.h1, M, h.h1, X, ldx, h.in, G + L.fW1, h.in, G + L.fb1, 0, st,
+                          skip));
   if (dxn <= 0) return SMI_OK;
   return launch_linear_bwd_dx(dH1, h.h1, M, h.h1, h.P + L.fW1 + dx0, h.in, dxn, dxmask, ldm, dXout,
                               dxn, st, skip);
@@ -929,45 +887,33 @@ static const float* head_in(const RnnDims& d, const RnnScratch& s, const float* 
   return d.H > 0 ? hbuf_of(d, s, d.L - 1) + (int64_t)d.B * d.H : X;
 }
 
-// backward of one head into G (+ the stem below it): LSTM BPTT and/or CNN,
-// with the head's weight gradients overlapped on the side stream
+// backward of one head into G (+ the stem below it): LSTM BPTT and/or CNN
 static int stem_backward_chain(const smi_ppo_rnn_args& a, const RnnDims& d, const Head& hd,
                                const LstmP& lm, const float* cnn, float* G, const RnnScratch& s,
-                               int64_t n_head, hipStream_t st, const int* skip, SideStream* side) {
+                               int64_t n_head, hipStream_t st, const int* skip) {
   const float* X = head_in(d, s, s.Xz);
   if (d.H > 0) {
     RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, 0, d.H, nullptr, 0,
-                s.dh, st, skip, side));
+                s.dh, st, skip));
     RC(lstm_backward(d, a.lstm, G + n_head, s, st, skip));
     return cnn_grad(a, d, lm, cnn, G + n_head + d.nL, s, st, skip);
   }
   // MLP policy: the first head layer's input gradient over the CNN columns only
   RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, d.D, d.F, s.Xz + d.D,
-              d.ldx, s.dF, st, skip, side));
+              d.ldx, s.dF, st, skip));
   if (d.F == 0) return SMI_OK;
   return cnn_bwd_from_dF(a, d, cnn, G + n_head, s, st, skip);
 }
 
+// every weight gradient of the phase (head layers + LSTM) queued and run as
+// one grouped launch after the input-gradient chain and BPTT
 static int stem_backward(const smi_ppo_rnn_args& a, const RnnDims& d, const Head& hd,
                          const LstmP& lm, const float* cnn, float* G, const RnnScratch& s,
                          int64_t n_head, hipStream_t st, const int* skip) {
-  // default: every weight gradient of the phase (head layers + LSTM) queued
-  // and run as one grouped launch after the input-gradient chain and BPTT
-  // (SMI_DW_GROUP=0: per-layer launches with the head's on the side stream)
-  static const int grouped = [] { const char* e = getenv("SMI_DW_GROUP"); return e ? atoi(e) : 1; }();
-  if (grouped) {
-    dw_group_begin();
-    const int rc = stem_backward_chain(a, d, hd, lm, cnn, G, s, n_head, st, skip, nullptr);
-    const int rf = dw_group_flush(st);     // always flush: nothing stays queued after an error
-    return rc ? rc : rf;
-  }
-  SideStream* side = side_stream();
-  const int rc = stem_backward_chain(a, d, hd, lm, cnn, G, s, n_head, st, skip, side);
-  if (side) {   // join even on error, so no side work outlives the phase
-    const int rj = stream_after(st, side->st, side->join);
-    if (!rc) return rj;
-  }
-  return rc;
+  dw_group_begin();
+  const int rc = stem_backward_chain(a, d, hd, lm, cnn, G, s, n_head, st, skip);
+  const int rf = dw_group_flush(st);     // always flush: nothing stays queued after an error
+  return rc ? rc : rf;
 }
 
 static float c_loglik_of(int A) { return (float)(0.5 * log(2.0 * 3.141592653589793) * (double)A); }

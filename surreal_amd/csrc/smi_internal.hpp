@@ -21,12 +21,11 @@ enum { KT_GEMM_FWD = 0, KT_GEMM_DX, KT_GEMM_DW, KT_GEMM_REDUCE, KT_LSTM_FWD, KT_
 bool ktime_on();
 int ktime_begin(hipStream_t st);                       // returns a slot, -1 when off/full
 void ktime_end(int slot, int cls, double flops, hipStream_t st);
-// registered device workspace (smi_set_workspace): capacity in floats of the
-// current slot (half of the buffer); workspace_slot() selects the half the
-// next launches use (0: the caller's stream, 1: the RNN phases' side stream)
+// device workspace of the calling thread's current smi_context (or the default
+// one of smi_set_workspace): capacity in floats, and its base for a request of
+// nfloats (nullptr when it does not fit)
 int64_t smi_workspace_floats();
 float* workspace_f32(int64_t nfloats);
-int workspace_slot(int slot);
 int launch_linear_fwd(const float* X, int64_t ldx, int M, int K, const float* W, int64_t ldw,
                       const float* b, int N, int act, float* Y, int64_t ldy, hipStream_t st,
                       const int* skip = nullptr);

@@ -272,6 +272,7 @@ class DDPGLearner(object):
         self.device = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         L.ensure_workspace(self.device)
+        self._ctx = L.Context(self.device)      # this learner's own workspace (re-entrancy)
         self.current_iteration = 0
         self.batch_size = lc.replay.batch_size
         self.discount_factor = lc.algo.gamma
@@ -565,6 +566,7 @@ class DDPGLearner(object):
     # ------------------------------------------------------- reference API
     def learn(self, batch):                                              # ddpg.py:354-376
         self.current_iteration += 1
+        self._ctx.make_current()
         if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
             batch = self.preprocess(batch)
         obs = batch['obs']

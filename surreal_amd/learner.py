@@ -141,6 +141,7 @@ class PPOLearner(object):
         self.device = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         L.ensure_workspace(self.device)
+        self._ctx = L.Context(self.device)      # this learner's own workspace (re-entrancy)
 
         self.current_iteration = 0
         self.global_step = 0
@@ -434,6 +435,7 @@ class PPOLearner(object):
         # phases of [rank-local gradients -> all-reduce (dp only) -> apply]
         mom = self._buf('adv_moments', (3,), torch.float64)
         L.call('smi_moments', L.ptr(adv_raw), B, None, 0, L.ptr(mom), st)
+        self._phase_tag = 'moments'
         yield mom
         a.adv_moments = mom.data_ptr()
         nx = L.lib().smi_ppo_xbuf_floats(D, a_h1, a_h2, A, c_h1, c_h2, a.mode)
@@ -444,12 +446,14 @@ class PPOLearner(object):
         for e in range(max(self.epoch_policy + 1, self.epoch_baseline)):
             with self._ev('ppo_epoch_grad_kernel'):
                 L.check(L.lib().smi_ppo_epoch_grad(a, e, st), 'smi_ppo_epoch_grad')
+            self._phase_tag = 'epoch_grad'          # actor AND critic gradients of epoch e
             yield xbuf
             with self._ev('ppo_epoch_apply_kernel'):
                 L.check(L.lib().smi_ppo_epoch_apply(a, e, st), 'smi_ppo_epoch_apply')
         if zf is not None:                                    # global z_update
             zbuf = self._buf('zbuf', (2, D))
             L.call('smi_zfilter_colstats', L.ptr(x), B, D, T * D, L.ptr(zbuf[0]), L.ptr(zbuf[1]), st)
+            self._phase_tag = 'zstats'
             yield zbuf
             L.call('smi_zfilter_accumulate', L.ptr(zbuf[0]), L.ptr(zbuf[1]), D, float(a.B_global),
                    L.ptr(zf.running_sum), L.ptr(zf.running_sumsq), L.ptr(zf.count), st)
@@ -574,28 +578,38 @@ class PPOLearner(object):
                 L.check(lib.smi_ppo_rnn_phase(a, p, e, st), 'smi_ppo_rnn_phase')
 
         ph(L.RNN_PH_GAE)
+        self._phase_tag = 'moments'
         yield moments
         ph(L.RNN_PH_PREP)
         for e in range(self.epoch_policy + 1):                  # ppo.py:541-557
             ph(L.RNN_PH_POLICY_FWD, e)
+            self._phase_tag = 'policy_stats'
             yield pstat
             ph(L.RNN_PH_POLICY_DECIDE, e)
             if e < self.epoch_policy:
                 ph(L.RNN_PH_POLICY_BWD, e)
+                self._phase_tag = 'policy_grad'
                 yield xbuf[:nA]
                 ph(L.RNN_PH_POLICY_APPLY, e)
         for e in range(self.epoch_baseline):                    # ppo.py:561-562
             ph(L.RNN_PH_VALUE_GRAD, e)
+            self._phase_tag = 'value_grad'
             yield xbuf[nA:nA + nC]
             ph(L.RNN_PH_VALUE_APPLY, e)
         ph(L.RNN_PH_ZSTATS)                                      # ppo.py:578-582
+        self._phase_tag = 'zstats'
         yield zbuf
         ph(L.RNN_PH_ZAPPLY)
 
     def _learn_phases(self, batch):
         """learn() as a generator of the buffers a data-parallel learner must
-        all-reduce (SUM) between its launches; yields nothing when dp is None."""
+        all-reduce (SUM) between its launches (the single-CU C2 kernel yields
+        nothing).  Before each yield `_phase_tag` names the buffer: 'moments',
+        'policy_stats', 'policy_grad' / 'value_grad' (the parameters are still
+        those the gradient was taken at), 'epoch_grad' (MLP phases: both),
+        'zstats', 'reward_filter'."""
         self.current_iteration += 1
+        self._ctx.make_current()
         if self._hyper_values() != self._hyper_key:       # e.g. schedulers restored from a checkpoint
             self._write_hyper()
         if self.dp is not None and self.use_r_filter:
@@ -603,13 +617,17 @@ class PPOLearner(object):
             # over the global batch, as one learner would see it)
             rf = self._buf('rf_sums', (3,), torch.float64)
             batch = self._preprocess_batch_ppo(batch, rf_sums=rf)
+            self._phase_tag = 'reward_filter'
             yield rf
+            self._ctx.make_current()
             self.reward_filter.commit_(rf)
         else:
             batch = self._preprocess_batch_ppo(batch)
-        yield from self._optimize(batch['obs'], batch['actions'], batch['rewards'],
+        for buf in self._optimize(batch['obs'], batch['actions'], batch['rewards'],
                                   batch['obs_next'], batch['persistent_infos'],
-                                  batch['onetime_infos'], batch['dones'])
+                                  batch['onetime_infos'], batch['dones']):
+            yield buf
+            self._ctx.make_current()      # whatever ran on this thread meanwhile
         if self.metrics is not None:
             self.metrics(self.last_stats(), self.global_step)
         self.exp_counter += self.batch_size * (self.dp.world_size if self.dp is not None else 1)

@@ -29,8 +29,10 @@ import torch
 
 
 def binary_hash(binary):
-    """surreal/utils/serializer.py:55-65: 16-char hash of the serialized bytes."""
-    return base64.b64encode(hashlib.md5(binary).digest())[:16].decode('ascii').replace('/', '_')
+    """surreal/utils/serializer.py:55-66: the first 16 base64 characters of the
+    md5 digest, returned as they are (the reference's `.replace('/', '_')` is
+    commented out at :65, so '/' and '+' stay in the hash)."""
+    return base64.b64encode(hashlib.md5(binary).digest())[:16].decode('utf-8')
 
 
 class _Layout(object):

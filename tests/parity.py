@@ -1,0 +1,529 @@
+"""Parity machinery of the pinned learn() tests (test infrastructure only).
+
+Three pieces, shared by the GPU tests and by tests/golden/make_envelopes.py:
+
+1. THE ENVELOPE.  The CPU oracle (oracle/ppo_ref.py, surreal/learner/ppo.py:
+   355-418,487-586) in fp64 is the "truth" of the reference algorithm.  Around
+   it, equally valid executions measure how far fp32 arithmetic may land from
+   that truth: the oracle in fp32 (the reference's own precision) over segment
+   orders (given, reversed, shuffled: only the order of every batch reduction
+   changes) and the oracle in fp64 on inputs / initial weights carrying one
+   fp32 rounding of relative noise (2^-24 N(0,1)).  A tensor passes when
+
+       max|GPU - fp64| <= 2 * max_variants max|variant - fp64| + SLACK * scale,
+
+   scale = max|fp64|, SLACK = 1e-6.  The envelope bounds TRAJECTORY quantities
+   (advantages, returns, post-step parameters, ZFilter sums, first-step
+   gradients).  Why an envelope and not the fp32 oracle alone: a ReLU
+   pre-activation within rounding distance of 0 flips its mask in any two fp32
+   implementations and Adam's m/sqrt(v) amplifies such differences over epochs
+   (DESIGN.md §2).
+
+2. FIXTURES.  For the full-size cases (C3 at 1024 segments, C5 at 128, their
+   first-step gradients) the fp64 truth and the per-tensor envelope widths are
+   computed once in the build container by tests/golden/make_envelopes.py and
+   committed (tests/golden/envelope_<case>.npz): the GPU box then runs only
+   the HIP side.  Initial weights come from the oracle's own seeded init
+   (regenerated on the box's CPU, digest-checked), batches from
+   surreal_amd.synthetic (seeded, digest-checked).  Parameters are stored as
+   fp32 differences from the initial weights (the truth to ~1e-10 of the
+   update), advantages / returns as fp32 (6e-8 of scale, far under SLACK).
+
+3. STATISTIC SELF-CONSISTENCY.  A last_stats() entry is a deterministic
+   reduction of the state it is computed from, so it is checked exactly rather
+   than against the chaotic trajectory: every entry is recomputed in fp64 from
+   the GPU's OWN state at the point the reference computes it (ppo.py:
+   194-331, 553-575) — the parameters the last policy / value update took its
+   loss at, the parameters after the policy loop, the reference policy, the
+   advantages and returns exactly as the epochs used them (GPU export) and the
+   batch — and must agree within RTOL_STAT = 1e-5 (north_star) of its
+   magnitude.  A mean over rows whose terms cancel (a surrogate loss over
+   zero-mean advantages, the mean return) is judged relative to the mean
+   |term| (no fp32 sum can carry relative accuracy beyond its terms'); a KL
+   divergence between nearby policies (ppo_net.py:48-62: sum log(s1/s0) +
+   (s0^2 + (m0 - m1)^2) / (2 s1^2) - A/2, O(1) terms cancelling to ~1e-3)
+   relative to the mean magnitude of those terms — the fp32 oracle itself
+   lands 2e-4 of the KL away from fp64 (tests/test_cpu_stats_consistency.py);
+   the explained variance relative to max(|ev|, |1 - ev|).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import torch
+
+from oracle import ppo_ref as R
+from tests.helpers import load_lstm_flat, load_seq_flat, lstm_flat, oracle_batch, ppo_config, seq_flat
+
+SLACK = 1e-6
+RTOL_STAT = 1e-5
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+# ------------------------------------------------------------------ cases
+def c3_cfg(mode, B, epochs=(10, 10)):
+    return ppo_config(B=B, T=25, mode=mode, use_z_filter=True, hidden=(300, 200), lam=1.0,
+                      rnn=True, rnn_hidden=100, horizon=5, epochs=epochs)
+
+
+def c5_cfg(B, epochs=(10, 10)):
+    lc = c3_cfg('adapt', B, epochs)
+    lc.model.cnn_feature_dim = 256
+    return lc
+
+
+# name -> everything a fixture needs; 'grad' cases store the raw gradients of
+# the first policy (epochs 1 + 0) or value (0 + 1) update instead of a trajectory
+CASES = {
+    # bench.py --config c3: the full 1024-segment batch, 10 + 10 epochs
+    'c3_adapt': dict(cfg=lambda: c3_cfg('adapt', 1024), D=42, A=8, Hd=100, pixel=None,
+                     init_seed=11, batch_seeds=[1100, 1101], n_ulp=6,
+                     orders=['given', 'reversed', ['shuffled', 1]]),
+    'c3_clip': dict(cfg=lambda: c3_cfg('clip', 1024), D=42, A=8, Hd=100, pixel=None,
+                    init_seed=12, batch_seeds=[1200], n_ulp=6,
+                    orders=['given', 'reversed', ['shuffled', 1]]),
+    'c3_grad_policy': dict(cfg=lambda: c3_cfg('adapt', 1024, (1, 0)), D=42, A=8, Hd=100, pixel=None,
+                           init_seed=13, batch_seeds=[1300], n_ulp=6,
+                           orders=['given', 'reversed', ['shuffled', 1]], grad='policy'),
+    'c3_grad_value': dict(cfg=lambda: c3_cfg('adapt', 1024, (0, 1)), D=42, A=8, Hd=100, pixel=None,
+                          init_seed=13, batch_seeds=[1300], n_ulp=6,
+                          orders=['given', 'reversed', ['shuffled', 1]], grad='value'),
+    # bench.py --config c5 --local-segments 128: C3 + camera0 3x84x84 -> CNN (FC 256)
+    'c5': dict(cfg=lambda: c5_cfg(128), D=42, A=8, Hd=100, pixel=(3, 84, 84),
+               init_seed=15, batch_seeds=[1500], n_ulp=3, orders=['given', 'reversed']),
+    'c5_grad_policy': dict(cfg=lambda: c5_cfg(128, (1, 0)), D=42, A=8, Hd=100, pixel=(3, 84, 84),
+                           init_seed=16, batch_seeds=[1600], n_ulp=4,
+                           orders=['given', 'reversed'], grad='policy'),
+    'c5_grad_value': dict(cfg=lambda: c5_cfg(128, (0, 1)), D=42, A=8, Hd=100, pixel=(3, 84, 84),
+                          init_seed=16, batch_seeds=[1600], n_ulp=4,
+                          orders=['given', 'reversed'], grad='value'),
+}
+
+
+def case_batch(case, it):
+    c = CASES[case]
+    from surreal_amd import synthetic
+    lc = c['cfg']()
+    return synthetic.ppo_batch(lc.replay.batch_size, lc.algo.n_step, c['D'], c['A'],
+                               seed=c['batch_seeds'][it], rnn_hidden=c['Hd'], pixel=c['pixel'])
+
+
+def digest(arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()[:32]
+
+
+def batch_digest(batch):
+    ob = oracle_batch(batch)
+    parts = [ob[k] for k in ('obs', 'obs_next', 'actions', 'rewards', 'dones', 'pds')
+             if ob.get(k) is not None]
+    parts += list(ob['onetime'] or []) + [ob[k] for k in ('pixels', 'pixels_next') if k in ob]
+    return digest(parts)
+
+
+# ----------------------------------------------------------- initial state
+def init_state(case):
+    """Initial fp32 weights of a case: the oracle's own seeded init (torch CPU
+    RNG), as flat buffers in the C-ABI layouts."""
+    c = CASES[case]
+    ref = R.PPOLearnerRef(c['cfg'](), c['D'], c['A'], seed=c['init_seed'], pixel=c['pixel'])
+    st = {'actor': ref.model.actor.flat().clone(), 'critic': ref.model.critic.flat().clone()}
+    if ref.rnn:
+        st['lstm'] = lstm_flat(ref.model.rnn_stem).clone()
+    if ref.model.cnn_stem is not None:
+        st['cnn'] = seq_flat(ref.model.cnn_stem).clone()
+    return st
+
+
+def load_state_into_learner(learner, st):
+    """initial weights -> the GPU learner's model and ref_target_model"""
+    with torch.no_grad():
+        for m in (learner.model, learner.ref_target_model):
+            m.actor.flat.copy_(st['actor'])
+            m.critic.flat.copy_(st['critic'])
+            if 'lstm' in st:
+                m.rnn_stem.flat.copy_(st['lstm'])
+            if 'cnn' in st:
+                m.cnn_stem.flat.copy_(st['cnn'])
+
+
+def load_state_into_oracle(ref, st, zf=None):
+    """flat state -> an oracle learner's model and ref_target_model; zf =
+    (running_sum, running_sumsq, count) or None (defaults)"""
+    for m in (ref.model, ref.ref_target_model):
+        dt = m.actor.log_var.dtype
+        m.actor.load_flat(torch.as_tensor(st['actor']).to(dt))
+        m.critic.load_flat(torch.as_tensor(st['critic']).to(dt))
+        if 'lstm' in st:
+            load_lstm_flat(m.rnn_stem, torch.as_tensor(st['lstm']).to(dt))
+        if 'cnn' in st:
+            load_seq_flat(m.cnn_stem, torch.as_tensor(st['cnn']).to(dt))
+        if zf is not None and m.use_z_filter:
+            with torch.no_grad():
+                for b, v in zip(('running_sum', 'running_sumsq', 'count'), zf):
+                    getattr(m.z_filter, b).copy_(torch.as_tensor(v).to(dt))
+
+
+# ---------------------------------------------------------------- envelope
+PERTURBED = ('obs', 'obs_next', 'actions', 'rewards', 'pds', 'onetime')
+
+
+class Variant(object):
+    """One execution of the envelope: the fp32 oracle over a segment order, or
+    the fp64 oracle with one ulp of relative noise on its inputs / weights."""
+
+    def __init__(self, kind, key, st, lc, D, A, pixel):
+        self.kind, self.key = kind, key
+        self.ref = R.PPOLearnerRef(lc, D, A, pixel=pixel,
+                                   dtype=torch.float32 if kind == 'order' else torch.float64)
+        load_state_into_oracle(self.ref, st)
+        self.gen = torch.Generator().manual_seed(4242 + 17 * key if kind == 'ulp' else 0)
+        self.p = None
+        if kind == 'ulp':
+            with torch.no_grad():
+                for q in self.ref.model.parameters():
+                    q.copy_(self._noisy(q))
+            self.ref.ref_target_model.update_target_params(self.ref.model)
+
+    def _noisy(self, x):
+        x = torch.as_tensor(x).to(torch.float32).double()
+        return x * (1 + 2.0 ** -24 * torch.randn(x.shape, generator=self.gen, dtype=torch.float64))
+
+    def learn(self, ob, seed):
+        B = np.asarray(ob['rewards']).shape[0]
+        if self.kind == 'order':
+            if self.key == 'given':
+                self.p = np.arange(B)
+            elif self.key == 'reversed':
+                self.p = np.arange(B)[::-1].copy()
+            else:                                   # ('shuffled', k)
+                self.p = np.random.RandomState(1000 * self.key[1] + seed).permutation(B)
+            b = {}
+            for k, v in ob.items():
+                if v is None:
+                    b[k] = None
+                elif isinstance(v, (list, tuple)):
+                    b[k] = [np.asarray(x)[self.p] for x in v]
+                else:
+                    b[k] = np.asarray(v)[self.p]
+        else:
+            b = {}
+            for k, v in ob.items():
+                if v is None or k not in PERTURBED:
+                    b[k] = v
+                elif isinstance(v, (list, tuple)):
+                    b[k] = [self._noisy(x) for x in v]
+                else:
+                    b[k] = self._noisy(v)
+        return self.ref.learn(b)
+
+    def per_segment(self, t):
+        """a per-segment output in the original segment order"""
+        t = np.asarray(t)
+        if self.kind != 'order':
+            return t
+        out = np.empty_like(t)
+        out[self.p] = t
+        return out
+
+
+def envelope(st, lc, D, A, pixel, n_ulp=6, orders=('given', 'reversed', ('shuffled', 1))):
+    r64 = R.PPOLearnerRef(lc, D, A, pixel=pixel, dtype=torch.float64)
+    load_state_into_oracle(r64, st)
+    vs = [Variant('order', tuple(k) if isinstance(k, list) else k, st, lc, D, A, pixel)
+          for k in orders]
+    vs += [Variant('ulp', k, st, lc, D, A, pixel) for k in range(1, n_ulp + 1)]
+    return r64, vs
+
+
+def oracle_params(ref):
+    out = {'actor': ref.model.actor.flat(), 'critic': ref.model.critic.flat()}
+    if ref.rnn:
+        out['lstm'] = lstm_flat(ref.model.rnn_stem)
+    if ref.model.cnn_stem is not None:
+        out['cnn'] = seq_flat(ref.model.cnn_stem)
+    return {k: v.detach().double().numpy() for k, v in out.items()}
+
+
+def oracle_grads(ref, phase):
+    m = ref.model
+    f = lambda ps: torch.cat([q.grad.detach().reshape(-1) for q in ps]).double().numpy()  # noqa: E731
+    out = {}
+    if phase == 'policy':
+        out['actor'] = f(list(m.actor.model.parameters()) + [m.actor.log_var])
+    else:
+        out['critic'] = f(m.critic.model.parameters())
+    if ref.rnn:
+        out['lstm'] = f(list(m.rnn_stem.parameters()))
+    if m.cnn_stem is not None:
+        out['cnn'] = f(list(m.cnn_stem.parameters()))
+    return out
+
+
+def width(r64, variants):
+    """(max_k max|variant_k - r64|, max|r64|) of one tensor"""
+    r64 = np.asarray(r64, dtype=np.float64).reshape(-1)
+    vs = [np.asarray(v, dtype=np.float64).reshape(-1) for v in variants]
+    if not r64.size:
+        return 0.0, 0.0
+    return max(float(np.abs(v - r64).max()) for v in vs), float(np.abs(r64).max())
+
+
+def check(name, got, r64, env, scale, report, slack=SLACK, factor=2.0):
+    """max|got - r64| <= factor * env + slack * scale"""
+    got = np.asarray(got, dtype=np.float64).reshape(-1)
+    r64 = np.asarray(r64, dtype=np.float64).reshape(-1)
+    assert got.shape == r64.shape, (name, got.shape, r64.shape)
+    scale = max(float(scale), 1e-30)
+    e = float(np.abs(got - r64).max()) if r64.size else 0.0
+    ok = e <= factor * env + slack * scale
+    report[name] = (e / scale, env / scale, ok)
+    if not ok:
+        report.setdefault('_fail', []).append(name)
+
+
+def print_report(report):
+    print('\n(GPU err / scale, envelope err / scale) vs the fp64 oracle:')
+    for k, v in report.items():
+        if k != '_fail':
+            print(f'  {k:30s} gpu {v[0]:.3e}  bar {v[1]:.3e}  {"" if v[2] else "FAIL"}')
+    assert not report.get('_fail'), report.get('_fail')
+
+
+# ---------------------------------------------------------------- fixtures
+def fixture_path(case):
+    return os.path.join(GOLDEN, f'envelope_{case}.npz')
+
+
+def save_fixture(case, meta, arrays):
+    arrays = {k: np.asarray(v) for k, v in arrays.items()}
+    arrays['meta'] = np.frombuffer(json.dumps(meta, sort_keys=True).encode(), dtype=np.uint8)
+    np.savez_compressed(fixture_path(case), **arrays)
+
+
+def load_fixture(case):
+    with np.load(fixture_path(case), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    meta = json.loads(bytes(d.pop('meta')).decode())
+    return meta, d
+
+
+def truth(meta, fx, name, it, st0):
+    """fp64 truth of tensor `name` after learn() `it` (parameters: stored as
+    fp32 differences from the initial state st0)"""
+    key = f'{name}@{it}'
+    v = fx[key].astype(np.float64)
+    if name in st0:
+        v = v + np.asarray(st0[name], dtype=np.float64)
+    return v, float(meta['width'][key]), float(meta['scale'][key])
+
+
+# ------------------------------------------------- learn() with state capture
+def gpu_state(learner):
+    m = learner.model
+    out = {'actor': m.actor.flat.detach().cpu().clone(), 'critic': m.critic.flat.detach().cpu().clone()}
+    if learner.if_rnn_policy:
+        out['lstm'] = m.rnn_stem.flat.detach().cpu().clone()
+    if learner.if_pixel_input:
+        out['cnn'] = m.cnn_stem.flat.detach().cpu().clone()
+    if learner.use_z_filter:
+        out['zf'] = tuple(getattr(m.z_filter, b).detach().cpu().clone()
+                          for b in ('running_sum', 'running_sumsq', 'count'))
+    return out
+
+
+def gpu_ref_state(learner):
+    m = learner.ref_target_model
+    out = {'actor': m.actor.flat.detach().cpu().clone(), 'critic': m.critic.flat.detach().cpu().clone()}
+    if learner.if_rnn_policy:
+        out['lstm'] = m.rnn_stem.flat.detach().cpu().clone()
+    if learner.if_pixel_input:
+        out['cnn'] = m.cnn_stem.flat.detach().cpu().clone()
+    if learner.use_z_filter:
+        out['zf'] = tuple(getattr(m.z_filter, b).detach().cpu().clone()
+                          for b in ('running_sum', 'running_sumsq', 'count'))
+    return out
+
+
+def learn_capture(learner, batch):
+    """learner.learn(batch) — the same launches and (with dp) the same
+    all-reduces — recording the GPU state where the reference computes its
+    statistics: the parameters every policy / value update took its loss at,
+    the parameters after the policy loop, the reference model, and the
+    ZFilter as the epochs saw it.  Returns the capture dict."""
+    cap = {'ref': gpu_ref_state(learner), 'pol_in': [], 'val_in': [], 'pol_final': None,
+           'hyper': (learner.clip_epsilon, learner.beta)}
+    start = gpu_state(learner)
+    for buf in learner._learn_phases(batch):
+        tag = getattr(learner, '_phase_tag', None)
+        if tag in ('policy_grad', 'epoch_grad'):
+            cap['pol_in'].append(gpu_state(learner))
+        if tag in ('value_grad', 'epoch_grad'):
+            if tag == 'value_grad' and cap['pol_final'] is None:
+                cap['pol_final'] = gpu_state(learner)
+            cap['val_in'].append(gpu_state(learner))
+        if learner.dp is not None:
+            learner.dp.allreduce_(buf)
+    cap['final'] = gpu_state(learner)
+    if cap['pol_final'] is None:        # no value phase yielded (or MLP: no shared stem)
+        cap['pol_final'] = cap['final']
+    cap['zf_epochs'] = start.get('zf')  # z_update runs after the epochs (ppo.py:578)
+    return cap
+
+
+def learn_capture_fused(learner, batch, clone_fn):
+    """The single-CU C2 kernel yields nothing: the states before the last
+    policy and value updates come from a bit-identical re-run of the same
+    learn() with one epoch fewer of each (the kernel is deterministic), on a
+    clone of the learner made by clone_fn() BEFORE this learn()."""
+    twin = clone_fn()
+    cap = {'ref': gpu_ref_state(learner), 'hyper': (learner.clip_epsilon, learner.beta)}
+    start = gpu_state(learner)
+    learner.learn(batch)
+    s = learner.last_stats()
+    k = s['epochs_run']
+    twin.epoch_policy = max(k - 1, 0)
+    twin.epoch_baseline = max(learner.epoch_baseline - 1, 0)
+    twin.learn(batch)
+    prev = gpu_state(twin)
+    cap['final'] = gpu_state(learner)
+    cap['pol_final'] = cap['final']
+    cap['pol_in'] = [prev] * k if k else []
+    cap['val_in'] = [prev] * learner.epoch_baseline
+    cap['zf_epochs'] = start.get('zf')
+    return cap
+
+
+# --------------------------------------------- statistic self-consistency
+def _kl_terms(p0, p1, A):
+    """mean over rows of the magnitudes of the terms DiagGauss.kl sums
+    (ppo_net.py:48-62)"""
+    p0, p1 = p0.reshape(-1, 2 * A), p1.reshape(-1, 2 * A)
+    m0, s0, m1, s1 = p0[:, :A], p0[:, A:], p1[:, :A], p1[:, A:]
+    t = (s1 / s0).log().abs() + (s0.pow(2) + (m0 - m1).pow(2)) / (2.0 * s1.pow(2))
+    return float((t.sum(1) + 0.5 * A).mean())
+
+
+def _stat_model(lc, D, A, pixel, st, zf):
+    ref = R.PPOLearnerRef(lc, D, A, pixel=pixel, dtype=torch.float64)
+    load_state_into_oracle(ref, st, zf)
+    return ref
+
+
+def recompute_stats(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run):
+    """every last_stats() entry in fp64 from the GPU's own state (module
+    docstring, item 3).  ob: oracle batch of the (global) batch; adv_used /
+    ret_used: the advantages / returns exactly as the epochs used them
+    ([B][E] batch-major, or [B]).  Returns {key: (value, scale)}."""
+    f64 = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32).double()  # noqa: E731
+    rnn = bool(lc.algo.rnn.if_rnn_policy)
+    E = lc.algo.n_step - lc.algo.rnn.horizon + 1 if rnn else 1
+    obs = None if ob['obs'] is None else f64(ob['obs'])
+    if rnn:
+        obs_iter = None if obs is None else obs[:, :E].contiguous()
+        actions = f64(ob['actions'])[:, :E].contiguous()
+        behave = f64(ob['pds'])[:, :E].contiguous()
+    else:
+        obs_iter = None if obs is None else obs[:, 0].contiguous()
+        actions = f64(ob['actions'])[:, 0].contiguous()
+        behave = f64(ob['pds'])[:, 0].contiguous()
+    if pixel is not None:
+        pix = torch.as_tensor(ob['pixels'])
+        obs_iter = (obs_iter, pix[:, :E].contiguous() if rnn else pix[:, 0].contiguous())
+    cells = None
+    if rnn:
+        cells = (f64(ob['onetime'][0]).transpose(0, 1).contiguous(),
+                 f64(ob['onetime'][1]).transpose(0, 1).contiguous())
+    adv = torch.as_tensor(np.asarray(adv_used), dtype=torch.float32).double().reshape(-1, 1)
+    ret = torch.as_tensor(np.asarray(ret_used), dtype=torch.float32).double()
+    if not rnn:
+        ret = ret.reshape(-1, 1)
+    clip_eps, beta = cap['hyper']
+    zf = cap['zf_epochs']
+    out = {}
+    pd = R.DiagGaussRef(A)
+    refm = _stat_model(lc, D, A, pixel, cap['ref'], cap['ref'].get('zf'))
+    with torch.no_grad():
+        ref_pol = refm.model.forward_actor(obs_iter, cells)
+    # --- the last policy update's loss (ppo.py:194-225, 250-285)
+    if epochs_run > 0:
+        m = _stat_model(lc, D, A, pixel, cap['pol_in'][epochs_run - 1], zf)
+        m.cells, m.beta, m.clip_epsilon = cells, beta, clip_eps
+        learn_pol = m.model.forward_actor(obs_iter, cells)
+        lp = pd.likelihood(actions, learn_pol)
+        bp = pd.likelihood(actions, behave)
+        ent = pd.entropy(learn_pol).mean().detach()
+        out['_entropy'] = (float(ent), abs(float(ent)))
+        if lc.algo.ppo_mode == 'clip':
+            ratio = lp / bp
+            surr = -ratio * adv
+            csurr = -torch.clamp(ratio, 1 - clip_eps, 1 + clip_eps) * adv
+            mx = torch.cat([surr, csurr], 1).max(1)[0]
+            loss = mx.mean()
+            out['_surr_loss'] = (float(surr.mean()), float(surr.abs().mean()))
+            out['_clip_surr_loss'] = (float(loss), float(mx.abs().mean()))
+        else:
+            kl = pd.kl(ref_pol, learn_pol).mean()
+            terms = adv * (lp / torch.clamp(bp, min=1e-2))
+            surr = -terms.mean()
+            loss = surr + beta * kl
+            mag = float(terms.abs().mean()) + abs(beta) * _kl_terms(ref_pol, learn_pol.detach(), A)
+            if float(kl) - 2.0 * lc.algo.consts.kl_target > 0:
+                pen = lc.algo.adapt_consts.kl_cutoff_coeff * (kl - 2.0 * lc.algo.consts.kl_target).pow(2)
+                loss = loss + pen
+                mag += float(pen)
+            out['_surr_loss'] = (float(surr), float(terms.abs().mean()))
+            out['_kl_loss_adapt'] = (float(loss), max(abs(float(loss)), mag))
+        if lc.algo.network.clip_actor_gradient:
+            ps = m.model.actor_params()
+            gs = torch.autograd.grad(loss, ps, allow_unused=True)
+            n = float(torch.sqrt(sum((g * g).sum() for g in gs if g is not None)))
+            out['grad_norm_actor'] = (n, n)
+    # --- after the policy loop (ppo.py:553-575)
+    mf = _stat_model(lc, D, A, pixel, cap['pol_final'], zf)
+    with torch.no_grad():
+        curr_pol = mf.model.forward_actor(obs_iter, cells)
+        kl = pd.kl(ref_pol, curr_pol).mean()
+        bl = pd.likelihood(actions, behave)
+        cl = pd.likelihood(actions, curr_pol)
+        if epochs_run > 0:
+            out['_pol_kl'] = (float(kl), _kl_terms(ref_pol, curr_pol, A))
+        out['_avg_behave_likelihood'] = (float(bl.mean()), abs(float(bl.mean())))
+        isw = cl / (bl + 1e-4)
+        out['_avg_is_weight'] = (float(isw.mean()), abs(float(isw.mean())))
+        rbd = pd.kl(ref_pol, behave).mean()
+        out['_ref_behave_diff'] = (float(rbd), _kl_terms(ref_pol, behave, A))
+        out['_avg_return_targ'] = (float(ret.mean()), float(ret.abs().mean()))
+        lv = torch.as_tensor(cap['final']['actor'])[-A:].double()
+        out['_avg_log_sig'] = (float(lv.mean()), float(lv.abs().mean()))
+    # --- the last value update's loss (ppo.py:311-353)
+    nv = lc.algo.consts.epoch_baseline
+    if nv > 0:
+        mv = _stat_model(lc, D, A, pixel, cap['val_in'][nv - 1], zf)
+        values = mv.model.forward_critic(obs_iter, cells)
+        if values.dim() == 3:
+            values = values.squeeze(2)
+        ev = 1 - torch.var(ret - values) / torch.var(ret)
+        loss = (values - ret).pow(2).mean()
+        out['_val_loss'] = (float(loss), abs(float(loss)))
+        out['_val_explained_var'] = (float(ev), max(abs(float(ev)), abs(1 - float(ev))))
+        if lc.algo.network.clip_critic_gradient:
+            ps = mv.model.critic_params()
+            gs = torch.autograd.grad(loss, ps, allow_unused=True)
+            n = float(torch.sqrt(sum((g * g).sum() for g in gs if g is not None)))
+            out['grad_norm_critic'] = (n, n)
+    return out
+
+
+def check_stats(stats, recomputed, report, rtol=RTOL_STAT, tag=''):
+    for k, (v, scale) in recomputed.items():
+        assert k in stats, (k, sorted(stats))
+        e = abs(stats[k] - v) / max(scale, 1e-30)
+        ok = e <= rtol
+        report[f'stat{tag}:{k}'] = (e, rtol, ok)
+        if not ok:
+            report.setdefault('_fail', []).append(f'stat{tag}:{k}')

@@ -175,3 +175,28 @@ def test_product_does_not_import_oracle():
             if f.endswith('.py'):
                 src = open(os.path.join(dp, f)).read()
                 assert 'oracle' not in re.findall(r'^\s*(?:from|import)\s+(\w+)', src, re.M), f
+
+
+def test_binary_hash_matches_reference_serializer():
+    """surreal/utils/serializer.py:55-66: the first 16 base64 characters of
+    the md5 digest, '/' kept (the replace at :65 is commented out)."""
+    from surreal_amd.publish import binary_hash
+    assert binary_hash(b'payload3') == '1RTGU+Gd/jOICPXV'
+    assert len(binary_hash(b'')) == 16
+
+
+def test_context_lifecycle_without_device_work():
+    """smi_context (include/surreal_mi.h, re-entrancy): create / make current /
+    destroy are host-only; bad arguments are refused with a message."""
+    import ctypes
+    from surreal_amd import _lib
+    lib = _lib.lib()
+    assert not lib.smi_context_create(None, 1024)
+    assert b'context_create' in lib.smi_last_error()
+    fake = ctypes.c_void_p(0x1000)            # never dereferenced: no launch is made
+    h = lib.smi_context_create(fake, 1 << 20)
+    assert h
+    assert lib.smi_context_make_current(ctypes.c_void_p(h)) == 0
+    assert lib.smi_context_make_current(None) == 0
+    assert lib.smi_context_destroy(ctypes.c_void_p(h)) == 0
+    assert lib.smi_context_destroy(None) == -1

@@ -144,7 +144,7 @@ def test_ddpg_checkpoint_full_state():
 
 
 @pytest.mark.parametrize('rnn', [False, True])
-def test_publish_snapshot_overlaps_next_learn(rnn):
+def test_publish_snapshot_bytes_match_state_dict(rnn):
     lc, D, A, Hd = _ppo_setup(rnn)
     B, T = lc.replay.batch_size, lc.algo.n_step
     got = []
@@ -176,6 +176,48 @@ def test_publish_snapshot_overlaps_next_learn(rnn):
     for k, v in agents.model.state_dict().items():
         assert np.array_equal(v.cpu().numpy(), pickle.loads(got[-1][0])['ppo'][k])
     pub.close()
+
+
+def test_publish_snapshot_does_not_serialize_learn():
+    """The snapshot's D2H runs on a side stream and its serialisation on a
+    worker thread, so learn() + publish with a pending snapshot costs what
+    learn() + publish without a publisher costs (both run _post_publish,
+    ppo.py:637-666, whose KL record read is the reference's own host sync):
+    within 5 %, at C3 widths (LSTM 100, heads 300x200, 256 segments)."""
+    import time
+    from surreal_amd.publish import binary_hash
+    lc = ppo_config(B=256, T=25, mode='adapt', use_z_filter=True, hidden=(300, 200), lam=1.0,
+                    rnn=True, rnn_hidden=100, horizon=5)
+    lc.parameter_publish.exp_interval = lc.replay.batch_size      # publish after every learn()
+    D, A, Hd = 42, 8, 100
+    learner = PPOLearner(lc, env_config(D, A), seed=1)
+    batch = synthetic.to_device(synthetic.ppo_batch(256, 25, D, A, seed=3, rnn_hidden=Hd), DEV)
+    got = []
+    pub = DeviceParameterPublisher(learner.module_dict(), sink=lambda b, i: got.append(i['hash']))
+
+    def run(publisher, n=8):
+        learner.publisher = publisher
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for it in range(n):
+            learner.learn(batch)
+            learner.publish_parameter(it)
+        torch.cuda.synchronize()
+        if publisher is not None:
+            publisher.flush()
+        return time.perf_counter() - t0
+    run(None, 2)
+    run(pub, 2)                                    # warm: pinned slots, worker thread
+    t_plain, t_pub = [], []
+    for _ in range(4):                             # interleaved trials, best of each
+        t_plain.append(run(None))
+        t_pub.append(run(pub))
+    pub.close()
+    assert len(got) == 2 + 4 * 8 and all(len(h) == 16 for h in got)
+    assert min(t_pub) <= 1.05 * min(t_plain), (t_pub, t_plain)
+    # the hash is the reference's binary_hash (serializer.py:55-66), '/' kept
+    assert binary_hash(b'surreal') == __import__('base64').b64encode(
+        __import__('hashlib').md5(b'surreal').digest())[:16].decode('utf-8')
 
 
 @pytest.mark.parametrize('rnn,mode', [(True, 'training'), (False, 'training'),
@@ -260,3 +302,65 @@ def test_ddpg_agent_batch_matches_sequential_reference_agents(noise):
         # actions live in [-1, 1]: judge against that scale (floor 1e-2), not
         # against the largest entry of a small OU-noise step
         assert max_rel_err(a, ra, floor=1e-2) < 1e-5, (step, a, ra)
+
+
+def test_learners_on_two_streams_in_three_threads_match_sequential_runs():
+    """Re-entrancy (SURVEY §8(b) Threading): two PPO learners and a DDPG learner
+    running at the same time on their own streams in their own threads end
+    bit-identical to the same learners run one after another.  Every learner
+    owns an smi_context (its split-K / reduction partials never meet another
+    learner's) and grouped weight-gradient queues are per thread."""
+    import threading
+    lc = ppo_config(B=96, T=12, mode='adapt', use_z_filter=True, hidden=(300, 200), lam=1.0,
+                    epochs=(3, 3), rnn=True, rnn_hidden=100, horizon=4)
+    D, A, Hd = 42, 8, 100
+    lcd = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
+    lcd.replay.batch_size = 512
+    ecd = gym_env_config(17, 6)
+    pb = {s: [synthetic.to_device(synthetic.ppo_batch(96, 12, D, A, seed=100 * s + i, rnn_hidden=Hd), DEV)
+              for i in range(4)] for s in (1, 2)}
+    db = [synthetic.to_device(synthetic.ddpg_batch(512, 17, 6, seed=i), DEV) for i in range(8)]
+    torch.cuda.synchronize()
+
+    def make():
+        return (PPOLearner(lc, env_config(D, A), seed=1), PPOLearner(lc, env_config(D, A), seed=2),
+                DDPGLearner(lcd, ecd, seed=3))
+
+    def state(p1, p2, d):
+        return [t.detach().cpu().clone() for t in (p1.model.actor.flat, p1.model.critic.flat, p1.model.stem_flat,
+                                                    p2.model.actor.flat, p2.model.critic.flat, p2.model.stem_flat,
+                                                    d.model.actor.flat, d.model.critic.flat)]
+    seq = make()
+    for b in pb[1]:
+        seq[0].learn(b)
+    for b in pb[2]:
+        seq[1].learn(b)
+    for b in db:
+        seq[2].learn(b)
+    torch.cuda.synchronize()
+    want = state(*seq)
+    conc = make()
+    torch.cuda.synchronize()
+    errs = []
+
+    def run(learner, batches, stream):
+        try:
+            with torch.cuda.stream(stream):
+                for b in batches:
+                    learner.learn(b)
+            stream.synchronize()
+        except Exception as e:          # surfaced below
+            errs.append(e)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    ths = [threading.Thread(target=run, args=(conc[0], pb[1], streams[0])),
+           threading.Thread(target=run, args=(conc[1], pb[2], streams[1])),
+           threading.Thread(target=run, args=(conc[2], db, streams[2]))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    got = state(*conc)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert torch.equal(a, b), i

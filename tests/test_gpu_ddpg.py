@@ -13,8 +13,6 @@ from surreal_amd import _lib as L
 from surreal_amd import synthetic
 from surreal_amd.config import DDPG_DEFAULT_LEARNER_CONFIG, gym_env_config
 from surreal_amd.ddpg import DDPGLearner
-from tests.helpers import max_rel_err
-from tests.test_gpu_ppo import _compare_params
 
 pytestmark = pytest.mark.gpu
 
@@ -163,70 +161,162 @@ def test_layernorm_kernels_vs_torch(rows, n):
     assert torch.allclose(mu.double().cpu(), x.mean(1), rtol=1e-5, atol=1e-6)
 
 
+# --------------------------------------------------- learn() on the envelope
+# The C4 step on the same bar as the PPO learner (tests/parity.py): the fp64
+# oracle is the truth; the envelope is the fp32 oracle over row orders (given,
+# reversed, shuffled) and the fp64 oracle with one fp32 rounding of relative
+# noise on its inputs and initial weights (6 seeds).  Parameters (actor,
+# critic, critic2, target critics) must satisfy max|GPU - fp64| <= 2 *
+# envelope + 1e-6 * scale; a statistic (a mean over the step's rows, taken at
+# the step's starting parameters) likewise, or within 1e-5 of its magnitude.
+DDPG_ORDERS = ('given', 'reversed', 'shuffled')
+
+
+class _DVariant(object):
+    def __init__(self, kind, key, lc, D, A, init):
+        self.kind, self.key = kind, key
+        self.ref = R.DDPGLearnerRef(lc, D, A, dtype=torch.float32 if kind == 'order' else torch.float64)
+        self.gen = torch.Generator().manual_seed(777 + 13 * key if kind == 'ulp' else 0)
+        _load_ddpg(self.ref, init, self._noisy if kind == 'ulp' else None)
+
+    def _noisy(self, x):
+        x = torch.as_tensor(x).to(torch.float32).double()
+        return x * (1 + 2.0 ** -24 * torch.randn(x.shape, generator=self.gen, dtype=torch.float64))
+
+    def optimize(self, b, it):
+        B = b['rewards'].shape[0]
+        if self.kind == 'order':
+            p = (np.arange(B) if self.key == 'given' else np.arange(B)[::-1].copy()
+                 if self.key == 'reversed' else np.random.RandomState(50 + it).permutation(B))
+            self.ref.noise_perm = p
+            x = {k: torch.as_tensor(np.asarray(v)[p]) for k, v in b.items()}
+        else:
+            x = {k: self._noisy(v) for k, v in b.items()}
+            x['dones'] = torch.as_tensor(b['dones'], dtype=torch.float64)
+        return self.ref.optimize(x['obs'], x['actions'], x['rewards'], x['obs_next'], x['dones'])
+
+
+def _load_ddpg(ref, init, noisy=None):
+    f = (lambda t: t) if noisy is None else noisy
+    R.load_flat(ref.actor.params(), f(init['actor']))
+    R.load_flat(ref.critic.params(), f(init['critic']))
+    if 'critic2' in init:
+        R.load_flat(ref.critic2.params(), f(init['critic2']))
+    ref.hard_update()
+
+
+def _ddpg_state(learner):
+    out = {'actor': learner.model.actor.flat.detach().cpu().clone(),
+           'critic': learner.model.critic.flat.detach().cpu().clone(),
+           'critic_t': learner.model_target.critic.flat.detach().cpu().clone(),
+           'actor_t': learner.model_target.actor.flat.detach().cpu().clone()}
+    if learner.use_double_critic:
+        out['critic2'] = learner.model2.critic.flat.detach().cpu().clone()
+        out['critic2_t'] = learner.model_target2.critic.flat.detach().cpu().clone()
+    return out
+
+
+def _ddpg_ref_state(ref):
+    out = {'actor': R.flat_of(ref.actor.params()), 'critic': R.flat_of(ref.critic.params()),
+           'critic_t': R.flat_of(ref.critic_t.params()), 'actor_t': R.flat_of(ref.actor_t.params())}
+    if ref.double:
+        out['critic2'] = R.flat_of(ref.critic2.params())
+        out['critic2_t'] = R.flat_of(ref.critic2_t.params())
+    return {k: v.double().numpy() for k, v in out.items()}
+
+
+def ddpg_envelope_run(lc, D, A, iters=3, batches=None, n_ulp=6, learn_input=None, seed=2):
+    """the HIP learner vs the fp64 oracle within the envelope over `iters`
+    steps.  batches: list of numpy dicts (obs, actions, rewards (B,1),
+    obs_next, dones (B,1)); learn_input(learner, it) -> what learner.learn()
+    gets (default: the batch on the device)."""
+    from tests import parity as P
+    B = lc.replay.batch_size
+    learner = DDPGLearner(lc, gym_env_config(D, A), seed=seed)
+    init = {k: v for k, v in _ddpg_state(learner).items() if k in ('actor', 'critic', 'critic2')}
+    r64 = R.DDPGLearnerRef(lc, D, A, dtype=torch.float64)
+    _load_ddpg(r64, init)
+    vs = [_DVariant('order', k, lc, D, A, init) for k in DDPG_ORDERS]
+    vs += [_DVariant('ulp', k, lc, D, A, init) for k in range(1, n_ulp + 1)]
+    if batches is None:
+        batches = [{k: v.numpy() for k, v in synthetic.ddpg_batch(B, D, A, seed=it).items()}
+                   for it in range(iters)]
+    report = {}
+    for it, b in enumerate(batches):
+        np.random.seed(100 + it)
+        s64 = r64.optimize(*(torch.as_tensor(b[k], dtype=torch.float32).double()
+                             for k in ('obs', 'actions', 'rewards', 'obs_next', 'dones')))
+        svs = []
+        for v in vs:
+            np.random.seed(100 + it)
+            svs.append(v.optimize(b, it))
+        np.random.seed(100 + it)
+        if learn_input is None:
+            learner.learn({k: torch.as_tensor(v, dtype=torch.float32).cuda() for k, v in b.items()})
+        else:
+            learner.learn(learn_input(learner, it))
+        s = learner.last_stats()
+        got, p64 = _ddpg_state(learner), _ddpg_ref_state(r64)
+        pvs = [_ddpg_ref_state(v.ref) for v in vs]
+        for k in p64:
+            w, sc = P.width(p64[k], [x[k] for x in pvs])
+            P.check(f'{k}@{it}', got[k], p64[k], w, sc, report)
+        for k in s64:
+            w = max(abs(x[k] - s64[k]) for x in svs)
+            e, sc = abs(s[k] - s64[k]), max(abs(s64[k]), 1e-30)
+            ok = e <= 2 * w + 1e-6 * sc or e <= 1e-5 * sc
+            report[f'stat:{k}@{it}'] = (e / sc, max(w / sc, 1e-5), ok)
+            if not ok:
+                report.setdefault('_fail', []).append(f'stat:{k}@{it}')
+    P.print_report(report)
+    return learner
+
+
 @pytest.mark.parametrize('target,clip_critic,layernorm', [('hard', False, False), ('soft', True, False),
                                                           ('hard', False, True), ('soft', True, True)])
-def test_ddpg_learn_matches_oracle(target, clip_critic, layernorm):
-    B, D, A = 512, 17, 6
-    lc = _cfg(B, target, clip_critic, layernorm)
-    learner = DDPGLearner(lc, gym_env_config(D, A), seed=2)
-    ref = R.DDPGLearnerRef(lc, D, A)
-    _sync_weights(learner, ref)
-    report = {}
-    for it in range(3):
-        b = synthetic.ddpg_batch(B, D, A, seed=it)
-        rs = ref.optimize(b['obs'], b['actions'], b['rewards'], b['obs_next'], b['dones'])
-        learner.learn({k: v.cuda() for k, v in b.items()})
-        s = learner.last_stats()
-        for k in rs:
-            assert abs(s[k] - rs[k]) <= 1e-4 * abs(rs[k]) + 1e-5, (it, k, s[k], rs[k])
-        _compare_params(f'critic{it}', learner.model.critic.flat.cpu(), R.flat_of(ref.critic.params()),
-                        1e-3, it + 1, report)
-        # the DDPG actor gradient is the critic's input gradient pushed back
-        # through the actor (ddpg.py:325-329): more of its entries are fp32
-        # rounding noise than in PPO, so the Adam sign-flip budget is 0.5 %
-        _compare_params(f'actor{it}', learner.model.actor.flat.cpu(), R.flat_of(ref.actor.params()),
-                        1e-4, it + 1, report, max_frac=5e-3)
-        _compare_params(f'tcritic{it}', learner.model_target.critic.flat.cpu(),
-                        R.flat_of(ref.critic_t.params()), 1e-3, it + 1, report)
-    print('ddpg parity report:', report)
+def test_ddpg_learn_envelope(target, clip_critic, layernorm):
+    # BASELINE configs[3]: batch 512, HalfCheetah dims, actor 300x200, critic 400x300, n 3
+    ddpg_envelope_run(_cfg(512, target, clip_critic, layernorm), 17, 6, iters=3)
 
 
 @pytest.mark.parametrize('target,action_reg', [('hard', False), ('soft', True)])
-def test_ddpg_td3_matches_oracle(target, action_reg):
+def test_ddpg_td3_envelope(target, action_reg):
     """TD3 options (ddpg.py:267-283,312-320): twin critic with min target, and
-    target-policy smoothing noise drawn from numpy's global RNG on the host (the
-    reference's own generator: both sides are seeded identically per step)."""
-    B, D, A = 512, 17, 6
-    lc = _cfg(B, target, False)
+    target-policy smoothing noise from numpy's global RNG on the host (the
+    reference's own generator: every execution is seeded identically per step,
+    row-permuted executions permute the noise rows with the batch rows)."""
+    lc = _cfg(512, target, False)
     lc.algo.network.use_double_critic = True
     lc.algo.network.use_action_regularization = action_reg
-    learner = DDPGLearner(lc, gym_env_config(D, A), seed=2)
-    ref = R.DDPGLearnerRef(lc, D, A)
-    _sync_weights(learner, ref)
-    R.load_flat(ref.critic2.params(), learner.model2.critic.flat.cpu())
-    ref.hard_update()
-    report = {}
+    ddpg_envelope_run(lc, 17, 6, iters=3)
+
+
+def test_ddpg_host_path_ssar_envelope():
+    """experience lists as ExpSenderWrapperSSAR sends them ->
+    DDPGLearner._prefetcher_preprocess (SSARAggregator, aggregator.py:52-103) ->
+    preprocess (the host -> device copy, ddpg.py:186-242) -> learn(), on the
+    envelope bar against the oracle fed the same aggregated arrays."""
+    from oracle import aggregator_ref as AR
+    B, D, A = 512, 17, 6
+    lc = _cfg(B, 'hard', False)
+    ec = gym_env_config(D, A)
+    host = [AR.make_ssar_exp_list(AR.ssar_exp_arrays(B, D, A, 900 + it)) for it in range(3)]
+
+    def learn_input(learner, it):            # the learner's own host path
+        return learner.preprocess(learner._prefetcher_preprocess(host[it]))
+    # the oracle sees the aggregator's output as the reference's preprocess
+    # converts it (float32 tensors)
+    from surreal_amd.aggregator import SSARAggregator
+    aggs = []
     for it in range(3):
-        b = synthetic.ddpg_batch(B, D, A, seed=it)
-        np.random.seed(100 + it)
-        rs = ref.optimize(b['obs'], b['actions'], b['rewards'], b['obs_next'], b['dones'])
-        np.random.seed(100 + it)
-        learner.learn({k: v.cuda() for k, v in b.items()})
-        s = learner.last_stats()
-        for k in rs:
-            assert abs(s[k] - rs[k]) <= 1e-4 * abs(rs[k]) + 1e-5, (it, k, s[k], rs[k])
-        _compare_params(f'critic{it}', learner.model.critic.flat.cpu(), R.flat_of(ref.critic.params()),
-                        1e-3, it + 1, report)
-        _compare_params(f'critic2_{it}', learner.model2.critic.flat.cpu(),
-                        R.flat_of(ref.critic2.params()), 1e-3, it + 1, report)
-        # min(y1, y2) picks per row; rows with y1 ~ y2 within fp32 noise may pick
-        # differently in any two implementations (like a ReLU mask flip), on
-        # top of the DDPG actor's sign-flip budget: 1 %
-        _compare_params(f'actor{it}', learner.model.actor.flat.cpu(), R.flat_of(ref.actor.params()),
-                        1e-4, it + 1, report, max_frac=1e-2)
-        _compare_params(f'tcritic2_{it}', learner.model_target2.critic.flat.cpu(),
-                        R.flat_of(ref.critic2_t.params()), 1e-3, it + 1, report)
-    print('ddpg td3 parity report:', report)
+        a = SSARAggregator(ec.obs_spec, ec.action_spec).aggregate(host[it])
+        aggs.append({'obs': np.asarray(a['obs']['low_dim']['flat_inputs'], np.float32),
+                     'actions': np.asarray(a['actions'], np.float32),
+                     'rewards': np.asarray(a['rewards'], np.float32),
+                     'obs_next': np.asarray(a['obs_next']['low_dim']['flat_inputs'], np.float32),
+                     'dones': np.asarray(a['dones'], np.float32)})
+        assert aggs[-1]['rewards'].shape == (B, 1) and aggs[-1]['dones'].shape == (B, 1)
+    ddpg_envelope_run(lc, D, A, batches=aggs, learn_input=learn_input)
 
 
 def test_replay_sample_feeds_learner_with_cpython_indices():

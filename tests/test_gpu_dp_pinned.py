@@ -1,0 +1,107 @@
+"""Data-parallel PPOLearner.learn() at the benched widths, pinned to the same
+fp64 truth and envelope as the single-GPU full-size cases
+(tests/golden/envelope_<case>.npz, tests/parity.py).
+
+Two processes share cuda:0 and exchange over torch.distributed (gloo: RCCL
+refuses two ranks on one GPU; on a multi-GPU node the same code runs over
+'nccl' = RCCL/xGMI, as bench.py does).  Each rank learns its half of the
+global batch (segments sharded on the batch axis).  Required:
+  * the ranks end bit-identical (parameters, ZFilter);
+  * rank 0's parameters, advantages (both halves), returns and ZFilter sums lie
+    within the fp32 envelope of the fp64 oracle's learn() on the GLOBAL batch;
+  * every statistic is self-consistent in fp64 with the global state.
+Cases: C3 (LSTM 100, heads 300x200, obs 42, act 8, 10 + 10 epochs) as 2 x 512
+segments, adapt over two learns and clip; C5 (C3 + camera stem, FC 256) as
+2 x 64 segments.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, case, outdir):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from surreal_amd import synthetic
+    from surreal_amd.learner import TorchDistAllReduce
+    from tests import parity as P
+    from tests.test_gpu_parity_pinned import _used, fixture_learner
+    meta, fx, c, st, learner = fixture_learner(case, dp=TorchDistAllReduce())
+    B = learner.batch_size
+    lo, hi = rank * B, (rank + 1) * B
+    res = []
+    for it in range(len(c['batch_seeds'])):
+        full = P.case_batch(case, it)
+
+        def cut(x):
+            if x is None:
+                return None
+            if isinstance(x, dict):
+                return {k: cut(v) for k, v in x.items()}
+            if isinstance(x, list):
+                return [cut(v) for v in x]
+            return x[lo:hi].contiguous()
+        cap = P.learn_capture(learner, synthetic.to_device(cut(full), 'cuda:0'))
+        adv, ret = _used(learner)
+        r = {'stats': learner.last_stats(), 'adv': torch.from_numpy(adv), 'ret': torch.from_numpy(ret)}
+        if rank == 0:
+            r['cap'] = cap
+        else:
+            r['final'] = cap['final']
+        res.append(r)
+    torch.save(res, os.path.join(outdir, f'rank{rank}.pt'))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('case', ['c3_adapt', 'c3_clip', 'c5'])
+def test_dp_two_ranks_match_global_fixture(case):
+    from tests import parity as P
+    from tests.helpers import oracle_batch
+    world = 2
+    with tempfile.TemporaryDirectory() as outdir:
+        mp.spawn(_worker, args=(world, _free_port(), case, outdir), nprocs=world, join=True)
+        out = [torch.load(os.path.join(outdir, f'rank{r}.pt'), weights_only=True)
+               for r in range(world)]
+    meta, fx = P.load_fixture(case)
+    c = P.CASES[case]
+    lc = c['cfg']()
+    st = P.init_state(case)
+    report = {}
+    for it in range(len(c['batch_seeds'])):
+        r0, r1 = out[0][it], out[1][it]
+        fin = r0['cap']['final']
+        for k in ('actor', 'critic', 'lstm', 'cnn'):
+            if k in fin:
+                assert torch.equal(fin[k], r1['final'][k]), (it, k)
+        for a, b in zip(fin['zf'], r1['final']['zf']):
+            assert torch.equal(a, b), it
+        assert r0['stats']['epochs_run'] == r1['stats']['epochs_run'] == meta['epochs_run'][it]
+        adv = np.concatenate([r0['adv'].numpy(), r1['adv'].numpy()])
+        ret = np.concatenate([r0['ret'].numpy(), r1['ret'].numpy()])
+        from tests.test_gpu_parity_pinned import check_fixture_state
+        check_fixture_state(meta, fx, st, it, fin, adv, ret, fin['zf'], report, tag='_dp')
+        batch = P.case_batch(case, it)
+        rec = P.recompute_stats(lc, c['D'], c['A'], c['pixel'], oracle_batch(batch), r0['cap'],
+                                adv, ret, r0['stats']['epochs_run'])
+        P.check_stats(r0['stats'], rec, report, tag=f'_dp@{it}')
+        assert r0['stats'] == r1['stats']
+    P.print_report(report)

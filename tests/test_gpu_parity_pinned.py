@@ -1,414 +1,303 @@
 """PPOLearner.learn() pinned at the configurations bench.py measures.
 
-Each case runs the HIP learner (fp32, GPU) and the CPU oracle
-(oracle/ppo_ref.py, surreal/learner/ppo.py:355-418,487-586) from identical
-initial weights on identical batches.  The oracle in fp64 is the "truth" of
-the reference algorithm.  Around it, an ENVELOPE of equally valid executions
-measures how far fp32 arithmetic may land from that truth:
-  * the oracle in fp32 (the reference's own precision) in 3 summation orders —
-    segments as given, reversed, and in a seeded random order (per-row math
-    identical, only the order of every batch reduction changes);
-  * the oracle in fp64 on inputs and initial weights carrying one fp32
-    rounding of relative noise (2^-24 N(0,1)), 6 seeds.
-For every tensor and statistic:
+Bars (tests/parity.py has the full statement):
+  * trajectory quantities — advantages as the epochs use them, raw advantages,
+    returns, post-step actor / critic / LSTM / CNN parameters, ZFilter sums,
+    first-step raw gradients — against the fp64 oracle within the fp32
+    ENVELOPE: max|GPU - fp64| <= 2 * max_variants max|variant - fp64| +
+    1e-6 * scale;
+  * every last_stats() entry by SELF-CONSISTENCY: recomputed in fp64 from the
+    GPU's own state at the point the reference computes it (ppo.py:194-331,
+    553-575) and required within 1e-5 (north_star) of its magnitude;
+  * the number of policy epochs run equal in every execution.
 
-    max|GPU - fp64| <= 2 * max_variants max|variant - fp64| + SLACK * scale
-
-with scale = max|fp64| (|fp64| for a scalar; for the explained variance
-max(|ev|, |1 - ev|), the magnitude of the variance ratio it is one minus),
-SLACK = 1e-6, and the number of
-policy epochs run equal in all executions.  A scalar statistic (last_stats())
-passes within 3x the envelope, or within the north_star's fixed fp32
-tolerance, 1e-5 relative: after 10 epochs a statistic is ONE draw from the
-chaotic spread, and 9 envelope draws bound a single draw less tightly than
-the max over the 1e5 entries of a parameter tensor does — so a statistic's
-envelope is pooled over the run's learn() calls.  (Measured at
-C3 adapt: the envelope of a post-training statistic is set by the perturbed
-fp64 executions; the fp32 summation orders sit 10-100x closer to fp64.)
-
-Why the envelope and not the fp32 oracle alone: the CPU fp32 oracle runs the
-same torch operations in the same order as the fp64 oracle, so its rounding
-errors are correlated with the truth and unusually small; any independently
-ordered fp32 implementation sits farther away.  The learner is a ReLU network
-trained by Adam: a pre-activation within rounding distance of 0 flips its mask
-(one row of 21504 changes a weight-gradient row by ~5e-5 of scale), and after
-several epochs m/sqrt(v) amplifies such differences.  Measured (tools/
-diag_epochs.py envelope, tools/diag_grads.py): at the --unit-test shape after
-10+10 epochs the fp32 oracle is 1.5e-6 of scale from fp64 while fp64 with one
-ulp of input noise is 4.9e-5 away; at C3 a single ReLU near-tie moves a
-first-step head gradient by 4e-5 of scale in either direction.  Where nothing
-amplifies (GAE, advantages, returns, ZFilter sums) the envelope is ~1e-7 and
-the bar is correspondingly tight.
-
-Compared: advantages exactly as the policy epochs use them (device-normalised)
-and raw, returns, every statistic of last_stats(), post-step actor / critic /
-LSTM / CNN parameters, ZFilter sums, and (test_pinned_c3_first_step_gradients)
-the raw gradients of the first policy and first value update at the full C3
-batch.
-
-Cases: C2 (B 64 x T 50, 64x64 MLP, clip and adapt, 2 learn() calls), C3 (the
-full 1024-segment batch the bench times: LSTM 100, heads 300x200, T 25,
-horizon 5, D 42, A 8, 10+10 epochs), C5 (C3 + the 84x84 camera stem at the
-128 segments per GPU the bench times, 10+10 epochs), a KL-early-stop case, and
-the host-numpy input path (experience lists -> _prefetcher_preprocess ->
-learn(), staged through the single-H2D arena) at the reference --unit-test
-shape (BASELINE configs[0]) and at C2.
+Cases: C2 (B 64 x T 50, 64x64 MLP, clip and adapt, 2 learn() calls), the MLP
+phase path at B = 1024, a KL early stop, stacked LSTMs, the host-numpy input
+path (experience lists -> _prefetcher_preprocess -> learn()) at the reference
+--unit-test shape (BASELINE configs[0]), at C2 and with pixels — their oracle
+envelopes run live; and the full-size cases, whose fp64 truth and envelope
+widths were computed in the build container (tests/golden/make_envelopes.py ->
+tests/golden/envelope_<case>.npz): C3 (the full 1024-segment batch bench.py
+times, adapt x 2 learns and clip), C5 (C3 + the 84x84 camera stem at 128
+segments, one GPU's share at N = 8), and the raw first-step policy / value
+gradients at C3 and at C5 widths.  tests/test_gpu_dp_pinned.py runs the same
+fixtures through two data-parallel ranks.
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
 
 from oracle import aggregator_ref as AR
-from oracle import ppo_ref as R
 from surreal_amd import synthetic
 from surreal_amd.aggregator import StagingArena
 from surreal_amd.config import PPO_DEFAULT_LEARNER_CONFIG, gym_env_config, pixel_env_config
 from surreal_amd.learner import PPOLearner
-from tests.helpers import (copy_weights_to_oracle, env_config, lstm_flat, oracle_batch,
-                           ppo_config, seq_flat)
+from tests import parity as P
+from tests.helpers import env_config, oracle_batch, ppo_config
 
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
-SLACK = 1e-6
-RTOL_STAT = 1e-5      # north_star: "within a stated fp32 tolerance (1e-5 relative)"
-STAT_FACTOR = 3.0     # scalar statistics: one draw each (see the module docstring)
-STAT_KEYS = ('_surr_loss', '_entropy', '_pol_kl', '_val_loss', '_avg_return_targ',
-             '_avg_behave_likelihood', '_avg_is_weight', '_ref_behave_diff', 'grad_norm_actor',
-             'grad_norm_critic', '_avg_log_sig', '_val_explained_var')
 
 
-def as_good_as_fp32(name, got, variants, r64, report, slack=SLACK, rtol=None, factor=2.0,
-                    scale=None):
-    """max|got - r64| <= factor * max_k max|variants[k] - r64| + slack * scale
-    (or, when rtol is given, <= rtol * scale: the north_star's fixed fp32
-    tolerance, used for scalar statistics); scale = max|r64| unless given."""
-    got, r64 = (np.asarray(t, dtype=np.float64).reshape(-1) for t in (got, r64))
-    variants = [np.asarray(t, dtype=np.float64).reshape(-1) for t in variants]
-    assert all(got.shape == r64.shape == r.shape for r in variants), (name, got.shape, r64.shape)
-    if scale is None:
-        scale = float(np.abs(r64).max()) if r64.size else 0.0
-    scale = max(scale, 1e-30)
-    e_gpu = float(np.abs(got - r64).max()) if r64.size else 0.0
-    e_env = max(float(np.abs(r - r64).max()) for r in variants) if r64.size else 0.0
-    ok = e_gpu <= factor * e_env + slack * scale or (rtol is not None and e_gpu <= rtol * scale)
-    report[name] = (e_gpu / scale, e_env / scale, ok)
-    if not ok:
-        report.setdefault('_fail', []).append(name)
+def _env(D, A, pixel):
+    return pixel_env_config(D, A, pixel) if pixel is not None else env_config(D, A)
 
 
-def print_report(report):
-    print('\n(GPU err / scale, envelope err / scale) vs the fp64 oracle:')
-    for k, v in report.items():
-        if k != '_fail':
-            print(f'  {k:28s} gpu {v[0]:.3e}  envelope {v[1]:.3e}  {"" if v[2] else "FAIL"}')
-    assert not report.get('_fail'), report.get('_fail')
+def copy_learner_state(src, dst):
+    """dst continues exactly as src would (parameters, filters, Adam state,
+    adaptive hyper-parameters): the twin of learn_capture_fused"""
+    with torch.no_grad():
+        for a, b in ((src.model, dst.model), (src.ref_target_model, dst.ref_target_model)):
+            b.actor.flat.copy_(a.actor.flat)
+            b.critic.flat.copy_(a.critic.flat)
+            b.stem_flat.copy_(a.stem_flat)
+            if src.use_z_filter:
+                b.z_filter.load_state_dict(a.z_filter.state_dict())
+        for k, v in src.optimizer_state().items():
+            dst.optimizer_state()[k].copy_(v)
+    dst.beta, dst.clip_epsilon = src.beta, src.clip_epsilon
+    dst._write_hyper()
 
 
-PERTURBED = ('obs', 'obs_next', 'actions', 'rewards', 'pds', 'onetime')
+def _is_fused(learner, batch):
+    if learner.if_rnn_policy or learner.if_pixel_input or learner.dp is not None:
+        return False
+    return learner.batch_size <= 256
 
 
-class Variant(object):
-    """One execution of the envelope: the fp32 oracle over a segment order, or
-    the fp64 oracle with one ulp of relative noise on its inputs / weights."""
-
-    def __init__(self, kind, key, learner, lc, D, A, pixel):
-        self.kind, self.key = kind, key
-        self.ref = R.PPOLearnerRef(lc, D, A, pixel=pixel,
-                                   dtype=torch.float32 if kind == 'order' else torch.float64)
-        copy_weights_to_oracle(learner, self.ref)
-        self.gen = torch.Generator().manual_seed(4242 + 17 * key if kind == 'ulp' else 0)
-        self.p = None
-        if kind == 'ulp':
-            with torch.no_grad():
-                for q in self.ref.model.parameters():
-                    q.copy_(self._noisy(q))
-            self.ref.ref_target_model.update_target_params(self.ref.model)
-
-    def _noisy(self, x):
-        # the reference's fp32 value (host float64 arrays are rounded as learn()
-        # rounds them), then one fp32 rounding of relative noise, held exactly
-        x = torch.as_tensor(x).to(torch.float32).double()
-        return x * (1 + 2.0 ** -24 * torch.randn(x.shape, generator=self.gen, dtype=torch.float64))
-
-    def learn(self, ob, seed):
-        B = np.asarray(ob['rewards']).shape[0]
-        if self.kind == 'order':
-            if self.key == 'given':
-                self.p = np.arange(B)
-            elif self.key == 'reversed':
-                self.p = np.arange(B)[::-1].copy()
-            else:                                   # ('shuffled', k)
-                self.p = np.random.RandomState(1000 * self.key[1] + seed).permutation(B)
-            b = {}
-            for k, v in ob.items():
-                if v is None:
-                    b[k] = None
-                elif isinstance(v, (list, tuple)):
-                    b[k] = [np.asarray(x)[self.p] for x in v]
-                else:
-                    b[k] = np.asarray(v)[self.p]
-        else:
-            b = {}
-            for k, v in ob.items():
-                if v is None or k not in PERTURBED:
-                    b[k] = v
-                elif isinstance(v, (list, tuple)):
-                    b[k] = [self._noisy(x) for x in v]
-                else:
-                    b[k] = self._noisy(v)
-        return self.ref.learn(b)
-
-    def per_segment(self, t):
-        """a per-segment output in the original segment order"""
-        t = np.asarray(t)
-        if self.kind != 'order':
-            return t
-        out = np.empty_like(t)
-        out[self.p] = t
-        return out
+def _used(learner):
+    """advantages / returns exactly as the epochs used them"""
+    b = learner._bufs
+    return b['adv_used'].cpu().numpy(), (b['ret_used'] if 'ret_used' in b else b['ret']).cpu().numpy()
 
 
-def _run_oracles(r64, vs, ob, seed):
-    """learn() of the fp64 oracle and every envelope variant on one batch
-    (sequential: each already uses torch's whole intra-op thread pool).
-    Returns (fp64 stats, [variant stats])."""
-    return r64.learn(ob), [v.learn(ob, seed) for v in vs]
+def _check_stats(lc, D, A, pixel, ob, cap, learner, report, tag):
+    s = learner.last_stats()
+    adv, ret = _used(learner)
+    rec = P.recompute_stats(lc, D, A, pixel, ob, cap, adv, ret, s['epochs_run'])
+    P.check_stats(s, rec, report, tag=tag)
 
 
-def _envelope(learner, lc, D, A, pixel, n_ulp=6, orders=('given', 'reversed', ('shuffled', 1))):
-    r64 = R.PPOLearnerRef(lc, D, A, pixel=pixel, dtype=torch.float64)
-    copy_weights_to_oracle(learner, r64)
-    vs = [Variant('order', k, learner, lc, D, A, pixel) for k in orders]
-    vs += [Variant('ulp', k, learner, lc, D, A, pixel) for k in range(1, n_ulp + 1)]
-    return r64, vs
-
-
-def _params(learner):
-    out = {'actor': learner.model.actor.flat, 'critic': learner.model.critic.flat}
-    if learner.if_rnn_policy:
-        out['lstm'] = learner.model.rnn_stem.flat
-    if learner.if_pixel_input:
-        out['cnn'] = learner.model.cnn_stem.flat
-    return {k: v.detach().cpu() for k, v in out.items()}
-
-
-def _ref_params(ref):
-    out = {'actor': ref.model.actor.flat(), 'critic': ref.model.critic.flat()}
-    if ref.rnn:
-        out['lstm'] = lstm_flat(ref.model.rnn_stem)
-    if ref.model.cnn_stem is not None:
-        out['cnn'] = seq_flat(ref.model.cnn_stem)
-    return out
-
-
+# ------------------------------------------------------------- live cases
 def _host_batch(learner, B, T, D, A, seed, rnn_hidden, pixel):
-    """experience list in the reference senders' format -> the learner's own
-    _prefetcher_preprocess (MultistepAggregatorWithInfo, host numpy)"""
     arr = AR.ppo_exp_arrays(B, T, D, A, seed, rnn_hidden=rnn_hidden, pixel=pixel)
     return learner._prefetcher_preprocess(AR.make_ppo_exp_list(arr))
 
 
-def pinned_run(lc, D, A, iters=1, pixel=None, seed=0, rnn_hidden=None, source='synthetic',
-               n_ulp=6, orders=('given', 'reversed', ('shuffled', 1))):
-    """source 'synthetic': device batches (surreal_amd.synthetic, the bench's
-    input); 'host': experience lists aggregated on the host and handed to
-    learn() as numpy (staged through the learner's single-H2D arena)."""
+def pinned_live(lc, D, A, iters=1, pixel=None, seed=0, rnn_hidden=None, source='synthetic',
+                n_ulp=6, orders=('given', 'reversed', ('shuffled', 1))):
+    """envelope computed here (small configurations).  source 'synthetic':
+    device batches; 'host': experience lists aggregated on the host and handed
+    to learn() as numpy (the single-H2D arena)."""
     B, T = lc.replay.batch_size, lc.algo.n_step
-    ec = pixel_env_config(D, A, pixel) if pixel is not None else env_config(D, A)
-    learner = PPOLearner(lc, ec, seed=seed + 7, device=DEV)
+    learner = PPOLearner(lc, _env(D, A, pixel), seed=seed + 7, device=DEV)
     learner.export_advantages = True
-    r64, vs = _envelope(learner, lc, D, A, pixel, n_ulp, orders)
+    st = P.gpu_state(learner)
+    st.pop('zf', None)
+    r64, vs = P.envelope(st, lc, D, A, pixel, n_ulp, orders)
     report = {}
-    stat_rec = {}
     for it in range(iters):
         if source == 'host':
             batch = _host_batch(learner, B, T, D, A, seed * 100 + it, rnn_hidden, pixel)
+            ob = oracle_batch(batch)
+            dev_batch = batch
         else:
             batch = synthetic.ppo_batch(B, T, D, A, seed=seed * 100 + it, rnn_hidden=rnn_hidden,
                                         pixel=pixel, rnn_layers=lc.algo.rnn.rnn_layer)
-        ob = oracle_batch(batch)
-        s64, svs = _run_oracles(r64, vs, ob, seed * 100 + it)
-        learner.learn(batch if source == 'host' else synthetic.to_device(batch, DEV))
+            ob = oracle_batch(batch)
+            dev_batch = synthetic.to_device(batch, DEV)
+        s64 = r64.learn(ob)
+        svs = [v.learn(ob, seed * 100 + it) for v in vs]
+        if _is_fused(learner, dev_batch):
+            def clone():
+                twin = PPOLearner(lc, _env(D, A, pixel), seed=seed + 7, device=DEV)
+                copy_learner_state(learner, twin)
+                return twin
+            cap = P.learn_capture_fused(learner, dev_batch, clone)
+        else:
+            cap = P.learn_capture(learner, dev_batch)
         s = learner.last_stats()
         runs = [s['epochs_run'], s64['epochs_run']] + [x['epochs_run'] for x in svs]
         assert len(set(runs)) == 1, (it, runs)
-        keys = STAT_KEYS + (('_clip_surr_loss',) if lc.algo.ppo_mode == 'clip' else ('_kl_loss_adapt',))
-        for k in keys:
-            # explained variance 1 - var(R - V)/var(R) (ppo.py:324-331) is a
-            # difference from 1: its error is that of the variance ratio, so its
-            # scale is the ratio's magnitude (near-zero values would otherwise be
-            # held to a relative bar they cannot carry)
-            sc = max(abs(s64[k]), abs(1.0 - s64[k])) if k == '_val_explained_var' else abs(s64[k])
-            sc = max(sc, 1e-30)
-            stat_rec.setdefault(k, []).append(
-                (it, abs(s[k] - s64[k]) / sc, max(abs(x[k] - s64[k]) for x in svs) / sc))
-        # advantages as the epochs use them, raw advantages, returns (per segment)
-        rnn = 'ret_used' in learner._bufs          # the phase path exports (B, E) windows
-        seg =lambda name: [v.per_segment(getattr(v.ref, name).numpy()) for v in vs]  # noqa: E731
-        as_good_as_fp32(f'adv@{it}', learner._bufs['adv_used'].cpu(), seg('last_adv'),
-                        r64.last_adv, report)
-        if rnn:
-            as_good_as_fp32(f'ret@{it}', learner._bufs['ret_used'].cpu(), seg('last_ret'),
-                            r64.last_ret, report)
-        else:
-            as_good_as_fp32(f'adv_raw@{it}', learner._bufs['adv_raw'].cpu(), seg('last_adv_raw'),
-                            r64.last_adv_raw, report)
-            as_good_as_fp32(f'ret@{it}', learner._bufs['ret'].cpu(), seg('last_ret'),
-                            r64.last_ret, report)
-        p, p64 = _params(learner), _ref_params(r64)
-        pvs = [_ref_params(v.ref) for v in vs]
-        for k in p:
-            as_good_as_fp32(f'{k}@{it}', p[k], [x[k] for x in pvs], p64[k], report)
+        seg = lambda name: [v.per_segment(getattr(v.ref, name).double().numpy()) for v in vs]  # noqa: E731
+        adv, ret = _used(learner)
+        w, sc = P.width(r64.last_adv.double().numpy(), seg('last_adv'))
+        P.check(f'adv@{it}', adv, r64.last_adv.double().numpy(), w, sc, report)
+        w, sc = P.width(r64.last_ret.double().numpy(), seg('last_ret'))
+        P.check(f'ret@{it}', ret, r64.last_ret.double().numpy(), w, sc, report)
+        if 'adv_raw' in learner._bufs and learner._bufs['adv_raw'].dim() == 1:
+            w, sc = P.width(r64.last_adv_raw.double().numpy(), seg('last_adv_raw'))
+            P.check(f'adv_raw@{it}', learner._bufs['adv_raw'].cpu(), r64.last_adv_raw.double().numpy(),
+                    w, sc, report)
+        p64 = P.oracle_params(r64)
+        pvs = [P.oracle_params(v.ref) for v in vs]
+        fin = cap['final']
+        for k in p64:
+            w, sc = P.width(p64[k], [x[k] for x in pvs])
+            P.check(f'{k}@{it}', fin[k], p64[k], w, sc, report)
         if learner.use_z_filter:
             zf, z64 = learner.model.z_filter, r64.model.z_filter
             for b in ('running_sum', 'running_sumsq'):
-                as_good_as_fp32(f'zf_{b}@{it}', getattr(zf, b).cpu(),
-                                [getattr(v.ref.model.z_filter, b) for v in vs], getattr(z64, b), report)
+                r = getattr(z64, b).double().numpy()
+                w, sc = P.width(r, [getattr(v.ref.model.z_filter, b).double().numpy() for v in vs])
+                P.check(f'zf_{b}@{it}', getattr(zf, b).cpu(), r, w, sc, report)
             assert float(zf.count.item()) == float(vs[0].ref.model.z_filter.count.item())
-    # scalar statistics: one draw each per learn(); their envelope is pooled over
-    # the run's learn() calls (the fp32 spread of a statistic is a property of
-    # the configuration — e.g. the post-update KL is quadratic in mean
-    # differences of ~1e-2 and moves ~1e-5..1e-4 relative per fp32 draw)
-    for k, rec in stat_rec.items():
-        env = max(r[2] for r in rec)
-        for it, e_gpu, e_env in rec:
-            ok = e_gpu <= STAT_FACTOR * env + SLACK or e_gpu <= RTOL_STAT
-            report[f'{k}@{it}'] = (e_gpu, env, ok)
-            if not ok:
-                report.setdefault('_fail', []).append(f'{k}@{it}')
-    print_report(report)
+        _check_stats(lc, D, A, pixel, ob, cap, learner, report, f'@{it}')
+    P.print_report(report)
     return report
 
 
 @pytest.mark.parametrize('mode', ['clip', 'adapt'])
 def test_pinned_c2(mode):
     # BASELINE configs[1]: HalfCheetah dims, 64x64 MLP, 64 segments x n_step 50
-    lc = ppo_config(B=64, T=50, mode=mode, use_z_filter=True)
-    pinned_run(lc, 17, 6, iters=2)
+    pinned_live(ppo_config(B=64, T=50, mode=mode, use_z_filter=True), 17, 6, iters=2)
 
 
 @pytest.mark.parametrize('mode', ['clip', 'adapt'])
 def test_pinned_mlp_large_batch_phase_path(mode):
     # low-dim MLP policy with B > 256: the multi-workgroup phase sequence
-    # (ppo.py:408-418 takes any batch; the single-CU kernels stop at 256)
-    lc = ppo_config(B=1024, T=50, mode=mode, use_z_filter=True)
-    pinned_run(lc, 17, 6, iters=2, seed=4)
+    pinned_live(ppo_config(B=1024, T=50, mode=mode, use_z_filter=True), 17, 6, iters=2, seed=4)
 
 
 def test_pinned_c2_early_stop():
     lc = ppo_config(B=64, T=20, mode='adapt', use_z_filter=True, lr=(3e-2, 1e-3),
                     kl_target=0.002)
-    pinned_run(lc, 17, 6, iters=2, seed=3)
-
-
-def _c3_cfg(mode, B):
-    return ppo_config(B=B, T=25, mode=mode, use_z_filter=True, hidden=(300, 200), lam=1.0,
-                      rnn=True, rnn_hidden=100, horizon=5)
-
-
-# the full-size cases run 10 CPU oracle executions of a 1024-segment learn():
-# minutes on the GPU box's CPU share, above the suite's per-test default
-@pytest.mark.timeout(900)
-def test_pinned_c3_full_batch_adapt():
-    # the exact workload bench.py --config c3 times (1024 segments, 10 + 10 epochs)
-    pinned_run(_c3_cfg('adapt', 1024), 42, 8, iters=2, rnn_hidden=100, seed=1)
-
-
-@pytest.mark.timeout(900)
-def test_pinned_c3_full_batch_clip():
-    pinned_run(_c3_cfg('clip', 1024), 42, 8, iters=1, rnn_hidden=100, seed=2)
-
-
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize('phase', ['policy', 'value'])
-def test_pinned_c3_first_step_gradients(phase):
-    """Raw gradients of the first policy update (epochs 1 + 0) or the first
-    value update (0 + 1) at the full C3 batch, before any Adam amplification:
-    the per-step accuracy of the forward, loss, head backward, BPTT and the
-    weight-gradient GEMMs over B*E = 21504 rows."""
-    lc = _c3_cfg('adapt', 1024)
-    lc.algo.consts.epoch_policy, lc.algo.consts.epoch_baseline = (1, 0) if phase == 'policy' else (0, 1)
-    D, A, B, T = 42, 8, 1024, 25
-    learner = PPOLearner(lc, env_config(D, A), seed=9, device=DEV)
-    r64, vs = _envelope(learner, lc, D, A, None)
-    batch = synthetic.ppo_batch(B, T, D, A, seed=1, rnn_hidden=100)
-    ob = oracle_batch(batch)
-    _run_oracles(r64, vs, ob, 1)
-    learner.learn(synthetic.to_device(batch, DEV))
-    xbuf = learner._bufs['rnn_xbuf'].cpu().double()
-    nAh, nL = learner.model.actor.flat.numel(), learner.model.rnn_stem.flat.numel()
-    nCh = learner.model.critic.flat.numel()
-
-    def grads(r):
-        m = r.model
-        f = lambda ps: torch.cat([q.grad.detach().reshape(-1) for q in ps]).double()  # noqa: E731
-        lstm = [m.rnn_stem.weight_ih_l0, m.rnn_stem.weight_hh_l0, m.rnn_stem.bias_ih_l0,
-                m.rnn_stem.bias_hh_l0]
-        if phase == 'policy':
-            return {'actor': f(list(m.actor.model.parameters()) + [m.actor.log_var]), 'lstm': f(lstm)}
-        return {'critic': f(m.critic.model.parameters()), 'lstm': f(lstm)}
-    if phase == 'policy':
-        gpu = {'actor': xbuf[:nAh], 'lstm': xbuf[nAh:nAh + nL]}
-    else:
-        gpu = {'critic': xbuf[nAh + nL:nAh + nL + nCh], 'lstm': xbuf[nAh + nL + nCh:nAh + nL + nCh + nL]}
-    g64, gvs = grads(r64), [grads(v.ref) for v in vs]
-    report = {}
-    for k in gpu:
-        as_good_as_fp32(f'grad_{k}', gpu[k], [g[k] for g in gvs], g64[k], report)
-    print_report(report)
-
-
-@pytest.mark.timeout(900)
-def test_pinned_c5_full_batch():
-    # bench.py --config c5: C3 + camera0 3x84x84 -> CNN stem (FC 256), 128 segments.
-    # The CPU conv oracle dominates (10 + 10 epochs of 84x84 frames per
-    # execution): a 5-execution envelope (2 summation orders + 3 perturbed fp64)
-    lc = _c3_cfg('adapt', 128)
-    lc.model.cnn_feature_dim = 256
-    # two learn() calls: the scalar-statistic envelope is pooled over both (at
-    # these widths 10 + 10 epochs move parameters ~4e-2 of scale between any
-    # two fp32 executions, and the post-update KL is one draw from that spread)
-    pinned_run(lc, 42, 8, iters=2, pixel=(3, 84, 84), rnn_hidden=100, seed=4, n_ulp=3,
-               orders=('given', 'reversed'))
+    rep = pinned_live(lc, 17, 6, iters=2, seed=3)
+    assert rep
 
 
 @pytest.mark.parametrize('layers,Hd', [(2, 100), (3, 24)])
 def test_pinned_stacked_lstm(layers, Hd):
-    # nn.LSTM(num_layers = rnn_layer) (ppo_net.py:146-149): layer 0 on the fused
-    # input projection, layers >= 1 on the x-projection GEMM + recurrence, BPTT
-    # layer by layer with the inter-layer input gradient dgates W_ih
+    # nn.LSTM(num_layers = rnn_layer) (ppo_net.py:146-149)
     lc = ppo_config(B=64, T=10, mode='adapt', use_z_filter=True, hidden=(64, 64), lam=1.0,
                     epochs=(3, 3), rnn=True, rnn_hidden=Hd, horizon=3, rnn_layer=layers)
-    # a cheap case: 16 perturbed executions make the envelope a better estimate
-    # of the fp32 spread of the post-update KL (quadratic in mean differences
-    # of ~1e-2, so one fp32 draw moves it ~1e-5..1e-4 relative)
-    pinned_run(lc, 42, 8, iters=2, rnn_hidden=Hd, seed=8 + layers, n_ulp=16)
+    pinned_live(lc, 42, 8, iters=2, rnn_hidden=Hd, seed=8 + layers, n_ulp=16)
 
 
-# ------------------------------------------------ host numpy input path (a2/a18)
 def test_host_path_reference_unit_test_shape():
     # BASELINE configs[0]: the reference's --unit-test settings
-    # (main/ppo_configs.py:225-227: batch 2) on the default PPO config (LSTM 100,
-    # horizon 5, n_step 25, heads 300x200, adapt, lr 1e-4), HalfCheetah dims
-    import copy
+    # (main/ppo_configs.py:225-227: batch 2) on the default PPO config
     lc = copy.deepcopy(PPO_DEFAULT_LEARNER_CONFIG)
     lc.replay.batch_size = 2
     lc.replay.sampling_start_size = 2
-    pinned_run(lc, 17, 6, iters=3, rnn_hidden=100, seed=5, source='host')
+    pinned_live(lc, 17, 6, iters=3, rnn_hidden=100, seed=5, source='host')
 
 
 @pytest.mark.parametrize('mode', ['clip', 'adapt'])
 def test_host_path_c2(mode):
-    lc = ppo_config(B=64, T=50, mode=mode, use_z_filter=True)
-    pinned_run(lc, 17, 6, iters=2, seed=6, source='host')
+    pinned_live(ppo_config(B=64, T=50, mode=mode, use_z_filter=True), 17, 6, iters=2, seed=6,
+                source='host')
 
 
 def test_host_path_pixel_lstm():
     lc = ppo_config(B=3, T=6, mode='adapt', use_z_filter=True, hidden=(16, 16), lam=1.0,
                     epochs=(2, 2), rnn=True, rnn_hidden=12, horizon=2, cnn_feat=16)
-    pinned_run(lc, 5, 2, iters=2, pixel=(3, 84, 84), rnn_hidden=12, seed=7, source='host')
+    pinned_live(lc, 5, 2, iters=2, pixel=(3, 84, 84), rnn_hidden=12, seed=7, source='host')
 
 
+# --------------------------------------------------------- fixture cases
+def fixture_learner(case, dp=None):
+    meta, fx = P.load_fixture(case)
+    c = P.CASES[case]
+    lc = c['cfg']()
+    st = P.init_state(case)
+    assert P.digest([st[k] for k in sorted(st)]) == meta['init_digest'], 'initial weights differ'
+    if dp is not None:
+        lc.replay.batch_size //= dp.world_size
+    learner = PPOLearner(lc, _env(c['D'], c['A'], c['pixel']), seed=0, device=DEV, dp=dp)
+    P.load_state_into_learner(learner, st)
+    learner.export_advantages = True
+    return meta, fx, c, st, learner
+
+
+def check_fixture_state(meta, fx, st, it, fin, adv, ret, zf, report, tag=''):
+    for name in ('adv', 'ret'):
+        r, w, sc = P.truth(meta, fx, name, it, st)
+        P.check(f'{name}{tag}@{it}', adv if name == 'adv' else ret, r, w, sc, report)
+    for k in ('actor', 'critic', 'lstm', 'cnn'):
+        if f'{k}@{it}' in fx:
+            r, w, sc = P.truth(meta, fx, k, it, st)
+            P.check(f'{k}{tag}@{it}', fin[k], r, w, sc, report)
+    for b, v in zip(('running_sum', 'running_sumsq'), zf[:2]):
+        r, w, sc = P.truth(meta, fx, f'zf_{b}', it, st)
+        P.check(f'zf_{b}{tag}@{it}', v, r, w, sc, report)
+
+
+def pinned_fixture(case):
+    meta, fx, c, st, learner = fixture_learner(case)
+    lc = learner.learner_config
+    report = {}
+    for it in range(len(c['batch_seeds'])):
+        batch = P.case_batch(case, it)
+        assert P.batch_digest(batch) == meta['batch_digest'][it], 'synthetic batch differs'
+        cap = P.learn_capture(learner, synthetic.to_device(batch, DEV))
+        s = learner.last_stats()
+        assert s['epochs_run'] == meta['epochs_run'][it], (s['epochs_run'], meta['epochs_run'][it])
+        adv, ret = _used(learner)
+        check_fixture_state(meta, fx, st, it, cap['final'], adv, ret, cap['final']['zf'], report)
+        _check_stats(lc, c['D'], c['A'], c['pixel'], oracle_batch(batch), cap, learner, report,
+                     f'@{it}')
+    P.print_report(report)
+
+
+@pytest.mark.timeout(300)
+def test_pinned_c3_full_batch_adapt():
+    # the exact workload bench.py --config c3 times (1024 segments, 10 + 10 epochs)
+    pinned_fixture('c3_adapt')
+
+
+@pytest.mark.timeout(300)
+def test_pinned_c3_full_batch_clip():
+    pinned_fixture('c3_clip')
+
+
+@pytest.mark.timeout(300)
+def test_pinned_c5_full_batch():
+    # bench.py --config c5 --local-segments 128: C3 + camera0 3x84x84 -> CNN (FC 256)
+    pinned_fixture('c5')
+
+
+def gpu_first_step_grads(learner, phase):
+    """the raw gradient a backward phase left in the exchange buffer:
+    [actor head | lstm | cnn] then [critic head | lstm | cnn]"""
+    xbuf = learner._bufs['rnn_xbuf'].cpu().double().numpy()
+    m = learner.model
+    nAh, nCh = m.actor.flat.numel(), m.critic.flat.numel()
+    nL = m.rnn_stem.flat.numel() if learner.if_rnn_policy else 0
+    nCnn = m.cnn_stem.flat.numel() if learner.if_pixel_input else 0
+    off, head = (0, 'actor') if phase == 'policy' else (nAh + nL + nCnn, 'critic')
+    nh = nAh if phase == 'policy' else nCh
+    out = {head: xbuf[off:off + nh]}
+    if nL:
+        out['lstm'] = xbuf[off + nh:off + nh + nL]
+    if nCnn:
+        out['cnn'] = xbuf[off + nh + nL:off + nh + nL + nCnn]
+    return out
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('case', ['c3_grad_policy', 'c3_grad_value', 'c5_grad_policy',
+                                  'c5_grad_value'])
+def test_pinned_first_step_gradients(case):
+    """Raw gradients of the first policy update (epochs 1 + 0) or the first
+    value update (0 + 1) before any Adam amplification: the per-step accuracy
+    of the forward, loss, head backward, BPTT, CNN backward and the weight-
+    gradient GEMMs, at the full C3 batch (21504 rows) and at C5 widths."""
+    meta, fx, c, st, learner = fixture_learner(case)
+    batch = P.case_batch(case, 0)
+    assert P.batch_digest(batch) == meta['batch_digest'][0]
+    learner.learn(synthetic.to_device(batch, DEV))
+    got = gpu_first_step_grads(learner, c['grad'])
+    report = {}
+    for k, v in got.items():
+        r, w, sc = P.truth(meta, fx, f'grad_{k}', 0, st)
+        P.check(f'grad_{k}', v, r, w, sc, report)
+    P.print_report(report)
+
+
+# ------------------------------------------------------ staging (a2 / f2)
 def test_staging_arena_single_copy_bit_exact():
     """The arena's device tensors equal torch.as_tensor(x, float32) of every
     aggregated array (uint8 camera frames unchanged), over several batches
@@ -436,3 +325,4 @@ def test_staging_arena_single_copy_bit_exact():
         for k in ('obs', 'obs_next'):
             d, h = dev[k]['pixel']['camera0'], host[k]['pixel']['camera0']
             assert d.dtype == torch.uint8 and torch.equal(d.cpu(), torch.as_tensor(h))
+        np.testing.assert_equal(dev['dones'].cpu().numpy(), np.asarray(host['dones'], np.float32))
