@@ -852,6 +852,315 @@ lstm_bwd_r4_kernel(LstmBwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// VALU variants for small local batches (strong scaling: a rank of the N = 8
+// C3 job holds 128 segments).  The MFMA forms above waste the recurrence's
+// matrix pipe at few segments per workgroup (v_mfma_f32_4x4x1 always computes
+// 4 rows) and a step's latency does not fall with the batch.  Here a
+// workgroup owns R <= 4 segments and thread (u, q) = 4u + q owns ONE gate
+// column g = q*H + u (gate q of hidden unit u) with its W_hh row (and, fused,
+// its W_ih row) in registers:
+//   pre_g   = x_t W_ih[g] + b_ih[g] + h_{t-1} W_hh[g] + b_hh[g]   (FMA chains,
+//             h_{t-1} broadcast from LDS as 16-byte reads)
+//   a_g     = sigmoid / tanh (gate g lives in lane 4u + q)
+//   i,f,g,o of unit u gathered inside the lane quad with DPP quad broadcasts
+//   c, h    computed redundantly by the quad's 4 lanes (identical values)
+// so a step is one matvec, one quad exchange and ONE barrier (h_t published
+// to LDS).  With R = 1 the 128-segment batch fills 128 CUs and a step is ~100
+// dependent-free FMAs per thread.  The x part of step t+1 (independent of
+// h_t) is formed after h_t is published, in the barrier's shadow.
+// Backward: thread (u, q) holds column u of W_hh restricted to gate q's rows,
+// dh_rec[u] = sum_q sum_j dgates[q*H + j] W_hh[q*H + j][u] is a per-lane
+// partial over gate q plus a fixed-order quad sum.
+template <int K>
+__device__ __forceinline__ float quad_bcast(float v) {      // lane K of each quad
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), K * 0x55, 0xF, 0xF, false));
+}
+
+constexpr int kVT = 512;      // threads of the VALU recurrence workgroups (4H <= 512)
+
+template <int R, int KP, int KX>
+__global__ void __launch_bounds__(kVT)
+lstm_fwd_v_kernel(LstmFwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  constexpr int KXS = KX > 0 ? KX : 4;
+  __shared__ __attribute__((aligned(16))) float hS[2][R * KP];
+  __shared__ __attribute__((aligned(16))) float xS[3][R * KXS];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int tid = threadIdx.x, u = tid >> 2, q = tid & 3;
+  const bool act = u < H;
+  const int uc = act ? u : H - 1;
+  const int g = q * H + uc;
+  const int r0 = blockIdx.x * R;
+  const int64_t BH = (int64_t)B * H;
+  float w[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const float x = a.w_hh[(int64_t)g * H + (k < H ? k : H - 1)];
+    w[k] = k < H ? x : 0.f;
+  }
+  float bh = a.b_hh[g];
+  float wx[KXS];
+  if constexpr (KX > 0) {
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+      const float x = a.w_ih[(int64_t)g * a.din + (k < a.din ? k : a.din - 1)];
+      wx[k] = k < a.din ? x : 0.f;
+    }
+    bh += a.b_ih[g];
+  }
+  int bseg[R];
+  bool okr[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    okr[r] = act && r0 + r < B;
+    bseg[r] = r0 + r < B ? r0 + r : B - 1;
+  }
+  // x staging (KX > 0): thread e < R*KX owns (row e / KX, k e % KX) of x_t
+  const int xr = tid / KXS, xk = tid - (tid / KXS) * KXS;
+  const bool xown = KX > 0 && tid < R * KXS;
+  const int64_t xoff0 = (int64_t)min(r0 + xr, B - 1) * a.ldx + min(xk, a.din > 0 ? a.din - 1 : 0);
+  const bool xval = xk < a.din;
+  auto xload = [&](int t) -> float {
+    const float v = a.x[(int64_t)t * B * a.ldx + xoff0];
+    return xval ? v : 0.f;
+  };
+  float xnext = 0.f;
+  if constexpr (KX > 0) {
+    if (xown && a.S > 0) xS[0][xr * KXS + xk] = xload(0);
+    if (xown && a.S > 1) xS[1][xr * KXS + xk] = xload(1);
+    if (xown && a.S > 2) xnext = xload(2);
+  }
+  float creg[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    creg[r] = a.c0[(int64_t)bseg[r] * H + uc];
+    if (okr[r] && q == 0 && a.cbuf) a.cbuf[(int64_t)bseg[r] * H + u] = creg[r];
+  }
+  for (int e = tid; e < R * KP; e += blockDim.x) {
+    const int r = e / KP, k = e - r * KP;
+    const bool ok = k < H && r0 + r < B;
+    const float v = ok ? a.h0[(int64_t)(r0 + r) * H + k] : 0.f;
+    hS[0][e] = v;
+    hS[1][e] = 0.f;
+    if (ok) a.hbuf[(int64_t)(r0 + r) * H + k] = v;          // hbuf[0] = h0
+  }
+  __syncthreads();
+  // x part of step t (+ the combined bias)
+  float xacc[R];
+  auto x_part = [&](int t, int xb) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (KX > 0) {
+        const float4* xp = reinterpret_cast<const float4*>(xS[xb] + r * KXS);
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int k4 = 0; k4 < KX / 4; ++k4) {
+          const float4 v = xp[k4];
+          s0 = fmaf(v.x, wx[4 * k4], s0);
+          s1 = fmaf(v.y, wx[4 * k4 + 1], s1);
+          s2 = fmaf(v.z, wx[4 * k4 + 2], s2);
+          s3 = fmaf(v.w, wx[4 * k4 + 3], s3);
+          if (k4 & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        xacc[r] = (s0 + s1) + (s2 + s3);
+      } else {
+        xacc[r] = a.xproj[((int64_t)t * B + bseg[r]) * G4 + g];
+      }
+    }
+  };
+  if (a.S > 0) x_part(0, 0);
+  int xb = 1;                                    // x ring slot of step t+1
+  for (int t = 0; t < a.S; ++t) {
+    const float* hp = hS[t & 1];
+    float* hn = hS[(t + 1) & 1];
+    // one segment after the other (a sched_barrier between them): interleaving
+    // the R matvecs keeps R x (h reads + accumulators) live next to the
+    // KP + KX weight registers and spills from R = 2
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+      // chunks of 8 k: without the sched_barrier the compiler hoists every
+      // h_{t-1} LDS read of the step ahead of the FMAs
+#pragma unroll
+      for (int k4 = 0; k4 < KP / 4; ++k4) {
+        const float4 hv = *reinterpret_cast<const float4*>(hp + r * KP + 4 * k4);
+        acc0 = fmaf(hv.x, w[4 * k4], acc0);
+        acc1 = fmaf(hv.y, w[4 * k4 + 1], acc1);
+        acc2 = fmaf(hv.z, w[4 * k4 + 2], acc2);
+        acc3 = fmaf(hv.w, w[4 * k4 + 3], acc3);
+        if (k4 & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      const float pre = xacc[r] + (((acc0 + acc1) + (acc2 + acc3)) + bh);
+      const float av = q == 2 ? ftanh(pre) : sigm(pre);
+      const float ig = quad_bcast<0>(av), fg = quad_bcast<1>(av);
+      const float cg = quad_bcast<2>(av), og = quad_bcast<3>(av);
+      const float c = fg * creg[r] + ig * cg;
+      const float h = og * ftanh(c);
+      creg[r] = c;
+      if (okr[r]) {
+        const int b = bseg[r];
+        if (q == 0) {
+          hn[r * KP + u] = h;
+          a.hbuf[(int64_t)(t + 1) * BH + (int64_t)b * H + u] = h;
+          if (a.cbuf) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)b * H + u] = c;
+        }
+        if (a.gates) a.gates[((int64_t)t * B + b) * G4 + g] = av;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t + 1 < a.S) x_part(t + 1, xb);
+    if constexpr (KX > 0) {   // x_{t+2} into the ring slot x_{t-1} used, x_{t+3} in flight
+      const int wb = xb == 2 ? 0 : xb + 1;
+      if (xown && t + 2 < a.S) xS[wb][xr * KXS + xk] = xnext;
+      if (xown && t + 3 < a.S) xnext = xload(t + 3);
+    }
+    xb = xb == 2 ? 0 : xb + 1;
+    __syncthreads();
+  }
+}
+
+template <int R, int KP>
+__global__ void __launch_bounds__(kVT)
+lstm_bwd_v_kernel(LstmBwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  __shared__ __attribute__((aligned(16))) float dG[2][R * 4 * KP];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int tid = threadIdx.x, u = tid >> 2, q = tid & 3;
+  const bool act = u < H;
+  const int uc = act ? u : H - 1;
+  const int g = q * H + uc;
+  const int r0 = blockIdx.x * R;
+  const int64_t BH = (int64_t)B * H;
+  for (int e = tid; e < 2 * R * 4 * KP; e += blockDim.x) (&dG[0][0])[e] = 0.f;
+  float w[KP];                                   // W_hh[q*H + j][u]
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    const float x = a.w_hh[(int64_t)(q * H + (j < H ? j : H - 1)) * H + uc];
+    w[j] = j < H ? x : 0.f;
+  }
+  int bseg[R];
+  bool okr[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    okr[r] = act && r0 + r < B;
+    bseg[r] = r0 + r < B ? r0 + r : B - 1;
+  }
+  float gq[R], ct[R], ctm[R], dho[R], dcreg[R], dhr[R];
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t b = bseg[r];
+      gq[r] = a.gates[((int64_t)t * B + b) * G4 + g];
+      ct[r] = a.cbuf[(int64_t)(t + 1) * BH + b * H + uc];
+      ctm[r] = a.cbuf[(int64_t)t * BH + b * H + uc];
+      dho[r] = a.dh[(int64_t)t * BH + b * H + uc];
+    }
+  };
+#pragma unroll
+  for (int r = 0; r < R; ++r) dcreg[r] = dhr[r] = 0.f;
+  if (a.S > 0) fetch(a.S - 1);
+  __syncthreads();
+  for (int t = a.S - 1; t >= 0; --t) {
+    float* dgw = dG[t & 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float ig = quad_bcast<0>(gq[r]), fg = quad_bcast<1>(gq[r]);
+      const float cg = quad_bcast<2>(gq[r]), og = quad_bcast<3>(gq[r]);
+      const float dh = dho[r] + dhr[r];
+      const float tc = ftanh(ct[r]);
+      const float dc = dh * og * (1.f - tc * tc) + dcreg[r];
+      const float d_o = (dh * tc) * (og * (1.f - og));
+      const float d_i = (dc * cg) * (ig * (1.f - ig));
+      const float d_g = (dc * ig) * (1.f - cg * cg);
+      const float d_f = (dc * ctm[r]) * (fg * (1.f - fg));
+      dcreg[r] = okr[r] ? dc * fg : 0.f;
+      float dq = q == 0 ? d_i : q == 1 ? d_f : q == 2 ? d_g : d_o;
+      dq = okr[r] ? dq : 0.f;
+      if (act) dgw[r * 4 * KP + q * KP + u] = dq;
+      if (okr[r]) a.dgates[((int64_t)t * B + bseg[r]) * G4 + g] = dq;
+    }
+    if (t > 0) fetch(t - 1);
+    __syncthreads();
+    if (t == 0) break;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float4* dp = reinterpret_cast<const float4*>(dgw + r * 4 * KP + q * KP);
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+      for (int j4 = 0; j4 < KP / 4; ++j4) {
+        const float4 v = dp[j4];
+        s0 = fmaf(v.x, w[4 * j4], s0);
+        s1 = fmaf(v.y, w[4 * j4 + 1], s1);
+        s2 = fmaf(v.z, w[4 * j4 + 2], s2);
+        s3 = fmaf(v.w, w[4 * j4 + 3], s3);
+        if (j4 & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      const float p = (s0 + s1) + (s2 + s3);
+      // fixed-order quad sum: every lane of the quad gets the same dh_rec
+      dhr[r] = (quad_bcast<0>(p) + quad_bcast<1>(p)) + (quad_bcast<2>(p) + quad_bcast<3>(p));
+    }
+  }
+}
+
+// VALU recurrence selection: SMI_LSTM_VALU = 0 (never), 1 (always when the
+// shape fits), unset: when the batch leaves at least one segment group per CU
+// idle under the MFMA forms (B <= 2 x CUs, i.e. R <= 2)
+static int lstm_valu_mode() {
+  static int m = -2;
+  if (m == -2) {
+    const char* e = getenv("SMI_LSTM_VALU");
+    m = e ? atoi(e) : -1;
+  }
+  return m;
+}
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  return cus;
+}
+// segments per workgroup of the VALU forms, 0 = use the MFMA forms
+static int lstm_valu_r(int B, int H) {
+  if (H < 1 || H > 128) return 0;
+  const int m = lstm_valu_mode();
+  if (m == 0) return 0;
+  const int cus = device_cus();
+  int R = (B + cus - 1) / cus;
+  if (R < 1) R = 1;
+  if (R == 3) R = 4;
+  if (R > 4) return 0;
+  if (m < 0 && R > 2) return 0;
+  return R;
+}
+
+template <int R, int KX>
+static void fwd_v_dispatch_kp(const LstmFwdArgs& a, hipStream_t st) {
+  const dim3 grid((a.B + R - 1) / R), blk((4 * a.H + 63) & ~63);
+  if (a.H <= 64) hipLaunchKernelGGL((lstm_fwd_v_kernel<R, 64, KX>), grid, blk, 0, st, a);
+  else if (a.H <= 104) hipLaunchKernelGGL((lstm_fwd_v_kernel<R, 104, KX>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((lstm_fwd_v_kernel<R, 128, KX>), grid, blk, 0, st, a);
+}
+// x W_ih^T fused only at R = 1 (its W_ih row joins the W_hh row in registers:
+// at R >= 2 the two segments' operands no longer fit next to them); R >= 2
+// reads the xproj GEMM's output (launch_lstm_fwd_x returns SMI_E_NOFIT)
+static void fwd_v_dispatch(const LstmFwdArgs& a, int R, hipStream_t st) {
+  if (R == 1) fwd_v_dispatch_kp<1, 0>(a, st);
+  else if (R == 2) fwd_v_dispatch_kp<2, 0>(a, st);
+  else fwd_v_dispatch_kp<4, 0>(a, st);
+}
+template <int R>
+static void bwd_v_dispatch_kp(const LstmBwdArgs& a, hipStream_t st) {
+  const dim3 grid((a.B + R - 1) / R), blk((4 * a.H + 63) & ~63);
+  if (a.H <= 64) hipLaunchKernelGGL((lstm_bwd_v_kernel<R, 64>), grid, blk, 0, st, a);
+  else if (a.H <= 104) hipLaunchKernelGGL((lstm_bwd_v_kernel<R, 104>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((lstm_bwd_v_kernel<R, 128>), grid, blk, 0, st, a);
+}
+
 static int use_r4() {
   static int u = -1;
   if (u < 0) {
@@ -884,6 +1193,10 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
   // algorithmic flops: the recurrent GEMM h W_hh^T of every step
   struct End { int s; hipStream_t st; double f;
                ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{kslot, st, 8.0 * B * H * (double)H * S};
+  if (const int R = lstm_valu_r(B, H)) {
+    fwd_v_dispatch(a, R, st);
+    return check_launch("lstm_fwd_v_kernel");
+  }
   if (H <= 128 && use_r4()) {
     const dim3 g4((B + LR4 - 1) / LR4);
     if (H <= 32) hipLaunchKernelGGL((lstm_fwd_r4_kernel<32, 0>), g4, dim3(kWG8), 0, st, a);
@@ -928,12 +1241,19 @@ int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, c
                       hipStream_t st, const int* skip) {
   if (!use_r4() || din < 1 || din > 64 || H < 1 || H > 104) return SMI_E_NOFIT;
   if (B <= 0 || S < 0) return SMI_OK;
+  const int R = lstm_valu_r(B, H);
+  if (R > 1) return SMI_E_NOFIT;                 // xproj GEMM + the VALU recurrence
   LstmFwdArgs a{nullptr, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates, skip,
                 x, ldx, din, w_ih, b_ih};
   const int kslot = ktime_begin(st);
   struct End { int s; hipStream_t st; double f;
                ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{
       kslot, st, 8.0 * B * H * (double)(H + din) * S};
+  if (R == 1) {
+    if (din <= 48) fwd_v_dispatch_kp<1, 48>(a, st);
+    else fwd_v_dispatch_kp<1, 64>(a, st);
+    return check_launch("lstm_fwd_v_kernel");
+  }
   const dim3 g4((B + LR4 - 1) / LR4);
   if (din <= 48) {
     if (H <= 64) hipLaunchKernelGGL((lstm_fwd_r4_kernel<64, 48>), g4, dim3(kWG8), 0, st, a);
@@ -954,6 +1274,12 @@ int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, cons
   struct End { int s; hipStream_t st; double f;
                ~End() { ktime_end(s, KT_LSTM_BWD, f, st); } } end_{kslot, st,
                                                                  8.0 * B * H * (double)H * (S - 1)};
+  if (const int R = lstm_valu_r(B, H)) {
+    if (R == 1) bwd_v_dispatch_kp<1>(a, st);
+    else if (R == 2) bwd_v_dispatch_kp<2>(a, st);
+    else bwd_v_dispatch_kp<4>(a, st);
+    return check_launch("lstm_bwd_v_kernel");
+  }
   if (H <= 128 && use_r4()) {
     const int nu = (H + 63) / 64, wpg = 8 / nu;
     const int kw = (4 * H + wpg - 1) / wpg;

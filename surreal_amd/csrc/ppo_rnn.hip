@@ -88,6 +88,8 @@ __host__ __device__ inline RnnDims rnn_dims(int B, int T, int Hz, int D, int H, 
 // scratch carve (floats, 64-float aligned regions)
 struct RnnScratch {
   float *Xz, *Xr, *xproj, *hbuf, *cbuf, *gates, *HA1, *HA2, *OUT, *dOUT, *dH1, *dH2, *dh, *dgates;
+  // the PREP phase's own copies (it may run on a second stream beside GAE)
+  float *xprojR, *hbufR, *HA1R, *HA2R, *A2R;
   float *values, *adv, *ret, *refmu, *lvpart;
   float *A1, *A2, *dA2, *dF, *cpart;        // pixel stem (empty without one)
   double *part, *gaepart;
@@ -136,6 +138,11 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   const bool px = d.F > 0;
   s.A1 = take(px ? d.NE * 16 * d.G.P1 : 0);
   s.A2 = take(px ? d.NG * d.G.flat : 0);
+  s.xprojR = take(d.NE * d.G4);
+  s.hbufR = take((int64_t)d.L * (d.S1 + 1) * d.B * d.H);
+  s.HA1R = take(d.NE * hmax1);
+  s.HA2R = take(d.NE * hmax2);
+  s.A2R = take(px ? d.NE * d.G.flat : 0);
   s.dA2 = take(px ? d.NE * d.G.flat : 0);
   s.dF = take(px ? d.NE * d.F : 0);
   s.cpart = take(px ? (int64_t)cnn_bwd_grid(d.NE) * d.G.nconv : 0);
@@ -982,26 +989,29 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       return check_launch("set_count_kernel");
     }
     case SMI_RNN_PH_PREP: {
-      const float* X = s.Xz;
-      if (a.use_zf || d.F > 0) {   // the reference model's own z-filter / CNN stem
-        hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NE * d.D)), dim3(kWG), zlds, st, a.obs,
-                           a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
-                           a.rzf_count, a.zf_eps, s.Xr, d.ldx);
-        RC(check_launch("zf_tmajor_kernel"));
-        RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, s, st, nullptr));
-        X = s.Xr;
-      }
-      if (a.adv_out || a.ret_out) {
+      // ref_pol (ppo.py:539): the reference model's forward over obs_iter.
+      // Independent of GAE: it reads only the batch and the reference
+      // parameters and writes only its own buffers (sp) and refmu, so the host
+      // may run it on a second stream beside GAE (with its own smi_context).
+      RnnScratch sp = s;
+      sp.xproj = s.xprojR; sp.hbuf = s.hbufR; sp.HA1 = s.HA1R; sp.HA2 = s.HA2R; sp.A2 = s.A2R;
+      const float* X = s.Xr;
+      hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NE * d.D)), dim3(kWG), zlds, st, a.obs,
+                         a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
+                         a.rzf_count, a.zf_eps, s.Xr, d.ldx);
+      RC(check_launch("zf_tmajor_kernel"));
+      RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, sp, st, nullptr));
+      if (d.H > 0) RC(lstm_forward(d, a.ref_lstm, X, d.E, a.h0, a.c0, sp, false, st, nullptr));
+      const Head ref{a.ref_actor, d.LA, d.Hin, d.h1, d.h2, d.A, 1};
+      return head_fwd(ref, head_in(d, sp, X), d.Hld, d.NE, sp.HA1, sp.HA2, s.refmu, st,
+                      nullptr);
+    }
+    case SMI_RNN_PH_POLICY_FWD: {
+      if (e == 0 && (a.adv_out || a.ret_out)) {
         hipLaunchKernelGGL(adv_export_kernel, dim3(grid_of(d.NE)), dim3(kWG), 0, st,
                            pol_rows(a, d, s), a.adv_out, a.ret_out);
         RC(check_launch("adv_export_kernel"));
       }
-      if (d.H > 0) RC(lstm_forward(d, a.ref_lstm, X, d.E, a.h0, a.c0, s, false, st, nullptr));
-      const Head ref{a.ref_actor, d.LA, d.Hin, d.h1, d.h2, d.A, 1};
-      return head_fwd(ref, head_in(d, s, X), d.Hld, d.NE, s.HA1, s.HA2, s.refmu, st,
-                      nullptr);
-    }
-    case SMI_RNN_PH_POLICY_FWD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, stop));
       if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, stop));
       RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop));

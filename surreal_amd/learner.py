@@ -17,6 +17,7 @@ Construction needs no tensorplex/loggerplex/ZMQ: metrics go to an injectable
 `metrics` callable and parameters to an injectable `publisher` callable.
 """
 import math
+import os
 import time
 
 import numpy as np
@@ -250,6 +251,16 @@ class PPOLearner(object):
         # optional export of the advantages as the policy epochs use them (and
         # the RNN window returns) into self._bufs['adv_used'] / ['ret_used']
         self.export_advantages = False
+        # LSTM / pixel phases: ref_pol on a second stream beside the GAE pass
+        self.prep_side_stream = os.environ.get('SMI_PREP_SIDE', '1') != '0'
+        self._side = None
+        self._ctx_side = None
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+            self._ctx_side = L.Context(self.device)
+        return self._side
 
     def _replicated_state(self):
         """parameters and filter buffers every data-parallel replica must share"""
@@ -573,14 +584,30 @@ class PPOLearner(object):
         a.ret_out = self._buf('ret_used', (B, E)).data_ptr() if self.export_advantages else None
         self._rnn_args = a
 
-        def ph(p, e=0):
+        def ph(p, e=0, stream=st):
             with self._ev(_RNN_PHASE_NAMES[p]):
-                L.check(lib.smi_ppo_rnn_phase(a, p, e, st), 'smi_ppo_rnn_phase')
+                L.check(lib.smi_ppo_rnn_phase(a, p, e, stream), 'smi_ppo_rnn_phase')
 
+        # ref_pol (PREP, ppo.py:539) depends only on the batch and the reference
+        # parameters: it runs on a second stream with its own workspace beside
+        # the GAE phase's critic pass (two independent recurrences; at small
+        # local batches each fills a fraction of the CUs), joined before the
+        # first policy forward
+        side = self._side_stream() if self.prep_side_stream else None
+        if side is not None:
+            main = torch.cuda.current_stream(self.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._ctx_side.make_current()
+                ph(L.RNN_PH_PREP, stream=L.stream(self.device))
+            self._ctx.make_current()
         ph(L.RNN_PH_GAE)
         self._phase_tag = 'moments'
         yield moments
-        ph(L.RNN_PH_PREP)
+        if side is None:
+            ph(L.RNN_PH_PREP)
+        else:
+            torch.cuda.current_stream(self.device).wait_stream(side)
         for e in range(self.epoch_policy + 1):                  # ppo.py:541-557
             ph(L.RNN_PH_POLICY_FWD, e)
             self._phase_tag = 'policy_stats'

@@ -44,8 +44,12 @@ def _lstm_case(B, S, D, H, seed):
     return lstm, x, h0, c0, dh
 
 
+# B <= CUs: the VALU recurrence at one segment per workgroup; CUs < B <= 2 CUs:
+# two segments per workgroup; beyond: the 4-segment MFMA forms; H > 128: the
+# 16-segment register / streaming forms (lstm_kernels.hip)
 @pytest.mark.parametrize('B,S,D,H', [(37, 7, 11, 20), (64, 21, 42, 100), (16, 1, 5, 16),
-                                     (20, 5, 9, 130)])
+                                     (20, 5, 9, 130), (300, 9, 42, 100), (600, 6, 42, 100),
+                                     (1024, 5, 20, 64), (257, 4, 7, 128)])
 def test_lstm_kernels_vs_torch_lstm(B, S, D, H):
     lstm, x, h0, c0, dh = _lstm_case(B, S, D, H, B + S)
     flat = lstm_flat(lstm).to(DEV)
