@@ -445,6 +445,9 @@ def main():
     ap.add_argument('--scaling', choices=['strong', 'weak'], default=None,
                     help='strong (default for c3/c5): the workload\'s global batch split over '
                          'the ranks; weak (c2, c4): the per-GPU batch fixed')
+    ap.add_argument('--graph', choices=['on', 'off'], default='on',
+                    help='one GPU: learn() as a hipGraph replay of its device sequence '
+                         '(PPOLearner(use_graph=True), bit-identical to eager); ranks > 1 run eager')
     args = ap.parse_args()
 
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
@@ -472,7 +475,7 @@ def main():
     B, T = lc.replay.batch_size, lc.algo.n_step
     D, A = dims['D'], dims['A']
     dp = TorchDistAllReduce() if dist is not None else None
-    learner = PPOLearner(lc, ec, seed=1, device=dev, dp=dp)
+    learner = PPOLearner(lc, ec, seed=1, device=dev, dp=dp, use_graph=args.graph == 'on')
     pool = [synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=rank * 1000 + i,
                                                     rnn_hidden=dims['rnn_hidden'],
                                                     pixel=dims.get('pixel')), dev)
@@ -586,7 +589,8 @@ def main():
         'config': {'workload': wl, 'segments_per_gpu': B, 'n_step': T,
                    'env_steps_per_learn_per_gpu': B * T, 'global_segments': world * B,
                    'parallelism': f'dp{world}' if world > 1 else 'single',
-                   'epochs_run_last': epochs_run},
+                   'epochs_run_last': epochs_run,
+                   'launch': 'hipGraph replay' if learner._graph is not None else 'eager'},
         'roofline': roof,
         'kernels': kernels,
         'phase_ms_per_step': phases,

@@ -120,7 +120,8 @@ class PPOLearner(object):
     publish_parameter/checkpoint_attributes/preprocess/_prefetcher_preprocess."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
-                 publisher=None, device=None, seed=0, dp=None, checkpoint_full_state=False):
+                 publisher=None, device=None, seed=0, dp=None, checkpoint_full_state=False,
+                 use_graph=False):
         """dp: None (one GPU) or a data-parallel group exposing `world_size` and
         `allreduce_(tensor)` (in-place SUM, stream-ordered), e.g.
         TorchDistAllReduce() over RCCL.  Each rank passes its own shard of
@@ -130,7 +131,11 @@ class PPOLearner(object):
         moments / step counters and the adaptive state (beta, clip epsilon, KL
         record, experience counter), so a restored learner continues
         bit-identically.  The reference checkpoints neither (ppo.py:668-678);
-        off by default, which restores exactly what the reference restores."""
+        off by default, which restores exactly what the reference restores.
+        use_graph (one GPU): learn() replays a hipGraph of the whole device
+        sequence (preprocess, GAE, the epochs, z_update) captured after the
+        first call, with the batch copied into static buffers when it lives
+        elsewhere; bit-identical to eager learn() (test_ppo_graph_replay_bit_exact)."""
         L.require_gpu()
         self.dp = dp
         self.checkpoint_full_state = bool(checkpoint_full_state)
@@ -251,6 +256,9 @@ class PPOLearner(object):
         # optional export of the advantages as the policy epochs use them (and
         # the RNN window returns) into self._bufs['adv_used'] / ['ret_used']
         self.export_advantages = False
+        self.use_graph = bool(use_graph) and dp is None
+        self._graph = None
+        self._gin = None
         # LSTM / pixel phases: ref_pol on a second stream beside the GAE pass
         self.prep_side_stream = os.environ.get('SMI_PREP_SIDE', '1') != '0'
         self._side = None
@@ -628,6 +636,16 @@ class PPOLearner(object):
         yield zbuf
         ph(L.RNN_PH_ZAPPLY)
 
+    def _device_phases(self, batch, preprocessed=False):
+        """the device part of learn(): preprocess + _optimize (generator)"""
+        if not preprocessed:
+            batch = self._preprocess_batch_ppo(batch)
+        for buf in self._optimize(batch['obs'], batch['actions'], batch['rewards'],
+                                  batch['obs_next'], batch['persistent_infos'],
+                                  batch['onetime_infos'], batch['dones']):
+            yield buf
+            self._ctx.make_current()      # whatever ran on this thread meanwhile
+
     def _learn_phases(self, batch):
         """learn() as a generator of the buffers a data-parallel learner must
         all-reduce (SUM) between its launches (the single-CU C2 kernel yields
@@ -648,22 +666,86 @@ class PPOLearner(object):
             yield rf
             self._ctx.make_current()
             self.reward_filter.commit_(rf)
+            yield from self._device_phases(batch, preprocessed=True)
         else:
-            batch = self._preprocess_batch_ppo(batch)
-        for buf in self._optimize(batch['obs'], batch['actions'], batch['rewards'],
-                                  batch['obs_next'], batch['persistent_infos'],
-                                  batch['onetime_infos'], batch['dones']):
-            yield buf
-            self._ctx.make_current()      # whatever ran on this thread meanwhile
+            yield from self._device_phases(batch)
         if self.metrics is not None:
             self.metrics(self.last_stats(), self.global_step)
         self.exp_counter += self.batch_size * (self.dp.world_size if self.dp is not None else 1)
         self.global_step += 1
 
     def learn(self, batch):                                   # ppo.py:588-613
+        if self.use_graph and self.kernel_events is None:
+            return self._learn_graphed(batch)
         for buf in self._learn_phases(batch):
             if self.dp is not None:                           # single GPU: phases, no exchange
                 self.dp.allreduce_(buf)
+
+    # ------------------------------------------------------- hipGraph replay
+    @staticmethod
+    def _leaves(batch):
+        """the batch's tensors in a fixed order, and a function rebuilding the
+        same structure over another list of tensors"""
+        out = []
+
+        def walk(x):
+            if isinstance(x, dict):
+                return {k: walk(v) for k, v in x.items()}
+            if isinstance(x, (list, tuple)):
+                return [walk(v) for v in x]
+            if x is None:
+                return None
+            out.append(x)
+            return len(out) - 1
+        skel = walk(batch)
+
+        def build(ts):
+            def mk(x):
+                if isinstance(x, dict):
+                    return {k: mk(v) for k, v in x.items()}
+                if isinstance(x, list):
+                    return [mk(v) for v in x]
+                return None if x is None else ts[x]
+            return mk(skel)
+        return out, build
+
+    def _learn_graphed(self, batch):
+        """learn() as one hipGraph replay of the device sequence (module
+        docstring: no host synchronisation happens inside learn(), so the whole
+        phase sequence, the side-stream ref_pol pass included, is capturable).
+        The first call (and any call whose batch shapes differ) runs eagerly —
+        that call's update, sizing every scratch buffer — then captures the
+        same launches over static copies of the inputs."""
+        if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
+            batch = self._arena.stage(batch)
+        leaves, build = self._leaves(batch)
+        key = tuple((tuple(t.shape), t.dtype) for t in leaves)
+        self.current_iteration += 1
+        self._ctx.make_current()
+        if self._hyper_values() != self._hyper_key:
+            self._write_hyper()
+        if self._graph is None or self._graph_key != key:
+            for _ in self._device_phases(batch):
+                pass
+            self._gin = [t.detach().clone() for t in leaves]
+            static = build(self._gin)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._ctx.make_current()
+                for _ in self._device_phases(static):
+                    pass
+            self._ctx.make_current()
+            self._graph, self._graph_key = g, key
+        else:
+            for s_, t in zip(self._gin, leaves):
+                if s_.data_ptr() != t.data_ptr():
+                    s_.copy_(t)
+            self._graph.replay()
+        if self.metrics is not None:
+            self.metrics(self.last_stats(), self.global_step)
+        self.exp_counter += self.batch_size
+        self.global_step += 1
 
     def last_stats(self):
         """Statistics dict of the last learn() (ppo.py:219-224,278-284,328-331,555,571-582).

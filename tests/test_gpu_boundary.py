@@ -364,3 +364,41 @@ def test_learners_on_two_streams_in_three_threads_match_sequential_runs():
     got = state(*conc)
     for i, (a, b) in enumerate(zip(got, want)):
         assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize('kind', ['c3', 'mlp', 'pixel'])
+def test_ppo_graph_replay_bit_exact(kind):
+    """use_graph=True replays one hipGraph of the device sequence (the side-
+    stream ref_pol pass included): parameters, filters, Adam state and
+    statistics bit-identical to eager learn() over several calls, with fresh
+    batches copied into the static inputs and a publish (new hyper-parameters
+    and reference model) in between."""
+    if kind == 'c3':
+        lc = ppo_config(B=128, T=25, mode='adapt', use_z_filter=True, hidden=(300, 200), lam=1.0,
+                        epochs=(4, 4), rnn=True, rnn_hidden=100, horizon=5)
+        D, A, Hd, pix = 42, 8, 100, None
+    elif kind == 'mlp':
+        lc = ppo_config(B=64, T=20, mode='clip', use_z_filter=True, epochs=(4, 4))
+        D, A, Hd, pix = 17, 6, None, None
+    else:
+        lc = ppo_config(B=8, T=6, mode='adapt', use_z_filter=True, hidden=(32, 24), lam=1.0,
+                        epochs=(2, 2), rnn=True, rnn_hidden=16, horizon=2, cnn_feat=16)
+        D, A, Hd, pix = 9, 3, 16, (3, 84, 84)
+    from surreal_amd.config import pixel_env_config
+    ec = pixel_env_config(D, A, pix) if pix else env_config(D, A)
+    lc.parameter_publish.exp_interval = 2 * lc.replay.batch_size
+    B, T = lc.replay.batch_size, lc.algo.n_step
+    eager = PPOLearner(lc, ec, seed=4)
+    graph = PPOLearner(lc, ec, seed=4, use_graph=True)
+    for it in range(5):
+        b = synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=60 + it, rnn_hidden=Hd, pixel=pix), DEV)
+        eager.learn(b)
+        graph.learn(b)
+        eager.publish_parameter(it)
+        graph.publish_parameter(it)
+        torch.cuda.synchronize()
+        assert _same(_state(eager), _state(graph)), it
+        for k, v in eager.optimizer_state().items():
+            assert torch.equal(v, graph.optimizer_state()[k]), (it, k)
+        assert eager.last_stats() == graph.last_stats(), it
+    assert graph._graph is not None

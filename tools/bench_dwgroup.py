@@ -1,0 +1,81 @@
+"""The grouped weight-gradient launch of one C3 backward phase in isolation:
+the actor head's three layers (dW over 21504 rows: 300x101, 200x301, 8x201)
+and the LSTM's fused W_ih | W_hh over [x_t | h_{t-1}] (400 x (42 | 100) + bias),
+queued with smi_dw_group_begin / smi_linear_backward_weight and run by
+smi_dw_group_flush, as ppo_rnn.hip's stem_backward does.  Prints the median
+time per flush and the algorithmic TF/s; --rows / --segments change the row
+count (128 segments: 2688 rows).  Used for A/B timing and rocprofv3 passes.
+Usage: python tools/bench_dwgroup.py [--iters 50] [--segments 1024]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from surreal_amd import _lib as L  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--iters', type=int, default=50)
+    ap.add_argument('--segments', type=int, default=1024)
+    ap.add_argument('--steps', type=int, default=21)
+    args = ap.parse_args()
+    R = args.segments * args.steps
+    dev = torch.device('cuda', 0)
+    L.ensure_workspace(dev)
+    st = L.stream(dev)
+    P = L.ptr
+    g = torch.Generator(device=dev).manual_seed(0)
+    H, D, G4, h1, h2, A = 100, 42, 400, 300, 200, 8
+    # head: X0 = LSTM outputs [R][H], HA1 [R][h1], HA2 [R][h2]; dZ [R][A]
+    X0 = torch.randn(R, H, device=dev, generator=g)
+    HA1 = torch.relu(torch.randn(R, h1, device=dev, generator=g))
+    HA2 = torch.relu(torch.randn(R, h2, device=dev, generator=g))
+    dZ = torch.randn(R, A, device=dev, generator=g) * 1e-3
+    dH2 = torch.randn(R, h2, device=dev, generator=g) * 1e-3
+    dH1 = torch.randn(R, h1, device=dev, generator=g) * 1e-3
+    # LSTM: x_t [R][44] (ldx 44), h_{t-1} [R][H], dgates [R][4H]
+    Xz = torch.randn(R, 44, device=dev, generator=g)
+    hb = torch.randn(R, H, device=dev, generator=g)
+    dg = torch.randn(R, G4, device=dev, generator=g) * 1e-3
+    gW3, gb3 = torch.empty(A, h2, device=dev), torch.empty(A, device=dev)
+    gW2, gb2 = torch.empty(h2, h1, device=dev), torch.empty(h2, device=dev)
+    gW1, gb1 = torch.empty(h1, H, device=dev), torch.empty(h1, device=dev)
+    fl = 2.0 * R * (A * h2 + h2 * h1 + h1 * H + G4 * (D + H)) + R * (A + h2 + h1 + G4)
+    lstm = torch.empty(G4 * D + G4 * H + 2 * G4, device=dev)
+
+    def phase():
+        L.call('smi_dw_group_begin')
+        L.call('smi_linear_backward_weight', P(dZ), A, R, A, P(HA2), h2, h2, P(gW3), h2, P(gb3), 0, st)
+        L.call('smi_linear_backward_weight', P(dH2), h2, R, h2, P(HA1), h1, h1, P(gW2), h1, P(gb2), 0, st)
+        L.call('smi_linear_backward_weight', P(dH1), h1, R, h1, P(X0), H, H, P(gW1), H, P(gb1), 0, st)
+        # the LSTM's W_ih and W_hh as two GEMMs of the group (the learner fuses
+        # them over [x_t | h_{t-1}] through the internal two-source form)
+        L.call('smi_linear_backward_weight', P(dg), G4, R, G4, P(Xz), 44, D, P(lstm), D,
+               P(lstm[G4 * D + G4 * H:]), 0, st)
+        L.call('smi_linear_backward_weight', P(dg), G4, R, G4, P(hb), H, H, P(lstm[G4 * D:]), H,
+               P(lstm[G4 * D + G4 * H + G4:]), 0, st)
+        L.call('smi_dw_group_flush', st)
+    for _ in range(5):
+        phase()
+    torch.cuda.synchronize()
+    ev = []
+    for _ in range(args.iters):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        phase()
+        e.record()
+        ev.append((s, e))
+    torch.cuda.synchronize()
+    t = sorted(s.elapsed_time(e) for s, e in ev)
+    ms = t[len(t) // 2]
+    print(json.dumps({'bench': 'dw_group', 'rows': R, 'ms': round(ms, 4), 'gflop': round(fl / 1e9, 3),
+                      'tflops': round(fl / ms / 1e9, 2), 'frac_f32_mfma': round(fl / ms / 1e9 / 157.3, 3)}),
+          flush=True)
+
+
+if __name__ == '__main__':
+    main()
