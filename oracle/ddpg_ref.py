@@ -4,7 +4,11 @@ fp32 CPU restatement of the DDPG learner step (low-dim observations; the
 use_layernorm blocks of builders.py:41-48,65-75 — off by default,
 ddpg_configs.py:21 — with torchx's L.LayerNorm(1) taken as nn.LayerNorm(n)):
   ActorNetworkX / CriticNetworkX   surreal/model/model_builders/builders.py:35-84
-  DDPGModel.forward                surreal/model/ddpg_net.py:86-93
+  DDPGModel.forward                surreal/model/ddpg_net.py:86-93; with pixel=(C, H, W) the
+                                   perception CNNStemNetwork (builders.py:8-33, ddpg_net.py:
+                                   40-43,69-79) on camera0 / 255, concatenated [cnn | low_dim],
+                                   trained by the critic optimizer (ddpg_net.py:57-61), read
+                                   detached by the actor (ddpg.py:325-328)
   DDPGLearner._optimize            surreal/learner/ddpg.py:244-352 (incl. the TD3 options:
                                    twin critic ddpg.py:280-283,312-320; target policy
                                    smoothing noise from numpy's global RNG :267-277)
@@ -95,10 +99,18 @@ class DDPGLearnerRef:
     the TD3 smoothing noise rows as the batch rows were reordered, so a
     row-permuted execution draws the same noise per transition."""
 
-    def __init__(self, lc, obs_dim, act_dim, seed=0, dtype=torch.float32):
+    def __init__(self, lc, obs_dim, act_dim, seed=0, dtype=torch.float32, pixel=None):
         torch.manual_seed(seed)
         self.dtype = dtype
         self.noise_perm = None
+        self.pixel = pixel
+        self.low_dim = obs_dim
+        if pixel is not None:
+            from oracle.ppo_ref import cnn_stem_ref
+            F = int(lc['model'].get('conv_spec', {}).get('hidden_output_dim', 200))
+            self.cnn_dim = F
+            obs_dim = F + obs_dim                       # [cnn | low_dim]
+            mkp = lambda: cnn_stem_ref(*pixel, F)  # noqa: E731
         net = lc['algo']['network']
         self.gamma = lc['algo']['gamma']
         self.n_step = lc['algo']['n_step']
@@ -112,6 +124,10 @@ class DDPGLearnerRef:
         self.act_dim = act_dim
         if self.double:
             self.critic2, self.critic2_t = CriticX(obs_dim, act_dim, ch, ln), CriticX(obs_dim, act_dim, ch, ln)
+        if pixel is not None:
+            self.perc, self.perc_t = mkp(), mkp()
+            if self.double:
+                self.perc2, self.perc2_t = mkp(), mkp()
         for m in self.nets():
             m.to(dtype)
         self.hard_update()
@@ -119,12 +135,14 @@ class DDPGLearnerRef:
         self.actor_clip_value = net['actor_gradient_value_clip']
         self.clip_critic = net['clip_critic_gradient']
         self.critic_clip_value = net['critic_gradient_value_clip']
-        self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=net['lr_critic'],
+        cp = list(self.critic.parameters()) + (list(self.perc.parameters()) if pixel is not None else [])
+        self.critic_optim = torch.optim.Adam(cp, lr=net['lr_critic'],
                                              weight_decay=net['critic_regularization'])
         self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=net['lr_actor'],
                                             weight_decay=net['actor_regularization'])
         if self.double:
-            self.critic_optim2 = torch.optim.Adam(self.critic2.parameters(), lr=net['lr_critic'],
+            cp2 = list(self.critic2.parameters()) + (list(self.perc2.parameters()) if pixel is not None else [])
+            self.critic_optim2 = torch.optim.Adam(cp2, lr=net['lr_critic'],
                                                   weight_decay=net['critic_regularization'])
         tu = net['target_update']
         self.target_update_type = tu['type']
@@ -134,22 +152,52 @@ class DDPGLearnerRef:
 
     def nets(self):
         out = [self.actor, self.critic, self.actor_t, self.critic_t]
-        return out + ([self.critic2, self.critic2_t] if self.double else [])
+        out += [self.critic2, self.critic2_t] if self.double else []
+        if self.pixel is not None:
+            out += [self.perc, self.perc_t] + ([self.perc2, self.perc2_t] if self.double else [])
+        return out
+
+    def target_pairs(self):
+        pairs = [(self.actor_t, self.actor), (self.critic_t, self.critic)]
+        if self.double:
+            pairs.append((self.critic2_t, self.critic2))
+        if self.pixel is not None:
+            pairs.append((self.perc_t, self.perc))
+            if self.double:
+                pairs.append((self.perc2_t, self.perc2))
+        return pairs
 
     def hard_update(self):
-        self.actor_t.load_state_dict(self.actor.state_dict())
-        self.critic_t.load_state_dict(self.critic.state_dict())
-        if self.double:
-            self.critic2_t.load_state_dict(self.critic2.state_dict())
+        for t, s in self.target_pairs():
+            t.load_state_dict(s.state_dict())
+
+    def perception(self, net, obs):                                     # ddpg_net.py:69-79
+        if self.pixel is None:
+            return obs
+        low, pix = obs
+        img = torch.as_tensor(pix)
+        img = img.to(self.dtype) / 255.0 if self.dtype != torch.float32 else img.float() / 255.0
+        parts = [net(img)] + ([low] if low is not None and low.shape[-1] else [])
+        return torch.cat(parts, 1)
 
     def optimize(self, obs, actions, rewards, obs_next, done):          # ddpg.py:244-352
+        """obs / obs_next: (B, D) tensors, or with pixel=(C, H, W) pairs
+        (low_dim (B, D) or None, camera0 uint8 (B, C, H, W))"""
         cv = lambda t: t if (isinstance(t, torch.Tensor) and t.dtype == self.dtype) \
             else torch.as_tensor(t, dtype=torch.float32).to(self.dtype)  # noqa: E731
-        obs, actions, rewards, obs_next, done = (cv(t) for t in (obs, actions, rewards, obs_next, done))
+        if self.pixel is not None:
+            obs = (None if obs[0] is None else cv(obs[0]), obs[1])
+            obs_next = (None if obs_next[0] is None else cv(obs_next[0]), obs_next[1])
+        else:
+            obs, obs_next = cv(obs), cv(obs_next)
+        actions, rewards, done = (cv(t) for t in (actions, rewards, done))
         assert actions.max().item() <= 1.0 and actions.min().item() >= -1.0
         with torch.no_grad():
-            a_t = self.actor_t(obs_next)
-            q_t = self.critic_t(obs_next, a_t)
+            pt = self.perception(self.perc_t, obs_next) if self.pixel is not None else obs_next
+            pt2 = self.perception(self.perc2_t, obs_next) if self.pixel is not None and self.double \
+                else pt
+            a_t = self.actor_t(pt)
+            q_t = self.critic_t(pt, a_t)
             if self.action_reg:
                 noise = np.clip(np.random.normal(0, 0.2, size=(self.batch_size, self.act_dim)),
                                 -0.5, 0.5)
@@ -158,11 +206,14 @@ class DDPGLearnerRef:
                 a_t = (a_t + torch.tensor(noise, dtype=torch.float32).to(self.dtype)).clamp(-1, 1)
             y = rewards + pow(self.gamma, self.n_step) * q_t * (1.0 - done)
             if self.double:
-                q_t2 = self.critic2_t(obs_next, a_t)
+                q_t2 = self.critic2_t(pt2, a_t)
                 y2 = rewards + pow(self.gamma, self.n_step) * q_t2 * (1.0 - done)
                 y = torch.min(y, y2)
-        q = self.critic(obs, actions)
+        p_obs = self.perception(self.perc, obs) if self.pixel is not None else obs
+        q = self.critic(p_obs, actions)
         self.critic.zero_grad()
+        if self.pixel is not None:
+            self.perc.zero_grad()
         critic_loss = nn.MSELoss()(q, y)
         critic_loss.backward()
         if self.clip_critic:
@@ -170,15 +221,19 @@ class DDPGLearnerRef:
         self.critic_optim.step()
         q2 = None
         if self.double:
-            q2 = self.critic2(obs, actions)
+            p2 = self.perception(self.perc2, obs) if self.pixel is not None else obs
+            q2 = self.critic2(p2, actions)
             self.critic2.zero_grad()
+            if self.pixel is not None:
+                self.perc2.zero_grad()
             critic_loss = nn.MSELoss()(q2, y)
             critic_loss.backward()
             if self.clip_critic:
                 nn.utils.clip_grad_value_(self.critic2.parameters(), self.critic_clip_value)
             self.critic_optim2.step()
         self.actor.zero_grad()
-        actor_loss = -self.critic(obs, self.actor(obs)).mean()
+        pd_ = p_obs.detach()                                  # perception.detach(), ddpg.py:325-328
+        actor_loss = -self.critic(pd_, self.actor(pd_)).mean()
         actor_loss.backward()
         if self.clip_actor:
             nn.utils.clip_grad_value_(self.actor.parameters(), self.actor_clip_value)
@@ -194,13 +249,9 @@ class DDPGLearnerRef:
     def target_update(self):                                            # ddpg.py:403-428
         if self.target_update_type == 'soft':
             with torch.no_grad():
-                tp = list(self.actor_t.parameters()) + list(self.critic_t.parameters())
-                sp = list(self.actor.parameters()) + list(self.critic.parameters())
-                if self.double:
-                    tp += list(self.critic2_t.parameters())
-                    sp += list(self.critic2.parameters())
-                for t, s in zip(tp, sp):
-                    t.copy_(self.tau * s + (1 - self.tau) * t)
+                for tm, sm in self.target_pairs():
+                    for t, s in zip(tm.parameters(), sm.parameters()):
+                        t.copy_(self.tau * s + (1 - self.tau) * t)
         else:
             self.counter += 1
             if self.counter % self.interval == 0:

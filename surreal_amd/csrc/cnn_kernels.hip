@@ -50,10 +50,12 @@ __host__ __device__ inline int64_t lds_img_bytes(const CnnGeom& g) { return (g.i
 //   conv2: M = P2 pixels, N = 32, K = 256; wave w owns channel tile w>>1 and
 //          pixel tiles (w&1), (w&1)+2, ...; one lane reads 4 consecutive A1
 //          floats (kx = 0..3) per 4 MFMAs.
-// 3 waves per SIMD (168 VGPRs, a few bytes of scratch) beat 2 waves at 176:
-// 132 vs 143 us per 2688-image forward (tools/bench_cnn.py)
+// RGB (C = 3): 3 waves per SIMD (168 VGPRs, a few bytes of scratch) beat 2
+// waves at 176: 132 vs 143 us per 2688-image forward (tools/bench_cnn.py).
+// Three stacked RGB frames (C = 9, DDPG's frame_stacks = 3, ddpg_configs.py:
+// 114): the 144 conv-1 weight registers need one wave per SIMD.
 template <int C>
-__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(3, 3)))
+__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(C <= 3 ? 3 : 1, C <= 3 ? 3 : 1)))
 cnn_fwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t rows,
                float* __restrict__ A1g, float* __restrict__ A2g, const int* skip) {
   if (skip && skip[0] != 0) return;
@@ -349,7 +351,8 @@ cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
 
 // ------------------------------------------------------------------- host
 static int cnn_check(const CnnGeom& g) {
-  if (g.C != 3) return set_error(SMI_E_ARG, "cnn: only 3-channel cameras are built (camera0 RGB)");
+  if (g.C != 3 && g.C != 9)
+    return set_error(SMI_E_ARG, "cnn: 3 (one RGB frame) or 9 (three stacked RGB frames) channels");
   if (g.H1 < 4 || g.W1 < 4 || g.H2 < 1 || g.W2 < 1)
     return set_error(SMI_E_ARG, "cnn: image smaller than the two convolutions");
   if ((g.P2 + 15) / 16 > 6)
@@ -377,7 +380,7 @@ int cnn_forward(const float* prm, const PixRows& pr, int C, int H, int W, int F,
   if ((reinterpret_cast<uintptr_t>(pr.pix) | reinterpret_cast<uintptr_t>(pr.pix_next)) & 15)
     return set_error(SMI_E_ARG, "cnn: pixel buffers must be 16-byte aligned");
   const size_t lds = cnn_fwd_lds(g);
-  auto k = cnn_fwd_kernel<3>;
+  auto k = C == 9 ? cnn_fwd_kernel<9> : cnn_fwd_kernel<3>;
   allow_lds(k, lds);
   const int64_t rg = resident_grid(k, kWG, lds);
   const int grid = (int)(rows < rg ? rows : rg);
@@ -400,7 +403,7 @@ int cnn_backward(const float* prm, const PixRows& pr, int C, int H, int W, int F
   RC_CHECK(launch_linear_bwd_dx(dz, lddz, (int)rows, F, prm + g.oWf, g.flat, g.flat, A2, g.flat,
                                 dA2, g.flat, st, skip));
   const size_t lds = cnn_bwd_lds(g);
-  auto k = cnn_bwd_kernel<3>;
+  auto k = C == 9 ? cnn_bwd_kernel<9> : cnn_bwd_kernel<3>;
   allow_lds(k, lds);
   const int grid = cnn_bwd_grid(rows);
   const int kt = ktime_begin(st);

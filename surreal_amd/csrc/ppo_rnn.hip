@@ -91,6 +91,10 @@ struct RnnScratch {
   // the PREP phase's own copies (it may run on a second stream beside GAE)
   float *xprojR, *hbufR, *HA1R, *HA2R, *A2R;
   float *values, *adv, *ret, *refmu, *lvpart;
+  // time-major per-row inputs of the row kernels, packed once per learn:
+  // rowin[n] = {actions (A) | behave mu, sigma (2A) | raw advantage | pad},
+  // n = t*B + b, stride row_w(A); ret_tm[n] the window return
+  float *rowin, *ret_tm;
   float *A1, *A2, *dA2, *dF, *cpart;        // pixel stem (empty without one)
   double *part, *gaepart;
   int* ci; float* cf;
@@ -98,6 +102,8 @@ struct RnnScratch {
 };
 
 static inline int64_t al64(int64_t n) { return (n + 63) & ~(int64_t)63; }
+// packed row width: 3A + 1 floats rounded up to 16 bytes
+__host__ __device__ inline int row_w(int A) { return (3 * A + 1 + 3) & ~3; }
 
 __host__ __device__ inline int rnn_nblk(int64_t rows, int nt = kWG) {
   // at most 1024 four-wave blocks' worth of waves (4096 one-wave blocks)
@@ -134,6 +140,8 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   s.adv = take(d.NE);
   s.ret = take(d.NE);
   s.refmu = take(d.NE * d.A);
+  s.rowin = take(d.NE * row_w(d.A));
+  s.ret_tm = take(d.NE);
   s.lvpart = take((int64_t)4096 * d.A);
   const bool px = d.F > 0;
   s.A1 = take(px ? d.NE * 16 * d.G.P1 : 0);
@@ -157,6 +165,9 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
 // ------------------------------------------------------------ small kernels
 // out[t][b][:] = zfilter(obs[b][t][:]) for t < T, out[T][b][:] = zfilter(obs_next[b][0][:]),
 // for t < S (S <= T+1).  z_filter.py:59-79 (clamp +-5); use_zf == 0 copies.
+// One wave per row (32-bit row index math once per row, not per element):
+// lane j moves columns j, j + 64 of a D <= 128-wide row, so each load and
+// store instruction covers one contiguous row.
 __global__ void __launch_bounds__(kWG)
 zf_tmajor_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next, int B, int T,
                  int S, int D, int use_zf, const float* zs, const float* zq, const float* zc,
@@ -166,14 +177,28 @@ zf_tmajor_kernel(const float* __restrict__ obs, const float* __restrict__ obs_ne
   float* zd = sm + round4(D);
   if (use_zf) zfilter_colstats(zs, zq, zc, eps, D, zm, zd);
   __syncthreads();
-  const int64_t n = (int64_t)S * B * D;
-  for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < n; e += (int64_t)gridDim.x * kWG) {
-    const int64_t row = e / D;
-    const int c = (int)(e - row * D);
-    const int t = (int)(row / B), b = (int)(row - (int64_t)t * B);
-    float v = t < T ? obs[((int64_t)b * T + t) * D + c] : obs_next[(int64_t)b * D + c];
-    if (use_zf) v = fminf(fmaxf((v - zm[c]) / zd[c], -5.f), 5.f);
-    out[row * ldo + c] = v;
+  const int lane = threadIdx.x & 63;
+  const int nrows = S * B;
+  const int w0 = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6), nw = gridDim.x * (kWG / 64);
+  float m0 = 0.f, d0 = 1.f, m1 = 0.f, d1 = 1.f;
+  if (use_zf) {
+    if (lane < D) { m0 = zm[lane]; d0 = zd[lane]; }
+    if (lane + 64 < D) { m1 = zm[lane + 64]; d1 = zd[lane + 64]; }
+  }
+  for (int row = w0; row < nrows; row += nw) {
+    const int t = row / B, b = row - t * B;
+    const float* src = t < T ? obs + ((int64_t)b * T + t) * D : obs_next + (int64_t)b * D;
+    float* dst = out + (int64_t)row * ldo;
+    if (lane < D) {
+      float v = src[lane];
+      if (use_zf) v = fminf(fmaxf((v - m0) / d0, -5.f), 5.f);
+      dst[lane] = v;
+    }
+    if (lane + 64 < D) {
+      float v = src[lane + 64];
+      if (use_zf) v = fminf(fmaxf((v - m1) / d1, -5.f), 5.f);
+      dst[lane + 64] = v;
+    }
   }
 }
 
@@ -212,6 +237,8 @@ struct PolRowArgs {
   const float* behave;    // [B][T][2A]
   const float* adv;       // [B][E] raw
   const float* ret;       // [B][E]
+  const float* rowin;     // [NE][row_w(A)] time-major {actions | behave | raw adv}
+  const float* ret_tm;    // [NE] time-major returns
   const double* moments;  // [3] global (sum, sumsq, n) of adv, or null (no norm)
   int norm_adv;
   float c_ll;
@@ -304,6 +331,27 @@ __device__ __forceinline__ float row_kl(const float* mu0, const float* sd0, cons
   return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
 }
 
+// rowin / ret_tm from the batch-major inputs (once per learn): the per-row
+// kernels of every epoch then read whole rows in time-major order (coalesced)
+// instead of A- and E-strided gathers from [B][T][.] / [B][E]
+__global__ void __launch_bounds__(kWG)
+row_pack_kernel(PolRowArgs a, float* __restrict__ rowin, float* __restrict__ ret_tm) {
+  const int A = a.A, RW = row_w(A);
+  const int N = a.E * a.B;
+  for (int n = blockIdx.x * kWG + threadIdx.x; n < N; n += gridDim.x * kWG) {
+    const int t = n / a.B, b = n - t * a.B;
+    const int64_t src = (int64_t)b * a.T + t;
+    float* o = rowin + (int64_t)n * RW;
+    const float* ac = a.actions + src * A;
+    const float* bh = a.behave + src * 2 * A;
+    for (int j = 0; j < A; ++j) o[j] = ac[j];
+    for (int j = 0; j < 2 * A; ++j) o[A + j] = bh[j];
+    o[3 * A] = a.adv[(int64_t)b * a.E + t];
+    for (int j = 3 * A + 1; j < RW; ++j) o[j] = 0.f;
+    ret_tm[n] = a.ret[(int64_t)b * a.E + t];
+  }
+}
+
 // forward statistics of the policy over the E*B rows (ppo.py:203-224,
 // 262-284, 553-575)
 template <int NT, int AT>
@@ -314,6 +362,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
   __shared__ float ssig[32], slsig[32], srsig[32];
   __shared__ double scr[NT / 64][PS_N];
   const int A = AT > 0 ? AT : a.A;
+  const int RW = row_w(A);
   for (int j = threadIdx.x; j < A; j += NT) {
     ssig[j] = expf(a.lv[j]);                 // builders.py:127 std = exp(log_var)
     slsig[j] = logf(ssig[j]);                // std0.log() of ppo_net.py:40
@@ -329,15 +378,14 @@ policy_rows_stats_kernel(PolRowArgs a) {
   for (int k = 0; k < PS_N; ++k) acc[k] = 0.0;
   const int64_t N = (int64_t)a.E * a.B;
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
-    const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
     float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM];
     ld_row<AT>(m, a.mu + n * A, A);
     ld_row<AT>(rm, a.refmu + n * A, A);
-    ld_row<AT>(ac, a.actions + ((int64_t)b * a.T + t) * A, A);
-    const float* bp = a.behave + ((int64_t)b * a.T + t) * 2 * A;
-    ld_row<AT>(bmu, bp, A);
-    ld_row<AT>(bsd, bp + A, A);
-    const float av = norm_adv_of(a, a.adv[(int64_t)b * a.E + t]);
+    const float* rw = a.rowin + n * RW;
+    ld_row<AT>(ac, rw, A);
+    ld_row<AT>(bmu, rw + A, A);
+    ld_row<AT>(bsd, rw + 2 * A, A);
+    const float av = norm_adv_of(a, rw[3 * A]);
     const float lp = fmaxf(expf(row_loglik<AT>(ac, m, sig, lsig, A, a.c_ll)), 1e-5f);
 #pragma unroll
     for (int j = 0; j < (AT > 0 ? AT : A); ++j) blsd[j] = logf(bsd[j]);
@@ -355,7 +403,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
     acc[PS_ISW] += (double)(lp / (bl + 1e-4f));
     acc[PS_BL] += (double)bl;
     acc[PS_RBD] += (double)row_kl<AT>(rm, rsig, bmu, bsd, A);
-    acc[PS_RET] += (double)a.ret[(int64_t)b * a.E + t];
+    acc[PS_RET] += (double)a.ret_tm[n];
   }
   // all PS_N sums at once: wave butterflies, one barrier, fixed wave order
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -385,6 +433,7 @@ policy_rows_grad_kernel(PolRowArgs a) {
   __shared__ float ssig[32], slsig[32], srsig[32];
   __shared__ float gls[NT / 64][32];
   const int A = AT > 0 ? AT : a.A;
+  const int RW = row_w(A);
   for (int j = threadIdx.x; j < A; j += NT) {
     ssig[j] = expf(a.lv[j]);
     slsig[j] = logf(ssig[j]);
@@ -401,15 +450,14 @@ policy_rows_grad_kernel(PolRowArgs a) {
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
   const int64_t N = (int64_t)a.E * a.B;
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
-    const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
     float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM], dz[AM];
     ld_row<AT>(m, a.mu + n * A, A);
     ld_row<AT>(rm, a.refmu + n * A, A);
-    ld_row<AT>(ac, a.actions + ((int64_t)b * a.T + t) * A, A);
-    const float* bp = a.behave + ((int64_t)b * a.T + t) * 2 * A;
-    ld_row<AT>(bmu, bp, A);
-    ld_row<AT>(bsd, bp + A, A);
-    const float av = norm_adv_of(a, a.adv[(int64_t)b * a.E + t]);
+    const float* rw = a.rowin + n * RW;
+    ld_row<AT>(ac, rw, A);
+    ld_row<AT>(bmu, rw + A, A);
+    ld_row<AT>(bsd, rw + 2 * A, A);
+    const float av = norm_adv_of(a, rw[3 * A]);
     const float ll = row_loglik<AT>(ac, m, sig, lsig, A, a.c_ll);
     const float ex = expf(ll);
     const float lp = fmaxf(ex, 1e-5f);
@@ -551,18 +599,17 @@ reduce_decide_kernel(const double* __restrict__ part, int nb, DecideArgs a, cons
   if (threadIdx.x == 0) policy_decide_body(a);
 }
 
-// value loss rows: V (time-major [NE]) vs ret [B][E]; dV = 2 (V - R) / N and,
-// in the last epoch, the sums of ppo.py:324-331
+// value loss rows: V and the returns, both time-major [NE]; dV = 2 (V - R) / N
+// and, in the last epoch, the sums of ppo.py:324-331
 template <int NT>
 __global__ void __launch_bounds__(NT)
-value_rows_kernel(const float* __restrict__ V, const float* __restrict__ ret, int B, int E,
+value_rows_kernel(const float* __restrict__ V, const float* __restrict__ ret_tm, int B, int E,
                   float invN2, float* __restrict__ dV, double* part) {
   __shared__ double scr[NT / 64];
   double se = 0.0, d1 = 0.0, d2 = 0.0, r1 = 0.0, r2 = 0.0;
   const int64_t N = (int64_t)E * B;
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
-    const int t = (int)(n / B), b = (int)(n - (int64_t)t * B);
-    const float r = ret[(int64_t)b * E + t];
+    const float r = ret_tm[n];
     const float v = V[n];
     const float e = v - r;
     dV[n] = invN2 * e;
@@ -717,6 +764,13 @@ static int grid_of(int64_t n, int cap = 1024) {
 }
 
 #define RC(x) do { const int rc_ = (x); if (rc_) return rc_; } while (0)
+
+// zf_tmajor_kernel: one wave per row, 4 waves per block, at most 2048 blocks
+static int zf_grid(int64_t rows) {
+  int64_t g = (rows + 3) / 4;
+  if (g < 1) g = 1;
+  return (int)(g < 2048 ? g : 2048);
+}
 
 struct Head {   // one MLP head over rows of an activation matrix
   const float* P; MlpLayout L; int in, h1, h2, out, tanh_out;
@@ -939,6 +993,7 @@ static PolRowArgs pol_rows(const smi_ppo_rnn_args& a, const RnnDims& d, const Rn
   p.B = d.B; p.T = d.T; p.E = d.E; p.A = d.A; p.mode = a.mode;
   p.mu = s.OUT; p.lv = a.actor + d.LA.flv; p.refmu = s.refmu; p.ref_lv = a.ref_actor + d.LA.flv;
   p.actions = a.actions; p.behave = a.behave; p.adv = s.adv; p.ret = s.ret;
+  p.rowin = s.rowin; p.ret_tm = s.ret_tm;
   p.moments = a.moments; p.norm_adv = a.norm_adv; p.c_ll = c_loglik_of(d.A);
   p.hyper = a.hyper; p.skip = s.ci + CI_STOP;
   p.part = s.part; p.dz = s.dOUT; p.lvpart = s.lvpart; p.cf = s.cf;
@@ -965,7 +1020,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       hipLaunchKernelGGL(rnn_init_kernel, dim3(1), dim3(64), 0, st, s.ci, s.cf);
       RC(check_launch("rnn_init_kernel"));
       int kt = ktime_begin(st);
-      hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NG * d.D)), dim3(kWG), zlds, st, a.obs,
+      hipLaunchKernelGGL(zf_tmajor_kernel, dim3(zf_grid(d.NG)), dim3(kWG), zlds, st, a.obs,
                          a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum, a.zf_sumsq,
                          a.zf_count, a.zf_eps, s.Xz, d.ldx);
       ktime_end(kt, KT_ZF_TMAJOR, 8.0 * (double)d.NG * d.D, st);      // read x, write z(x)
@@ -996,7 +1051,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       RnnScratch sp = s;
       sp.xproj = s.xprojR; sp.hbuf = s.hbufR; sp.HA1 = s.HA1R; sp.HA2 = s.HA2R; sp.A2 = s.A2R;
       const float* X = s.Xr;
-      hipLaunchKernelGGL(zf_tmajor_kernel, dim3(grid_of(d.NE * d.D)), dim3(kWG), zlds, st, a.obs,
+      hipLaunchKernelGGL(zf_tmajor_kernel, dim3(zf_grid(d.NE)), dim3(kWG), zlds, st, a.obs,
                          a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
                          a.rzf_count, a.zf_eps, s.Xr, d.ldx);
       RC(check_launch("zf_tmajor_kernel"));
@@ -1007,6 +1062,11 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                       nullptr);
     }
     case SMI_RNN_PH_POLICY_FWD: {
+      if (e == 0) {
+        hipLaunchKernelGGL(row_pack_kernel, dim3(grid_of(d.NE)), dim3(kWG), 0, st, pol_rows(a, d, s),
+                           s.rowin, s.ret_tm);
+        RC(check_launch("row_pack_kernel"));
+      }
       if (e == 0 && (a.adv_out || a.ret_out)) {
         hipLaunchKernelGGL(adv_export_kernel, dim3(grid_of(d.NE)), dim3(kWG), 0, st,
                            pol_rows(a, d, s), a.adv_out, a.ret_out);
@@ -1097,7 +1157,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       const int nb = rnn_nblk(d.NE, kRowNT);
       const bool last = e == a.epoch_baseline - 1;
       const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(value_rows_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, s.OUT, s.ret, d.B, d.E,
+      hipLaunchKernelGGL(value_rows_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, s.OUT, s.ret_tm, d.B, d.E,
                          (float)(2.0 / (double)NEg), s.dOUT, last ? s.part : nullptr);
       ktime_end(kt, KT_VALUE_ROWS, 12.0 * (double)d.NE, st);     // V, R read, dV written
       RC(check_launch("value_rows_kernel"));

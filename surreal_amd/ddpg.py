@@ -8,7 +8,14 @@ gradient, critic backward, Adam; actor forward, critic forward with the
 updated critic, -mean(Q) gradient, backward through the critic's action block
 and the actor, Adam; target update; statistics.  With use_layernorm
 (off by default, ddpg_configs.py:21) every hidden ReLU is followed by a
-LayerNorm block (smi_layernorm_*); pixel inputs are not built.
+LayerNorm block (smi_layernorm_*).  Pixel observations (env pixel_input,
+ddpg_net.py:34-43,69-79): the perception CNNStemNetwork (16@8s4, 32@4s2, FC
+conv_spec.hidden_output_dim) of each model turns camera0 (uint8, / 255 fused
+into the conv kernel; 9 channels = 3 stacked RGB frames) into features that
+are concatenated [cnn | low_dim] before the actor and critic; it trains with
+the CRITIC's optimizer (get_critic_parameters, ddpg_net.py:57-61), the actor
+reads it detached (ddpg.py:325-328), and it follows the target updates
+(ddpg.py:414-428).
 
 Parameter layouts (flat, torch (out, in) order; [g b] = LayerNorm weight / bias
 with use_layernorm):
@@ -24,7 +31,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from .config import Config, ConfigError
-from .model import _FlatViews, _LinearView
+from .model import CNNStemNetwork, _FlatViews, _LinearView
 
 # group each backward's weight-gradient GEMMs into one launch (SMI_DDPG_DW_GROUP=0: A/B off)
 _DW_GROUP = os.environ.get('SMI_DDPG_DW_GROUP', '1') != '0'
@@ -123,11 +130,20 @@ class DDPGModel(nn.Module):
                  generator=None):
         super().__init__()
         L.require_gpu()
-        if 'pixel' in obs_spec:
-            raise NotImplementedError('surreal_amd: DDPG pixel inputs are SURVEY §8(f) rank 1')
         self.device = torch.device(device) if device is not None else torch.device('cuda')
         self.action_dim = action_dim
-        self.input_dim = int(obs_spec['low_dim']['flat_inputs'][0])
+        self.is_pixel_input = 'pixel' in obs_spec
+        self.low_dim = int(obs_spec['low_dim']['flat_inputs'][0]) if 'low_dim' in obs_spec else 0
+        self.perception = None
+        self.cnn_dim = 0
+        if self.is_pixel_input:                          # ddpg_net.py:40-43
+            self.cnn_dim = int(conv_hidden_dim if conv_hidden_dim is not None else 200)
+            self.perception = CNNStemNetwork(
+                obs_spec['pixel']['camera0'], self.cnn_dim,
+                conv_out_channels or (16, 32), conv_kernel_sizes or (8, 4), conv_strides or (4, 2),
+                device=self.device, generator=generator)
+        # concatenated perception: [cnn features | low_dim] (ddpg_net.py:69-79)
+        self.input_dim = self.cnn_dim + self.low_dim
         self.use_layernorm = bool(use_layernorm)
         self.actor = None if critic_only else ActorNetworkX(
             self.input_dim, action_dim, actor_fc_hidden_sizes, self.device, generator,
@@ -138,13 +154,21 @@ class DDPGModel(nn.Module):
     def get_actor_parameters(self):
         return self.actor.parameters()
 
-    def get_critic_parameters(self):
-        return self.critic.parameters()
+    def get_critic_parameters(self):                    # ddpg_net.py:57-61
+        ps = list(self.critic.parameters())
+        if self.is_pixel_input:
+            ps += list(self.perception.parameters())
+        return iter(ps)
 
-    def forward_perception(self, obs):
+    def forward_perception(self, obs):                 # ddpg_net.py:69-79
         if isinstance(obs, torch.Tensor):
             return obs
-        return obs['low_dim']['flat_inputs']
+        if not self.is_pixel_input:
+            return obs['low_dim']['flat_inputs']
+        net = _Net(self)
+        pix = obs['pixel']['camera0']
+        low = obs['low_dim']['flat_inputs'] if self.low_dim else None
+        return net.perception_fwd(self, pix.contiguous(), low, pix.shape[0], None).clone()
 
     def forward_actor(self, obs):
         net = _Net(self)
@@ -204,6 +228,40 @@ class _Net(object):
         L.call('smi_layernorm_backward', _p(dy), dy.stride(0), _p(x), x.stride(0),
                _p(self.bufs[tag + '_mu']), _p(self.bufs[tag + '_rs']), _p(ln.weight), rows, ln.n, 1,
                _p(dx), dx.stride(0), _p(dg), _p(db), self.st)
+
+    def perception_fwd(self, model, pix, low, rows, store, keep=False):
+        """[cnn(pix / 255) | low] (ddpg_net.py:69-79) into buffer store_P; keep:
+        the conv activations stay for a backward (store_A1 / store_A2)"""
+        cnn = model.perception
+        C, H, W = cnn.D_obs
+        F, D = model.cnn_dim, model.low_dim
+        pre = store or 'ptmp'
+        P = self.buf(pre + '_P', (rows, F + D))
+        A1 = self.buf(pre + '_A1', (rows, 16 * ((H - 8) // 4 + 1) * ((W - 8) // 4 + 1))) if keep else None
+        A2 = self.buf(pre + '_A2', (rows, cnn.flat_dim))
+        if pix.dtype != torch.uint8:
+            raise TypeError('DDPG camera observations must be uint8 (scaled by 1/255 in the kernel)')
+        L.call('smi_cnn_forward', _p(cnn.flat), _p(pix), None, rows, 1, rows, C, H, W, F,
+               _p(A1) if A1 is not None else None, _p(A2), _p(P), F + D, self.st)
+        if D:
+            L.call('smi_copy_cols', _p(low), low.stride(0), rows, D, _p(P[:, F:]), F + D, self.st)
+        return P
+
+    def perception_bwd(self, model, pix, rows, store, dH1, wo, ldwo, c1, grad):
+        """the critic's first-layer input gradient over the cnn columns, masked by
+        the FC ReLU, back through the CNN stem into grad (its flat layout)"""
+        cnn = model.perception
+        C, H, W = cnn.D_obs
+        F, D = model.cnn_dim, model.low_dim
+        P = self.bufs[store + '_P']
+        dF = self.buf(store + '_dF', (rows, F))
+        L.call('smi_linear_backward_input', _p(dH1), c1, rows, c1, _p(wo), ldwo, F, _p(P), F + D,
+               _p(dF), F, self.st)
+        nb = int(L.lib().smi_cnn_scratch_bytes(rows, C, H, W, F))
+        scratch = self.buf('cnn_scratch', ((nb + 3) // 4,))
+        L.call('smi_cnn_backward', _p(cnn.flat), _p(pix), None, rows, 1, rows, C, H, W, F,
+               _p(self.bufs[store + '_A1']), _p(self.bufs[store + '_A2']), _p(dF), F, _p(grad),
+               _p(scratch), nb, self.st)
 
     def actor_fwd(self, obs, rows, store='a', actor=None):
         actor = actor if actor is not None else self.m.actor
@@ -297,22 +355,30 @@ class DDPGLearner(object):
         self.critic_gradient_clip_value = net.critic_gradient_value_clip
         self.action_dim = ec.action_spec['dim'][0]
         gen = torch.Generator().manual_seed(seed)
+        cs = lc.model.get('conv_spec', {})
+        conv = dict(conv_out_channels=cs.get('out_channels'), conv_kernel_sizes=cs.get('kernel_sizes'),
+                    conv_strides=cs.get('strides'), conv_hidden_dim=cs.get('hidden_output_dim'))
         mk = lambda: DDPGModel(ec.obs_spec, self.action_dim, self.use_layernorm,  # noqa: E731
                                lc.model.actor_fc_hidden_sizes, lc.model.critic_fc_hidden_sizes,
-                               device=self.device, generator=gen)
+                               device=self.device, generator=gen, **conv)
         self.model = mk()
         self.model_target = mk()
         if self.use_double_critic:                      # ddpg.py:119-145 (critic_only twins)
             mk2 = lambda: DDPGModel(ec.obs_spec, self.action_dim, self.use_layernorm,  # noqa: E731
                                     lc.model.actor_fc_hidden_sizes,
                                     lc.model.critic_fc_hidden_sizes, critic_only=True,
-                                    device=self.device, generator=gen)
+                                    device=self.device, generator=gen, **conv)
             self.model2 = mk2()
             self.model_target2 = mk2()
+        self.is_pixel_input = self.model.is_pixel_input
         from .learner import replicate_from_rank0
         flats = [self.model.actor.flat, self.model.critic.flat]
         if self.use_double_critic:
             flats.append(self.model2.critic.flat)
+        if self.is_pixel_input:
+            flats.append(self.model.perception.flat)
+            if self.use_double_critic:
+                flats.append(self.model2.perception.flat)
         replicate_from_rank0(self.dp, flats)
         self._hard_update()
         dev = self.device
@@ -322,14 +388,22 @@ class DDPGLearner(object):
         if self.use_double_critic:                      # critic_optim2 (ddpg.py:163-168)
             groups.append(('critic2', self.model2.critic.flat, net.lr_critic,
                            net.critic_regularization))
-        # gradient buffers packed for the data-parallel exchange: [critic | critic2]
-        # (independent, one all-reduce) and [actor | 12 statistics] (one more)
+        if self.is_pixel_input:                         # the perception joins the critic optimizer
+            groups.append(('critic_cnn', self.model.perception.flat, net.lr_critic,
+                           net.critic_regularization))
+            if self.use_double_critic:
+                groups.append(('critic2_cnn', self.model2.perception.flat, net.lr_critic,
+                               net.critic_regularization))
+        # gradient buffers packed for the data-parallel exchange: [critic | cnn |
+        # critic2 | cnn2] (independent, one all-reduce) and [actor | 12 statistics]
         nc = self.model.critic.flat.numel()
+        nq = self.model.perception.flat.numel() if self.is_pixel_input else 0
         na = self.model.actor.flat.numel()
-        self._critic_pack = torch.zeros(nc * (2 if self.use_double_critic else 1), device=dev)
+        self._critic_pack = torch.zeros((nc + nq) * (2 if self.use_double_critic else 1), device=dev)
         self._actor_pack = torch.zeros(na + 12, device=dev)
-        packs = {'critic': self._critic_pack[:nc], 'critic2': self._critic_pack[nc:],
-                 'actor': self._actor_pack[:na]}
+        packs = {'critic': self._critic_pack[:nc], 'critic_cnn': self._critic_pack[nc:nc + nq],
+                 'critic2': self._critic_pack[nc + nq:2 * nc + nq],
+                 'critic2_cnn': self._critic_pack[2 * nc + nq:], 'actor': self._actor_pack[:na]}
         for name, flat, lr, wd in groups:
             self.opt[name] = {'m': torch.zeros_like(flat), 'v': torch.zeros_like(flat),
                               'step': torch.zeros(1, dtype=torch.int32, device=dev),
@@ -346,12 +420,22 @@ class DDPGLearner(object):
         self._gin = None
 
     # ------------------------------------------------------------ helpers
+    def _target_pairs(self):
+        """(target, source) flat buffers of the target update (ddpg.py:409-428)"""
+        pairs = [(self.model_target.actor.flat, self.model.actor.flat),
+                 (self.model_target.critic.flat, self.model.critic.flat)]
+        if self.use_double_critic:
+            pairs.append((self.model_target2.critic.flat, self.model2.critic.flat))
+            if self.is_pixel_input:
+                pairs.append((self.model_target2.perception.flat, self.model2.perception.flat))
+        if self.is_pixel_input:
+            pairs.append((self.model_target.perception.flat, self.model.perception.flat))
+        return pairs
+
     def _hard_update(self):
         with torch.no_grad():
-            self.model_target.actor.flat.copy_(self.model.actor.flat)
-            self.model_target.critic.flat.copy_(self.model.critic.flat)
-            if self.use_double_critic:
-                self.model_target2.critic.flat.copy_(self.model2.critic.flat)
+            for t, s_ in self._target_pairs():
+                t.copy_(s_)
 
     def _dp_mean_(self, t):
         """Average a per-rank gradient / statistics buffer over the ranks."""
@@ -366,13 +450,22 @@ class DDPGLearner(object):
                None, None, st)
 
     def preprocess(self, batch):                                         # ddpg.py:186-242
+        """numpy -> device tensors; camera frames stay uint8 (the reference's
+        .float() and the model's / 255, ddpg_net.py:90-95, happen in the conv
+        kernel, bit-equal to torch's u8 -> float / 255)"""
         out = {}
         for k in ('obs', 'obs_next'):
             v = batch[k]
             if isinstance(v, dict):
+                o = {}
                 if 'pixel' in v:
-                    raise NotImplementedError('surreal_amd: pixel inputs')
-                v = v['low_dim']['flat_inputs']
+                    o['pixel'] = {'camera0': torch.as_tensor(np.asarray(v['pixel']['camera0']),
+                                                             dtype=torch.uint8).to(self.device)}
+                if 'low_dim' in v:
+                    o['low_dim'] = {'flat_inputs': torch.as_tensor(
+                        v['low_dim']['flat_inputs'], dtype=torch.float32).to(self.device)}
+                out[k] = o if 'pixel' in v else o['low_dim']['flat_inputs']
+                continue
             out[k] = torch.as_tensor(v, dtype=torch.float32).to(self.device, non_blocking=True)
         for k in ('actions', 'rewards', 'dones'):
             out[k] = torch.as_tensor(batch[k], dtype=torch.float32).to(self.device, non_blocking=True)
@@ -388,6 +481,23 @@ class DDPGLearner(object):
         D, h1, h2, A = self.model.actor.dims
         _, c1, c2, _ = self.model.critic.dims
         rs = rewards.stride(0) if rewards.dim() == 2 else 1
+        pix = pix_n = None
+        obs_next2 = obs_next
+        if self.is_pixel_input:
+            # forward_perception (ddpg_net.py:69-79) of every model that reads the
+            # batch: the target model(s) on obs_next, the model(s) on obs (their
+            # conv activations kept for the critic backward)
+            pix, pix_n = obs['pixel']['camera0'].contiguous(), obs_next['pixel']['camera0'].contiguous()
+            low = obs['low_dim']['flat_inputs'] if 'low_dim' in obs else None
+            low_n = obs_next['low_dim']['flat_inputs'] if 'low_dim' in obs_next else None
+            obs_next = tnet.perception_fwd(self.model_target, pix_n, low_n, B, 'tp')
+            if self.use_double_critic:
+                obs_next2 = tnet.perception_fwd(self.model_target2, pix_n, low_n, B, 't2p')
+            obs2 = net.perception_fwd(self.model2, pix, low, B, 'q2p', keep=True) \
+                if self.use_double_critic else None
+            obs = net.perception_fwd(self.model, pix, low, B, 'cp', keep=True)
+        else:
+            obs2, obs_next2 = obs, obs_next
         # target: y = r + gamma^n * Q'(s', mu'(s')) * (1 - d)           (ddpg.py:266-284)
         a_t = tnet.actor_fwd(obs_next, B, store='ta')
         q_t = tnet.critic_fwd(self.model_target.critic, obs_next, a_t, B, store='tc')
@@ -404,7 +514,7 @@ class DDPGLearner(object):
                 noise = np.clip(np.random.normal(0, 0.2, size=(self.batch_size * W, self.action_dim)),
                                 -0.5, 0.5)[r * self.batch_size:(r + 1) * self.batch_size]
                 a_t2 = (a_t + torch.tensor(noise, dtype=torch.float32).to(self.device)).clamp(-1, 1)
-            q_t2 = tnet.critic_fwd(self.model_target2.critic, obs_next, a_t2.contiguous(), B,
+            q_t2 = tnet.critic_fwd(self.model_target2.critic, obs_next2, a_t2.contiguous(), B,
                                    store='t2c')
         y = net.buf('y', (B, 1))
         r1 = rewards if rewards.is_contiguous() else rewards.contiguous()
@@ -417,25 +527,32 @@ class DDPGLearner(object):
         dq = net.buf('dq', (B, 1))
         L.call('smi_mse_grad', _p(q), 1, _p(y), B, _p(dq), _p(self.stats_buf[1:2]), st)
         g = self.opt['critic']['g']
-        self._critic_backward(net, crit, obs, B, dq, 'c', g, st, need_obs_grad=True)
+        cnn = (self.model, pix, 'cp', self.opt['critic_cnn']['g']) if self.is_pixel_input else None
+        self._critic_backward(net, crit, obs, B, dq, 'c', g, st, need_obs_grad=True, cnn=cnn)
         cclip = self.critic_gradient_clip_value if self.clip_critic_gradient else 0.0
         if self.use_double_critic:                      # second critic (ddpg.py:312-320)
             # its gradient does not depend on the first critic's step: both are
             # computed first and averaged over the ranks in one exchange
             crit2 = self.model2.critic
-            q_2 = net.critic_fwd(crit2, obs, actions, B, store='q2c')
+            q_2 = net.critic_fwd(crit2, obs2, actions, B, store='q2c')
             dq_2 = net.buf('dq_2', (B, 1))
             # the reference reports this critic's loss as 'critic_loss'
             L.call('smi_mse_grad', _p(q_2), 1, _p(y), B, _p(dq_2), _p(self.stats_buf[1:2]), st)
-            self._critic_backward(net, crit2, obs, B, dq_2, 'q2c', self.opt['critic2']['g'], st,
-                                  need_obs_grad=True)
+            cnn2 = (self.model2, pix, 'q2p', self.opt['critic2_cnn']['g']) if self.is_pixel_input \
+                else None
+            self._critic_backward(net, crit2, obs2, B, dq_2, 'q2c', self.opt['critic2']['g'], st,
+                                  need_obs_grad=True, cnn=cnn2)
             L.call('smi_ddpg_stats', _p(actions), actions.stride(0), self.action_dim, _p(rewards),
                    rewards.stride(0) if rewards.dim() == 2 else 1, _p(y), _p(q_2), 1, B,
                    _p(self.stats_buf[8:12]), st)         # [.., .., .., Q_policy2]
         self._dp_mean_(self._critic_pack)
         self._adam('critic', crit.flat, cclip, st)
+        if self.is_pixel_input:         # the perception: critic optimizer, no value clip
+            self._adam('critic_cnn', self.model.perception.flat, 0.0, st)
         if self.use_double_critic:
             self._adam('critic2', self.model2.critic.flat, cclip, st)
+            if self.is_pixel_input:
+                self._adam('critic2_cnn', self.model2.perception.flat, 0.0, st)
         # actor update with the updated critic (ddpg.py:323-333)
         act = self.model.actor
         a = net.actor_fwd(obs, B, store='a')
@@ -454,19 +571,21 @@ class DDPGLearner(object):
         if target_update:
             self._target_update()
 
-    def _critic_backward(self, net, crit, obs, B, dq, pre, g, st, need_obs_grad):
+    def _critic_backward(self, net, crit, obs, B, dq, pre, g, st, need_obs_grad, cnn=None):
         """Backward through CriticNetworkX.  With g: weight grads into g (flat),
-        the three weight-gradient GEMMs as one grouped launch (smi_dw_group_*).
-        Always returns d loss / d action (B, A) when g is None."""
+        the three weight-gradient GEMMs as one grouped launch (smi_dw_group_*);
+        cnn = (model, pixels, perception store, gradient) continues through the
+        model's perception (pixel inputs).  Always returns d loss / d action
+        (B, A) when g is None."""
         if g is None or not _DW_GROUP:
-            return self._critic_backward_body(net, crit, obs, B, dq, pre, g, st)
+            return self._critic_backward_body(net, crit, obs, B, dq, pre, g, st, cnn)
         L.call('smi_dw_group_begin')
         try:
-            return self._critic_backward_body(net, crit, obs, B, dq, pre, g, st)
+            return self._critic_backward_body(net, crit, obs, B, dq, pre, g, st, cnn)
         finally:
             L.call('smi_dw_group_flush', st)   # always flush: nothing stays queued
 
-    def _critic_backward_body(self, net, crit, obs, B, dq, pre, g, st):
+    def _critic_backward_body(self, net, crit, obs, B, dq, pre, g, st, cnn=None):
         D, c1, c2, A = crit.dims
         ln = crit.use_layernorm
         CAT = net.bufs[pre + '_cat']
@@ -498,6 +617,9 @@ class DDPGLearner(object):
                        c1 + A, _p(dH1), c1, st)
             L.call('smi_linear_backward_weight', _p(dH1), c1, B, c1, _p(obs), obs.stride(0), D,
                    _p(g[crit.off(wo):]), D, _p(g[crit.off(bo):]), 0, st)
+            if cnn is not None:
+                model, pix, store, gc = cnn
+                net.perception_bwd(model, pix, B, store, dH1, wo, D, c1, gc)
             return None
         dA = net.buf('dA', (B, A))
         L.call('smi_linear_backward_input', _p(dH2), c2, B, c2, _p(wc[:, c1:]), c1 + A, A, None, 0,
@@ -552,11 +674,7 @@ class DDPGLearner(object):
     def _target_update(self):                                            # ddpg.py:403-428
         st = L.stream(self.device)
         if self.target_update_type == 'soft':
-            pairs = [(self.model_target.actor.flat, self.model.actor.flat),
-                     (self.model_target.critic.flat, self.model.critic.flat)]
-            if self.use_double_critic:
-                pairs.append((self.model_target2.critic.flat, self.model2.critic.flat))
-            for t, s in pairs:
+            for t, s in self._target_pairs():
                 L.call('smi_soft_update', _p(t), _p(s), t.numel(), float(self.target_update_tau), st)
         else:
             self.target_update_counter += 1
@@ -569,12 +687,12 @@ class DDPGLearner(object):
         self._ctx.make_current()
         if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
             batch = self.preprocess(batch)
-        obs = batch['obs']
-        obs = obs['low_dim']['flat_inputs'] if isinstance(obs, dict) else obs
-        obs_next = batch['obs_next']
-        obs_next = obs_next['low_dim']['flat_inputs'] if isinstance(obs_next, dict) else obs_next
+        obs, obs_next = batch['obs'], batch['obs_next']
+        if not self.is_pixel_input:
+            obs = obs['low_dim']['flat_inputs'] if isinstance(obs, dict) else obs
+            obs_next = obs_next['low_dim']['flat_inputs'] if isinstance(obs_next, dict) else obs_next
         ins = (obs, batch['actions'], batch['rewards'], obs_next, batch['dones'])
-        if self.use_graph:
+        if self.use_graph and not self.is_pixel_input:
             self._optimize_graphed(*ins)
         else:
             self._optimize(*ins)

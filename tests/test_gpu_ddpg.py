@@ -173,9 +173,11 @@ DDPG_ORDERS = ('given', 'reversed', 'shuffled')
 
 
 class _DVariant(object):
-    def __init__(self, kind, key, lc, D, A, init):
+    def __init__(self, kind, key, lc, D, A, init, pixel=None):
         self.kind, self.key = kind, key
-        self.ref = R.DDPGLearnerRef(lc, D, A, dtype=torch.float32 if kind == 'order' else torch.float64)
+        self.pixel = pixel
+        self.ref = R.DDPGLearnerRef(lc, D, A, dtype=torch.float32 if kind == 'order' else torch.float64,
+                                    pixel=pixel)
         self.gen = torch.Generator().manual_seed(777 + 13 * key if kind == 'ulp' else 0)
         _load_ddpg(self.ref, init, self._noisy if kind == 'ulp' else None)
 
@@ -191,9 +193,13 @@ class _DVariant(object):
             self.ref.noise_perm = p
             x = {k: torch.as_tensor(np.asarray(v)[p]) for k, v in b.items()}
         else:
-            x = {k: self._noisy(v) for k, v in b.items()}
+            x = {k: (torch.as_tensor(v) if k in ('pix', 'pix_next') else self._noisy(v))
+                 for k, v in b.items()}
             x['dones'] = torch.as_tensor(b['dones'], dtype=torch.float64)
-        return self.ref.optimize(x['obs'], x['actions'], x['rewards'], x['obs_next'], x['dones'])
+        obs, obs_next = x['obs'], x['obs_next']
+        if self.pixel is not None:                  # camera frames: uint8, exact in every execution
+            obs, obs_next = (obs, x['pix']), (obs_next, x['pix_next'])
+        return self.ref.optimize(obs, x['actions'], x['rewards'], obs_next, x['dones'])
 
 
 def _load_ddpg(ref, init, noisy=None):
@@ -202,6 +208,10 @@ def _load_ddpg(ref, init, noisy=None):
     R.load_flat(ref.critic.params(), f(init['critic']))
     if 'critic2' in init:
         R.load_flat(ref.critic2.params(), f(init['critic2']))
+    if 'perc' in init:
+        R.load_flat(list(ref.perc.parameters()), f(init['perc']))
+    if 'perc2' in init:
+        R.load_flat(list(ref.perc2.parameters()), f(init['perc2']))
     ref.hard_update()
 
 
@@ -213,6 +223,11 @@ def _ddpg_state(learner):
     if learner.use_double_critic:
         out['critic2'] = learner.model2.critic.flat.detach().cpu().clone()
         out['critic2_t'] = learner.model_target2.critic.flat.detach().cpu().clone()
+    if learner.is_pixel_input:
+        out['perc'] = learner.model.perception.flat.detach().cpu().clone()
+        out['perc_t'] = learner.model_target.perception.flat.detach().cpu().clone()
+        if learner.use_double_critic:
+            out['perc2'] = learner.model2.perception.flat.detach().cpu().clone()
     return out
 
 
@@ -222,36 +237,55 @@ def _ddpg_ref_state(ref):
     if ref.double:
         out['critic2'] = R.flat_of(ref.critic2.params())
         out['critic2_t'] = R.flat_of(ref.critic2_t.params())
+    if ref.pixel is not None:
+        out['perc'] = R.flat_of(list(ref.perc.parameters()))
+        out['perc_t'] = R.flat_of(list(ref.perc_t.parameters()))
+        if ref.double:
+            out['perc2'] = R.flat_of(list(ref.perc2.parameters()))
     return {k: v.double().numpy() for k, v in out.items()}
 
 
-def ddpg_envelope_run(lc, D, A, iters=3, batches=None, n_ulp=6, learn_input=None, seed=2):
+def ddpg_envelope_run(lc, D, A, iters=3, batches=None, n_ulp=6, learn_input=None, seed=2,
+                      pixel=None):
     """the HIP learner vs the fp64 oracle within the envelope over `iters`
     steps.  batches: list of numpy dicts (obs, actions, rewards (B,1),
     obs_next, dones (B,1)); learn_input(learner, it) -> what learner.learn()
     gets (default: the batch on the device)."""
     from tests import parity as P
     B = lc.replay.batch_size
-    learner = DDPGLearner(lc, gym_env_config(D, A), seed=seed)
-    init = {k: v for k, v in _ddpg_state(learner).items() if k in ('actor', 'critic', 'critic2')}
-    r64 = R.DDPGLearnerRef(lc, D, A, dtype=torch.float64)
+    from surreal_amd.config import pixel_env_config
+    ec = pixel_env_config(D, A, pixel) if pixel is not None else gym_env_config(D, A)
+    learner = DDPGLearner(lc, ec, seed=seed)
+    init = {k: v for k, v in _ddpg_state(learner).items()
+            if k in ('actor', 'critic', 'critic2', 'perc', 'perc2')}
+    r64 = R.DDPGLearnerRef(lc, D, A, dtype=torch.float64, pixel=pixel)
     _load_ddpg(r64, init)
-    vs = [_DVariant('order', k, lc, D, A, init) for k in DDPG_ORDERS]
-    vs += [_DVariant('ulp', k, lc, D, A, init) for k in range(1, n_ulp + 1)]
+    vs = [_DVariant('order', k, lc, D, A, init, pixel) for k in DDPG_ORDERS]
+    vs += [_DVariant('ulp', k, lc, D, A, init, pixel) for k in range(1, n_ulp + 1)]
     if batches is None:
         batches = [{k: v.numpy() for k, v in synthetic.ddpg_batch(B, D, A, seed=it).items()}
                    for it in range(iters)]
     report = {}
     for it, b in enumerate(batches):
         np.random.seed(100 + it)
-        s64 = r64.optimize(*(torch.as_tensor(b[k], dtype=torch.float32).double()
-                             for k in ('obs', 'actions', 'rewards', 'obs_next', 'dones')))
+        f64 = lambda k: torch.as_tensor(b[k], dtype=torch.float32).double()  # noqa: E731
+        o64, on64 = f64('obs'), f64('obs_next')
+        if pixel is not None:
+            o64, on64 = (o64, torch.as_tensor(b['pix'])), (on64, torch.as_tensor(b['pix_next']))
+        s64 = r64.optimize(o64, f64('actions'), f64('rewards'), on64, f64('dones'))
         svs = []
         for v in vs:
             np.random.seed(100 + it)
             svs.append(v.optimize(b, it))
         np.random.seed(100 + it)
-        if learn_input is None:
+        if learn_input is None and pixel is not None:
+            dev = {k: torch.as_tensor(b[k], dtype=torch.float32).cuda()
+                   for k in ('actions', 'rewards', 'dones')}
+            for k, pk in (('obs', 'pix'), ('obs_next', 'pix_next')):
+                dev[k] = {'low_dim': {'flat_inputs': torch.as_tensor(b[k], dtype=torch.float32).cuda()},
+                          'pixel': {'camera0': torch.as_tensor(b[pk]).cuda()}}
+            learner.learn(dev)
+        elif learn_input is None:
             learner.learn({k: torch.as_tensor(v, dtype=torch.float32).cuda() for k, v in b.items()})
         else:
             learner.learn(learn_input(learner, it))
@@ -289,6 +323,31 @@ def test_ddpg_td3_envelope(target, action_reg):
     lc.algo.network.use_double_critic = True
     lc.algo.network.use_action_regularization = action_reg
     ddpg_envelope_run(lc, 17, 6, iters=3)
+
+
+@pytest.mark.parametrize('target,td3', [('hard', False), ('soft', True)])
+def test_ddpg_pixel_envelope(target, td3):
+    """DDPG with camera observations (ddpg_net.py:34-43,57-79; ddpg.py:207-223,
+    287-333,409-428): 3 stacked RGB frames (9 x 84 x 84 uint8, frame_stacks 3,
+    ddpg_configs.py:114) -> CNNStemNetwork (16@8s4, 32@4s2, FC 200) concatenated
+    with the low-dim state before actor and critic; the perception trains with
+    the critic optimizer (no value clip: the reference clips model.critic only),
+    the actor reads it detached, the targets copy / track it.  TD3: the twin has
+    its own perception and target perception."""
+    B, D, A, cam = 64, 17, 6, (9, 84, 84)
+    lc = _cfg(B, target, False)
+    if td3:
+        lc.algo.network.use_double_critic = True
+        lc.algo.network.use_action_regularization = True
+    batches = []
+    for it in range(3):
+        b = {k: v.numpy() for k, v in synthetic.ddpg_batch(B, D, A, seed=70 + it).items()}
+        g = torch.Generator().manual_seed(170 + it)
+        b['pix'] = torch.randint(0, 256, (B,) + cam, generator=g, dtype=torch.uint8).numpy()
+        b['pix_next'] = torch.randint(0, 256, (B,) + cam, generator=g, dtype=torch.uint8).numpy()
+        batches.append(b)
+    learner = ddpg_envelope_run(lc, D, A, batches=batches, pixel=cam, n_ulp=3)
+    assert learner.is_pixel_input
 
 
 def test_ddpg_host_path_ssar_envelope():

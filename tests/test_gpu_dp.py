@@ -76,8 +76,10 @@ def test_dp_equals_global_batch(mode, world, B_loc, rf):
         # the reference's one fp32 sum): after 10 + 10 Adam epochs the learner
         # is compared with the fp64 oracle against the fp32 envelope
         # (test_gpu_parity_pinned.py), the bar every learn() parity test uses
-        from tests.test_gpu_parity_pinned import _envelope, as_good_as_fp32, print_report
-        r64, vs = _envelope(learners[0], lcg, D, A, None, n_ulp=4)
+        from tests import parity as P
+        st0 = P.gpu_state(learners[0])
+        st0.pop('zf', None)
+        r64, vs = P.envelope(st0, lcg, D, A, None, n_ulp=4)
     report = {}
     for it in range(2):
         batch = synthetic.ppo_batch(B_loc * world, T, D, A, seed=300 + it)
@@ -96,13 +98,14 @@ def test_dp_equals_global_batch(mode, world, B_loc, rf):
             rep = {}
             for name, got, ref_of in (('actor', learners[0].model.actor.flat, lambda r: r.model.actor.flat()),
                                       ('critic', learners[0].model.critic.flat, lambda r: r.model.critic.flat())):
-                as_good_as_fp32(f'{name}@{it}', got.cpu(), [ref_of(v.ref) for v in vs], ref_of(r64), rep)
+                w, sc = P.width(ref_of(r64).double().numpy(), [ref_of(v.ref).double().numpy() for v in vs])
+                P.check(f'{name}@{it}', got.cpu(), ref_of(r64).double().numpy(), w, sc, rep)
             for b in ('running_sum', 'running_sumsq', 'count'):
                 got, exp = float(getattr(learners[0].reward_filter, b).item()), float(getattr(r64.reward_filter, b).item())
                 assert abs(got - exp) <= 1e-6 * abs(exp) + 1e-6, (it, b, got, exp)
                 assert all(torch.equal(getattr(l.reward_filter, b), getattr(learners[0].reward_filter, b))
                            for l in learners)
-            print_report(rep)
+            P.print_report(rep)
             for l in learners[1:]:
                 assert torch.equal(l.model.actor.flat, learners[0].model.actor.flat)
             continue

@@ -157,9 +157,9 @@ def test_rnn_learn_no_zfilter_early_stop():
     # gradient flips LSTM entries in any two fp32 implementations: parity is
     # held to the fp32 envelope (test_gpu_parity_pinned.py), which also requires
     # the same number of policy epochs in every execution
-    from tests.test_gpu_parity_pinned import pinned_run
+    from tests.test_gpu_parity_pinned import pinned_live
     lc = _rnn_cfg('adapt', 16, 6, 2, 16, (16, 24), zf=False, lr=(3e-2, 1e-3), kl_target=0.002)
-    pinned_run(lc, 7, 3, iters=2, rnn_hidden=16, seed=0)
+    pinned_live(lc, 7, 3, iters=2, rnn_hidden=16, seed=0)
 
 
 @pytest.mark.parametrize('mode', ['adapt', 'clip'])
