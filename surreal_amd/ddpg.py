@@ -474,7 +474,7 @@ class DDPGLearner(object):
     # --------------------------------------------------------- _optimize
     def _optimize(self, obs, actions, rewards, obs_next, done,           # ddpg.py:244-352
                   target_update=True):
-        B = obs.shape[0]
+        B = actions.shape[0]
         st = L.stream(self.device)
         net = _Net(self.model, self._bufs)
         tnet = _Net(self.model_target, self._bufs)
