@@ -165,6 +165,29 @@ int smi_mlp_forward(const float* params, int in_dim, int h1, int h2, int out_dim
                     const float* zf_count, float zf_eps,
                     float* out, void* stream);
 
+/* The learner's head passes over tall activation matrices, each ONE launch
+ * (head_kernels.hip; the RNN learner's phases call them internally):
+ *   forward:  ha1 = relu(x W1^T + b1), ha2 = relu(ha1 W2^T + b2),
+ *             y = act(ha2 W3^T + b3) (tanh_out: tanh) — PPO_ActorNetwork /
+ *             PPO_CriticNetwork (builders.py:86-175) without log_var;
+ *             wT (nullable, in*h1 + h1*h2 floats) receives W1^T | W2^T for the
+ *             backward below.
+ *   backward_input: from dz = dL/d(pre-activation of the last layer):
+ *             dh2 = (dz W3) * [ha2 > 0], dh1 = (dh2 W2) * [ha1 > 0],
+ *             dx[:, 0:dxn] = (dh1 W1[:, dx0:dx0+dxn]) (* [mask > 0] when mask)
+ *             using the forward's wT; dxn == 0: no dx.
+ * params: the flat [W1 b1 W2 b2 W3 b3] layout of smi_mlp_forward.  Rows of x
+ * are ldx floats apart.  Shapes: in, h1, h2 multiples of 4 in [4, 512] (in
+ * <= 320), out <= 16, dxn <= 320, 16-byte aligned x / params; otherwise
+ * SMI_E_NOFIT (use smi_linear_* per layer). */
+int smi_head_forward(const float* params, int in_dim, int h1, int h2, int out_dim, int tanh_out,
+                     const float* x, int64_t ldx, int64_t rows, float* ha1, float* ha2,
+                     float* y, float* wT, void* stream);
+int smi_head_backward_input(const float* params, int in_dim, int h1, int h2, int out_dim,
+                            const float* wT, const float* dz, int64_t rows, const float* ha1,
+                            const float* ha2, float* dh2, float* dh1, int dx0, int dxn, float* dx,
+                            int64_t lddx, const float* mask, int64_t ldm, void* stream);
+
 /* ------------------------------------------------------- PPO: GAE/returns */
 /* Replaces PPOLearner._gae_and_return, non-RNN branch
  * (surreal/learner/ppo.py:355-387,408-418): the critic forward over
@@ -554,6 +577,12 @@ int smi_layernorm_backward(const float* dy, int64_t ldg, const float* x, int64_t
                            int n, int relu_input, float* dx, int64_t lddx, float* dgamma,
                            float* dbeta, void* stream);
 
+/* Parameter publish (module_dict.py:22-35, parameter_server.py:40-55: the
+ * state_dict D2H of ModuleDict.dumps): copy nbytes (multiple of 16, 16-byte
+ * aligned) from device memory into PINNED host memory with a kernel on
+ * `stream` (the publisher's side stream), so the caller's thread never waits
+ * in a DMA copy call.  Fails when host_dst is not pinned, mapped memory. */
+int smi_copy_to_host(void* host_dst, const void* src, int64_t nbytes, void* stream);
 /* target <- tau*src + (1-tau)*target (soft target update, ddpg.py:409-417) */
 int smi_soft_update(float* target, const float* src, int64_t n, float tau, void* stream);
 /* action_norm, rewards, Q_target, Q_policy means of ddpg.py:335-345 -> stats4 */

@@ -161,6 +161,11 @@ _SIGS = {
     'smi_neg_mean_grad': (c_int, [P, c_i64, c_i64, P, P, P]),
     'smi_tanh_backward': (c_int, [P, c_i64, P, c_i64, c_i64, c_int, P, c_i64, P]),
     'smi_copy_cols': (c_int, [P, c_i64, c_i64, c_int, P, c_i64, P]),
+    'smi_copy_to_host': (c_int, [P, P, c_i64, P]),
+    'smi_head_forward': (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_i64, c_i64, P, P, P, P,
+                                 P]),
+    'smi_head_backward_input': (c_int, [P, c_int, c_int, c_int, c_int, P, P, c_i64, P, P, P, P,
+                                        c_int, c_int, P, c_i64, P, c_i64, P]),
     'smi_soft_update': (c_int, [P, P, c_i64, c_f32, P]),
     'smi_ddpg_stats': (c_int, [P, c_i64, c_int, P, c_i64, P, P, c_i64, c_i64, P, P]),
     'smi_ddpg_target': (c_int, [P, P, P, P, c_i64, c_f32, P, P]),

@@ -98,6 +98,19 @@ int launch_tanh_backward(const float*, int64_t, const float*, int64_t, int64_t, 
                          int64_t, hipStream_t);
 int launch_copy_cols(const float*, int64_t, int64_t, int, float*, int64_t, hipStream_t);
 int launch_soft_update(float*, const float*, int64_t, float, hipStream_t);
+int launch_copy_bytes16(const void*, void*, int64_t, hipStream_t);
+bool head_fused_ok(int in, int64_t ldx, int h1, int h2, int out, const float* X,
+                   const float* W1, const float* W2, const float* W3);
+int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
+                          const float* b1, int h1, const float* W2, const float* b2, int h2,
+                          const float* W3, const float* b3, int out, int tanh_out, float* HA1,
+                          float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
+                          hipStream_t st, const int* skip);
+int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
+                          const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
+                          const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
+                          int64_t lddx, const float* mask, int64_t ldm, hipStream_t st,
+                          const int* skip);
 int launch_ddpg_stats(const float*, int64_t, int, const float*, int64_t, const float*,
                       const float*, int64_t, int64_t, float*, hipStream_t);
 int launch_ddpg_target(const float*, const float*, const float*, const float*, int64_t, float,
@@ -259,6 +272,37 @@ int smi_mlp_forward(const float* params, int in_dim, int h1, int h2, int out_dim
   REQUIRE(!use_zf || (zs && zsq && zc), "mlp_forward: zfilter buffers required");
   return launch_mlp_forward(params, in_dim, h1, h2, out_dim, out_act, with_log_var, x, rows,
                             row_stride, use_zf, zs, zsq, zc, zeps, out, SMI_STREAM(stream));
+}
+
+int smi_head_forward(const float* params, int in_dim, int h1, int h2, int out_dim, int tanh_out,
+                     const float* x, int64_t ldx, int64_t rows, float* ha1, float* ha2, float* y,
+                     float* wT, void* stream) {
+  REQUIRE(params && x && ha1 && ha2 && y && rows >= 0 && ldx >= in_dim, "head_forward: bad args");
+  const MlpLayout L = mlp_layout(in_dim, h1, h2, out_dim, 0);
+  if (!head_fused_ok(in_dim, ldx, h1, h2, out_dim, x, params + L.fW1, params + L.fW2,
+                     params + L.fW3))
+    return set_error(SMI_E_NOFIT, "head_forward: shape not supported by the fused head");
+  return launch_head_fwd_fused(x, ldx, rows, in_dim, params + L.fW1, params + L.fb1, h1,
+                               params + L.fW2, params + L.fb2, h2, params + L.fW3,
+                               params + L.fb3, out_dim, tanh_out, ha1, ha2, y, out_dim, wT,
+                               wT ? wT + (int64_t)in_dim * h1 : nullptr, SMI_STREAM(stream),
+                               nullptr);
+}
+
+int smi_head_backward_input(const float* params, int in_dim, int h1, int h2, int out_dim,
+                            const float* wT, const float* dz, int64_t rows, const float* ha1,
+                            const float* ha2, float* dh2, float* dh1, int dx0, int dxn, float* dx,
+                            int64_t lddx, const float* mask, int64_t ldm, void* stream) {
+  REQUIRE(params && wT && dz && ha1 && ha2 && dh2 && dh1 && rows >= 0 && dx0 >= 0 && dxn >= 0 &&
+          dx0 + dxn <= in_dim && (dxn == 0 || (dx && lddx >= dxn)),
+          "head_backward_input: bad args");
+  const MlpLayout L = mlp_layout(in_dim, h1, h2, out_dim, 0);
+  if (dxn > 320 || !head_fused_ok(in_dim, in_dim, h1, h2, out_dim, params, params + L.fW1,
+                                  params + L.fW2, params + L.fW3))
+    return set_error(SMI_E_NOFIT, "head_backward_input: shape not supported by the fused head");
+  return launch_head_bwd_fused(dz, out_dim, rows, params + L.fW3, wT + (int64_t)in_dim * h1, wT,
+                               h1, h2, dx0, dxn, ha1, ha2, dh2, dh1, dx, lddx, mask, ldm,
+                               SMI_STREAM(stream), nullptr);
 }
 
 int smi_ppo_critic_gae(const float* critic_params, int obs_dim, int h1, int h2, int use_zf,
@@ -426,6 +470,18 @@ int smi_copy_cols(const float* src, int64_t lds, int64_t rows, int cols, float* 
   REQUIRE(src && dst && rows >= 0 && cols > 0, "copy_cols: bad args");
   if (rows == 0) return SMI_OK;
   return launch_copy_cols(src, lds, rows, cols, dst, ldd, SMI_STREAM(stream));
+}
+
+int smi_copy_to_host(void* host_dst, const void* src, int64_t nbytes, void* stream) {
+  REQUIRE(host_dst && src && nbytes >= 0 && nbytes % 16 == 0 &&
+          (reinterpret_cast<uintptr_t>(host_dst) & 15) == 0 &&
+          (reinterpret_cast<uintptr_t>(src) & 15) == 0,
+          "copy_to_host: 16-byte aligned pointers and a multiple of 16 bytes required");
+  if (nbytes == 0) return SMI_OK;
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, host_dst, 0) != hipSuccess || !dev)
+    return set_error(SMI_E_ARG, "copy_to_host: destination is not pinned (mapped) host memory");
+  return launch_copy_bytes16(src, dev, nbytes / 16, SMI_STREAM(stream));
 }
 
 int smi_soft_update(float* target, const float* src, int64_t n, float tau, void* stream) {

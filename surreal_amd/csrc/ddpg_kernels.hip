@@ -68,6 +68,15 @@ copy_cols_kernel(const float* __restrict__ src, int64_t lds, int64_t rows, int c
   }
 }
 
+// 16-byte grid-stride copy; dst may be pinned host memory mapped into the
+// device address space (the publisher's D2H: a kernel on the side stream
+// instead of an SDMA copy, so the host thread never blocks in the runtime)
+__global__ void __launch_bounds__(kWG)
+copy_bytes16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kWG)
+    dst[i] = src[i];
+}
+
 __global__ void __launch_bounds__(kWG)
 soft_update_kernel(float* __restrict__ t, const float* __restrict__ s, int64_t n, float tau) {
   for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG)
@@ -242,6 +251,14 @@ int launch_copy_cols(const float* src, int64_t lds, int64_t rows, int cols, floa
   hipLaunchKernelGGL(copy_cols_kernel, dim3(grid_of(rows * cols)), dim3(kWG), 0, st, src, lds, rows,
                      cols, dst, ldd);
   return check_launch("copy_cols_kernel");
+}
+int launch_copy_bytes16(const void* src, void* dst, int64_t n16, hipStream_t st) {
+  int64_t g = (n16 + kWG - 1) / kWG;
+  if (g > 256) g = 256;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(copy_bytes16_kernel, dim3((unsigned)g), dim3(kWG), 0, st,
+                     reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16);
+  return check_launch("copy_bytes16_kernel");
 }
 int launch_soft_update(float* t, const float* s, int64_t n, float tau, hipStream_t st) {
   hipLaunchKernelGGL(soft_update_kernel, dim3(grid_of(n)), dim3(kWG), 0, st, t, s, n, tau);

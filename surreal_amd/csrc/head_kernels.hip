@@ -1,0 +1,545 @@
+// head_kernels.hip — the PPO actor / critic MLP heads over the learner's tall
+// activation matrices (builders.py:86-175: Linear-ReLU-Linear-ReLU-Linear
+// [-Tanh], PPO_ActorNetwork / PPO_CriticNetwork; ppo_net.py:143-152,277-315
+// feed them the LSTM outputs), the forward and the input-gradient chain each
+// as ONE launch instead of three GEMM launches (+ split-K reduces at small
+// batches).
+//
+// A workgroup owns 16 rows (one MFMA row tile) and runs every layer of the
+// chain over them; the activations between layers stay in LDS, the weights
+// stream from L2 straight into MFMA registers.  Layer Y = X W^T with W [N][K]
+// row-major (k contiguous):
+//   * output features in 16-column tiles, tile nt on wave nt % 4;
+//   * k in chunks of 16: lane (li, lk) reads X[li][16c + 4lk .. +3] from LDS
+//     and W[16 nt + li][16c + 4lk .. +3] from global memory (16-byte reads),
+//     and MFMA j of the chunk (v_mfma_f32_16x16x4_f32) takes element j of
+//     both: the k order inside a chunk is permuted identically on the two
+//     operands, so every chunk adds its exact 16-term dot product (an fmaf
+//     chain, like every f32 MFMA);
+//   * the weight reads of the next two chunks are in flight behind the MFMAs
+//     of the current one (register ring, sched_barrier pins the refills);
+//   * the epilogue (bias + ReLU, or the ReLU mask of the backward) writes the
+//     tile to LDS for the next layer and the workgroup copies the rows out to
+//     HBM as 16-byte stores (HA1 / HA2 for the backward, dH2 / dH1 for the
+//     weight gradients).
+// The narrow last layer (<= 16 outputs: the 8 action means, the value) splits
+// its k chunks over the four waves and sums the four partials in a fixed order.
+//
+// The backward chain dH2 = (dZ W3) * [HA2 > 0], dH1 = (dH2 W2) * [HA1 > 0],
+// dX = dH1 W1[:, cols] reads W2 and W1 TRANSPOSED (k contiguous again): the
+// forward of the same phase writes W1^T and W2^T as a side job (the weights do
+// not change between a phase's forward and backward), so the backward's
+// weight reads are 16-byte reads too.  dZ W3 has K = out <= 16 (8 actions or
+// the value): a VALU pass in the order of the streaming small-K kernel.
+//
+// Rows are the learner's [step][segment] rows; the weight gradients of the
+// three layers stay in the phase's grouped dW launch (linear_kernels.hip).
+#include "smi_device.hpp"
+#include "smi_internal.hpp"
+
+namespace smi {
+
+constexpr int HC_R = 16;                 // rows per workgroup
+constexpr int HC_MAXK = 512;             // widest layer input / output handled here
+constexpr int HC_SR = 32 * 33 + 32;     // last-layer partials (1024) / a transpose tile (1056)
+
+struct HeadFwdArgs {
+  const float* X; int64_t ldx; int K0;   // input rows [rows][ldx], K0 features
+  const float* W1; const float* b1;      // [h1][K0]
+  const float* W2; const float* b2;      // [h2][h1]
+  const float* W3; const float* b3;      // [out][h2]
+  int h1, h2, out, tanh_out;
+  float* HA1; float* HA2;                // [rows][h1], [rows][h2] (post-ReLU)
+  float* Y; int64_t ldy;                 // [rows][ldy]
+  float* W1T; float* W2T;                // optional: [K0][h1], [h1][h2] for the backward
+  int64_t rows; const int* skip;
+  int ld0, ld1, ld2;                     // LDS leading dims (floats)
+};
+
+struct HeadBwdArgs {
+  const float* dZ; int out;              // [rows][out]: gradient at the last pre-activation
+  const float* W3;                       // [out][h2]
+  const float* W2T;                      // [h1][h2] (forward's transpose)
+  const float* W1T;                      // [in][h1] (forward's transpose)
+  int h1, h2, dx0, dxn;                  // dX columns [dx0, dx0 + dxn) of the head input
+  const float* HA1; const float* HA2;    // forward activations (ReLU masks)
+  float* dH2; float* dH1;                // [rows][h2], [rows][h1]
+  float* dX; int64_t lddx;               // [rows][lddx]
+  const float* mask; int64_t ldm;        // optional: dX zero where mask <= 0
+  int64_t rows; const int* skip;
+  int ld2, ld1;                          // LDS leading dims
+};
+
+// LDS leading dim of a K-wide activation tile: K rounded up to the 16-k chunk,
+// + 4 (an odd multiple of 4 floats: the 16 rows of a chunk read land on 16
+// distinct 16-byte bank groups)
+__host__ __device__ inline int hc_ld(int k) { return ((k + 15) & ~15) + 4; }
+
+// A barrier for LDS hand-offs between the waves only: the fences are limited
+// to the LDS address space, so global loads in flight (the next layer's weight
+// prefetch) stay in flight across it instead of being drained (a plain
+// __syncthreads() waits vmcnt(0))
+__device__ __forceinline__ void hc_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// The weight stream of one layer: output tiles nt = nt0 + ntst * t (t < NT,
+// nt < ceil(N / 16)) over the k chunks c0, c0 + cst, ... (< ceil(K / 16)).
+// init() issues the weight reads of the first two chunks, which need nothing
+// from the layer's input: a layer's init runs before the previous layer's
+// epilogue and barrier, so those reads are in flight meanwhile.
+template <int NT>
+struct HcStream {
+  const float* wp[NT];
+  float4 b0[NT], b1[NT];
+  int K, nch, c0, cst, ntv;
+  // k past K (the last chunk of a K % 16 != 0 layer) reads the row's last
+  // float4 instead (clamped address: no branch, no select after the load) and
+  // meets A = 0 there: the LDS tiles are zero-padded up to the chunk.  Loads
+  // are issued unconditionally (chunk indices clamped): a load issued on one
+  // path only made the waitcnt pass assume the shorter queue everywhere and
+  // wait for nearly every load in flight.
+  __device__ __forceinline__ void ldb(int c, float4 (&b)[NT]) {
+    const int lk = (threadIdx.x & 63) >> 4;
+    const int kk = min(16 * c + 4 * lk, K - 4);     // K % 4 == 0
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b[t] = *reinterpret_cast<const float4*>(wp[t] + kk);
+  }
+  __device__ __forceinline__ void init(const float* __restrict__ W, int64_t ldw, int K_, int N,
+                                       int nt0, int ntst, int c0_, int cst_) {
+    const int li = threadIdx.x & 15;
+    const int CT = (N + 15) >> 4;
+    K = K_; nch = (K + 15) >> 4; c0 = c0_; cst = cst_;
+    // tiles of this wave that exist (wave-uniform)
+    ntv = __builtin_amdgcn_readfirstlane(nt0 < CT ? (CT - 1 - nt0) / ntst + 1 : 0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = min(16 * (nt0 + ntst * t) + li, N - 1);
+      wp[t] = W + (int64_t)n * ldw;
+    }
+    ldb(min(c0, nch - 1), b0);
+    ldb(min(c0 + cst, nch - 1), b1);
+  }
+};
+
+// acc[t] = A[16][K] (LDS, lda) x W^T over the stream's tiles and chunks
+template <int NT>
+__device__ __forceinline__ void hc_run(HcStream<NT>& S, const float* sA, int lda,
+                                       f32x4 (&acc)[NT]) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (S.ntv == 0) return;
+  const float* ap = sA + li * lda + 4 * lk;
+  // every tile slot runs (a slot past the last tile reads clamped rows and its
+  // result is dropped): per-tile guards made the compiler move the
+  // accumulators out of AGPRs every chunk.  NT is chosen per layer so that at
+  // most one slot per wave is idle.
+  auto mm = [&](const float4& a, const float4 (&b)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc[t] = mfma4(a.x, b[t].x, acc[t]);
+      acc[t] = mfma4(a.y, b[t].y, acc[t]);
+      acc[t] = mfma4(a.z, b[t].z, acc[t]);
+      acc[t] = mfma4(a.w, b[t].w, acc[t]);
+    }
+  };
+  auto lda_ = [&](int c) { return *reinterpret_cast<const float4*>(ap + 16 * c); };
+  const int nch = S.nch, cst = S.cst, cl = nch - 1;
+  int c = S.c0;
+  float4 a0 = lda_(min(c, cl)), a1 = lda_(min(c + cst, cl));
+  // steady state without conditionals (two chunks per trip, both refills
+  // issued): the waitcnt pass then sees the two slots' loads in flight and
+  // waits for exactly the slot it consumes
+  for (; c + 3 * cst < nch; c += 2 * cst) {
+    mm(a0, S.b0);
+    a0 = lda_(c + 2 * cst);
+    S.ldb(c + 2 * cst, S.b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(a1, S.b1);
+    a1 = lda_(c + 3 * cst);
+    S.ldb(c + 3 * cst, S.b1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // the last <= 3 chunks
+  if (c < nch) mm(a0, S.b0);
+  a0 = lda_(min(c + 2 * cst, cl));
+  S.ldb(min(c + 2 * cst, cl), S.b0);
+  if (c + cst < nch) mm(a1, S.b1);
+  if (c + 2 * cst < nch) mm(a0, S.b0);
+}
+
+// the wave's tiles of a full-width layer into LDS rows: D(row 4lk + i, col li)
+// of tile nt is element [4lk + i][16 nt + li]; EPI 0: + bias, ReLU; 1: * [mask > 0]
+// (mask row-major [rows][N] in global memory, rows r0..); columns N..16*CT-1
+// are written as zeros (the next layer's last chunk reads them)
+// Its operands (the bias, or the 4 mask values of each of the lane's rows)
+// are fetched by hc_epi_load BEFORE the layer's k loop, so their latency hides
+// behind it instead of serializing one tile at a time after it.
+template <int NT, int EPI>
+__device__ __forceinline__ void hc_epi_load(int nt0, int N, const float* bias, const float* mask,
+                                            int64_t r0, int64_t rows, float (&e)[NT][4]) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int nc = min(16 * (nt0 + 4 * t) + li, N - 1);     // clamped: unconditional loads
+    if constexpr (EPI == 0) {
+      e[t][0] = bias[nc];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t r = r0 + 4 * lk + i;
+        e[t][i] = mask[(r < rows ? r : rows - 1) * N + nc];
+      }
+    }
+  }
+}
+
+template <int NT, int EPI>
+__device__ __forceinline__ void hc_store(const f32x4 (&acc)[NT], const float (&e)[NT][4], int nt0,
+                                         int N, float* sO, int ldo) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int CT = (N + 15) >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int nt = nt0 + 4 * t;
+    if (nt >= CT) break;
+    const int n = 16 * nt + li;
+    const bool nv = n < N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * lk + i;
+      float v;
+      if constexpr (EPI == 0) {
+        v = acc[t][i] + e[t][0];
+        v = v > 0.f ? v : 0.f;
+      } else {
+        v = e[t][i] > 0.f ? acc[t][i] : 0.f;
+      }
+      sO[r * ldo + n] = nv ? v : 0.f;
+    }
+  }
+}
+
+// rows r0.. of an LDS tile [16][ld] (N columns, N % 4 == 0, N <= HC_MAXK) to
+// global [rows][N]: thread (r, q0) copies row r's float4 columns q0, q0 + 16,
+// ...; every LDS read first, into distinct registers, then every store (a
+// loop reusing one register made each store wait for the previous one)
+__device__ __forceinline__ void hc_copy_out(const float* sO, int ld, int N, float* __restrict__ G,
+                                           int64_t r0, int64_t rows) {
+  constexpr int J = HC_MAXK / 4 / 16;
+  const int nq = N >> 2, r = threadIdx.x >> 4, q0 = threadIdx.x & 15;
+  float4 v[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int q = q0 + 16 * j;
+    v[j] = q < nq ? *reinterpret_cast<const float4*>(sO + r * ld + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (r0 + r >= rows) return;
+  float* g = G + (r0 + r) * N;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int q = q0 + 16 * j;
+    if (q < nq) *reinterpret_cast<float4*>(g + 4 * q) = v[j];
+  }
+}
+
+// W [M][K] -> WT [K][M] in 32 x 32 tiles (tile index tix over both matrices)
+__device__ __forceinline__ void hc_transpose_tile(const float* __restrict__ W, int M, int K,
+                                                  float* __restrict__ WT, int tix, float* sT) {
+  const int tk = (K + 31) >> 5;
+  const int m0 = (tix / tk) * 32, k0 = (tix % tk) * 32;
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * 32; e += kWG) {
+    const int r = e >> 5, c = e & 31;
+    if (m0 + r < M && k0 + c < K) sT[r * 33 + c] = W[(int64_t)(m0 + r) * K + k0 + c];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * 32; e += kWG) {
+    const int r = e >> 5, c = e & 31;           // WT row k0 + r, column m0 + c
+    if (k0 + r < K && m0 + c < M) WT[(int64_t)(k0 + r) * M + m0 + c] = sT[c * 33 + r];
+  }
+}
+
+template <int NT1, int NT2>
+__global__ void __launch_bounds__(kWG)
+head_fwd_kernel(HeadFwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  float* s0 = hsm;                                // [16][ld0]  X
+  float* s1 = s0 + HC_R * a.ld0;                  // [16][ld1]  HA1
+  float* s2 = s1 + HC_R * a.ld1;                  // [16][ld2]  HA2
+  float* sR = s2 + HC_R * a.ld2;                  // [4][64][4] partials of the last layer;
+                                                  // [32][33] transpose tile
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * HC_R;
+  if (r0 < a.rows) {
+    // layer 1's weight stream and bias first: in flight while X arrives
+    HcStream<NT1> S1;
+    S1.init(a.W1, a.K0, a.K0, a.h1, wave, 4, 0, 1);
+    float e1[NT1][4];
+    hc_epi_load<NT1, 0>(wave, a.h1, a.b1, nullptr, r0, a.rows, e1);
+    // X rows into LDS (columns K0 .. ld0 - 4 zero: the last chunk's padding)
+    const int q0 = (a.ld0 - 4) >> 2;
+    for (int e = threadIdx.x; e < HC_R * q0; e += kWG) {
+      const int r = e / q0, q = e - r * q0;
+      const int64_t rr = r0 + r < a.rows ? r0 + r : a.rows - 1;
+      float4 v = {0.f, 0.f, 0.f, 0.f};
+      if (4 * q < a.K0) v = *reinterpret_cast<const float4*>(a.X + rr * a.ldx + 4 * q);
+      *reinterpret_cast<float4*>(s0 + r * a.ld0 + 4 * q) = v;
+    }
+    __syncthreads();
+    HcStream<NT2> S2;
+    float e2[NT2][4];
+    {   // layer 1: HA1 = relu(X W1^T + b1)
+      f32x4 acc[NT1];
+      hc_run<NT1>(S1, s0, a.ld0, acc);
+      S2.init(a.W2, a.h1, a.h1, a.h2, wave, 4, 0, 1);     // layer 2's stream, in flight
+      hc_epi_load<NT2, 0>(wave, a.h2, a.b2, nullptr, r0, a.rows, e2);
+      hc_store<NT1, 0>(acc, e1, wave, a.h1, s1, a.ld1);
+    }
+    hc_sync();
+    hc_copy_out(s1, a.ld1, a.h1, a.HA1, r0, a.rows);
+    HcStream<1> S3;
+    {   // layer 2: HA2 = relu(HA1 W2^T + b2)
+      f32x4 acc[NT2];
+      hc_run<NT2>(S2, s1, a.ld1, acc);
+      S3.init(a.W3, a.h2, a.h2, a.out, 0, 1, wave, 4);    // layer 3's stream
+      hc_store<NT2, 0>(acc, e2, wave, a.h2, s2, a.ld2);
+    }
+    hc_sync();
+    hc_copy_out(s2, a.ld2, a.h2, a.HA2, r0, a.rows);
+    {   // layer 3 (out <= 16): the waves split the k chunks, fixed-order sum
+      const float bn = a.b3[li < a.out ? li : a.out - 1];
+      f32x4 acc[1];
+      hc_run<1>(S3, s2, a.ld2, acc);
+      *reinterpret_cast<float4*>(sR + (wave * 64 + lane) * 4) =
+          float4{acc[0][0], acc[0][1], acc[0][2], acc[0][3]};
+      hc_sync();
+      if (wave == 0 && li < a.out) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * lk + i;
+          if (r0 + r >= a.rows) continue;
+          const float v = ((sR[(0 * 64 + lane) * 4 + i] + sR[(1 * 64 + lane) * 4 + i]) +
+                           (sR[(2 * 64 + lane) * 4 + i] + sR[(3 * 64 + lane) * 4 + i])) + bn;
+          a.Y[(r0 + r) * a.ldy + li] = a.tanh_out ? tanhf(v) : v;
+        }
+      }
+    }
+  }
+  // side job for the backward of the same phase: W1^T, W2^T
+  if (a.W1T) {
+    const int t1 = ((a.h1 + 31) >> 5) * ((a.K0 + 31) >> 5);
+    const int t2 = ((a.h2 + 31) >> 5) * ((a.h1 + 31) >> 5);
+    for (int tix = blockIdx.x; tix < t1 + t2; tix += gridDim.x) {
+      if (tix < t1) hc_transpose_tile(a.W1, a.h1, a.K0, a.W1T, tix, sR);
+      else hc_transpose_tile(a.W2, a.h2, a.h1, a.W2T, tix - t1, sR);
+    }
+  }
+}
+
+template <int NTA, int NTB>
+__global__ void __launch_bounds__(kWG)
+head_bwd_kernel(HeadBwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  float* s2 = hsm;                                // [16][ld2]  dH2
+  float* s1 = s2 + HC_R * a.ld2;                  // [16][ld1]  dH1
+  float* sZ = s1 + HC_R * a.ld1;                  // [16][16]   dZ
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * HC_R;
+  const int out = a.out;
+  // dZ rows (zero past out: the dH2 pass runs whole groups of 8 k), loaded
+  // first; dH1's weight stream (W2^T) and its masks are issued behind them and
+  // stay in flight through the dZ W3 pass
+  const int zr = threadIdx.x >> 4, zk = threadIdx.x & 15;
+  const float zv = a.dZ[min(r0 + zr, a.rows - 1) * out + min(zk, out - 1)];
+  HcStream<NTA> SA;
+  SA.init(a.W2T, a.h2, a.h2, a.h1, wave, 4, 0, 1);
+  float eA[NTA][4];
+  hc_epi_load<NTA, 1>(wave, a.h1, nullptr, a.HA1, r0, a.rows, eA);
+  sZ[zr * 16 + zk] = zk < out ? zv : 0.f;
+  // padding columns of dH2 (the next layer's last chunk)
+  const int h2p = a.ld2 - 4;
+  for (int e = threadIdx.x; e < HC_R * (h2p - a.h2); e += kWG) {
+    const int r = e / (h2p - a.h2), c = e - r * (h2p - a.h2);
+    s2[r * a.ld2 + a.h2 + c] = 0.f;
+  }
+  __syncthreads();
+  {   // dH2 = (dZ W3) * [HA2 > 0], K = out: lane = a 4-column group, wave = 4
+      // rows; the k-ordered fmaf chain from 0 (steps k >= out add 0 * w)
+    const int nq = a.h2 >> 2;            // <= 128: at most two passes, unrolled (a loop
+#pragma unroll                           // header made the first pass drain every load
+    for (int q0 = 0; q0 < 128; q0 += 64) {  // in flight, the weight prefetch included)
+      if (q0 >= nq) break;
+      const bool qv = q0 + lane < nq;
+      const int q = qv ? q0 + lane : nq - 1;
+      float4 m[4], v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t rr = min(r0 + 4 * wave + i, a.rows - 1);
+        m[i] = *reinterpret_cast<const float4*>(a.HA2 + rr * a.h2 + 4 * q);
+        v[i] = float4{0.f, 0.f, 0.f, 0.f};
+      }
+      for (int kg = 0; kg < out; kg += 8) {
+        float4 w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          w[j] = *reinterpret_cast<const float4*>(a.W3 + (int64_t)min(kg + j, out - 1) * a.h2 + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float z = sZ[(4 * wave + i) * 16 + kg + j];
+            v[i].x = fmaf(z, w[j].x, v[i].x); v[i].y = fmaf(z, w[j].y, v[i].y);
+            v[i].z = fmaf(z, w[j].z, v[i].z); v[i].w = fmaf(z, w[j].w, v[i].w);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * wave + i;
+        const float4 o = {m[i].x > 0.f ? v[i].x : 0.f, m[i].y > 0.f ? v[i].y : 0.f,
+                          m[i].z > 0.f ? v[i].z : 0.f, m[i].w > 0.f ? v[i].w : 0.f};
+        if (qv) {
+          *reinterpret_cast<float4*>(s2 + r * a.ld2 + 4 * q) = o;
+          if (r0 + r < a.rows) *reinterpret_cast<float4*>(a.dH2 + (r0 + r) * a.h2 + 4 * q) = o;
+        }
+      }
+    }
+  }
+  hc_sync();
+  HcStream<NTB> SB;
+  {   // dH1 = (dH2 W2) * [HA1 > 0] = dH2 (W2^T)^T
+    f32x4 acc[NTA];
+    hc_run<NTA>(SA, s2, a.ld2, acc);
+    if (a.dxn > 0)      // dX's weight stream (rows dx0.. of W1^T), in flight
+      SB.init(a.W1T + (int64_t)a.dx0 * a.h1, a.h1, a.h1, a.dxn, wave, 4, 0, 1);
+    hc_store<NTA, 1>(acc, eA, wave, a.h1, s1, a.ld1);
+  }
+  hc_sync();
+  hc_copy_out(s1, a.ld1, a.h1, a.dH1, r0, a.rows);
+  if (a.dxn <= 0) return;
+  {   // dX = dH1 W1[:, dx0 : dx0 + dxn]
+    f32x4 acc[NTB];
+    hc_run<NTB>(SB, s1, a.ld1, acc);
+    const int CT = (a.dxn + 15) >> 4;
+#pragma unroll
+    for (int t = 0; t < NTB; ++t) {
+      const int nt = wave + 4 * t;
+      if (nt >= CT) break;
+      const int n = 16 * nt + li;
+      if (n >= a.dxn) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t r = r0 + 4 * lk + i;
+        if (r >= a.rows) continue;
+        float v = acc[t][i];
+        if (a.mask) v = a.mask[r * a.ldm + n] > 0.f ? v : 0.f;
+        a.dX[r * a.lddx + n] = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host side
+static int use_head_fused() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("SMI_HEAD_FUSED");
+    u = (e && e[0] == '0') ? 0 : 1;
+  }
+  return u;
+}
+
+static int hc_nt(int n) {                        // tiles per wave, rounded to an instantiation
+  const int t = (((n + 15) >> 4) + 3) >> 2;
+  return t <= 2 ? 2 : t <= 4 ? t : t <= 5 ? 5 : 8;     // 2, 3, 4, 5, 8
+}
+
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// shapes the fused chains take (the caller falls back to the layer GEMMs
+// otherwise); the backward additionally needs dxn <= 320 (its dX tiles)
+bool head_fused_ok(int in, int64_t ldx, int h1, int h2, int out, const float* X,
+                   const float* W1, const float* W2, const float* W3) {
+  return use_head_fused() && in >= 4 && in <= 320 && in % 4 == 0 && ldx % 4 == 0 &&
+         h1 >= 4 && h1 <= HC_MAXK && h1 % 4 == 0 && h2 >= 4 && h2 <= HC_MAXK && h2 % 4 == 0 &&
+         out >= 1 && out <= 16 && al16(X) && al16(W1) && al16(W2) && al16(W3);
+}
+
+int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
+                          const float* b1, int h1, const float* W2, const float* b2, int h2,
+                          const float* W3, const float* b3, int out, int tanh_out, float* HA1,
+                          float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
+                          hipStream_t st, const int* skip) {
+  if (rows <= 0) return SMI_OK;
+  HeadFwdArgs a{X, ldx, in, W1, b1, W2, b2, W3, b3, h1, h2, out, tanh_out, HA1, HA2, Y, ldy,
+                W1T, W2T, rows, skip, hc_ld(in), hc_ld(h1), hc_ld(h2)};
+  const size_t lds = (size_t)(HC_R * (a.ld0 + a.ld1 + a.ld2) + HC_SR) * 4;
+  const dim3 grid((unsigned)((rows + HC_R - 1) / HC_R));
+  const int n1 = hc_nt(h1), n2 = hc_nt(h2);
+  const int kslot = ktime_begin(st);
+#define SMI_HF(A, B)                                                              \
+  do {                                                                            \
+    allow_lds(head_fwd_kernel<A, B>, lds);                                        \
+    hipLaunchKernelGGL((head_fwd_kernel<A, B>), grid, dim3(kWG), lds, st, a);     \
+  } while (0)
+  // layer-1 slots {2, 5, 8} x layer-2 slots {2, 3, 4, 5, 8} (C3 / C5: 300 x 200 -> 5, 4)
+  const int m1 = n1 <= 2 ? 2 : n1 <= 5 ? 5 : 8;
+#define SMI_HF2(A)                                        \
+  do {                                                    \
+    switch (n2) {                                         \
+      case 2: SMI_HF(A, 2); break;                        \
+      case 3: SMI_HF(A, 3); break;                        \
+      case 4: SMI_HF(A, 4); break;                        \
+      case 5: SMI_HF(A, 5); break;                        \
+      default: SMI_HF(A, 8); break;                       \
+    }                                                     \
+  } while (0)
+  if (m1 == 2) SMI_HF2(2);
+  else if (m1 == 5) SMI_HF2(5);
+  else SMI_HF2(8);
+#undef SMI_HF2
+#undef SMI_HF
+  ktime_end(kslot, KT_GEMM_FWD,
+            2.0 * (double)rows * ((double)in * h1 + (double)h1 * h2 + (double)h2 * out), st);
+  return check_launch("head_fwd_kernel");
+}
+
+int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
+                          const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
+                          const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
+                          int64_t lddx, const float* mask, int64_t ldm, hipStream_t st,
+                          const int* skip) {
+  if (rows <= 0) return SMI_OK;
+  HeadBwdArgs a{dZ, out, W3, W2T, W1T, h1, h2, dx0, dxn, HA1, HA2, dH2, dH1, dX, lddx, mask, ldm,
+                rows, skip, hc_ld(h2), hc_ld(h1)};
+  const size_t lds = (size_t)(HC_R * (a.ld2 + a.ld1) + HC_R * 16) * 4;
+  const dim3 grid((unsigned)((rows + HC_R - 1) / HC_R));
+  int na = hc_nt(h1), nb = hc_nt(dxn > 0 ? dxn : 1);
+  na = na <= 2 ? 2 : na <= 5 ? 5 : 8;
+  nb = nb <= 2 ? 2 : 5;
+  const int kslot = ktime_begin(st);
+#define SMI_HB(A, B)                                                              \
+  do {                                                                            \
+    allow_lds(head_bwd_kernel<A, B>, lds);                                        \
+    hipLaunchKernelGGL((head_bwd_kernel<A, B>), grid, dim3(kWG), lds, st, a);     \
+  } while (0)
+  if (na == 2 && nb == 2) SMI_HB(2, 2);
+  else if (na == 2) SMI_HB(2, 5);
+  else if (na == 5 && nb == 2) SMI_HB(5, 2);
+  else if (na == 5) SMI_HB(5, 5);
+  else if (nb == 2) SMI_HB(8, 2);
+  else SMI_HB(8, 5);
+#undef SMI_HB
+  ktime_end(kslot, KT_GEMM_DX,
+            2.0 * (double)rows * ((double)out * h2 + (double)h2 * h1 + (double)h1 * dxn), st);
+  return check_launch("head_bwd_kernel");
+}
+
+}  // namespace smi

@@ -1248,17 +1248,22 @@ static bool dw_group_add(const GemmArgs& g) {
   return true;
 }
 
-// target workgroups of a grouped launch (SMI_DWD_GROUP_TARGET; tuning knob)
-static int dw_group_target() {
-  static int t = 0;
-  if (!t) {
-    // measured at C3 (bench, one MI355X): 256 -> 4.44 ms of dW per learn, 512 ->
-    // 3.71, 768 -> 3.17, 1024 -> 2.83 (45 TF/s), 1536 -> 3.32, 3072 -> 4.43
+// target workgroups of a grouped launch for `work` tile-rows (SMI_DWD_GROUP_TARGET
+// overrides; tuning knob).  Measured at C3 (bench, one MI355X), 21504 rows:
+// 256 -> 4.44 ms of dW per learn, 512 -> 3.71, 768 -> 3.17, 1024 -> 2.83
+// (45 TF/s), 1536 -> 3.32, 3072 -> 4.43; at 2688 rows (one rank of eight,
+// tools/bench_dwgroup.py --segments 128): 1024 -> 65 us per launch (128-row
+// slabs), 512 -> 48, 256 -> 46: slabs shorter than ~384 rows are all ramp.
+static int dw_group_target(double work) {
+  static int t = -1;
+  if (t < 0) {
     const char* e = getenv("SMI_DWD_GROUP_TARGET");
-    t = e ? atoi(e) : 1024;
-    if (t < 64) t = 64;
+    t = e ? atoi(e) : 0;
+    if (e && t < 64) t = 64;
   }
-  return t;
+  if (t > 0) return t;
+  const double w = work / 384.0;
+  return w >= 1024.0 ? 1024 : w <= 128.0 ? 128 : (int)w;
 }
 
 // narrow 16-wide tail tiles in grouped launches (SMI_DWD_NARROW=0: off; A/B knob)
@@ -1289,7 +1294,7 @@ int dw_group_flush(hipStream_t st) {
     work += (double)tiles[i] * g.K;
   }
   const int64_t cap = smi_workspace_floats();
-  int64_t rows = (int64_t)(work / dw_group_target()) + 1;
+  int64_t rows = (int64_t)(work / dw_group_target(work)) + 1;
   rows = (rows + rs - 1) / rs * rs;
   if (rows < 2 * rs) rows = 2 * rs;                 // >= 8 MFMA steps per wave
   int64_t need = 0;

@@ -885,7 +885,15 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   constexpr int KXS = KX > 0 ? KX : 4;
   __shared__ __attribute__((aligned(16))) float hS[2][R * KP];
-  __shared__ __attribute__((aligned(16))) float xS[3][R * KXS];
+  // KX > 0: the segment rows' x for EVERY step, staged once before the
+  // recurrence (S x R x KXS floats, dynamic LDS): the step loop then issues no
+  // loads at all, so nothing in it waits on memory (a per-step prefetch made
+  // each step wait for its own stores: vmcnt counts loads and stores in order).
+  // Then every step's x part x_t W_ih[g] + biases is formed up front, off the
+  // recurrence's critical path, into xP [S][R][blockDim] (each thread reads
+  // back only its own values: no barrier).
+  extern __shared__ __attribute__((aligned(16))) float xS[];
+  float* xP = xS + (((int64_t)a.S * R * KXS + 3) & ~3);
   const int H = a.H, B = a.B, G4 = 4 * H;
   const int tid = threadIdx.x, u = tid >> 2, q = tid & 3;
   const bool act = u < H;
@@ -917,19 +925,14 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
     bseg[r] = r0 + r < B ? r0 + r : B - 1;
   }
   // x staging (KX > 0): thread e < R*KX owns (row e / KX, k e % KX) of x_t
-  const int xr = tid / KXS, xk = tid - (tid / KXS) * KXS;
-  const bool xown = KX > 0 && tid < R * KXS;
-  const int64_t xoff0 = (int64_t)min(r0 + xr, B - 1) * a.ldx + min(xk, a.din > 0 ? a.din - 1 : 0);
-  const bool xval = xk < a.din;
-  auto xload = [&](int t) -> float {
-    const float v = a.x[(int64_t)t * B * a.ldx + xoff0];
-    return xval ? v : 0.f;
-  };
-  float xnext = 0.f;
   if constexpr (KX > 0) {
-    if (xown && a.S > 0) xS[0][xr * KXS + xk] = xload(0);
-    if (xown && a.S > 1) xS[1][xr * KXS + xk] = xload(1);
-    if (xown && a.S > 2) xnext = xload(2);
+    for (int e = tid; e < a.S * R * KXS; e += blockDim.x) {
+      const int t = e / (R * KXS), q = e - t * (R * KXS);
+      const int r = q / KXS, k = q - r * KXS;
+      float v = 0.f;
+      if (k < a.din && r0 + r < B) v = a.x[((int64_t)t * B + r0 + r) * a.ldx + k];
+      xS[e] = v;
+    }
   }
   float creg[R];
 #pragma unroll
@@ -948,11 +951,11 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
   __syncthreads();
   // x part of step t (+ the combined bias)
   float xacc[R];
-  auto x_part = [&](int t, int xb) {
+  auto x_part = [&](int t) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if constexpr (KX > 0) {
-        const float4* xp = reinterpret_cast<const float4*>(xS[xb] + r * KXS);
+        const float4* xp = reinterpret_cast<const float4*>(xS + (t * R + r) * KXS);
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
         for (int k4 = 0; k4 < KX / 4; ++k4) {
@@ -961,7 +964,7 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
           s1 = fmaf(v.y, wx[4 * k4 + 1], s1);
           s2 = fmaf(v.z, wx[4 * k4 + 2], s2);
           s3 = fmaf(v.w, wx[4 * k4 + 3], s3);
-          if (k4 & 1) __builtin_amdgcn_sched_barrier(0);
+          if ((k4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         xacc[r] = (s0 + s1) + (s2 + s3);
       } else {
@@ -969,19 +972,42 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
       }
     }
   };
-  if (a.S > 0) x_part(0, 0);
-  int xb = 1;                                    // x ring slot of step t+1
+  float xpn[R];                                  // KX == 0: xproj of step t+1, in flight
+  if constexpr (KX > 0) {
+    for (int t = 0; t < a.S; ++t) {
+      x_part(t);
+#pragma unroll
+      for (int r = 0; r < R; ++r) xP[(t * R + r) * blockDim.x + tid] = xacc[r];
+    }
+  } else {
+    if (a.S > 0) x_part(0);
+  }
+  // drain the prologue's loads here: otherwise the waitcnt pass sees the c0
+  // load (creg) possibly in flight at the loop header and puts a vmcnt(0)
+  // INSIDE the loop, before every step's cell update
+  __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
   for (int t = 0; t < a.S; ++t) {
     const float* hp = hS[t & 1];
     float* hn = hS[(t + 1) & 1];
+    // x_{t+2}: issued before this step's stores, so the LDS write at the end
+    // of the step waits for this load only (vmcnt counts in issue order)
+    if constexpr (KX == 0) {       // xproj of step t+1, issued before this step's stores
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        xpn[r] = a.xproj[((int64_t)(t + 1 < a.S ? t + 1 : t) * B + bseg[r]) * G4 + g];
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) xacc[r] = xP[(t * R + r) * blockDim.x + tid];
+    }
     // one segment after the other (a sched_barrier between them): interleaving
     // the R matvecs keeps R x (h reads + accumulators) live next to the
     // KP + KX weight registers and spills from R = 2
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-      // chunks of 8 k: without the sched_barrier the compiler hoists every
-      // h_{t-1} LDS read of the step ahead of the FMAs
+      // chunks of 16 k (4 LDS reads in flight per round trip): without the
+      // sched_barrier the compiler hoists every h_{t-1} LDS read of the step
+      // ahead of the FMAs
 #pragma unroll
       for (int k4 = 0; k4 < KP / 4; ++k4) {
         const float4 hv = *reinterpret_cast<const float4*>(hp + r * KP + 4 * k4);
@@ -989,7 +1015,7 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
         acc1 = fmaf(hv.y, w[4 * k4 + 1], acc1);
         acc2 = fmaf(hv.z, w[4 * k4 + 2], acc2);
         acc3 = fmaf(hv.w, w[4 * k4 + 3], acc3);
-        if (k4 & 1) __builtin_amdgcn_sched_barrier(0);
+        if ((k4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
       const float pre = xacc[r] + (((acc0 + acc1) + (acc2 + acc3)) + bh);
       const float av = q == 2 ? ftanh(pre) : sigm(pre);
@@ -1009,13 +1035,10 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (t + 1 < a.S) x_part(t + 1, xb);
-    if constexpr (KX > 0) {   // x_{t+2} into the ring slot x_{t-1} used, x_{t+3} in flight
-      const int wb = xb == 2 ? 0 : xb + 1;
-      if (xown && t + 2 < a.S) xS[wb][xr * KXS + xk] = xnext;
-      if (xown && t + 3 < a.S) xnext = xload(t + 3);
+    if constexpr (KX == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) xacc[r] = xpn[r];
     }
-    xb = xb == 2 ? 0 : xb + 1;
     __syncthreads();
   }
 }
@@ -1046,43 +1069,52 @@ lstm_bwd_v_kernel(LstmBwdArgs a) {
     okr[r] = act && r0 + r < B;
     bseg[r] = r0 + r < B ? r0 + r : B - 1;
   }
-  float gq[R], ct[R], ctm[R], dho[R], dcreg[R], dhr[R];
-  auto fetch = [&](int t) {
+  // per-step inputs, fetched two steps ahead into alternating register sets:
+  // a step's loads are issued right after its dgates store and used two steps
+  // later, so neither their latency nor the stores ahead of them (vmcnt counts
+  // loads and stores in issue order) reach the critical path
+  struct In { float gq[R], ct[R], ctm[R], dho[R]; };
+  In A, Bn;
+  float dcreg[R], dhr[R];
+  auto fetch = [&](int t, In& X) {               // t clamped by the caller: always issued
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t b = bseg[r];
-      gq[r] = a.gates[((int64_t)t * B + b) * G4 + g];
-      ct[r] = a.cbuf[(int64_t)(t + 1) * BH + b * H + uc];
-      ctm[r] = a.cbuf[(int64_t)t * BH + b * H + uc];
-      dho[r] = a.dh[(int64_t)t * BH + b * H + uc];
+      X.gq[r] = a.gates[((int64_t)t * B + b) * G4 + g];
+      X.ct[r] = a.cbuf[(int64_t)(t + 1) * BH + b * H + uc];
+      X.ctm[r] = a.cbuf[(int64_t)t * BH + b * H + uc];
+      X.dho[r] = a.dh[(int64_t)t * BH + b * H + uc];
     }
   };
 #pragma unroll
   for (int r = 0; r < R; ++r) dcreg[r] = dhr[r] = 0.f;
-  if (a.S > 0) fetch(a.S - 1);
+  if (a.S <= 0) return;
+  fetch(a.S - 1, A);
+  fetch(a.S >= 2 ? a.S - 2 : 0, Bn);
   __syncthreads();
-  for (int t = a.S - 1; t >= 0; --t) {
+  // one step; false after step 0
+  auto step = [&](int t, In& X) -> bool {
     float* dgw = dG[t & 1];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const float ig = quad_bcast<0>(gq[r]), fg = quad_bcast<1>(gq[r]);
-      const float cg = quad_bcast<2>(gq[r]), og = quad_bcast<3>(gq[r]);
-      const float dh = dho[r] + dhr[r];
-      const float tc = ftanh(ct[r]);
+      const float ig = quad_bcast<0>(X.gq[r]), fg = quad_bcast<1>(X.gq[r]);
+      const float cg = quad_bcast<2>(X.gq[r]), og = quad_bcast<3>(X.gq[r]);
+      const float dh = X.dho[r] + dhr[r];
+      const float tc = ftanh(X.ct[r]);
       const float dc = dh * og * (1.f - tc * tc) + dcreg[r];
       const float d_o = (dh * tc) * (og * (1.f - og));
       const float d_i = (dc * cg) * (ig * (1.f - ig));
       const float d_g = (dc * ig) * (1.f - cg * cg);
-      const float d_f = (dc * ctm[r]) * (fg * (1.f - fg));
+      const float d_f = (dc * X.ctm[r]) * (fg * (1.f - fg));
       dcreg[r] = okr[r] ? dc * fg : 0.f;
       float dq = q == 0 ? d_i : q == 1 ? d_f : q == 2 ? d_g : d_o;
       dq = okr[r] ? dq : 0.f;
       if (act) dgw[r * 4 * KP + q * KP + u] = dq;
       if (okr[r]) a.dgates[((int64_t)t * B + bseg[r]) * G4 + g] = dq;
     }
-    if (t > 0) fetch(t - 1);
+    fetch(t >= 2 ? t - 2 : 0, X);
     __syncthreads();
-    if (t == 0) break;
+    if (t == 0) return false;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const float4* dp = reinterpret_cast<const float4*>(dgw + r * 4 * KP + q * KP);
@@ -1094,12 +1126,17 @@ lstm_bwd_v_kernel(LstmBwdArgs a) {
         s1 = fmaf(v.y, w[4 * j4 + 1], s1);
         s2 = fmaf(v.z, w[4 * j4 + 2], s2);
         s3 = fmaf(v.w, w[4 * j4 + 3], s3);
-        if (j4 & 1) __builtin_amdgcn_sched_barrier(0);
+        if ((j4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
       const float p = (s0 + s1) + (s2 + s3);
       // fixed-order quad sum: every lane of the quad gets the same dh_rec
       dhr[r] = (quad_bcast<0>(p) + quad_bcast<1>(p)) + (quad_bcast<2>(p) + quad_bcast<3>(p));
     }
+    return true;
+  };
+  for (int t = a.S - 1; t >= 0; t -= 2) {
+    if (!step(t, A)) break;
+    if (!step(t - 1, Bn)) break;
   }
 }
 
@@ -1138,12 +1175,25 @@ static int lstm_valu_r(int B, int H) {
   return R;
 }
 
+// LDS of the staged x sequence and the precomputed x parts (KX > 0); the fused
+// form is used up to kVxMax (S <= 52 steps at H = 100, x width <= 64)
+constexpr size_t kVxMax = 120 * 1024;
+static size_t lstm_fwd_v_lds(int S, int R, int KX, int blk) {
+  return ((((size_t)S * R * KX + 3) & ~(size_t)3) + (size_t)S * R * blk) * 4;
+}
 template <int R, int KX>
 static void fwd_v_dispatch_kp(const LstmFwdArgs& a, hipStream_t st) {
   const dim3 grid((a.B + R - 1) / R), blk((4 * a.H + 63) & ~63);
-  if (a.H <= 64) hipLaunchKernelGGL((lstm_fwd_v_kernel<R, 64, KX>), grid, blk, 0, st, a);
-  else if (a.H <= 104) hipLaunchKernelGGL((lstm_fwd_v_kernel<R, 104, KX>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((lstm_fwd_v_kernel<R, 128, KX>), grid, blk, 0, st, a);
+  const size_t lds = KX > 0 ? lstm_fwd_v_lds(a.S, R, KX, blk.x) : 0;
+#define SMI_FV(KP)                                                                 \
+  do {                                                                             \
+    allow_lds(lstm_fwd_v_kernel<R, KP, KX>, lds);                                  \
+    hipLaunchKernelGGL((lstm_fwd_v_kernel<R, KP, KX>), grid, blk, lds, st, a);     \
+  } while (0)
+  if (a.H <= 64) SMI_FV(64);
+  else if (a.H <= 104) SMI_FV(104);
+  else SMI_FV(128);
+#undef SMI_FV
 }
 // x W_ih^T fused only at R = 1 (its W_ih row joins the W_hh row in registers:
 // at R >= 2 the two segments' operands no longer fit next to them); R >= 2
@@ -1243,6 +1293,8 @@ int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, c
   if (B <= 0 || S < 0) return SMI_OK;
   const int R = lstm_valu_r(B, H);
   if (R > 1) return SMI_E_NOFIT;                 // xproj GEMM + the VALU recurrence
+  if (R == 1 && lstm_fwd_v_lds(S, 1, din <= 48 ? 48 : 64, (4 * H + 63) & ~63) > kVxMax)
+    return SMI_E_NOFIT;                            // staged x + x parts > the LDS budget
   LstmFwdArgs a{nullptr, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates, skip,
                 x, ldx, din, w_ih, b_ih};
   const int kslot = ktime_begin(st);

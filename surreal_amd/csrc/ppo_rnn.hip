@@ -90,6 +90,8 @@ struct RnnScratch {
   float *Xz, *Xr, *xproj, *hbuf, *cbuf, *gates, *HA1, *HA2, *OUT, *dOUT, *dH1, *dH2, *dh, *dgates;
   // the PREP phase's own copies (it may run on a second stream beside GAE)
   float *xprojR, *hbufR, *HA1R, *HA2R, *A2R;
+  // W1^T | W2^T of the head a phase's fused forward wrote for its backward
+  float *wT;
   float *values, *adv, *ret, *refmu, *lvpart;
   // time-major per-row inputs of the row kernels, packed once per learn:
   // rowin[n] = {actions (A) | behave mu, sigma (2A) | raw advantage | pad},
@@ -151,6 +153,11 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   s.HA1R = take(d.NE * hmax1);
   s.HA2R = take(d.NE * hmax2);
   s.A2R = take(px ? d.NE * d.G.flat : 0);
+  {
+    const int64_t wa = (int64_t)d.Hin * d.h1 + (int64_t)d.h1 * d.h2;
+    const int64_t wc = (int64_t)d.Hin * d.c1 + (int64_t)d.c1 * d.c2;
+    s.wT = take(wa > wc ? wa : wc);
+  }
   s.dA2 = take(px ? d.NE * d.G.flat : 0);
   s.dF = take(px ? d.NE * d.F : 0);
   s.cpart = take(px ? (int64_t)cnn_bwd_grid(d.NE) * d.G.nconv : 0);
@@ -776,9 +783,35 @@ struct Head {   // one MLP head over rows of an activation matrix
   const float* P; MlpLayout L; int in, h1, h2, out, tanh_out;
 };
 
-// forward: X[rows][ldx] -> HA1 -> HA2 -> Y ([rows][out])
+bool head_fused_ok(int in, int64_t ldx, int h1, int h2, int out, const float* X,
+                   const float* W1, const float* W2, const float* W3);
+int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
+                          const float* b1, int h1, const float* W2, const float* b2, int h2,
+                          const float* W3, const float* b3, int out, int tanh_out, float* HA1,
+                          float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
+                          hipStream_t st, const int* skip);
+int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
+                          const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
+                          const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
+                          int64_t lddx, const float* mask, int64_t ldm, hipStream_t st,
+                          const int* skip);
+
+static bool head_fused(const Head& h, const float* X, int64_t ldx) {
+  return head_fused_ok(h.in, ldx, h.h1, h.h2, h.out, X, h.P + h.L.fW1, h.P + h.L.fW2,
+                       h.P + h.L.fW3);
+}
+
+// forward: X[rows][ldx] -> HA1 -> HA2 -> Y ([rows][out]); one fused launch
+// (head_kernels.hip) when the shapes allow, which with wT also writes W1^T | W2^T
+// for a fused backward of the same parameters
 static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, float* HA1,
-                    float* HA2, float* Y, hipStream_t st, const int* skip) {
+                    float* HA2, float* Y, hipStream_t st, const int* skip, float* wT = nullptr) {
+  const MlpLayout& L = h.L;
+  if (head_fused(h, X, ldx))
+    return launch_head_fwd_fused(X, ldx, rows, h.in, h.P + L.fW1, h.P + L.fb1, h.h1, h.P + L.fW2,
+                                 h.P + L.fb2, h.h2, h.P + L.fW3, h.P + L.fb3, h.out, h.tanh_out,
+                                 HA1, HA2, Y, h.out, wT, wT ? wT + (int64_t)h.in * h.h1 : nullptr,
+                                 st, skip);
   const int M = (int)rows;
   RC(launch_linear_fwd(X, ldx, M, h.in, h.P + h.L.fW1, h.in, h.P + h.L.fb1, h.h1, ACT_RELU, HA1,
                        h.h1, st, skip));
@@ -796,9 +829,22 @@ static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, fl
 static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx, int64_t rows,
                     const float* HA1, const float* HA2, float* dH1, float* dH2, float* G,
                     int dx0, int dxn, const float* dxmask, int64_t ldm, float* dXout,
-                    hipStream_t st, const int* skip) {
+                    hipStream_t st, const int* skip, const float* wT = nullptr) {
   const int M = (int)rows;
   const MlpLayout& L = h.L;
+  if (wT && dxn <= 320 && head_fused(h, X, ldx)) {
+    // the input-gradient chain in one launch (dH2, dH1, dX), then the three
+    // weight gradients (queued into the phase's dW group when one is open)
+    RC(launch_head_bwd_fused(dZ, h.out, rows, h.P + L.fW3, wT + (int64_t)h.in * h.h1, wT, h.h1,
+                             h.h2, dx0, dxn, HA1, HA2, dH2, dH1, dXout, dxn, dxmask, ldm, st,
+                             skip));
+    RC(launch_linear_bwd_dw(dZ, h.out, M, h.out, HA2, h.h2, h.h2, G + L.fW3, h.h2, G + L.fb3, 0,
+                            st, skip));
+    RC(launch_linear_bwd_dw(dH2, h.h2, M, h.h2, HA1, h.h1, h.h1, G + L.fW2, h.h1, G + L.fb2, 0,
+                            st, skip));
+    return launch_linear_bwd_dw(dH1, h.h1, M, h.h1, X, ldx, h.in, G + L.fW1, h.in, G + L.fb1, 0,
+                                st, skip);
+  }
   RC(launch_linear_bwd_dw(dZ, h.out, M, h.out, HA2, h.h2, h.h2, G + L.fW3, h.h2, G + L.fb3, 0, st,
                           skip));
   RC(launch_linear_bwd_dx(dZ, h.out, M, h.out, h.P + L.fW3, h.h2, h.h2, HA2, h.h2, dH2, h.h2, st,
@@ -955,13 +1001,13 @@ static int stem_backward_chain(const smi_ppo_rnn_args& a, const RnnDims& d, cons
   const float* X = head_in(d, s, s.Xz);
   if (d.H > 0) {
     RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, 0, d.H, nullptr, 0,
-                s.dh, st, skip));
+                s.dh, st, skip, s.wT));
     RC(lstm_backward(d, a.lstm, G + n_head, s, st, skip));
     return cnn_grad(a, d, lm, cnn, G + n_head + d.nL, s, st, skip);
   }
   // MLP policy: the first head layer's input gradient over the CNN columns only
   RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, d.D, d.F, s.Xz + d.D,
-              d.ldx, s.dF, st, skip));
+              d.ldx, s.dF, st, skip, s.wT));
   if (d.F == 0) return SMI_OK;
   return cnn_bwd_from_dF(a, d, cnn, G + n_head, s, st, skip);
 }
@@ -1074,7 +1120,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       }
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, stop));
       if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, stop));
-      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop));
+      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop, s.wT));
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE, kRowNT);
       const int kt = ktime_begin(st);
@@ -1153,7 +1199,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_VALUE_GRAD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
       if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, nullptr));
-      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr));
+      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr,
+                  s.wT));
       const int nb = rnn_nblk(d.NE, kRowNT);
       const bool last = e == a.epoch_baseline - 1;
       const int kt = ktime_begin(st);

@@ -11,13 +11,19 @@ MI355X side: the learner's parameters live in a handful of flat device
 buffers (model.py), so a snapshot is a few device-to-device copies into a
 snapshot arena, enqueued on the learner's stream right after the last
 learn() (stream-ordered: no host wait), followed by ONE device-to-host copy of
-the arena into pinned memory on a side stream.  The next learn() is enqueued
-immediately and overlaps the D2H; its parameter updates cannot race the copy
-because the copy reads the arena, not the parameters.  A background thread
-waits for the copy and hands the numpy dict — views of the pinned arena
-reshaped to the state_dict shapes, copied out — to the sink.
+the arena into pinned memory on a side stream.  The D2H is a copy KERNEL
+writing the mapped pinned buffer (smi_copy_to_host), not a runtime DMA copy:
+an SDMA hipMemcpyAsync D2H held the learner thread ~0.25 ms per publish
+(tools/diag_publish.py), which the GPU then spent idle.  The next learn() is
+enqueued immediately and overlaps the D2H; its parameter updates cannot race
+the copy because the copy reads the arena, not the parameters.  A background
+thread waits for the copy and hands the numpy dict — views of the pinned
+arena reshaped to the state_dict shapes — to the serializer, then frees the
+slot (no host-side copies: the worker holds the GIL as briefly as possible,
+since any Python it runs delays the learner thread's launches).
 """
 import base64
+import ctypes
 import hashlib
 import pickle
 import queue
@@ -26,6 +32,8 @@ import time
 
 import numpy as np
 import torch
+
+from surreal_amd import _lib as L
 
 
 def binary_hash(binary):
@@ -73,17 +81,19 @@ class Snapshot(object):
         self.time = time.time()
 
     def ready(self):
-        return self._event.query()
+        return self._event.is_set()
 
-    def numpy_dict(self):
-        """{module name: {state_dict key: ndarray}} as ModuleDict.dumps builds it
-        (copies, so the pinned slot can be reused)."""
-        self._event.synchronize()
+    def numpy_dict(self, copy=True):
+        """{module name: {state_dict key: ndarray}} as ModuleDict.dumps builds it.
+        copy=False returns views of the pinned slot (valid until the slot is
+        reused: the publisher's worker serializes from them, then frees it)."""
+        self._event.wait()
         raw = self._host.numpy()
         out = {}
         for name, key, boff, shape, dt in self._layout.keys:
             n = int(np.prod(shape)) * dt.itemsize
-            out.setdefault(name, {})[key] = raw[boff:boff + n].view(dt).reshape(shape).copy()
+            v = raw[boff:boff + n].view(dt).reshape(shape)
+            out.setdefault(name, {})[key] = v.copy() if copy else v
         return out
 
 
@@ -102,6 +112,7 @@ class DeviceParameterPublisher(object):
 
     def __init__(self, module_dict, sink=None, serializer=pickle.dumps, slots=2):
         self.layout = _Layout(module_dict)
+        L.lib()
         dev = self.layout.storages[0][0].device
         self.device = dev
         self.sink = sink
@@ -134,16 +145,29 @@ class DeviceParameterPublisher(object):
             slot['dev'][off:off + nbytes].copy_(view, non_blocking=True)
         taken = torch.cuda.Event()
         taken.record(cur)
-        with torch.cuda.stream(self.side):
-            self.side.wait_event(taken)
-            slot['host'].copy_(slot['dev'], non_blocking=True)   # ONE D2H, off the learner stream
-            done = torch.cuda.Event()
-            done.record(self.side)
-        snap = Snapshot(self.layout, slot['host'], done, iteration, message, slot)
-        # neither half of the slot is rewritten before the worker has copied the
-        # host half out (slot['free'], set after the D2H completed and was read)
+        # the D2H is issued by the worker once the snapshot's D2D has run (it
+        # then overlaps the NEXT learn(); issued here it landed in the window
+        # where the learner thread syncs for the KL record and re-launches)
+        snap = Snapshot(self.layout, slot['host'], threading.Event(), iteration, message, slot)
+        snap._taken = taken
+        # neither half of the slot is rewritten before the worker has serialized
+        # it (slot['free'], set after the D2H completed and was read)
         self._q.put(snap)
         return snap
+
+    def _d2h(self, snap):
+        """worker side: ONE D2H of the slot, off the learner stream, as a kernel
+        into the mapped pinned slot (smi_copy_to_host)"""
+        snap._taken.synchronize()
+        slot = snap._slot
+        with torch.cuda.device(self.device):
+            L.call('smi_copy_to_host', ctypes.c_void_p(slot['host'].data_ptr()),
+                   ctypes.c_void_p(slot['dev'].data_ptr()), self.layout.nbytes,
+                   ctypes.c_void_p(self.side.cuda_stream))
+            done = torch.cuda.Event()
+            done.record(self.side)
+        done.synchronize()
+        snap._event.set()
 
     def _run(self):
         while True:
@@ -151,9 +175,11 @@ class DeviceParameterPublisher(object):
             if snap is None:
                 return
             try:
-                nd = snap.numpy_dict()
-                snap._slot['free'].set()
+                self._d2h(snap)
+                nd = snap.numpy_dict(copy=False)
                 binary = self.serializer(nd)
+                del nd
+                snap._slot['free'].set()
                 info = {'time': snap.time, 'iteration': snap.iteration, 'message': snap.message,
                         'hash': binary_hash(binary)}
                 if self.sink is not None:

@@ -219,18 +219,23 @@ def test_publish_snapshot_does_not_serialize_learn():
     for p_ in (None, fast, full, sync_reference):   # warm: pinned slots, worker threads
         run(p_, 2)
     t = {'plain': [], 'fast': [], 'full': [], 'sync': []}
-    for _ in range(4):                             # interleaved trials, best of each
+    trials = 8
+    for _ in range(trials):                        # interleaved trials
         t['plain'].append(run(None))
         t['fast'].append(run(fast))
         t['full'].append(run(full))
         t['sync'].append(run(sync_reference))
     fast.close()
     full.close()
-    assert len(got) == 2 * (2 + 4 * 8) and all(len(h) == 16 for h in got)
-    best = {k: min(v) for k, v in t.items()}
-    print('publish timing (s per 8 learn + publish):', best)
-    assert best['fast'] <= 1.05 * best['plain'], t
-    assert best['full'] <= best['sync'], t
+    assert len(got) == 2 * (2 + trials * 8) and all(len(h) == 16 for h in got)
+    # paired ratios (each trial's variants ran back to back, so box-level drift
+    # cancels), median over the trials
+    ratio = float(np.median([f / p for f, p in zip(t['fast'], t['plain'])]))
+    ratio_full = float(np.median([f / s for f, s in zip(t['full'], t['sync'])]))
+    print('publish timing (s per 8 learn + publish):', {k: min(v) for k, v in t.items()},
+          'fast/plain', ratio, 'full/sync', ratio_full)
+    assert ratio <= 1.05, t
+    assert ratio_full <= 1.0, t
     # the hash is the reference's binary_hash (serializer.py:55-66), '/' kept
     assert binary_hash(b'surreal') == __import__('base64').b64encode(
         __import__('hashlib').md5(b'surreal').digest())[:16].decode('utf-8')
