@@ -41,7 +41,11 @@ VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             # LSTM activation A/B (the pre-round-2 cancelling tanh)
             'oldtanh': ['-DSMI_OLD_TANH'],
             # dW: the checked loop everywhere (A/B of the unchecked full-slab loop)
-            'nofast': ['-DSMI_DWD_FAST=0']}
+            'nofast': ['-DSMI_DWD_FAST=0'],
+            # fused-head weight ring depth A/B (product: 2)
+            'hcd3': ['-DSMI_HC_DEPTH=3'], 'hcd4': ['-DSMI_HC_DEPTH=4'],
+            # grouped dW tile A/B: 64 x 64 tiles at 3 waves per SIMD
+            'dwg4': ['-DSMI_DWG_NT=4', '-DSMI_DWD_OCC=3']}
 
 
 def lib_path(variant=None):

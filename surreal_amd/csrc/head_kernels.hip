@@ -86,14 +86,23 @@ __device__ __forceinline__ void hc_sync() {
 }
 
 // The weight stream of one layer: output tiles nt = nt0 + ntst * t (t < NT,
-// nt < ceil(N / 16)) over the k chunks c0, c0 + cst, ... (< ceil(K / 16)).
-// init() issues the weight reads of the first two chunks, which need nothing
-// from the layer's input: a layer's init runs before the previous layer's
-// epilogue and barrier, so those reads are in flight meanwhile.
+// nt < ceil(N / 16)) over the k chunks c0, c0 + cst, ... (< ceil(K / 16)),
+// through a ring of HC_D chunk slots.  init() issues the weight reads of the
+// first two chunks, which need nothing from the layer's input: a layer's init
+// runs before the previous layer's epilogue and barrier, so those reads are
+// in flight meanwhile; hc_run issues the rest of the ring.
+#ifndef SMI_HC_DEPTH
+#define SMI_HC_DEPTH 2
+#endif
+// chunks in flight per wave; measured (C3 bench, one MI355X, interleaved
+// trials): 2 -> 8.45 ms, 3 -> 8.59, 4 -> 8.67 per learn: the deeper rings cost
+// occupancy (124 -> 184 VGPRs) and gain nothing
+constexpr int HC_D = SMI_HC_DEPTH;
+static_assert(HC_D >= 2, "ring of at least two chunks");
 template <int NT>
 struct HcStream {
   const float* wp[NT];
-  float4 b0[NT], b1[NT];
+  float4 b[HC_D][NT];
   int K, nch, c0, cst, ntv;
   // k past K (the last chunk of a K % 16 != 0 layer) reads the row's last
   // float4 instead (clamped address: no branch, no select after the load) and
@@ -101,11 +110,11 @@ struct HcStream {
   // are issued unconditionally (chunk indices clamped): a load issued on one
   // path only made the waitcnt pass assume the shorter queue everywhere and
   // wait for nearly every load in flight.
-  __device__ __forceinline__ void ldb(int c, float4 (&b)[NT]) {
+  __device__ __forceinline__ void ldb(int c, float4 (&bb)[NT]) {
     const int lk = (threadIdx.x & 63) >> 4;
     const int kk = min(16 * c + 4 * lk, K - 4);     // K % 4 == 0
 #pragma unroll
-    for (int t = 0; t < NT; ++t) b[t] = *reinterpret_cast<const float4*>(wp[t] + kk);
+    for (int t = 0; t < NT; ++t) bb[t] = *reinterpret_cast<const float4*>(wp[t] + kk);
   }
   __device__ __forceinline__ void init(const float* __restrict__ W, int64_t ldw, int K_, int N,
                                        int nt0, int ntst, int c0_, int cst_) {
@@ -119,8 +128,8 @@ struct HcStream {
       const int n = min(16 * (nt0 + ntst * t) + li, N - 1);
       wp[t] = W + (int64_t)n * ldw;
     }
-    ldb(min(c0, nch - 1), b0);
-    ldb(min(c0 + cst, nch - 1), b1);
+    ldb(min(c0, nch - 1), b[0]);
+    ldb(min(c0 + cst, nch - 1), b[1]);
   }
 };
 
@@ -137,38 +146,45 @@ __device__ __forceinline__ void hc_run(HcStream<NT>& S, const float* sA, int lda
   // result is dropped): per-tile guards made the compiler move the
   // accumulators out of AGPRs every chunk.  NT is chosen per layer so that at
   // most one slot per wave is idle.
-  auto mm = [&](const float4& a, const float4 (&b)[NT]) {
+  auto mm = [&](const float4& a, const float4 (&bb)[NT]) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      acc[t] = mfma4(a.x, b[t].x, acc[t]);
-      acc[t] = mfma4(a.y, b[t].y, acc[t]);
-      acc[t] = mfma4(a.z, b[t].z, acc[t]);
-      acc[t] = mfma4(a.w, b[t].w, acc[t]);
+      acc[t] = mfma4(a.x, bb[t].x, acc[t]);
+      acc[t] = mfma4(a.y, bb[t].y, acc[t]);
+      acc[t] = mfma4(a.z, bb[t].z, acc[t]);
+      acc[t] = mfma4(a.w, bb[t].w, acc[t]);
     }
   };
   auto lda_ = [&](int c) { return *reinterpret_cast<const float4*>(ap + 16 * c); };
   const int nch = S.nch, cst = S.cst, cl = nch - 1;
   int c = S.c0;
-  float4 a0 = lda_(min(c, cl)), a1 = lda_(min(c + cst, cl));
-  // steady state without conditionals (two chunks per trip, both refills
-  // issued): the waitcnt pass then sees the two slots' loads in flight and
-  // waits for exactly the slot it consumes
-  for (; c + 3 * cst < nch; c += 2 * cst) {
-    mm(a0, S.b0);
-    a0 = lda_(c + 2 * cst);
-    S.ldb(c + 2 * cst, S.b0);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(a1, S.b1);
-    a1 = lda_(c + 3 * cst);
-    S.ldb(c + 3 * cst, S.b1);
-    __builtin_amdgcn_sched_barrier(0);
+  float4 a[HC_D];
+#pragma unroll
+  for (int d = 2; d < HC_D; ++d) S.ldb(min(c + d * cst, cl), S.b[d]);
+#pragma unroll
+  for (int d = 0; d < HC_D; ++d) a[d] = lda_(min(c + d * cst, cl));
+  // steady state without conditionals (HC_D chunks per trip, every refill
+  // issued): the waitcnt pass then sees the ring's loads in flight and waits
+  // for exactly the slot it consumes
+  for (; c + (2 * HC_D - 1) * cst < nch; c += HC_D * cst) {
+#pragma unroll
+    for (int d = 0; d < HC_D; ++d) {
+      mm(a[d], S.b[d]);
+      a[d] = lda_(c + (d + HC_D) * cst);
+      S.ldb(c + (d + HC_D) * cst, S.b[d]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
-  // the last <= 3 chunks
-  if (c < nch) mm(a0, S.b0);
-  a0 = lda_(min(c + 2 * cst, cl));
-  S.ldb(min(c + 2 * cst, cl), S.b0);
-  if (c + cst < nch) mm(a1, S.b1);
-  if (c + 2 * cst < nch) mm(a0, S.b0);
+  // the last < 2 HC_D chunks
+#pragma unroll
+  for (int d = 0; d < HC_D; ++d) {
+    if (c + d * cst < nch) mm(a[d], S.b[d]);
+    a[d] = lda_(min(c + (d + HC_D) * cst, cl));
+    S.ldb(min(c + (d + HC_D) * cst, cl), S.b[d]);
+  }
+#pragma unroll
+  for (int d = 0; d < HC_D; ++d)
+    if (c + (d + HC_D) * cst < nch) mm(a[d], S.b[d]);
 }
 
 // the wave's tiles of a full-width layer into LDS rows: D(row 4lk + i, col li)

@@ -917,6 +917,13 @@ struct DwGroup {
   int n;
 };
 
+// output tile width of the grouped launch in 16-column sub-tiles (A/B knob;
+// SMI_DWG_NT=4 gives 64 x 64 tiles, half the accumulators)
+#ifndef SMI_DWG_NT
+#define SMI_DWG_NT 8
+#endif
+constexpr int DWG_NT = SMI_DWG_NT;
+
 template <int WV>
 __global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWD_OCC : 1)
 gemm_dwd_group_kernel(DwGroup G) {
@@ -940,15 +947,15 @@ gemm_dwd_group_kernel(DwGroup G) {
     // a tail of <= 16 gradient rows (M 8 / 200 / 400 at C3) on one 16-wide
     // m sub-tile instead of a 64-wide tile that is >= 75 % padding
     ti.mt *= 4;                                   // m0 = 16 * mt = 64 * (gm - 1)
-    if (G.vec[gi] & 1) dwd_tile<1, 8, false, true, WV>(g, ti, dwd_red);
-    else dwd_tile<1, 8, false, false, WV>(g, ti, dwd_red);
+    if (G.vec[gi] & 1) dwd_tile<1, DWG_NT, false, true, WV>(g, ti, dwd_red);
+    else dwd_tile<1, DWG_NT, false, false, WV>(g, ti, dwd_red);
     return;
   }
   switch (G.vec[gi]) {
-    case 3: dwd_tile<4, 8, true, true, WV>(g, ti, dwd_red); break;
-    case 2: dwd_tile<4, 8, true, false, WV>(g, ti, dwd_red); break;
-    case 1: dwd_tile<4, 8, false, true, WV>(g, ti, dwd_red); break;
-    default: dwd_tile<4, 8, false, false, WV>(g, ti, dwd_red); break;
+    case 3: dwd_tile<4, DWG_NT, true, true, WV>(g, ti, dwd_red); break;
+    case 2: dwd_tile<4, DWG_NT, true, false, WV>(g, ti, dwd_red); break;
+    case 1: dwd_tile<4, DWG_NT, false, true, WV>(g, ti, dwd_red); break;
+    default: dwd_tile<4, DWG_NT, false, false, WV>(g, ti, dwd_red); break;
   }
 }
 
@@ -1280,7 +1287,7 @@ int dw_group_flush(hipStream_t st) {
   g_grp_on = false;
   DwGroup& G = g_grp;
   if (G.n == 0) return SMI_OK;
-  constexpr int MT = 4, NT = 8;
+  constexpr int MT = 4, NT = DWG_NT;
   const int rs = 4 * dwd_waves() * DWD_P;           // rows per prefetch window
   double work = 0.0;                                 // sum of tiles x rows
   int64_t tiles[kDwGroupMax];

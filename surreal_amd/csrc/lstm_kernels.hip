@@ -1166,6 +1166,12 @@ static int lstm_valu_r(int B, int H) {
   if (H < 1 || H > 128) return 0;
   const int m = lstm_valu_mode();
   if (m == 0) return 0;
+  static const int force_r = [] {                 // SMI_LSTM_VALU_R = 1 | 2 | 4: A/B knob
+    const char* e = getenv("SMI_LSTM_VALU_R");
+    const int r = e ? atoi(e) : 0;
+    return (r == 1 || r == 2 || r == 4) ? r : 0;
+  }();
+  if (force_r) return force_r;
   const int cus = device_cus();
   int R = (B + cus - 1) / cus;
   if (R < 1) R = 1;

@@ -260,7 +260,7 @@ class PPOLearner(object):
         self._graph = None
         self._gin = None
         # LSTM / pixel phases: ref_pol on a second stream beside the GAE pass
-        self.prep_side_stream = os.environ.get('SMI_PREP_SIDE', '1') != '0'
+        self.prep_side_stream = os.environ.get('SMI_PREP_SIDE', '0') == '1'
         self._side = None
         self._ctx_side = None
 

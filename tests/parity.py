@@ -89,6 +89,18 @@ CASES = {
     'c3_grad_value': dict(cfg=lambda: c3_cfg('adapt', 1024, (0, 1)), D=42, A=8, Hd=100, pixel=None,
                           init_seed=13, batch_seeds=[1300], n_ulp=6,
                           orders=['given', 'reversed', ['shuffled', 1]], grad='value'),
+    # bench.py --config c3 --local-segments 128: one rank's share of the C3 job
+    # at N = 8 (the VALU LSTM recurrence path), 10 + 10 epochs, and the raw
+    # first-step gradients there
+    'c3_l128': dict(cfg=lambda: c3_cfg('adapt', 128), D=42, A=8, Hd=100, pixel=None,
+                    init_seed=17, batch_seeds=[1700, 1701], n_ulp=6,
+                    orders=['given', 'reversed', ['shuffled', 1]]),
+    'c3_l128_grad_policy': dict(cfg=lambda: c3_cfg('adapt', 128, (1, 0)), D=42, A=8, Hd=100,
+                                pixel=None, init_seed=18, batch_seeds=[1800], n_ulp=6,
+                                orders=['given', 'reversed', ['shuffled', 1]], grad='policy'),
+    'c3_l128_grad_value': dict(cfg=lambda: c3_cfg('adapt', 128, (0, 1)), D=42, A=8, Hd=100,
+                               pixel=None, init_seed=18, batch_seeds=[1800], n_ulp=6,
+                               orders=['given', 'reversed', ['shuffled', 1]], grad='value'),
     # bench.py --config c5 --local-segments 128: C3 + camera0 3x84x84 -> CNN (FC 256)
     'c5': dict(cfg=lambda: c5_cfg(128), D=42, A=8, Hd=100, pixel=(3, 84, 84),
                init_seed=15, batch_seeds=[1500], n_ulp=3, orders=['given', 'reversed']),

@@ -254,6 +254,13 @@ def test_pinned_c3_full_batch_clip():
 
 
 @pytest.mark.timeout(300)
+def test_pinned_c3_rank_of_eight():
+    # bench.py --config c3 --local-segments 128: one rank's share of the C3 job at
+    # N = 8 (the VALU LSTM recurrence, the adaptive dW split), 10 + 10 epochs
+    pinned_fixture('c3_l128')
+
+
+@pytest.mark.timeout(300)
 def test_pinned_c5_full_batch():
     # bench.py --config c5 --local-segments 128: C3 + camera0 3x84x84 -> CNN (FC 256)
     pinned_fixture('c5')
@@ -278,8 +285,8 @@ def gpu_first_step_grads(learner, phase):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize('case', ['c3_grad_policy', 'c3_grad_value', 'c5_grad_policy',
-                                  'c5_grad_value'])
+@pytest.mark.parametrize('case', ['c3_grad_policy', 'c3_grad_value', 'c3_l128_grad_policy',
+                                  'c3_l128_grad_value', 'c5_grad_policy', 'c5_grad_value'])
 def test_pinned_first_step_gradients(case):
     """Raw gradients of the first policy update (epochs 1 + 0) or the first
     value update (0 + 1) before any Adam amplification: the per-step accuracy
