@@ -44,8 +44,8 @@ VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             'nofast': ['-DSMI_DWD_FAST=0'],
             # fused-head weight ring depth A/B (product: 2)
             'hcd3': ['-DSMI_HC_DEPTH=3'], 'hcd4': ['-DSMI_HC_DEPTH=4'],
-            # grouped dW tile A/B: 64 x 64 tiles at 3 waves per SIMD
-            'dwg4': ['-DSMI_DWG_NT=4', '-DSMI_DWD_OCC=3']}
+            # grouped dW tile A/B: 64 x 128 tiles at 2 waves per SIMD (round 2)
+            'dwg8': ['-DSMI_DWG_NT=8'], 'dwgocc4': ['-DSMI_DWG_OCC=4']}   # (occupancy 4: 122 us)
 
 
 def lib_path(variant=None):

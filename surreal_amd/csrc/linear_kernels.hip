@@ -917,15 +917,24 @@ struct DwGroup {
   int n;
 };
 
-// output tile width of the grouped launch in 16-column sub-tiles (A/B knob;
-// SMI_DWG_NT=4 gives 64 x 64 tiles, half the accumulators)
+// output tile width of the grouped launch in 16-column sub-tiles, and its
+// occupancy.  Measured (C3 bench, one MI355X, interleaved trials): 64 x 64
+// tiles at 3 waves per SIMD (130 VGPRs) 120.5 us per grouped launch (0.336 of
+// the f32 MFMA peak), learn 8.21 ms, against 64 x 128 tiles at 2 waves per
+// SIMD (222 VGPRs) 129.6 us, 8.46 ms: the third wave hides more of the
+// operand-stream latency (the launch waits on memory ~60 % of its wave
+// cycles, PMC SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES) than the halved MFMA reuse
+// per loaded byte costs.
 #ifndef SMI_DWG_NT
-#define SMI_DWG_NT 8
+#define SMI_DWG_NT 4
+#endif
+#ifndef SMI_DWG_OCC
+#define SMI_DWG_OCC (SMI_DWG_NT == 4 ? 3 : 2)
 #endif
 constexpr int DWG_NT = SMI_DWG_NT;
 
 template <int WV>
-__global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWD_OCC : 1)
+__global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWG_OCC : 1)
 gemm_dwd_group_kernel(DwGroup G) {
   extern __shared__ float4 dwd_red[];
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -1261,16 +1270,18 @@ static bool dw_group_add(const GemmArgs& g) {
 // (45 TF/s), 1536 -> 3.32, 3072 -> 4.43; at 2688 rows (one rank of eight,
 // tools/bench_dwgroup.py --segments 128): 1024 -> 65 us per launch (128-row
 // slabs), 512 -> 48, 256 -> 46: slabs shorter than ~384 rows are all ramp.
+// With the 64 x 64 tiles at 3 waves per SIMD (DWG_NT below): 1024 -> 120.5 us
+// per C3 launch, 1536 -> 110.0 (0.37 of the f32 MFMA peak), 2048 -> 110.5.
 static int dw_group_target(double work) {
   static int t = -1;
   if (t < 0) {
     const char* e = getenv("SMI_DWD_GROUP_TARGET");
-    t = e ? atoi(e) : 0;
-    if (e && t < 64) t = 64;
+    t = (e && e[0]) ? atoi(e) : 0;
+    if (e && e[0] && t < 64) t = 64;
   }
   if (t > 0) return t;
   const double w = work / 384.0;
-  return w >= 1024.0 ? 1024 : w <= 128.0 ? 128 : (int)w;
+  return w >= 1536.0 ? 1536 : w <= 128.0 ? 128 : (int)w;
 }
 
 // narrow 16-wide tail tiles in grouped launches (SMI_DWD_NARROW=0: off; A/B knob)
