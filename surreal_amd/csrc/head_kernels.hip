@@ -284,10 +284,13 @@ __global__ void __launch_bounds__(kWG)
 head_fwd_kernel(HeadFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   extern __shared__ __attribute__((aligned(16))) float hsm[];
+  // X and HA2 share one region (X is dead once layer 1's k loop is done: the
+  // barrier after its epilogue orders that before layer 2 writes HA2): 37.5 KB
+  // at C3 widths, four workgroups per CU
   float* s0 = hsm;                                // [16][ld0]  X
-  float* s1 = s0 + HC_R * a.ld0;                  // [16][ld1]  HA1
-  float* s2 = s1 + HC_R * a.ld1;                  // [16][ld2]  HA2
-  float* sR = s2 + HC_R * a.ld2;                  // [4][64][4] partials of the last layer;
+  float* s2 = hsm;                                // [16][ld2]  HA2
+  float* s1 = hsm + HC_R * (a.ld0 > a.ld2 ? a.ld0 : a.ld2);   // [16][ld1]  HA1
+  float* sR = s1 + HC_R * a.ld1;                  // [4][64][4] partials of the last layer;
                                                   // [32][33] transpose tile
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
@@ -359,7 +362,7 @@ head_fwd_kernel(HeadFwdArgs a) {
 }
 
 template <int NTA, int NTB>
-__global__ void __launch_bounds__(kWG)
+__global__ void __launch_bounds__(kWG, 3)
 head_bwd_kernel(HeadBwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   extern __shared__ __attribute__((aligned(16))) float hsm[];
@@ -370,15 +373,13 @@ head_bwd_kernel(HeadBwdArgs a) {
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
   const int64_t r0 = (int64_t)blockIdx.x * HC_R;
   const int out = a.out;
-  // dZ rows (zero past out: the dH2 pass runs whole groups of 8 k), loaded
+  // dZ rows (zero past out: the dH2 pass runs whole groups of 4 k), loaded
   // first; dH1's weight stream (W2^T) and its masks are issued behind them and
   // stay in flight through the dZ W3 pass
   const int zr = threadIdx.x >> 4, zk = threadIdx.x & 15;
   const float zv = a.dZ[min(r0 + zr, a.rows - 1) * out + min(zk, out - 1)];
   HcStream<NTA> SA;
   SA.init(a.W2T, a.h2, a.h2, a.h1, wave, 4, 0, 1);
-  float eA[NTA][4];
-  hc_epi_load<NTA, 1>(wave, a.h1, nullptr, a.HA1, r0, a.rows, eA);
   sZ[zr * 16 + zk] = zk < out ? zv : 0.f;
   // padding columns of dH2 (the next layer's last chunk)
   const int h2p = a.ld2 - 4;
@@ -402,13 +403,13 @@ head_bwd_kernel(HeadBwdArgs a) {
         m[i] = *reinterpret_cast<const float4*>(a.HA2 + rr * a.h2 + 4 * q);
         v[i] = float4{0.f, 0.f, 0.f, 0.f};
       }
-      for (int kg = 0; kg < out; kg += 8) {
-        float4 w[8];
+      for (int kg = 0; kg < out; kg += 4) {
+        float4 w[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < 4; ++j)
           w[j] = *reinterpret_cast<const float4*>(a.W3 + (int64_t)min(kg + j, out - 1) * a.h2 + 4 * q);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float z = sZ[(4 * wave + i) * 16 + kg + j];
@@ -428,6 +429,10 @@ head_bwd_kernel(HeadBwdArgs a) {
       }
     }
   }
+  // dH1's masks, in flight behind its k loop (issued here rather than with the
+  // weight prefetch: fewer registers live through the dZ W3 pass)
+  float eA[NTA][4];
+  hc_epi_load<NTA, 1>(wave, a.h1, nullptr, a.HA1, r0, a.rows, eA);
   hc_sync();
   HcStream<NTB> SB;
   {   // dH1 = (dH2 W2) * [HA1 > 0] = dH2 (W2^T)^T
@@ -496,7 +501,7 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
   if (rows <= 0) return SMI_OK;
   HeadFwdArgs a{X, ldx, in, W1, b1, W2, b2, W3, b3, h1, h2, out, tanh_out, HA1, HA2, Y, ldy,
                 W1T, W2T, rows, skip, hc_ld(in), hc_ld(h1), hc_ld(h2)};
-  const size_t lds = (size_t)(HC_R * (a.ld0 + a.ld1 + a.ld2) + HC_SR) * 4;
+  const size_t lds = (size_t)(HC_R * ((a.ld0 > a.ld2 ? a.ld0 : a.ld2) + a.ld1) + HC_SR) * 4;
   const dim3 grid((unsigned)((rows + HC_R - 1) / HC_R));
   const int n1 = hc_nt(h1), n2 = hc_nt(h2);
   const int kslot = ktime_begin(st);
