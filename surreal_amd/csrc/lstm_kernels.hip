@@ -879,6 +879,42 @@ __device__ __forceinline__ float quad_bcast(float v) {      // lane K of each qu
 
 constexpr int kVT = 512;      // threads of the VALU recurrence workgroups (4H <= 512)
 
+// s0..s3 += v[k] * w[k] over k < KP, v read from LDS as KP / 4 float4s in
+// chunks of kVC, the next chunk's reads issued before the current chunk's FMAs
+#ifndef SMI_LSTM_VC
+#define SMI_LSTM_VC 4
+#endif
+constexpr int kVC = SMI_LSTM_VC;
+template <int KP>
+__device__ __forceinline__ void v_dot_pipelined(const float4* __restrict__ v, const float (&w)[KP],
+                                                float& s0, float& s1, float& s2, float& s3) {
+  constexpr int N4 = KP / 4, NC = (N4 + kVC - 1) / kVC;
+  float4 buf[2][kVC];
+  auto ld = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < kVC; ++i)
+      if (c * kVC + i < N4) buf[c & 1][i] = v[c * kVC + i];
+  };
+  ld(0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c + 1 < NC) ld(c + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < kVC; ++i) {
+      const int k4 = c * kVC + i;
+      if (k4 < N4) {
+        const float4 hv = buf[c & 1][i];
+        s0 = fmaf(hv.x, w[4 * k4], s0);
+        s1 = fmaf(hv.y, w[4 * k4 + 1], s1);
+        s2 = fmaf(hv.z, w[4 * k4 + 2], s2);
+        s3 = fmaf(hv.w, w[4 * k4 + 3], s3);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int R, int KP, int KX>
 __global__ void __launch_bounds__(kVT)
 lstm_fwd_v_kernel(LstmFwdArgs a) {
@@ -1005,18 +1041,13 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-      // chunks of 16 k (4 LDS reads in flight per round trip): without the
-      // sched_barrier the compiler hoists every h_{t-1} LDS read of the step
-      // ahead of the FMAs
-#pragma unroll
-      for (int k4 = 0; k4 < KP / 4; ++k4) {
-        const float4 hv = *reinterpret_cast<const float4*>(hp + r * KP + 4 * k4);
-        acc0 = fmaf(hv.x, w[4 * k4], acc0);
-        acc1 = fmaf(hv.y, w[4 * k4 + 1], acc1);
-        acc2 = fmaf(hv.z, w[4 * k4 + 2], acc2);
-        acc3 = fmaf(hv.w, w[4 * k4 + 3], acc3);
-        if ((k4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-      }
+      // h_{t-1} in chunks of kVC 16-byte LDS reads, software-pipelined one
+      // chunk ahead into two register sets: the FMAs of chunk c run while the
+      // reads of chunk c + 1 are in flight (lgkmcnt(kVC) instead of a full
+      // drain per chunk); the sched_barriers keep the compiler from hoisting
+      // every read of the step (which needs KP more VGPRs than the weights leave)
+      const float4* hp4 = reinterpret_cast<const float4*>(hp + r * KP);
+      v_dot_pipelined<KP>(hp4, w, acc0, acc1, acc2, acc3);
       const float pre = xacc[r] + (((acc0 + acc1) + (acc2 + acc3)) + bh);
       const float av = q == 2 ? ftanh(pre) : sigm(pre);
       const float ig = quad_bcast<0>(av), fg = quad_bcast<1>(av);
@@ -1119,15 +1150,7 @@ lstm_bwd_v_kernel(LstmBwdArgs a) {
     for (int r = 0; r < R; ++r) {
       const float4* dp = reinterpret_cast<const float4*>(dgw + r * 4 * KP + q * KP);
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-#pragma unroll
-      for (int j4 = 0; j4 < KP / 4; ++j4) {
-        const float4 v = dp[j4];
-        s0 = fmaf(v.x, w[4 * j4], s0);
-        s1 = fmaf(v.y, w[4 * j4 + 1], s1);
-        s2 = fmaf(v.z, w[4 * j4 + 2], s2);
-        s3 = fmaf(v.w, w[4 * j4 + 3], s3);
-        if ((j4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-      }
+      v_dot_pipelined<KP>(dp, w, s0, s1, s2, s3);
       const float p = (s0 + s1) + (s2 + s3);
       // fixed-order quad sum: every lane of the quad gets the same dh_rec
       dhr[r] = (quad_bcast<0>(p) + quad_bcast<1>(p)) + (quad_bcast<2>(p) + quad_bcast<3>(p));
