@@ -47,7 +47,12 @@ VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             # grouped dW tile A/B: 64 x 128 tiles at 2 waves per SIMD (round 2)
             'dwg8': ['-DSMI_DWG_NT=8'], 'dwgocc4': ['-DSMI_DWG_OCC=4'],   # (occupancy 4: 122 us)
             # VALU recurrence: LDS reads per pipelined chunk (product: 4)
-            'vc2': ['-DSMI_LSTM_VC=2'], 'vc8': ['-DSMI_LSTM_VC=8']}
+            'vc2': ['-DSMI_LSTM_VC=2'], 'vc8': ['-DSMI_LSTM_VC=8'],
+            # grouped-dW anatomy (tools/bench_dwgroup.py only; wrong results by design):
+            # MFMAs without the operand stream / the stream without the MFMAs
+            'dwdiag_mfma': ['-DSMI_DWD_DIAG=1'], 'dwdiag_load': ['-DSMI_DWD_DIAG=2'],
+            # per-workgroup start / end clock of the grouped dW launch (product results)
+            'dwtrace': ['-DSMI_DWD_DIAG=3']}
 
 
 def lib_path(variant=None):

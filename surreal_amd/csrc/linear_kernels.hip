@@ -19,6 +19,8 @@
 // contiguous dimension (leading dims 36 / 80: conflict-free MFMA operand
 // reads and contiguous-dimension stores).  Global loads use clamped addresses
 // and are zeroed afterwards (no predicated loads: see cdna_hip_programming.md).
+#include <cmath>
+#include <algorithm>
 #include <stdlib.h>
 #include <type_traits>
 #include "smi_device.hpp"
@@ -626,6 +628,9 @@ gemm_dw128_kernel(GemmArgs g) {
 // steps prefetched in registers) and are combined through LDS in a fixed
 // order; slabs go to the split-K partials.  Row-major dY/X of the heads, the
 // LSTM input/recurrent weights and the DDPG nets all take this path.
+#ifndef SMI_DWD_DIAG
+#define SMI_DWD_DIAG 0
+#endif
 #ifndef SMI_DWD_P
 #define SMI_DWD_P 4
 #endif
@@ -737,6 +742,12 @@ __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nst
   };
   auto step = [&](int p) {
     const float a4[4] = {av[p].x, av[p].y, av[p].z, av[p].w};
+#if SMI_DWD_DIAG == 2
+    // diagnostic (bench_dwgroup A/B only): the operand stream without the MFMAs
+    acc[0][0][0] += (a4[0] + a4[1]) + (a4[2] + a4[3]);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc[0][0][1] += (bv[p][h].x + bv[p][h].y) + (bv[p][h].z + bv[p][h].w);
+#else
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const float4 q = bv[p][b >> 2];
@@ -744,6 +755,7 @@ __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nst
 #pragma unroll
       for (int a = 0; a < MT; ++a) acc[a][b] = mfma4(a4[a], bb, acc[a][b]);
     }
+#endif
   };
 #pragma unroll
   for (int p = 0; p < DWD_P; ++p) load(p);
@@ -751,16 +763,39 @@ __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nst
   // replaces: without it the scheduler sinks all DWD_P refills to the end of
   // the unrolled body and the next iteration waits on them (vmcnt(9..0)), i.e.
   // no prefetch distance at all
+  // 16-wide tail tiles (MT == 1) run the longest slabs of a balanced grouped
+  // launch (~2.5x the rows of a full tile's slab): their MFMA chain restarts
+  // every DWD_P steps and the blocks are summed in a second register set, so
+  // a wave's fp32 chain is DWD_P + steps / DWD_P long instead of steps long
+  // (the value head's 1-row gradient sums 21504 rows with heavy cancellation)
+  f32x4 tot[MT][NT];
+  if constexpr (MT == 1) {
+#pragma unroll
+    for (int b = 0; b < NT; ++b) tot[0][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   for (int s0 = DWD_P; s0 < nsteps; s0 += DWD_P) {
 #pragma unroll
     for (int p = 0; p < DWD_P; ++p) {
       step(p);
-      load(p);
+      // diagnostic SMI_DWD_DIAG 1 (bench_dwgroup A/B only): the MFMAs without
+      // the operand stream (the first DWD_P steps' operands reused)
+      if constexpr (SMI_DWD_DIAG != 1) load(p);
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (MT == 1) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        tot[0][b] += acc[0][b];
+        acc[0][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   }
 #pragma unroll
   for (int p = 0; p < DWD_P; ++p) step(p);
+  if constexpr (MT == 1) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[0][b] = tot[0][b] + acc[0][b];
+  }
 }
 
 // WV waves per workgroup (4: one per SIMD; 8: two per SIMD, each wave takes
@@ -933,9 +968,35 @@ struct DwGroup {
 #endif
 constexpr int DWG_NT = SMI_DWG_NT;
 
+#if SMI_DWD_DIAG == 3
+// diagnostic (bench_dwgroup only): per-workgroup {start, end, HW_ID, XCC_ID |
+// group << 8} in 100 MHz wall-clock ticks, read back by smi_diag_dw_trace
+constexpr int kDwTraceMax = 8192;
+__device__ unsigned long long g_dw_trace[kDwTraceMax][4];
+extern "C" int smi_diag_dw_trace(void* dst, int n) {
+  if (n > kDwTraceMax) n = kDwTraceMax;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dw_trace), (size_t)n * 32, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+}
+#endif
+
 template <int WV>
 __global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWG_OCC : 1)
 gemm_dwd_group_kernel(DwGroup G) {
+#if SMI_DWD_DIAG == 3
+  const unsigned long long t_start = wall_clock64();
+  struct TraceEnd {
+    unsigned long long t0; int gi = 0;
+    __device__ ~TraceEnd() {
+      __syncthreads();
+      if (threadIdx.x == 0 && blockIdx.x < kDwTraceMax) {
+        g_dw_trace[blockIdx.x][0] = t0;
+        g_dw_trace[blockIdx.x][1] = wall_clock64();
+        g_dw_trace[blockIdx.x][2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        g_dw_trace[blockIdx.x][3] = __builtin_amdgcn_s_getreg((31 << 11) | 20) | (gi << 8);
+      }
+    }
+  } trace_end{t_start};
+#endif
   extern __shared__ float4 dwd_red[];
   const int nwg = gridDim.x, orig = blockIdx.x;
   int w = orig;
@@ -946,6 +1007,9 @@ gemm_dwd_group_kernel(DwGroup G) {
   int gi = 0;
   while (gi + 1 < G.n && w >= G.wg0[gi + 1]) ++gi;
   const GemmArgs& g = G.g[gi];
+#if SMI_DWD_DIAG == 3
+  trace_end.gi = gi;
+#endif
   if (g.skip && g.skip[0] != 0) return;
   const int local = w - G.wg0[gi], gn = G.gn[gi], gm = G.gm[gi];
   TileIdx ti;
@@ -1294,13 +1358,82 @@ static int use_dwd_narrow() {
   return u;
 }
 
+// relative time per row of a 16-wide tail tile against a full 64 x 64 tile
+// (per-workgroup clock trace of the C3 launch, tools/bench_dwgroup.py with the
+// `dwtrace` build: 832-row slabs took 18.3 us on tail tiles, 47 us on full ones)
+static double dwd_narrow_cost() {
+  static double c = -1.0;
+  if (c < 0.0) {
+    const char* e = getenv("SMI_DWD_NARROW_COST");
+    c = (e && e[0]) ? atof(e) : 0.4;
+    if (c <= 0.0 || c > 1.0) c = 0.4;
+  }
+  return c;
+}
+
+// Workgroups of one grouped launch resident at once (CUs x occupancy).
+static int dwd_group_slots(size_t lds) {
+  static int slots = 0;
+  if (!slots) {
+    slots = dwd_waves() == 8 ? resident_grid(gemm_dwd_group_kernel<8>, 512, lds)
+                             : resident_grid(gemm_dwd_group_kernel<4>, 256, lds);
+    if (slots < 1) slots = 256;
+  }
+  return slots;
+}
+
 int dw_group_flush(hipStream_t st) {
   g_grp_on = false;
   DwGroup& G = g_grp;
   if (G.n == 0) return SMI_OK;
   constexpr int MT = 4, NT = DWG_NT;
+  const size_t lds = (size_t)2 * MT * NT * 64 * sizeof(float4);
   const int rs = 4 * dwd_waves() * DWD_P;           // rows per prefetch window
-  double work = 0.0;                                 // sum of tiles x rows
+  auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  // A GEMM whose last m-tile is a <= 16-row tail (M 8 / 200 / 400 at C3) is
+  // split, while the group has room, into its full 64-row tiles and a tail
+  // entry: the tail's tiles then get their own, longer slabs (below).  The
+  // tail entry addresses rows m0.. of dY and of every destination.
+  {
+    const int n0 = G.n;
+    DwGroup E = G;
+    int n = 0;
+    for (int i = 0; i < n0; ++i) {
+      const GemmArgs& g = G.g[i];
+      const int tail = g.M % (16 * MT);
+      const bool split = use_dwd_narrow() && tail > 0 && tail <= 16 && g.M > 16 * MT &&
+                         g.a_rs == 1 && n + (n0 - i) + 1 <= kDwGroupMax;
+      E.g[n] = g;
+      E.vec[n] = G.vec[i];
+      if (!split) { ++n; continue; }
+      const int m0 = g.M - tail;
+      E.g[n].M = m0;                                  // the full tiles (vec unchanged)
+      ++n;
+      GemmArgs t = g;
+      t.M = tail;
+      t.A = g.A + m0;
+      if (t.C) t.C = g.C + (int64_t)m0 * g.ldc;
+      if (t.C2) t.C2 = g.C2 + (int64_t)m0 * g.ldc2;
+      if (t.bias_out) t.bias_out = g.bias_out + m0;
+      if (t.bias_out2) t.bias_out2 = g.bias_out2 + m0;
+      const bool va = al16(t.A) && t.M >= 4 && t.M % 4 == 0 && t.a_cs % 4 == 0;
+      E.g[n] = t;
+      E.vec[n] = (va ? 2 : 0) + (G.vec[i] & 1);
+      ++n;
+    }
+    E.n = n;
+    G = E;
+  }
+  // Balanced workgroups.  A launch with more work than one resident round
+  // (CUs x occupancy) runs as whole rounds (one at C3: a second, partly filled
+  // round was the launch's tail — the per-workgroup clock trace showed the
+  // last 40 % of the span at falling concurrency), and each entry's slab
+  // length is set so that its slabs cost about the same time (tail tiles ~0.4
+  // of a full tile per row).  Below one round every workgroup is resident
+  // anyway and the span is the longest slab: equal slab lengths (shorter
+  // fp32 chains on the tail tiles).
+  const int slots = dwd_group_slots(lds);
+  double cost[kDwGroupMax], work = 0.0, work_u = 0.0;  // tiles x rows (x cost)
   int64_t tiles[kDwGroupMax];
   for (int i = 0; i < G.n; ++i) {
     const GemmArgs& g = G.g[i];
@@ -1309,23 +1442,46 @@ int dw_group_flush(hipStream_t st) {
     G.gm[i] = (g.M + 16 * MT - 1) / (16 * MT);
     G.gn[i] = (g.N + 16 * NT - 1) / (16 * NT);
     tiles[i] = (int64_t)G.gm[i] * G.gn[i];
-    work += (double)tiles[i] * g.K;
+    cost[i] = G.narrow[i] ? ((G.gm[i] - 1) + dwd_narrow_cost()) / G.gm[i] : 1.0;
+    work_u += (double)tiles[i] * g.K;
+    work += (double)tiles[i] * g.K * cost[i];
+  }
+  int target = dw_group_target(work_u);
+  static const bool fixed_target = [] {
+    const char* e = getenv("SMI_DWD_GROUP_TARGET");
+    return e && e[0];
+  }();
+  if (!fixed_target && target >= slots) {
+    // whole rounds of at most ~2048 cost-rows per workgroup (SMI_DWD_ROUND_ROWS)
+    static const double round_rows = [] {
+      const char* e = getenv("SMI_DWD_ROUND_ROWS");
+      const double v = (e && e[0]) ? atof(e) : 2048.0;
+      return v >= 256.0 ? v : 2048.0;
+    }();
+    const int rounds = (int)std::max(1.0, std::ceil(work / (slots * round_rows)));
+    target = slots * rounds;
+  } else {
+    for (int i = 0; i < G.n; ++i) cost[i] = 1.0;
+    work = work_u;
   }
   const int64_t cap = smi_workspace_floats();
-  int64_t rows = (int64_t)(work / dw_group_target(work)) + 1;
-  rows = (rows + rs - 1) / rs * rs;
-  if (rows < 2 * rs) rows = 2 * rs;                 // >= 8 MFMA steps per wave
+  double r0 = work / target;                        // cost-rows per workgroup
   int64_t need = 0;
+  int64_t kcs[kDwGroupMax];
   for (int pass = 0; pass < 8; ++pass) {            // grow the slabs until the partials fit
     need = 0;
     for (int i = 0; i < G.n; ++i) {
       const GemmArgs& g = G.g[i];
-      const int64_t kc = rows < g.K ? rows : ((int64_t)g.K + rs - 1) / rs * rs;
-      const int S = (int)((g.K + kc - 1) / kc);
-      need += (int64_t)S * g.M * g.N;
+      int64_t S = (int64_t)(g.K * cost[i] / r0 + 0.5);
+      if (S < 1) S = 1;
+      int64_t kc = ((g.K + S - 1) / S + rs - 1) / rs * rs;
+      if (kc < 2 * rs) kc = 2 * rs;                 // >= 8 MFMA steps per wave
+      if (kc >= g.K) kc = ((int64_t)g.K + rs - 1) / rs * rs;
+      kcs[i] = kc;
+      need += (int64_t)((g.K + kc - 1) / kc) * g.M * g.N;
     }
     if (need <= cap) break;
-    rows *= 2;
+    r0 *= 2.0;
   }
   float* base = workspace_f32(need);
   if (!base) return set_error(SMI_E_ARG, "gemm: workspace too small for the grouped dW partials");
@@ -1334,16 +1490,14 @@ int dw_group_flush(hipStream_t st) {
   G.rb0[0] = 0;
   for (int i = 0; i < G.n; ++i) {
     GemmArgs& g = G.g[i];
-    const int64_t kc = rows < g.K ? rows : ((int64_t)g.K + rs - 1) / rs * rs;
-    g.kchunk = (int)kc;
-    G.S[i] = (int)((g.K + kc - 1) / kc);
+    g.kchunk = (int)kcs[i];
+    G.S[i] = (int)((g.K + kcs[i] - 1) / kcs[i]);
     g.part = base + off;
     off += (int64_t)G.S[i] * g.M * g.N;
     G.wg0[i + 1] = G.wg0[i] + (int)(tiles[i] * G.S[i]);
     G.rb0[i + 1] = G.rb0[i] + (int)(((int64_t)g.M * g.N + 63) / 64);
   }
   const int kslot = ktime_begin(st);
-  const size_t lds = (size_t)2 * MT * NT * 64 * sizeof(float4);
   if (dwd_waves() == 8)
     hipLaunchKernelGGL(gemm_dwd_group_kernel<8>, dim3(G.wg0[G.n]), dim3(512), lds, st, G);
   else

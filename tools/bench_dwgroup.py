@@ -44,8 +44,9 @@ def main():
     gW3, gb3 = torch.empty(A, h2, device=dev), torch.empty(A, device=dev)
     gW2, gb2 = torch.empty(h2, h1, device=dev), torch.empty(h2, device=dev)
     gW1, gb1 = torch.empty(h1, H, device=dev), torch.empty(h1, device=dev)
-    fl = 2.0 * R * (A * h2 + h2 * h1 + h1 * H + G4 * (D + H)) + R * (A + h2 + h1 + G4)
+    fl = 2.0 * R * (A * h2 + h2 * h1 + h1 * H + G4 * (D + H)) + R * (A + h2 + h1 + G4)   # algorithmic (D = 42)
     lstm = torch.empty(G4 * D + G4 * H + 2 * G4, device=dev)
+    gWih = torch.empty(G4, 44, device=dev)
 
     def phase():
         L.call('smi_dw_group_begin')
@@ -54,7 +55,9 @@ def main():
         L.call('smi_linear_backward_weight', P(dH1), h1, R, h1, P(X0), H, H, P(gW1), H, P(gb1), 0, st)
         # the LSTM's W_ih and W_hh as two GEMMs of the group (the learner fuses
         # them over [x_t | h_{t-1}] through the internal two-source form)
-        L.call('smi_linear_backward_weight', P(dg), G4, R, G4, P(Xz), 44, D, P(lstm), D,
+        # (x padded to 44 columns as the learner's [x_t | h_{t-1}] form reads it:
+        # 16-byte rows, the streaming loop)
+        L.call('smi_linear_backward_weight', P(dg), G4, R, G4, P(Xz), 44, 44, P(gWih), 44,
                P(lstm[G4 * D + G4 * H:]), 0, st)
         L.call('smi_linear_backward_weight', P(dg), G4, R, G4, P(hb), H, H, P(lstm[G4 * D:]), H,
                P(lstm[G4 * D + G4 * H + G4:]), 0, st)
@@ -72,6 +75,33 @@ def main():
     torch.cuda.synchronize()
     t = sorted(s.elapsed_time(e) for s, e in ev)
     ms = t[len(t) // 2]
+    if os.environ.get('SMI_LIB_VARIANT') == 'dwtrace':
+        # one more phase, then the per-workgroup clock trace of its dW launch
+        import ctypes
+        import numpy as np
+        phase()
+        torch.cuda.synchronize()
+        buf = np.zeros((8192, 4), dtype=np.uint64)
+        n = L.lib().smi_diag_dw_trace(ctypes.c_void_p(buf.ctypes.data), 8192)
+        tr = buf[:n]
+        tr = tr[tr[:, 1] > 0]
+        t0 = tr[:, 0].min()
+        st_, en = (tr[:, 0] - t0) / 100.0, (tr[:, 1] - t0) / 100.0      # us (100 MHz)
+        dur = en - st_
+        gi = (tr[:, 3] >> 8).astype(int)
+        xcc = (tr[:, 3] & 0xF).astype(int)
+        cu = ((tr[:, 2] >> 8) & 0xF).astype(int) + 16 * ((tr[:, 2] >> 13) & 0x7).astype(int)
+        grid = np.arange(0.0, float(en.max()) + 1.0, 1.0)
+        conc = [int(((st_ <= x) & (en > x)).sum()) for x in grid]
+        out = {'trace_wgs': int(len(tr)), 'span_us': round(float(en.max()), 1),
+               'dur_us_p10_50_90_max': [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90, 100)],
+               'start_us_p50_90_max': [round(float(np.percentile(st_, q)), 1) for q in (50, 90, 100)],
+               'per_group_dur_med': {int(k): round(float(np.median(dur[gi == k])), 1) for k in np.unique(gi)},
+               'per_group_wgs': {int(k): int((gi == k).sum()) for k in np.unique(gi)},
+               'per_xcc_wgs': {int(k): int((xcc == k).sum()) for k in np.unique(xcc)},
+               'max_wgs_per_xcc_cu': int(np.bincount(xcc * 64 + cu).max()),
+               'concurrency_every_5us': conc[::5]}
+        print(json.dumps(out), flush=True)
     print(json.dumps({'bench': 'dw_group', 'rows': R, 'ms': round(ms, 4), 'gflop': round(fl / 1e9, 3),
                       'tflops': round(fl / ms / 1e9, 2), 'frac_f32_mfma': round(fl / ms / 1e9 / 157.3, 3)}),
           flush=True)
