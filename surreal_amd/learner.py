@@ -789,12 +789,18 @@ class PPOLearner(object):
         serialization on a worker thread) or any callable(iteration, message,
         module_dict)."""
         if self.exp_counter >= self.learner_config.parameter_publish.exp_interval:
+            deferred = False
             if self.publisher is not None:
-                if hasattr(self.publisher, 'snapshot'):
+                if hasattr(self.publisher, 'commit'):
+                    self.publisher.snapshot(iteration, message, defer=True)
+                    deferred = True
+                elif hasattr(self.publisher, 'snapshot'):
                     self.publisher.snapshot(iteration, message)
                 else:
                     self.publisher(iteration, message, self.module_dict())
             self._post_publish()
+            if deferred:                  # the D2H after this thread's host reads
+                self.publisher.commit()
 
     def _post_publish(self):                                  # ppo.py:637-666
         n = int(self.kl_count.item())

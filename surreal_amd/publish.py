@@ -11,7 +11,8 @@ MI355X side: the learner's parameters live in a handful of flat device
 buffers (model.py), so a snapshot is a few device-to-device copies into a
 snapshot arena, enqueued on the learner's stream right after the last
 learn() (stream-ordered: no host wait), followed by ONE device-to-host copy of
-the arena into pinned memory on a side stream.  The D2H is a copy KERNEL
+the arena into pinned memory on a side stream, issued by the learner thread once
+its own post-publish host reads are done (commit()).  The D2H is a copy KERNEL
 writing the mapped pinned buffer (smi_copy_to_host), not a runtime DMA copy:
 an SDMA hipMemcpyAsync D2H held the learner thread ~0.25 ms per publish
 (tools/diag_publish.py), which the GPU then spent idle.  The next learn() is
@@ -124,6 +125,7 @@ class DeviceParameterPublisher(object):
         for sl in self.slots:
             sl['free'].set()
         self.next = 0
+        self._pending = None
         self.last = None
         self.published = 0
         self._q = queue.Queue()
@@ -131,11 +133,16 @@ class DeviceParameterPublisher(object):
         self._worker = threading.Thread(target=self._run, daemon=True)
         self._worker.start()
 
-    def snapshot(self, iteration=0, message=''):
+    def snapshot(self, iteration=0, message='', defer=False):
         """Enqueue the parameter snapshot on the current (learner) stream and its
-        D2H on the side stream; returns a Snapshot without waiting."""
+        D2H on the side stream; returns a Snapshot without waiting.  defer=True
+        leaves the D2H to the caller's commit() (the learner issues it after
+        _post_publish's host reads: a D2H in flight across those reads cost the
+        learner ~0.17 ms per publish whichever engine or thread ran it,
+        tools/diag_publish.py)."""
         if self._err is not None:
             raise RuntimeError('parameter publisher worker failed') from self._err
+        self.commit()                         # a deferred snapshot not yet committed
         slot = self.slots[self.next]
         self.next = (self.next + 1) % len(self.slots)
         slot['free'].wait()                   # the worker has copied this slot's last snapshot out
@@ -150,23 +157,44 @@ class DeviceParameterPublisher(object):
         # where the learner thread syncs for the KL record and re-launches)
         snap = Snapshot(self.layout, slot['host'], threading.Event(), iteration, message, slot)
         snap._taken = taken
+        snap._done = None
+        snap._issued = threading.Event()
+        if defer:
+            self._pending = snap
+        else:
+            snap._issued.set()                # the worker issues the D2H
         # neither half of the slot is rewritten before the worker has serialized
         # it (slot['free'], set after the D2H completed and was read)
         self._q.put(snap)
         return snap
 
-    def _d2h(self, snap):
-        """worker side: ONE D2H of the slot, off the learner stream, as a kernel
-        into the mapped pinned slot (smi_copy_to_host)"""
-        snap._taken.synchronize()
+    def _issue(self, snap):
+        """ONE D2H of the slot on the side stream, after the snapshot's D2D, as
+        a kernel into the mapped pinned slot (smi_copy_to_host)"""
         slot = snap._slot
         with torch.cuda.device(self.device):
+            self.side.wait_event(snap._taken)
             L.call('smi_copy_to_host', ctypes.c_void_p(slot['host'].data_ptr()),
                    ctypes.c_void_p(slot['dev'].data_ptr()), self.layout.nbytes,
                    ctypes.c_void_p(self.side.cuda_stream))
             done = torch.cuda.Event()
             done.record(self.side)
-        done.synchronize()
+        snap._done = done
+
+    def commit(self):
+        """Issue the D2H of the last snapshot(defer=True) (learner thread)."""
+        snap, self._pending = self._pending, None
+        if snap is not None:
+            self._issue(snap)
+            snap._issued.set()
+
+    def _d2h(self, snap):
+        """worker side: wait for the copy (issuing it unless deferred)"""
+        snap._issued.wait()
+        if snap._done is None:
+            snap._taken.synchronize()         # issued after the D2D ran: off the learner's launches
+            self._issue(snap)
+        snap._done.synchronize()
         snap._event.set()
 
     def _run(self):
@@ -194,6 +222,7 @@ class DeviceParameterPublisher(object):
 
     def flush(self):
         """Wait until every snapshot taken so far has reached the sink."""
+        self.commit()
         self._q.join()
         if self._err is not None:
             raise RuntimeError('parameter publisher worker failed') from self._err

@@ -3,7 +3,10 @@ segments, publish after every learn(); times 8 x (learn + publish) for:
 plain (no publisher), d2d (the snapshot's device copies only), d2h (+ the side-
 stream D2H, no worker), fast (the publisher with a trivial serializer), and
 the host time of snapshot() itself.
-Usage: python tools/diag_publish.py"""
+kd2h (the copy kernel issued from the learner thread), fast (the worker issues
+the D2H once the snapshot's D2D ran), late (the publisher as the learner drives
+it: snapshot(defer=True), then commit() after _post_publish's host reads).
+Usage: python tools/diag_publish.py [--graph]"""
 import json
 import os
 import sys
@@ -23,7 +26,7 @@ def main():
                     rnn=True, rnn_hidden=100, horizon=5)
     lc.parameter_publish.exp_interval = lc.replay.batch_size
     D, A, Hd = 42, 8, 100
-    learner = PPOLearner(lc, env_config(D, A), seed=1)
+    learner = PPOLearner(lc, env_config(D, A), seed=1, use_graph='--graph' in sys.argv)
     batch = synthetic.to_device(synthetic.ppo_batch(256, 25, D, A, seed=3, rnn_hidden=Hd), 'cuda')
     lay = _Layout(learner.module_dict())
     dev_arena = torch.empty(lay.nbytes, dtype=torch.uint8, device='cuda')
@@ -50,7 +53,19 @@ def main():
             fast.snapshot(it, msg)
             host_t.append(time.perf_counter() - t0)
 
-    variants = {'plain': None, 'd2d': d2d, 'd2h': d2h, 'fast': Timed()}
+    from surreal_amd import _lib as L
+    import ctypes
+
+    def kd2h(it, msg, md):                           # the copy kernel from the learner thread
+        d2d(it, msg, md)
+        ev = torch.cuda.Event()
+        ev.record()
+        side.wait_event(ev)
+        L.call('smi_copy_to_host', ctypes.c_void_p(host_arena.data_ptr()),
+               ctypes.c_void_p(dev_arena.data_ptr()), lay.nbytes, ctypes.c_void_p(side.cuda_stream))
+
+    variants = {'plain': None, 'd2d': d2d, 'd2h': d2h, 'kd2h': kd2h, 'fast': Timed(),
+                'late': fast}
 
     def run(p, n=8):
         learner.publisher = p
@@ -69,7 +84,7 @@ def main():
         for k, p in variants.items():
             t[k].append(run(p))
     best = {k: round(min(v) / 8 * 1e3, 4) for k, v in t.items()}
-    print(json.dumps({'ms_per_learn_publish': best, 'snapshot_host_ms_median':
+    print(json.dumps({'graph': '--graph' in sys.argv, 'ms_per_learn_publish': best, 'snapshot_host_ms_median':
                       round(sorted(host_t)[len(host_t) // 2] * 1e3, 4), 'arena_bytes': lay.nbytes,
                       'storages': len(lay.storages)}), flush=True)
     fast.close()
