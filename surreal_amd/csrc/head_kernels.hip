@@ -133,36 +133,48 @@ struct HcStream {
   }
 };
 
-// acc[t] = A[16][K] (LDS, lda) x W^T over the stream's tiles and chunks
-template <int NT>
+// acc[rt][t] = A[16 rt .. 16 rt + 15][K] (LDS, lda) x W^T over the stream's
+// tiles and chunks: RT row tiles share every weight chunk (RT = 2 halves the
+// weight traffic per flop at large batches)
+template <int NT, int RT>
 __device__ __forceinline__ void hc_run(HcStream<NT>& S, const float* sA, int lda,
-                                       f32x4 (&acc)[NT]) {
+                                       f32x4 (&acc)[RT][NT]) {
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (S.ntv == 0) return;
   const float* ap = sA + li * lda + 4 * lk;
   // every tile slot runs (a slot past the last tile reads clamped rows and its
   // result is dropped): per-tile guards made the compiler move the
   // accumulators out of AGPRs every chunk.  NT is chosen per layer so that at
   // most one slot per wave is idle.
-  auto mm = [&](const float4& a, const float4 (&bb)[NT]) {
+  auto mm = [&](const float4 (&a)[RT], const float4 (&bb)[NT]) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      acc[t] = mfma4(a.x, bb[t].x, acc[t]);
-      acc[t] = mfma4(a.y, bb[t].y, acc[t]);
-      acc[t] = mfma4(a.z, bb[t].z, acc[t]);
-      acc[t] = mfma4(a.w, bb[t].w, acc[t]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt][t] = mfma4(a[rt].x, bb[t].x, acc[rt][t]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt][t] = mfma4(a[rt].y, bb[t].y, acc[rt][t]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt][t] = mfma4(a[rt].z, bb[t].z, acc[rt][t]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt][t] = mfma4(a[rt].w, bb[t].w, acc[rt][t]);
     }
   };
-  auto lda_ = [&](int c) { return *reinterpret_cast<const float4*>(ap + 16 * c); };
+  auto lda_ = [&](int c, float4 (&o)[RT]) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+      o[rt] = *reinterpret_cast<const float4*>(ap + rt * 16 * lda + 16 * c);
+  };
   const int nch = S.nch, cst = S.cst, cl = nch - 1;
   int c = S.c0;
-  float4 a[HC_D];
+  float4 a[HC_D][RT];
 #pragma unroll
   for (int d = 2; d < HC_D; ++d) S.ldb(min(c + d * cst, cl), S.b[d]);
 #pragma unroll
-  for (int d = 0; d < HC_D; ++d) a[d] = lda_(min(c + d * cst, cl));
+  for (int d = 0; d < HC_D; ++d) lda_(min(c + d * cst, cl), a[d]);
   // steady state without conditionals (HC_D chunks per trip, every refill
   // issued): the waitcnt pass then sees the ring's loads in flight and waits
   // for exactly the slot it consumes
@@ -170,7 +182,7 @@ __device__ __forceinline__ void hc_run(HcStream<NT>& S, const float* sA, int lda
 #pragma unroll
     for (int d = 0; d < HC_D; ++d) {
       mm(a[d], S.b[d]);
-      a[d] = lda_(c + (d + HC_D) * cst);
+      lda_(c + (d + HC_D) * cst, a[d]);
       S.ldb(c + (d + HC_D) * cst, S.b[d]);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -179,7 +191,7 @@ __device__ __forceinline__ void hc_run(HcStream<NT>& S, const float* sA, int lda
 #pragma unroll
   for (int d = 0; d < HC_D; ++d) {
     if (c + d * cst < nch) mm(a[d], S.b[d]);
-    a[d] = lda_(min(c + (d + HC_D) * cst, cl));
+    lda_(min(c + (d + HC_D) * cst, cl), a[d]);
     S.ldb(min(c + (d + HC_D) * cst, cl), S.b[d]);
   }
 #pragma unroll
@@ -188,34 +200,38 @@ __device__ __forceinline__ void hc_run(HcStream<NT>& S, const float* sA, int lda
 }
 
 // the wave's tiles of a full-width layer into LDS rows: D(row 4lk + i, col li)
-// of tile nt is element [4lk + i][16 nt + li]; EPI 0: + bias, ReLU; 1: * [mask > 0]
-// (mask row-major [rows][N] in global memory, rows r0..); columns N..16*CT-1
-// are written as zeros (the next layer's last chunk reads them)
+// of tile nt, row tile rt, is element [16 rt + 4lk + i][16 nt + li]; EPI 0:
+// + bias, ReLU; 1: * [mask > 0] (mask row-major [rows][N] in global memory,
+// rows r0..); columns N..16*CT-1 are written as zeros (the next layer's last
+// chunk reads them)
 // Its operands (the bias, or the 4 mask values of each of the lane's rows)
 // are fetched by hc_epi_load BEFORE the layer's k loop, so their latency hides
-// behind it instead of serializing one tile at a time after it.
-template <int NT, int EPI>
+// behind it instead of serializing one tile at a time after it.  EPI 0 uses
+// e[0] only (the bias is the same for every row tile).
+template <int NT, int EPI, int RT>
 __device__ __forceinline__ void hc_epi_load(int nt0, int N, const float* bias, const float* mask,
-                                            int64_t r0, int64_t rows, float (&e)[NT][4]) {
+                                            int64_t r0, int64_t rows, float (&e)[RT][NT][4]) {
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int nc = min(16 * (nt0 + 4 * t) + li, N - 1);     // clamped: unconditional loads
     if constexpr (EPI == 0) {
-      e[t][0] = bias[nc];
+      e[0][t][0] = bias[nc];
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t r = r0 + 4 * lk + i;
-        e[t][i] = mask[(r < rows ? r : rows - 1) * N + nc];
-      }
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t r = r0 + 16 * rt + 4 * lk + i;
+          e[rt][t][i] = mask[(r < rows ? r : rows - 1) * N + nc];
+        }
     }
   }
 }
 
-template <int NT, int EPI>
-__device__ __forceinline__ void hc_store(const f32x4 (&acc)[NT], const float (&e)[NT][4], int nt0,
-                                         int N, float* sO, int ldo) {
+template <int NT, int EPI, int RT>
+__device__ __forceinline__ void hc_store(const f32x4 (&acc)[RT][NT], const float (&e)[RT][NT][4],
+                                         int nt0, int N, float* sO, int ldo) {
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
   const int CT = (N + 15) >> 4;
 #pragma unroll
@@ -225,40 +241,48 @@ __device__ __forceinline__ void hc_store(const f32x4 (&acc)[NT], const float (&e
     const int n = 16 * nt + li;
     const bool nv = n < N;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 4 * lk + i;
-      float v;
-      if constexpr (EPI == 0) {
-        v = acc[t][i] + e[t][0];
-        v = v > 0.f ? v : 0.f;
-      } else {
-        v = e[t][i] > 0.f ? acc[t][i] : 0.f;
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * rt + 4 * lk + i;
+        float v;
+        if constexpr (EPI == 0) {
+          v = acc[rt][t][i] + e[0][t][0];
+          v = v > 0.f ? v : 0.f;
+        } else {
+          v = e[rt][t][i] > 0.f ? acc[rt][t][i] : 0.f;
+        }
+        sO[r * ldo + n] = nv ? v : 0.f;
       }
-      sO[r * ldo + n] = nv ? v : 0.f;
-    }
   }
 }
 
-// rows r0.. of an LDS tile [16][ld] (N columns, N % 4 == 0, N <= HC_MAXK) to
+// rows r0.. of an LDS tile [16 RT][ld] (N columns, N % 4 == 0, N <= HC_MAXK) to
 // global [rows][N]: thread (r, q0) copies row r's float4 columns q0, q0 + 16,
-// ...; every LDS read first, into distinct registers, then every store (a
-// loop reusing one register made each store wait for the previous one)
+// ... of each row tile; every LDS read of a row tile first, into distinct
+// registers, then its stores (a loop reusing one register made each store wait
+// for the previous one)
+template <int RT>
 __device__ __forceinline__ void hc_copy_out(const float* sO, int ld, int N, float* __restrict__ G,
                                            int64_t r0, int64_t rows) {
   constexpr int J = HC_MAXK / 4 / 16;
-  const int nq = N >> 2, r = threadIdx.x >> 4, q0 = threadIdx.x & 15;
-  float4 v[J];
+  const int nq = N >> 2, q0 = threadIdx.x & 15;
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int q = q0 + 16 * j;
-    v[j] = q < nq ? *reinterpret_cast<const float4*>(sO + r * ld + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
-  }
-  if (r0 + r >= rows) return;
-  float* g = G + (r0 + r) * N;
+  for (int rt = 0; rt < RT; ++rt) {
+    const int r = (threadIdx.x >> 4) + 16 * rt;
+    float4 v[J];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int q = q0 + 16 * j;
-    if (q < nq) *reinterpret_cast<float4*>(g + 4 * q) = v[j];
+    for (int j = 0; j < J; ++j) {
+      const int q = q0 + 16 * j;
+      v[j] = q < nq ? *reinterpret_cast<const float4*>(sO + r * ld + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (r0 + r >= rows) continue;
+    float* g = G + (r0 + r) * N;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int q = q0 + 16 * j;
+      if (q < nq) *reinterpret_cast<float4*>(g + 4 * q) = v[j];
+    }
   }
 }
 
@@ -279,31 +303,35 @@ __device__ __forceinline__ void hc_transpose_tile(const float* __restrict__ W, i
   }
 }
 
-template <int NT1, int NT2>
+// LDS floats of the forward's last-layer partials / transpose tile
+__host__ __device__ constexpr int hc_sr(int RT) { return RT * 1024 > HC_SR ? RT * 1024 : HC_SR; }
+
+template <int NT1, int NT2, int RT>
 __global__ void __launch_bounds__(kWG)
 head_fwd_kernel(HeadFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  constexpr int R = HC_R * RT;                    // rows per workgroup
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   // X and HA2 share one region (X is dead once layer 1's k loop is done: the
   // barrier after its epilogue orders that before layer 2 writes HA2): 37.5 KB
-  // at C3 widths, four workgroups per CU
-  float* s0 = hsm;                                // [16][ld0]  X
-  float* s2 = hsm;                                // [16][ld2]  HA2
-  float* s1 = hsm + HC_R * (a.ld0 > a.ld2 ? a.ld0 : a.ld2);   // [16][ld1]  HA1
-  float* sR = s1 + HC_R * a.ld1;                  // [4][64][4] partials of the last layer;
+  // at C3 widths and RT = 1, four workgroups per CU
+  float* s0 = hsm;                                // [R][ld0]  X
+  float* s2 = hsm;                                // [R][ld2]  HA2
+  float* s1 = hsm + R * (a.ld0 > a.ld2 ? a.ld0 : a.ld2);   // [R][ld1]  HA1
+  float* sR = s1 + R * a.ld1;                     // [4][RT][64][4] partials of the last layer;
                                                   // [32][33] transpose tile
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
-  const int64_t r0 = (int64_t)blockIdx.x * HC_R;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
   if (r0 < a.rows) {
     // layer 1's weight stream and bias first: in flight while X arrives
     HcStream<NT1> S1;
     S1.init(a.W1, a.K0, a.K0, a.h1, wave, 4, 0, 1);
-    float e1[NT1][4];
-    hc_epi_load<NT1, 0>(wave, a.h1, a.b1, nullptr, r0, a.rows, e1);
+    float e1[RT][NT1][4];
+    hc_epi_load<NT1, 0, RT>(wave, a.h1, a.b1, nullptr, r0, a.rows, e1);
     // X rows into LDS (columns K0 .. ld0 - 4 zero: the last chunk's padding)
     const int q0 = (a.ld0 - 4) >> 2;
-    for (int e = threadIdx.x; e < HC_R * q0; e += kWG) {
+    for (int e = threadIdx.x; e < R * q0; e += kWG) {
       const int r = e / q0, q = e - r * q0;
       const int64_t rr = r0 + r < a.rows ? r0 + r : a.rows - 1;
       float4 v = {0.f, 0.f, 0.f, 0.f};
@@ -312,41 +340,45 @@ head_fwd_kernel(HeadFwdArgs a) {
     }
     __syncthreads();
     HcStream<NT2> S2;
-    float e2[NT2][4];
+    float e2[RT][NT2][4];
     {   // layer 1: HA1 = relu(X W1^T + b1)
-      f32x4 acc[NT1];
-      hc_run<NT1>(S1, s0, a.ld0, acc);
+      f32x4 acc[RT][NT1];
+      hc_run<NT1, RT>(S1, s0, a.ld0, acc);
       S2.init(a.W2, a.h1, a.h1, a.h2, wave, 4, 0, 1);     // layer 2's stream, in flight
-      hc_epi_load<NT2, 0>(wave, a.h2, a.b2, nullptr, r0, a.rows, e2);
-      hc_store<NT1, 0>(acc, e1, wave, a.h1, s1, a.ld1);
+      hc_epi_load<NT2, 0, RT>(wave, a.h2, a.b2, nullptr, r0, a.rows, e2);
+      hc_store<NT1, 0, RT>(acc, e1, wave, a.h1, s1, a.ld1);
     }
     hc_sync();
-    hc_copy_out(s1, a.ld1, a.h1, a.HA1, r0, a.rows);
+    hc_copy_out<RT>(s1, a.ld1, a.h1, a.HA1, r0, a.rows);
     HcStream<1> S3;
     {   // layer 2: HA2 = relu(HA1 W2^T + b2)
-      f32x4 acc[NT2];
-      hc_run<NT2>(S2, s1, a.ld1, acc);
+      f32x4 acc[RT][NT2];
+      hc_run<NT2, RT>(S2, s1, a.ld1, acc);
       S3.init(a.W3, a.h2, a.h2, a.out, 0, 1, wave, 4);    // layer 3's stream
-      hc_store<NT2, 0>(acc, e2, wave, a.h2, s2, a.ld2);
+      hc_store<NT2, 0, RT>(acc, e2, wave, a.h2, s2, a.ld2);
     }
     hc_sync();
-    hc_copy_out(s2, a.ld2, a.h2, a.HA2, r0, a.rows);
+    hc_copy_out<RT>(s2, a.ld2, a.h2, a.HA2, r0, a.rows);
     {   // layer 3 (out <= 16): the waves split the k chunks, fixed-order sum
       const float bn = a.b3[li < a.out ? li : a.out - 1];
-      f32x4 acc[1];
-      hc_run<1>(S3, s2, a.ld2, acc);
-      *reinterpret_cast<float4*>(sR + (wave * 64 + lane) * 4) =
-          float4{acc[0][0], acc[0][1], acc[0][2], acc[0][3]};
+      f32x4 acc[RT][1];
+      hc_run<1, RT>(S3, s2, a.ld2, acc);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        *reinterpret_cast<float4*>(sR + ((wave * RT + rt) * 64 + lane) * 4) =
+            float4{acc[rt][0][0], acc[rt][0][1], acc[rt][0][2], acc[rt][0][3]};
       hc_sync();
       if (wave == 0 && li < a.out) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 4 * lk + i;
-          if (r0 + r >= a.rows) continue;
-          const float v = ((sR[(0 * 64 + lane) * 4 + i] + sR[(1 * 64 + lane) * 4 + i]) +
-                           (sR[(2 * 64 + lane) * 4 + i] + sR[(3 * 64 + lane) * 4 + i])) + bn;
-          a.Y[(r0 + r) * a.ldy + li] = a.tanh_out ? tanhf(v) : v;
-        }
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 16 * rt + 4 * lk + i;
+            if (r0 + r >= a.rows) continue;
+            const float v = ((sR[((0 * RT + rt) * 64 + lane) * 4 + i] + sR[((1 * RT + rt) * 64 + lane) * 4 + i]) +
+                             (sR[((2 * RT + rt) * 64 + lane) * 4 + i] + sR[((3 * RT + rt) * 64 + lane) * 4 + i])) + bn;
+            a.Y[(r0 + r) * a.ldy + li] = a.tanh_out ? tanhf(v) : v;
+          }
       }
     }
   }
@@ -361,35 +393,42 @@ head_fwd_kernel(HeadFwdArgs a) {
   }
 }
 
-template <int NTA, int NTB>
-__global__ void __launch_bounds__(kWG, 3)
+template <int NTA, int NTB, int RT>
+__global__ void __launch_bounds__(kWG, RT == 1 ? 3 : 2)
 head_bwd_kernel(HeadBwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  constexpr int R = HC_R * RT;                    // rows per workgroup
   extern __shared__ __attribute__((aligned(16))) float hsm[];
-  float* s2 = hsm;                                // [16][ld2]  dH2
-  float* s1 = s2 + HC_R * a.ld2;                  // [16][ld1]  dH1
-  float* sZ = s1 + HC_R * a.ld1;                  // [16][16]   dZ
+  float* s2 = hsm;                                // [R][ld2]  dH2
+  float* s1 = s2 + R * a.ld2;                     // [R][ld1]  dH1
+  float* sZ = s1 + R * a.ld1;                     // [R][16]   dZ
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
-  const int64_t r0 = (int64_t)blockIdx.x * HC_R;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
   const int out = a.out;
   // dZ rows (zero past out: the dH2 pass runs whole groups of 4 k), loaded
   // first; dH1's weight stream (W2^T) and its masks are issued behind them and
   // stay in flight through the dZ W3 pass
   const int zr = threadIdx.x >> 4, zk = threadIdx.x & 15;
-  const float zv = a.dZ[min(r0 + zr, a.rows - 1) * out + min(zk, out - 1)];
+  float zv[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+    zv[rt] = a.dZ[min(r0 + 16 * rt + zr, a.rows - 1) * out + min(zk, out - 1)];
   HcStream<NTA> SA;
   SA.init(a.W2T, a.h2, a.h2, a.h1, wave, 4, 0, 1);
-  sZ[zr * 16 + zk] = zk < out ? zv : 0.f;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) sZ[(16 * rt + zr) * 16 + zk] = zk < out ? zv[rt] : 0.f;
   // padding columns of dH2 (the next layer's last chunk)
   const int h2p = a.ld2 - 4;
-  for (int e = threadIdx.x; e < HC_R * (h2p - a.h2); e += kWG) {
+  for (int e = threadIdx.x; e < R * (h2p - a.h2); e += kWG) {
     const int r = e / (h2p - a.h2), c = e - r * (h2p - a.h2);
     s2[r * a.ld2 + a.h2 + c] = 0.f;
   }
   __syncthreads();
-  {   // dH2 = (dZ W3) * [HA2 > 0], K = out: lane = a 4-column group, wave = 4
-      // rows; the k-ordered fmaf chain from 0 (steps k >= out add 0 * w)
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    // dH2 = (dZ W3) * [HA2 > 0], K = out: lane = a 4-column group, wave = 4
+    // rows of row tile rt; the k-ordered fmaf chain from 0 (steps k >= out add 0 * w)
     const int nq = a.h2 >> 2;            // <= 128: at most two passes, unrolled (a loop
 #pragma unroll                           // header made the first pass drain every load
     for (int q0 = 0; q0 < 128; q0 += 64) {  // in flight, the weight prefetch included)
@@ -399,7 +438,7 @@ head_bwd_kernel(HeadBwdArgs a) {
       float4 m[4], v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int64_t rr = min(r0 + 4 * wave + i, a.rows - 1);
+        const int64_t rr = min(r0 + 16 * rt + 4 * wave + i, a.rows - 1);
         m[i] = *reinterpret_cast<const float4*>(a.HA2 + rr * a.h2 + 4 * q);
         v[i] = float4{0.f, 0.f, 0.f, 0.f};
       }
@@ -412,14 +451,14 @@ head_bwd_kernel(HeadBwdArgs a) {
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float z = sZ[(4 * wave + i) * 16 + kg + j];
+            const float z = sZ[(16 * rt + 4 * wave + i) * 16 + kg + j];
             v[i].x = fmaf(z, w[j].x, v[i].x); v[i].y = fmaf(z, w[j].y, v[i].y);
             v[i].z = fmaf(z, w[j].z, v[i].z); v[i].w = fmaf(z, w[j].w, v[i].w);
           }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int r = 4 * wave + i;
+        const int r = 16 * rt + 4 * wave + i;
         const float4 o = {m[i].x > 0.f ? v[i].x : 0.f, m[i].y > 0.f ? v[i].y : 0.f,
                           m[i].z > 0.f ? v[i].z : 0.f, m[i].w > 0.f ? v[i].w : 0.f};
         if (qv) {
@@ -431,23 +470,23 @@ head_bwd_kernel(HeadBwdArgs a) {
   }
   // dH1's masks, in flight behind its k loop (issued here rather than with the
   // weight prefetch: fewer registers live through the dZ W3 pass)
-  float eA[NTA][4];
-  hc_epi_load<NTA, 1>(wave, a.h1, nullptr, a.HA1, r0, a.rows, eA);
+  float eA[RT][NTA][4];
+  hc_epi_load<NTA, 1, RT>(wave, a.h1, nullptr, a.HA1, r0, a.rows, eA);
   hc_sync();
   HcStream<NTB> SB;
   {   // dH1 = (dH2 W2) * [HA1 > 0] = dH2 (W2^T)^T
-    f32x4 acc[NTA];
-    hc_run<NTA>(SA, s2, a.ld2, acc);
+    f32x4 acc[RT][NTA];
+    hc_run<NTA, RT>(SA, s2, a.ld2, acc);
     if (a.dxn > 0)      // dX's weight stream (rows dx0.. of W1^T), in flight
       SB.init(a.W1T + (int64_t)a.dx0 * a.h1, a.h1, a.h1, a.dxn, wave, 4, 0, 1);
-    hc_store<NTA, 1>(acc, eA, wave, a.h1, s1, a.ld1);
+    hc_store<NTA, 1, RT>(acc, eA, wave, a.h1, s1, a.ld1);
   }
   hc_sync();
-  hc_copy_out(s1, a.ld1, a.h1, a.dH1, r0, a.rows);
+  hc_copy_out<RT>(s1, a.ld1, a.h1, a.dH1, r0, a.rows);
   if (a.dxn <= 0) return;
   {   // dX = dH1 W1[:, dx0 : dx0 + dxn]
-    f32x4 acc[NTB];
-    hc_run<NTB>(SB, s1, a.ld1, acc);
+    f32x4 acc[RT][NTB];
+    hc_run<NTB, RT>(SB, s1, a.ld1, acc);
     const int CT = (a.dxn + 15) >> 4;
 #pragma unroll
     for (int t = 0; t < NTB; ++t) {
@@ -456,13 +495,15 @@ head_bwd_kernel(HeadBwdArgs a) {
       const int n = 16 * nt + li;
       if (n >= a.dxn) continue;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t r = r0 + 4 * lk + i;
-        if (r >= a.rows) continue;
-        float v = acc[t][i];
-        if (a.mask) v = a.mask[r * a.ldm + n] > 0.f ? v : 0.f;
-        a.dX[r * a.lddx + n] = v;
-      }
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t r = r0 + 16 * rt + 4 * lk + i;
+          if (r >= a.rows) continue;
+          float v = acc[rt][t][i];
+          if (a.mask) v = a.mask[r * a.ldm + n] > 0.f ? v : 0.f;
+          a.dX[r * a.lddx + n] = v;
+        }
     }
   }
 }
@@ -493,6 +534,20 @@ bool head_fused_ok(int in, int64_t ldx, int h1, int h2, int out, const float* X,
          out >= 1 && out <= 16 && al16(X) && al16(W1) && al16(W2) && al16(W3);
 }
 
+// row tiles per workgroup: 2 (32 rows: the weight chunks feed twice the MFMAs)
+// once the batch leaves at least ~2 workgroups per CU of them, else 1
+// (SMI_HEAD_RT = 1 | 2 forces one: A/B knob)
+static int hc_rt(int64_t rows) {
+  static int force = -1;
+  if (force < 0) {
+    const char* e = getenv("SMI_HEAD_RT");
+    force = e ? atoi(e) : 0;
+    if (force != 1 && force != 2) force = 0;
+  }
+  if (force) return force;
+  return rows >= 16384 ? 2 : 1;
+}
+
 int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
                           const float* b1, int h1, const float* W2, const float* b2, int h2,
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
@@ -501,14 +556,21 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
   if (rows <= 0) return SMI_OK;
   HeadFwdArgs a{X, ldx, in, W1, b1, W2, b2, W3, b3, h1, h2, out, tanh_out, HA1, HA2, Y, ldy,
                 W1T, W2T, rows, skip, hc_ld(in), hc_ld(h1), hc_ld(h2)};
-  const size_t lds = (size_t)(HC_R * ((a.ld0 > a.ld2 ? a.ld0 : a.ld2) + a.ld1) + HC_SR) * 4;
-  const dim3 grid((unsigned)((rows + HC_R - 1) / HC_R));
+  const int rt = hc_rt(rows);
+  const int R = HC_R * rt;
+  const size_t lds = (size_t)(R * ((a.ld0 > a.ld2 ? a.ld0 : a.ld2) + a.ld1) + hc_sr(rt)) * 4;
+  const dim3 grid((unsigned)((rows + R - 1) / R));
   const int n1 = hc_nt(h1), n2 = hc_nt(h2);
   const int kslot = ktime_begin(st);
-#define SMI_HF(A, B)                                                              \
-  do {                                                                            \
-    allow_lds(head_fwd_kernel<A, B>, lds);                                        \
-    hipLaunchKernelGGL((head_fwd_kernel<A, B>), grid, dim3(kWG), lds, st, a);     \
+#define SMI_HF(A, B)                                                                    \
+  do {                                                                                  \
+    if (rt == 2) {                                                                      \
+      allow_lds(head_fwd_kernel<A, B, 2>, lds);                                         \
+      hipLaunchKernelGGL((head_fwd_kernel<A, B, 2>), grid, dim3(kWG), lds, st, a);      \
+    } else {                                                                            \
+      allow_lds(head_fwd_kernel<A, B, 1>, lds);                                         \
+      hipLaunchKernelGGL((head_fwd_kernel<A, B, 1>), grid, dim3(kWG), lds, st, a);      \
+    }                                                                                   \
   } while (0)
   // layer-1 slots {2, 5, 8} x layer-2 slots {2, 3, 4, 5, 8} (C3 / C5: 300 x 200 -> 5, 4)
   const int m1 = n1 <= 2 ? 2 : n1 <= 5 ? 5 : 8;
@@ -540,16 +602,23 @@ int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W
   if (rows <= 0) return SMI_OK;
   HeadBwdArgs a{dZ, out, W3, W2T, W1T, h1, h2, dx0, dxn, HA1, HA2, dH2, dH1, dX, lddx, mask, ldm,
                 rows, skip, hc_ld(h2), hc_ld(h1)};
-  const size_t lds = (size_t)(HC_R * (a.ld2 + a.ld1) + HC_R * 16) * 4;
-  const dim3 grid((unsigned)((rows + HC_R - 1) / HC_R));
+  const int rt = hc_rt(rows);
+  const int R = HC_R * rt;
+  const size_t lds = (size_t)(R * (a.ld2 + a.ld1) + R * 16) * 4;
+  const dim3 grid((unsigned)((rows + R - 1) / R));
   int na = hc_nt(h1), nb = hc_nt(dxn > 0 ? dxn : 1);
   na = na <= 2 ? 2 : na <= 5 ? 5 : 8;
   nb = nb <= 2 ? 2 : 5;
   const int kslot = ktime_begin(st);
-#define SMI_HB(A, B)                                                              \
-  do {                                                                            \
-    allow_lds(head_bwd_kernel<A, B>, lds);                                        \
-    hipLaunchKernelGGL((head_bwd_kernel<A, B>), grid, dim3(kWG), lds, st, a);     \
+#define SMI_HB(A, B)                                                                   \
+  do {                                                                                 \
+    if (rt == 2) {                                                                     \
+      allow_lds(head_bwd_kernel<A, B, 2>, lds);                                        \
+      hipLaunchKernelGGL((head_bwd_kernel<A, B, 2>), grid, dim3(kWG), lds, st, a);     \
+    } else {                                                                           \
+      allow_lds(head_bwd_kernel<A, B, 1>, lds);                                        \
+      hipLaunchKernelGGL((head_bwd_kernel<A, B, 1>), grid, dim3(kWG), lds, st, a);     \
+    }                                                                                  \
   } while (0)
   if (na == 2 && nb == 2) SMI_HB(2, 2);
   else if (na == 2) SMI_HB(2, 5);
