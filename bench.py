@@ -437,6 +437,8 @@ def main():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', choices=['c2', 'c3', 'c4', 'c5'], default='c3')
+    ap.add_argument('--ppo-mode', choices=['adapt', 'clip'], default=None,
+                    help='override the workload\'s PPO surrogate (A/B only; C2-C5 are adapt)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
     ap.add_argument('--local-segments', type=int, default=None,
@@ -464,6 +466,8 @@ def main():
     from surreal_amd import synthetic
     from surreal_amd.learner import PPOLearner, TorchDistAllReduce
     lc, ec, dims = make_config(args.config)
+    if args.ppo_mode:               # A/B of the clip surrogate (the workloads are adapt)
+        lc.algo.ppo_mode = args.ppo_mode
     scaling = args.scaling or ('weak' if args.config == 'c2' else 'strong')
     if scaling == 'strong':
         if dims['B_global'] % world:
@@ -589,7 +593,7 @@ def main():
         'config': {'workload': wl, 'segments_per_gpu': B, 'n_step': T,
                    'env_steps_per_learn_per_gpu': B * T, 'global_segments': world * B,
                    'parallelism': f'dp{world}' if world > 1 else 'single',
-                   'epochs_run_last': epochs_run,
+                   'epochs_run_last': epochs_run, 'ppo_mode': lc.algo.ppo_mode,
                    'launch': 'hipGraph replay' if learner._graph is not None else 'eager'},
         'roofline': roof,
         'kernels': kernels,

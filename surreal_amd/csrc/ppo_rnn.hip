@@ -174,11 +174,15 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
 // for t < S (S <= T+1).  z_filter.py:59-79 (clamp +-5); use_zf == 0 copies.
 // One wave per row (32-bit row index math once per row, not per element):
 // lane j moves columns j, j + 64 of a D <= 128-wide row, so each load and
-// store instruction covers one contiguous row.
+// store instruction covers one contiguous row.  A wave takes kZfRows rows per
+// trip with every load issued before the first store (one row in flight per
+// wave held the launch at ~0.24 of HBM at > 256 MB working sets).
+constexpr int kZfRows = 8;
 __global__ void __launch_bounds__(kWG)
 zf_tmajor_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next, int B, int T,
                  int S, int D, int use_zf, const float* zs, const float* zq, const float* zc,
                  float eps, float* __restrict__ out, int ldo) {
+  if (D <= 0) return;                            // pixel-only: no low-dim columns
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* zm = sm;
   float* zd = sm + round4(D);
@@ -192,20 +196,139 @@ zf_tmajor_kernel(const float* __restrict__ obs, const float* __restrict__ obs_ne
     if (lane < D) { m0 = zm[lane]; d0 = zd[lane]; }
     if (lane + 64 < D) { m1 = zm[lane + 64]; d1 = zd[lane + 64]; }
   }
-  for (int row = w0; row < nrows; row += nw) {
-    const int t = row / B, b = row - t * B;
-    const float* src = t < T ? obs + ((int64_t)b * T + t) * D : obs_next + (int64_t)b * D;
-    float* dst = out + (int64_t)row * ldo;
-    if (lane < D) {
-      float v = src[lane];
-      if (use_zf) v = fminf(fmaxf((v - m0) / d0, -5.f), 5.f);
-      dst[lane] = v;
+  if ((D & 1) == 0 && (ldo & 1) == 0 && (reinterpret_cast<uintptr_t>(obs) & 7) == 0 &&
+      (reinterpret_cast<uintptr_t>(obs_next) & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0) {
+    // even widths: 8-byte lanes, floor(128 / D) rows per load instruction
+    // (D = 42: three rows on 63 lanes instead of one row on 42)
+    const int D2 = D >> 1, rpi = 64 / D2;
+    const int lr = lane / D2, lc = lane - lr * D2;
+    const bool lv = lr < rpi;
+    const int cc = lv ? 2 * lc : 0;
+    float2 zm2 = {0.f, 0.f}, zd2 = {1.f, 1.f};
+    if (use_zf) { zm2 = float2{zm[cc], zm[cc + 1]}; zd2 = float2{zd[cc], zd[cc + 1]}; }
+    const int rpt = kZfRows * rpi;                  // rows per wave and trip
+    for (int row0 = w0 * rpt; row0 < nrows; row0 += nw * rpt) {
+      float2 v[kZfRows];
+#pragma unroll
+      for (int j = 0; j < kZfRows; ++j) {
+        const int row = min(row0 + j * rpi + (lv ? lr : 0), nrows - 1);
+        const int t = row / B, b = row - t * B;
+        const float* src = t < T ? obs + ((int64_t)b * T + t) * D : obs_next + (int64_t)b * D;
+        v[j] = *reinterpret_cast<const float2*>(src + cc);
+      }
+#pragma unroll
+      for (int j = 0; j < kZfRows; ++j) {
+        const int row = row0 + j * rpi + lr;
+        if (!lv || row >= nrows) continue;
+        float2 o = v[j];
+        if (use_zf) {
+          o.x = fminf(fmaxf((o.x - zm2.x) / zd2.x, -5.f), 5.f);
+          o.y = fminf(fmaxf((o.y - zm2.y) / zd2.y, -5.f), 5.f);
+        }
+        *reinterpret_cast<float2*>(out + (int64_t)row * ldo + cc) = o;
+      }
     }
-    if (lane + 64 < D) {
-      float v = src[lane + 64];
-      if (use_zf) v = fminf(fmaxf((v - m1) / d1, -5.f), 5.f);
-      dst[lane + 64] = v;
+    return;
+  }
+  const int c0 = lane < D ? lane : D - 1;               // clamped: unconditional loads
+  const int c1 = lane + 64 < D ? lane + 64 : D - 1;
+  const bool two = D > 64;
+  for (int row0 = w0 * kZfRows; row0 < nrows; row0 += nw * kZfRows) {
+    float v0[kZfRows], v1[kZfRows];
+#pragma unroll
+    for (int j = 0; j < kZfRows; ++j) {
+      const int row = min(row0 + j, nrows - 1);
+      const int t = row / B, b = row - t * B;
+      const float* src = t < T ? obs + ((int64_t)b * T + t) * D : obs_next + (int64_t)b * D;
+      v0[j] = src[c0];
+      v1[j] = two ? src[c1] : 0.f;
     }
+#pragma unroll
+    for (int j = 0; j < kZfRows; ++j) {
+      const int row = row0 + j;
+      if (row >= nrows) break;
+      float* dst = out + (int64_t)row * ldo;
+      if (lane < D) {
+        float v = v0[j];
+        if (use_zf) v = fminf(fmaxf((v - m0) / d0, -5.f), 5.f);
+        dst[lane] = v;
+      }
+      if (lane + 64 < D) {
+        float v = v1[j];
+        if (use_zf) v = fminf(fmaxf((v - m1) / d1, -5.f), 5.f);
+        dst[lane + 64] = v;
+      }
+    }
+  }
+}
+
+// The same transform as a tile transpose through LDS (even D <= 128, 8-byte
+// aligned rows): a workgroup takes kZfSeg segments, reads each one's S rows as
+// ONE contiguous run (obs[b][0..T-1] is contiguous; the t = T row comes from
+// obs_next) and writes, for every step t, the kZfSeg consecutive output rows
+// t*B + b0 .. (contiguous too).  The row-per-wave kernel above reads 168-byte
+// rows 4.4 KB apart: partial cache lines on every row, 0.42 of HBM at > 256 MB.
+constexpr int kZfSeg = 8;
+__global__ void __launch_bounds__(kWG)
+zf_tile_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next, int B, int T,
+               int S, int D, int use_zf, const float* zs, const float* zq, const float* zc,
+               float eps, float* __restrict__ out, int ldo) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* zm = sm;                                  // [round4(D)]
+  float* zd = sm + round4(D);
+  float* tile = sm + 2 * round4(D);                // [kZfSeg][S][D]
+  if (use_zf) zfilter_colstats(zs, zq, zc, eps, D, zm, zd);
+  const int b0 = blockIdx.x * kZfSeg;
+  const int nseg = min(kZfSeg, B - b0);
+  const int D2 = D >> 1, ST = min(S, T);
+  // phase 1: each segment's rows, contiguous in obs, as float2 runs; eight
+  // loads in flight per thread before their LDS stores (one at a time left
+  // the block latency-bound: 0.34 of HBM)
+  {
+    const int per = ST * D2;                        // float2 per segment from obs
+    const int tot = nseg * per;
+    float2* t2 = reinterpret_cast<float2*>(tile);
+    const float2* o2 = reinterpret_cast<const float2*>(obs + (int64_t)b0 * T * D);
+    for (int base = 0; base < tot; base += 8 * kWG) {
+      float2 r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = min(base + k * kWG + (int)threadIdx.x, tot - 1);
+        const int bl = e / per, q = e - bl * per;
+        r[k] = o2[(int64_t)bl * T * D2 + q];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = base + k * kWG + threadIdx.x;
+        if (e < tot) {
+          const int bl = e / per, q = e - bl * per;
+          t2[(int64_t)bl * S * D2 + q] = r[k];
+        }
+      }
+    }
+    if (S > T) {
+      for (int e = threadIdx.x; e < nseg * D2; e += kWG) {
+        const int bl = e / D2, c = e - bl * D2;
+        t2[(int64_t)bl * S * D2 + T * D2 + c] =
+            reinterpret_cast<const float2*>(obs_next + (int64_t)(b0 + bl) * D)[c];
+      }
+    }
+  }
+  __syncthreads();
+  // phase 2: thread (bl, c2) writes column pair c2 of segment bl at every step
+  const int bl = threadIdx.x / D2, c2 = threadIdx.x - bl * D2;
+  if (bl >= nseg) return;
+  float2 m = {0.f, 0.f}, dd = {1.f, 1.f};
+  if (use_zf) { m = float2{zm[2 * c2], zm[2 * c2 + 1]}; dd = float2{zd[2 * c2], zd[2 * c2 + 1]}; }
+  const float2* tp = reinterpret_cast<const float2*>(tile + (int64_t)bl * S * D) + c2;
+  float* op = out + (int64_t)(b0 + bl) * ldo + 2 * c2;
+  for (int t = 0; t < S; ++t) {
+    float2 v = tp[t * D2];
+    if (use_zf) {
+      v.x = fminf(fmaxf((v.x - m.x) / dd.x, -5.f), 5.f);
+      v.y = fminf(fmaxf((v.y - m.y) / dd.y, -5.f), 5.f);
+    }
+    *reinterpret_cast<float2*>(op + (int64_t)t * B * ldo) = v;
   }
 }
 
@@ -361,13 +484,18 @@ row_pack_kernel(PolRowArgs a, float* __restrict__ rowin, float* __restrict__ ret
 
 // forward statistics of the policy over the E*B rows (ppo.py:203-224,
 // 262-284, 553-575)
-template <int NT, int AT>
+// FUSE (clip mode): the same pass also writes the per-row gradient dz and the
+// d/dstd block partials that policy_rows_grad_kernel would compute for this
+// epoch (the clip surrogate's gradient needs no global statistic: weight 1/N,
+// no KL term), bit-identically, so the gradient phase skips its row pass
+template <int NT, int AT, bool FUSE>
 __global__ void __launch_bounds__(NT)
 policy_rows_stats_kernel(PolRowArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   constexpr int AM = AT > 0 ? AT : 32;
   __shared__ float ssig[32], slsig[32], srsig[32];
   __shared__ double scr[NT / 64][PS_N];
+  __shared__ float gls[FUSE ? NT / 64 : 1][32];
   const int A = AT > 0 ? AT : a.A;
   const int RW = row_w(A);
   for (int j = threadIdx.x; j < A; j += NT) {
@@ -383,6 +511,11 @@ policy_rows_stats_kernel(PolRowArgs a) {
   double acc[PS_N];
 #pragma unroll
   for (int k = 0; k < PS_N; ++k) acc[k] = 0.0;
+  float glv[AM];
+  if constexpr (FUSE) {
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
+  }
   const int64_t N = (int64_t)a.E * a.B;
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
     float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM];
@@ -393,7 +526,8 @@ policy_rows_stats_kernel(PolRowArgs a) {
     ld_row<AT>(bmu, rw + A, A);
     ld_row<AT>(bsd, rw + 2 * A, A);
     const float av = norm_adv_of(a, rw[3 * A]);
-    const float lp = fmaxf(expf(row_loglik<AT>(ac, m, sig, lsig, A, a.c_ll)), 1e-5f);
+    const float ex = expf(row_loglik<AT>(ac, m, sig, lsig, A, a.c_ll));
+    const float lp = fmaxf(ex, 1e-5f);
 #pragma unroll
     for (int j = 0; j < (AT > 0 ? AT : A); ++j) blsd[j] = logf(bsd[j]);
     const float bl = fmaxf(expf(row_loglik<AT>(ac, bmu, bsd, blsd, A, a.c_ll)), 1e-5f);
@@ -411,6 +545,38 @@ policy_rows_stats_kernel(PolRowArgs a) {
     acc[PS_BL] += (double)bl;
     acc[PS_RBD] += (double)row_kl<AT>(rm, rsig, bmu, bsd, A);
     acc[PS_RET] += (double)a.ret_tm[n];
+    if constexpr (FUSE) {          // policy_rows_grad_kernel's clip branch, weight a.invN
+      const float ratio = lp / bl;
+      const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
+      const float surr = -ratio * av, csur = -cr * av;
+      const float g_lp = ((surr >= csur) ? -(a.invN * av) : 0.f) / bl;
+      const float g_ll = (ex >= 1e-5f) ? g_lp * ex : 0.f;
+      float dz[AM];
+#pragma unroll
+      for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+        const float s1 = sig[j];
+        const float u = (ac[j] - m[j]) / s1;
+        const float gmu = g_ll * (u / s1);
+        const float gsd = g_ll * (u * u / s1 - 1.f / s1);
+        glv[j] += gsd;
+        dz[j] = gmu * (1.f - m[j] * m[j]);
+      }
+      st_row<AT>(a.dz + n * A, dz, A);
+    }
+  }
+  if constexpr (FUSE) {            // block partials of sum_rows d/dstd, as the grad kernel
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+      const float sg = wave_sum(glv[j]);
+      if (lane == 0) gls[wave][j] = sg;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < A; j += NT) {
+      float sg = 0.f;
+      for (int w = 0; w < NT / 64; ++w) sg += gls[w][j];
+      a.lvpart[(int64_t)blockIdx.x * A + j] = sg;
+    }
   }
   // all PS_N sums at once: wave butterflies, one barrier, fixed wave order
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -607,30 +773,41 @@ reduce_decide_kernel(const double* __restrict__ part, int nb, DecideArgs a, cons
 }
 
 // value loss rows: V and the returns, both time-major [NE]; dV = 2 (V - R) / N
-// and, in the last epoch, the sums of ppo.py:324-331
+// and, in the last epoch, the sums of ppo.py:324-331.  A thread takes 4 rows
+// per trip as float4s (V, R and dV are 16-byte aligned scratch rows), the
+// NE % 4 tail one row per thread.
 template <int NT>
 __global__ void __launch_bounds__(NT)
 value_rows_kernel(const float* __restrict__ V, const float* __restrict__ ret_tm, int B, int E,
                   float invN2, float* __restrict__ dV, double* part) {
   __shared__ double scr[NT / 64];
   double se = 0.0, d1 = 0.0, d2 = 0.0, r1 = 0.0, r2 = 0.0;
-  const int64_t N = (int64_t)E * B;
-  for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
-    const float r = ret_tm[n];
-    const float v = V[n];
+  auto acc = [&](float v, float r) {
     const float e = v - r;
-    dV[n] = invN2 * e;
-    if (part) {
-      se += (double)(e * e);
-      const double dd = (double)r - (double)v;
-      d1 += dd; d2 += dd * dd;
-      r1 += (double)r; r2 += (double)r * (double)r;
-    }
+    se += (double)(e * e);
+    const double dd = (double)r - (double)v;
+    d1 += dd; d2 += dd * dd;
+    r1 += (double)r; r2 += (double)r * (double)r;
+  };
+  const int64_t N = (int64_t)E * B, N4 = N >> 2;
+  const int64_t g0 = (int64_t)blockIdx.x * NT + threadIdx.x, gs = (int64_t)gridDim.x * NT;
+  const float4* V4 = reinterpret_cast<const float4*>(V);
+  const float4* R4 = reinterpret_cast<const float4*>(ret_tm);
+  float4* D4 = reinterpret_cast<float4*>(dV);
+  for (int64_t g = g0; g < N4; g += gs) {
+    const float4 r = R4[g], v = V4[g];
+    D4[g] = float4{invN2 * (v.x - r.x), invN2 * (v.y - r.y), invN2 * (v.z - r.z), invN2 * (v.w - r.w)};
+    if (part) { acc(v.x, r.x); acc(v.y, r.y); acc(v.z, r.z); acc(v.w, r.w); }
+  }
+  for (int64_t n = 4 * N4 + g0; n < N; n += gs) {
+    const float r = ret_tm[n], v = V[n];
+    dV[n] = invN2 * (v - r);
+    if (part) acc(v, r);
   }
   if (!part) return;
-  const double s[5] = {se, d1, d2, r1, r2};
+  const double sv[5] = {se, d1, d2, r1, r2};
   for (int k = 0; k < 5; ++k) {
-    const double t = block_sum_d<NT>(s[k], scr);
+    const double t = block_sum_d<NT>(sv[k], scr);
     if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 5 + k] = t;
   }
 }
@@ -764,6 +941,22 @@ __global__ void rnn_init_kernel(int* ci, float* cf) {
 }
 
 // ------------------------------------------------------------ host phases
+
+template <bool FUSE>
+static void launch_pol_stats(int A, int nb, const PolRowArgs& p, hipStream_t st) {
+  switch (A) {   // compile-time action widths 1..8 (registers); others generic
+    case 1: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 1, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 2, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 3, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 4, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+    case 5: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 5, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 6, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+    case 7: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 7, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 8, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+    default: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 0, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+  }
+}
+
 static int grid_of(int64_t n, int cap = 1024) {
   int64_t g = (n + kWG - 1) / kWG;
   if (g < 1) g = 1;
@@ -772,11 +965,36 @@ static int grid_of(int64_t n, int cap = 1024) {
 
 #define RC(x) do { const int rc_ = (x); if (rc_) return rc_; } while (0)
 
-// zf_tmajor_kernel: one wave per row, 4 waves per block, at most 2048 blocks
+// zf_tmajor_kernel: kZfRows (x rows per load) rows per wave and trip, 4 waves
+// per block, at most 2048 blocks
 static int zf_grid(int64_t rows) {
-  int64_t g = (rows + 3) / 4;
+  int64_t g = (rows + 4 * kZfRows - 1) / (4 * kZfRows);
   if (g < 1) g = 1;
   return (int)(g < 2048 ? g : 2048);
+}
+
+// the time-major z-filtered copy of the batch's low-dim observations: the tile
+// transpose where its shape conditions hold, else the row-per-wave kernel
+static void launch_zf_tmajor(const float* obs, const float* obs_next, int B, int T, int S, int D,
+                             int use_zf, const float* zs, const float* zq, const float* zc,
+                             float eps, float* out, int ldo, hipStream_t st) {
+  if (D <= 0 || S <= 0) return;
+  auto a8 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; };
+  const size_t tl = ((size_t)2 * round4(D) + (size_t)kZfSeg * S * D) * 4;
+  static const bool tile_on = [] { const char* e = getenv("SMI_ZF_TILE"); return !(e && e[0] == '0'); }();
+  static const bool force = [] { const char* e = getenv("SMI_ZF_TILE_FORCE"); return e && e[0] == '1'; }();
+  // (from 4096 segments: at C3's 1024 the 128 tile workgroups took 14.5 us
+  // against 9.7 for the row kernel; at 65536, 146 against 169 us)
+  if (tile_on && (B >= 4096 || force) && D % 2 == 0 && D <= 128 && ldo % 2 == 0 && a8(obs) && a8(obs_next) && a8(out) &&
+      D / 2 * kZfSeg <= kWG && tl <= 64 * 1024) {
+    allow_lds(zf_tile_kernel, tl);
+    hipLaunchKernelGGL(zf_tile_kernel, dim3((B + kZfSeg - 1) / kZfSeg), dim3(kWG), tl, st, obs,
+                       obs_next, B, T, S, D, use_zf, zs, zq, zc, eps, out, ldo);
+    return;
+  }
+  const size_t zlds = (size_t)2 * round4(D) * 4;
+  hipLaunchKernelGGL(zf_tmajor_kernel, dim3(zf_grid((int64_t)S * B)), dim3(kWG), zlds, st, obs,
+                     obs_next, B, T, S, D, use_zf, zs, zq, zc, eps, out, ldo);
 }
 
 struct Head {   // one MLP head over rows of an activation matrix
@@ -1060,15 +1278,13 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
   float* gA = a.xbuf;                                  // [actor head | lstm | cnn]
   float* gC = a.xbuf + d.nA_head + d.nS;               // [critic head | lstm | cnn]
   const int64_t NEg = (int64_t)d.E * a.B_global;
-  const size_t zlds = (size_t)2 * round4(d.D) * 4;
   switch (phase) {
     case SMI_RNN_PH_GAE: {
       hipLaunchKernelGGL(rnn_init_kernel, dim3(1), dim3(64), 0, st, s.ci, s.cf);
       RC(check_launch("rnn_init_kernel"));
       int kt = ktime_begin(st);
-      hipLaunchKernelGGL(zf_tmajor_kernel, dim3(zf_grid(d.NG)), dim3(kWG), zlds, st, a.obs,
-                         a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum, a.zf_sumsq,
-                         a.zf_count, a.zf_eps, s.Xz, d.ldx);
+      launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum, a.zf_sumsq,
+                       a.zf_count, a.zf_eps, s.Xz, d.ldx, st);
       ktime_end(kt, KT_ZF_TMAJOR, 8.0 * (double)d.NG * d.D, st);      // read x, write z(x)
       RC(check_launch("zf_tmajor_kernel"));
       RC(cnn_features(a, d, cnn, d.S1, s.Xz, nullptr, s, st, nullptr));
@@ -1097,9 +1313,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       RnnScratch sp = s;
       sp.xproj = s.xprojR; sp.hbuf = s.hbufR; sp.HA1 = s.HA1R; sp.HA2 = s.HA2R; sp.A2 = s.A2R;
       const float* X = s.Xr;
-      hipLaunchKernelGGL(zf_tmajor_kernel, dim3(zf_grid(d.NE)), dim3(kWG), zlds, st, a.obs,
-                         a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
-                         a.rzf_count, a.zf_eps, s.Xr, d.ldx);
+      launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
+                       a.rzf_count, a.zf_eps, s.Xr, d.ldx, st);
       RC(check_launch("zf_tmajor_kernel"));
       RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, sp, st, nullptr));
       if (d.H > 0) RC(lstm_forward(d, a.ref_lstm, X, d.E, a.h0, a.c0, sp, false, st, nullptr));
@@ -1124,17 +1339,9 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE, kRowNT);
       const int kt = ktime_begin(st);
-      switch (d.A) {   // compile-time action widths 1..8 (registers); others generic
-        case 1: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 1>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 2: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 2>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 3: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 3>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 4: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 4>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 5: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 5>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 6: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 6>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 7: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 7>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 8: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 8>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        default: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 0>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-      }
+      p.invN = (float)(1.0 / (double)NEg);
+      if (a.mode == 0) launch_pol_stats<true>(d.A, nb, p, st);     // + the clip gradient
+      else launch_pol_stats<false>(d.A, nb, p, st);
       // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
       ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
       RC(check_launch("policy_rows_stats_kernel"));
@@ -1160,21 +1367,23 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_POLICY_BWD: {
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = rnn_nblk(d.NE, kRowNT);
-      const int kt = ktime_begin(st);
-      switch (d.A) {   // compile-time action widths 1..8 (registers); others generic
-        case 1: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 1>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 2: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 2>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 3: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 3>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 4: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 4>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 5: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 5>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 6: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 6>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 7: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 7>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        case 8: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 8>), dim3(nb), dim3(kRowNT), 0, st, p); break;
-        default: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 0>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+      if (a.mode != 0) {     // clip: dz and the log_var partials came with POLICY_FWD's pass
+        const int kt = ktime_begin(st);
+        switch (d.A) {   // compile-time action widths 1..8 (registers); others generic
+          case 1: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 1>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+          case 2: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 2>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+          case 3: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 3>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+          case 4: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 4>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+          case 5: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 5>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+          case 6: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 6>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+          case 7: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 7>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+          case 8: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 8>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+          default: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 0>), dim3(nb), dim3(kRowNT), 0, st, p); break;
+        }
+        // per row: mu, refmu, actions, behave (5A) + adv read, dz (A) written
+        ktime_end(kt, KT_POLICY_GRAD, 4.0 * (double)d.NE * (6 * d.A + 1), st);
+        RC(check_launch("policy_rows_grad_kernel"));
       }
-      // per row: mu, refmu, actions, behave (5A) + adv read, dz (A) written
-      ktime_end(kt, KT_POLICY_GRAD, 4.0 * (double)d.NE * (6 * d.A + 1), st);
-      RC(check_launch("policy_rows_grad_kernel"));
       RC(stem_backward(a, d, actor, lm, cnn, gA, s, d.nA_head, st, stop));
       hipLaunchKernelGGL(logvar_grad_kernel, dim3(1), dim3(kWG), 0, st, s.lvpart, nb, d.A,
                          a.actor + d.LA.flv, gA + d.LA.flv, stop);
@@ -1201,7 +1410,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, nullptr));
       RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr,
                   s.wT));
-      const int nb = rnn_nblk(d.NE, kRowNT);
+      const int nb = rnn_nblk((d.NE + 3) / 4, kRowNT);     // 4 rows per thread
       const bool last = e == a.epoch_baseline - 1;
       const int kt = ktime_begin(st);
       hipLaunchKernelGGL(value_rows_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, s.OUT, s.ret_tm, d.B, d.E,
