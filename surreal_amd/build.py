@@ -48,6 +48,8 @@ VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             'dwg8': ['-DSMI_DWG_NT=8'], 'dwgocc4': ['-DSMI_DWG_OCC=4'],   # (occupancy 4: 122 us)
             # VALU recurrence: LDS reads per pipelined chunk (product: 4)
             'vc2': ['-DSMI_LSTM_VC=2'], 'vc8': ['-DSMI_LSTM_VC=8'],
+            # VALU recurrence dot products on v_pk_fma_f32 (product: scalar FMAs)
+            'pk': ['-DSMI_LSTM_PK=1'],
             # grouped-dW anatomy (tools/bench_dwgroup.py only; wrong results by design):
             # MFMAs without the operand stream / the stream without the MFMAs
             'dwdiag_mfma': ['-DSMI_DWD_DIAG=1'], 'dwdiag_load': ['-DSMI_DWD_DIAG=2'],

@@ -885,11 +885,21 @@ constexpr int kVT = 512;      // threads of the VALU recurrence workgroups (4H <
 #define SMI_LSTM_VC 4
 #endif
 constexpr int kVC = SMI_LSTM_VC;
+// SMI_LSTM_PK=1: the dot products on v_pk_fma_f32 (same sums, half the
+// instructions) — measured slower at 128 segments (1.70 / 1.61 us per forward /
+// BPTT step against 1.62 / 1.50 on scalar FMAs): A/B only
+#ifndef SMI_LSTM_PK
+#define SMI_LSTM_PK 0
+#endif
+typedef float vf2 __attribute__((ext_vector_type(2)));
 template <int KP>
 __device__ __forceinline__ void v_dot_pipelined(const float4* __restrict__ v, const float (&w)[KP],
                                                 float& s0, float& s1, float& s2, float& s3) {
   constexpr int N4 = KP / 4, NC = (N4 + kVC - 1) / kVC;
   float4 buf[2][kVC];
+#if SMI_LSTM_PK
+  vf2 a01 = {s0, s1}, a23 = {s2, s3};
+#endif
   auto ld = [&](int c) {
 #pragma unroll
     for (int i = 0; i < kVC; ++i)
@@ -905,14 +915,24 @@ __device__ __forceinline__ void v_dot_pipelined(const float4* __restrict__ v, co
       const int k4 = c * kVC + i;
       if (k4 < N4) {
         const float4 hv = buf[c & 1][i];
+#if SMI_LSTM_PK
+        // v_pk_fma_f32: (s0, s1) and (s2, s3) as packed pairs, each lane an
+        // fmaf of the same operands as the scalar form (bit-identical sums)
+        a01 = __builtin_elementwise_fma(vf2{hv.x, hv.y}, vf2{w[4 * k4], w[4 * k4 + 1]}, a01);
+        a23 = __builtin_elementwise_fma(vf2{hv.z, hv.w}, vf2{w[4 * k4 + 2], w[4 * k4 + 3]}, a23);
+#else
         s0 = fmaf(hv.x, w[4 * k4], s0);
         s1 = fmaf(hv.y, w[4 * k4 + 1], s1);
         s2 = fmaf(hv.z, w[4 * k4 + 2], s2);
         s3 = fmaf(hv.w, w[4 * k4 + 3], s3);
+#endif
       }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+#if SMI_LSTM_PK
+  s0 = a01.x; s1 = a01.y; s2 = a23.x; s3 = a23.y;
+#endif
 }
 
 template <int R, int KP, int KX>

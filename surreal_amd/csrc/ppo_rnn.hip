@@ -461,6 +461,23 @@ __device__ __forceinline__ float row_kl(const float* mu0, const float* sd0, cons
   return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
 }
 
+// row_kl with BOTH distributions' stds fixed per column (the reference policy
+// against the learner: log(sd1 / sd0), sd0^2 and 2 sd1^2 are hoisted out of the
+// row loop as lkl, s02, den2 — the same operations in the same order, computed
+// once per workgroup instead of once per row)
+template <int AT>
+__device__ __forceinline__ float row_kl_cc(const float* mu0, const float* mu1, const float* lkl,
+                                           const float* s02, const float* den2, int A) {
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    s1 += lkl[j];
+    const float d = mu0[j] - mu1[j];
+    s2 += (s02[j] + d * d) / den2[j];
+  }
+  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
+}
+
 // rowin / ret_tm from the batch-major inputs (once per learn): the per-row
 // kernels of every epoch then read whole rows in time-major order (coalesced)
 // instead of A- and E-strided gathers from [B][T][.] / [B][E]
@@ -504,9 +521,14 @@ policy_rows_stats_kernel(PolRowArgs a) {
     srsig[j] = expf(a.ref_lv[j]);
   }
   __syncthreads();
-  float sig[AM], lsig[AM], rsig[AM];
+  float sig[AM], lsig[AM], rsig[AM], lkl[AM], s02[AM], den2[AM];
 #pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) { sig[j] = ssig[j]; lsig[j] = slsig[j]; rsig[j] = srsig[j]; }
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    sig[j] = ssig[j]; lsig[j] = slsig[j]; rsig[j] = srsig[j];
+    lkl[j] = logf(sig[j] / rsig[j]);            // row_kl(rm, rsig, m, sig)'s per-column terms
+    s02[j] = rsig[j] * rsig[j];
+    den2[j] = 2.f * (sig[j] * sig[j]);
+  }
   const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   double acc[PS_N];
 #pragma unroll
@@ -531,7 +553,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
 #pragma unroll
     for (int j = 0; j < (AT > 0 ? AT : A); ++j) blsd[j] = logf(bsd[j]);
     const float bl = fmaxf(expf(row_loglik<AT>(ac, bmu, bsd, blsd, A, a.c_ll)), 1e-5f);
-    acc[PS_KL] += (double)row_kl<AT>(rm, rsig, m, sig, A);
+    acc[PS_KL] += (double)row_kl_cc<AT>(rm, m, lkl, s02, den2, A);
     if (a.mode == 0) {
       const float ratio = lp / bl;
       const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
@@ -613,9 +635,16 @@ policy_rows_grad_kernel(PolRowArgs a) {
     srsig[j] = expf(a.ref_lv[j]);
   }
   __syncthreads();
-  float sig[AM], lsig[AM], rsig[AM];
+  float sig[AM], lsig[AM], rsig[AM], inv1[AM], s1sq[AM], s1cu[AM], rs2[AM];
 #pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) { sig[j] = ssig[j]; lsig[j] = slsig[j]; rsig[j] = srsig[j]; }
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    sig[j] = ssig[j]; lsig[j] = slsig[j]; rsig[j] = srsig[j];
+    // per-column factors of the row loop, hoisted (same operations, same order)
+    inv1[j] = 1.f / sig[j];
+    s1sq[j] = sig[j] * sig[j];
+    s1cu[j] = sig[j] * sig[j] * sig[j];
+    rs2[j] = rsig[j] * rsig[j];
+  }
   const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   const float wsurr = a.cf[CF_SURRW], wkl = a.cf[CF_KLCOEF];
   float glv[AM];
@@ -654,11 +683,11 @@ policy_rows_grad_kernel(PolRowArgs a) {
       const float s1 = sig[j];
       const float u = (ac[j] - m[j]) / s1;
       float gmu = g_ll * (u / s1);
-      float gsd = g_ll * (u * u / s1 - 1.f / s1);
+      float gsd = g_ll * (u * u / s1 - inv1[j]);
       if (wkl != 0.f) {
         const float d = rm[j] - m[j];
-        gmu += wkl * (-d / (s1 * s1));
-        gsd += wkl * (1.f / s1 - (rsig[j] * rsig[j] + d * d) / (s1 * s1 * s1));
+        gmu += wkl * (-d / s1sq[j]);
+        gsd += wkl * (inv1[j] - (rs2[j] + d * d) / s1cu[j]);
       }
       glv[j] += gsd;
       dz[j] = gmu * (1.f - m[j] * m[j]);                    // tanh backward
@@ -941,6 +970,32 @@ __global__ void rnn_init_kernel(int* ci, float* cf) {
 }
 
 // ------------------------------------------------------------ host phases
+
+// workgroups of the statistics pass: at most one resident round (its register
+// count leaves 3 one-wave blocks per SIMD, so the 4096-block cap of rnn_nblk
+// ran a second, partly filled round: 0.34 of HBM at 65536 segments)
+template <bool FUSE>
+static int pol_stats_blocks(int A, int64_t rows) {
+  static int cap[2][9] = {};
+  const int ai = A >= 1 && A <= 8 ? A : 0;
+  int& c = cap[FUSE][ai];
+  if (!c) {
+    switch (ai) {
+      case 1: c = resident_grid(policy_rows_stats_kernel<kRowNT, 1, FUSE>, kRowNT, 0); break;
+      case 2: c = resident_grid(policy_rows_stats_kernel<kRowNT, 2, FUSE>, kRowNT, 0); break;
+      case 3: c = resident_grid(policy_rows_stats_kernel<kRowNT, 3, FUSE>, kRowNT, 0); break;
+      case 4: c = resident_grid(policy_rows_stats_kernel<kRowNT, 4, FUSE>, kRowNT, 0); break;
+      case 5: c = resident_grid(policy_rows_stats_kernel<kRowNT, 5, FUSE>, kRowNT, 0); break;
+      case 6: c = resident_grid(policy_rows_stats_kernel<kRowNT, 6, FUSE>, kRowNT, 0); break;
+      case 7: c = resident_grid(policy_rows_stats_kernel<kRowNT, 7, FUSE>, kRowNT, 0); break;
+      case 8: c = resident_grid(policy_rows_stats_kernel<kRowNT, 8, FUSE>, kRowNT, 0); break;
+      default: c = resident_grid(policy_rows_stats_kernel<kRowNT, 0, FUSE>, kRowNT, 0); break;
+    }
+    if (c < 1) c = 1;
+  }
+  const int nb = rnn_nblk(rows, kRowNT);
+  return nb < c ? nb : c;
+}
 
 template <bool FUSE>
 static void launch_pol_stats(int A, int nb, const PolRowArgs& p, hipStream_t st) {
@@ -1337,7 +1392,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, stop));
       RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop, s.wT));
       PolRowArgs p = pol_rows(a, d, s);
-      const int nb = rnn_nblk(d.NE, kRowNT);
+      const int nb = a.mode == 0 ? pol_stats_blocks<true>(d.A, d.NE) : pol_stats_blocks<false>(d.A, d.NE);
       const int kt = ktime_begin(st);
       p.invN = (float)(1.0 / (double)NEg);
       if (a.mode == 0) launch_pol_stats<true>(d.A, nb, p, st);     // + the clip gradient
@@ -1366,7 +1421,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     }
     case SMI_RNN_PH_POLICY_BWD: {
       PolRowArgs p = pol_rows(a, d, s);
-      const int nb = rnn_nblk(d.NE, kRowNT);
+      // clip: the log_var partials came from POLICY_FWD's fused pass, over its grid
+      const int nb = a.mode == 0 ? pol_stats_blocks<true>(d.A, d.NE) : rnn_nblk(d.NE, kRowNT);
       if (a.mode != 0) {     // clip: dz and the log_var partials came with POLICY_FWD's pass
         const int kt = ktime_begin(st);
         switch (d.A) {   // compile-time action widths 1..8 (registers); others generic
