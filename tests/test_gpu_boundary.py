@@ -188,14 +188,18 @@ def test_publish_snapshot_does_not_serialize_learn():
     the worker's wait; with pickle (the wire format) the whole publish path
     must still beat the reference's synchronous ModuleDict.dumps in the
     learner loop (state_dict -> cpu().numpy() -> serialize, module_dict.py:
-    22-35, parameter_server.py:40-55)."""
+    22-35, parameter_server.py:40-55).  learn() runs as the bench runs it, one
+    hipGraph replay: an eager learn() at this batch is bound by the host issue
+    of its ~400 launches, so the publish's host bookkeeping (an event, one
+    ctypes call) lands on its critical path — 3-5 % there against 2-3 % with
+    the replay (tools/diag_publish.py, profiles/r03/ab/diag_publish_*.json)."""
     import time
     from surreal_amd.publish import binary_hash
     lc = ppo_config(B=256, T=25, mode='adapt', use_z_filter=True, hidden=(300, 200), lam=1.0,
                     rnn=True, rnn_hidden=100, horizon=5)
     lc.parameter_publish.exp_interval = lc.replay.batch_size      # publish after every learn()
     D, A, Hd = 42, 8, 100
-    learner = PPOLearner(lc, env_config(D, A), seed=1)
+    learner = PPOLearner(lc, env_config(D, A), seed=1, use_graph=True)
     batch = synthetic.to_device(synthetic.ppo_batch(256, 25, D, A, seed=3, rnn_hidden=Hd), DEV)
     got = []
     fast = DeviceParameterPublisher(learner.module_dict(), sink=lambda b, i: got.append(i['hash']),
