@@ -276,10 +276,12 @@ def run_ddpg(args):
     HalfCheetah dims (obs 17, act 6), actor 300x200, critic 400x300, n_step 3,
     fed by UniformReplay over a 333,333-row shard resident in HBM.  A step =
     one CPython-exact index draw (MT19937 kernel) + row gather + learn().
-    With WORLD_SIZE > 1 (SURVEY §8(e) DDPG row): every rank holds its own
-    333,333-row shard, samples 512 rows per step from it, and the gradients are
-    averaged over the ranks (DDPGLearner dp=TorchDistAllReduce): weak scaling,
-    value = ranks x 512 x steps / max-over-ranks time."""
+    With WORLD_SIZE > 1 (SURVEY §8(e) DDPG row): the 512-row batch is sharded.
+    Every rank holds the same replicated ring and MT19937 state, draws the same
+    512 global indices (the single learner's CPython-exact stream) and gathers
+    its 512 / N rows; the gradients are averaged over the ranks (DDPGLearner
+    dp=TorchDistAllReduce), which equals the single learner's update on the
+    512 rows: strong scaling, value = 512 x steps / max-over-ranks time."""
     dist, world, rank, _ = init_dist()
     from surreal_amd import _lib as L
     from surreal_amd.config import DDPG_DEFAULT_LEARNER_CONFIG, gym_env_config
@@ -293,18 +295,22 @@ def run_ddpg(args):
     lc.replay.memory_size = NREP
     lc.replay.sampling_start_size = 1000
     ec = gym_env_config(D, A)
-    rep = UniformReplay(lc, ec, seed=rank, device=dev)
-    rows = np.random.RandomState(rank).randn(NREP, rep.width).astype(np.float32)
+    if B % world:
+        raise SystemExit(f'--config c4: batch {B} does not split over {world} ranks')
+    rep = UniformReplay(lc, ec, seed=0, device=dev)       # replicated ring, one index stream
+    rows = np.random.RandomState(0).randn(NREP, rep.width).astype(np.float32)
     rows[:, D:D + A] = np.tanh(rows[:, D:D + A])
     rows[:, 2 * D + A + 1] = (rows[:, 2 * D + A + 1] > 1.6).astype(np.float32)
     rep.insert_rows(rows)
     graph = os.environ.get('SMI_DDPG_GRAPH', '0') == '1' and dist is None  # measured neutral
     dp = TorchDistAllReduce() if dist is not None else None
-    learner = DDPGLearner(lc, ec, seed=1, device=dev, use_graph=graph, dp=dp)
-    buf = torch.empty(B, rep.width, device=dev)
+    llc = copy.deepcopy(lc)
+    llc.replay.batch_size = B // world                     # this rank's shard of the batch
+    learner = DDPGLearner(llc, ec, seed=1, device=dev, use_graph=graph, dp=dp)
+    buf = torch.empty(B // world, rep.width, device=dev)
 
     def step():
-        _, got = rep.sample(B, out=buf)
+        _, got = rep.sample(B, out=buf, rank=rank, world=world)
         learner.learn(rep.split(got))
 
     def barrier():
@@ -328,10 +334,10 @@ def run_ddpg(args):
     # instrumented pass on an eager learner (graph replays carry no per-kernel
     # events): same launches, same shapes
     n_inst = min(args.steps, 5)
-    learner_e = DDPGLearner(lc, ec, seed=1, device=dev, dp=dp) if graph else learner
+    learner_e = DDPGLearner(llc, ec, seed=1, device=dev, dp=dp) if graph else learner
 
     def step_e():
-        _, got = rep.sample(B, out=buf)
+        _, got = rep.sample(B, out=buf, rank=rank, world=world)
         learner_e.learn(rep.split(got))
 
     step_e()
@@ -347,15 +353,15 @@ def run_ddpg(args):
     c, ms_k, fl = kt[dom]
     ach = fl / (ms_k * 1e-3) / 1e12
     out = {
-        'metric': DDPG_METRIC, 'value': round(world * B * args.steps / elapsed, 1),
+        'metric': DDPG_METRIC, 'value': round(B * args.steps / elapsed, 1),
         'unit': 'env-steps/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32',
         'data': 'synthetic replay rows (seeded); random-init weights of the named architecture',
         'config': {'workload': 'C4: DDPG learner, batch 512 sampled CPython-exactly from a '
                                '333,333-row replay shard, obs 17, act 6, actor 300x200, critic '
                                '400x300, n_step 3, hard target update',
-                   'batch': B, 'replay_rows': NREP,
+                   'batch': B, 'batch_per_rank': B // world, 'replay_rows': NREP,
                    'parallelism': f'dp{world}' if world > 1 else 'single',
                    'update': 'hipGraph replay' if graph else 'eager launches'},
         'roofline': {'kernel': dom, 'bound': 'mfma', 'achieved': round(ach, 3),

@@ -56,6 +56,9 @@ int     smi_set_workspace(void* dev_ptr, int64_t bytes);
 typedef struct smi_context smi_context;
 smi_context* smi_context_create(void* workspace, int64_t bytes);   /* NULL on bad args */
 int          smi_context_make_current(smi_context* ctx);            /* this thread; NULL = default */
+/* Marks ctx dead (its 24-byte handle is kept, never freed): a thread that
+ * still has it current falls back to the default workspace; making a dead
+ * context current is an error.  The workspace may be freed afterwards. */
 int          smi_context_destroy(smi_context* ctx);
 
 /* Measurement only (not part of the reference API): per-launch HIP-event

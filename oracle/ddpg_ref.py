@@ -130,7 +130,7 @@ class DDPGLearnerRef:
                 self.perc2, self.perc2_t = mkp(), mkp()
         for m in self.nets():
             m.to(dtype)
-        self.hard_update()
+        self.hard_update(perception=False)    # ddpg.py:174-178: actor and critic(s) only
         self.clip_actor = net['clip_actor_gradient']
         self.actor_clip_value = net['actor_gradient_value_clip']
         self.clip_critic = net['clip_critic_gradient']
@@ -157,18 +157,20 @@ class DDPGLearnerRef:
             out += [self.perc, self.perc_t] + ([self.perc2, self.perc2_t] if self.double else [])
         return out
 
-    def target_pairs(self):
+    def target_pairs(self, perception=True):
         pairs = [(self.actor_t, self.actor), (self.critic_t, self.critic)]
         if self.double:
             pairs.append((self.critic2_t, self.critic2))
-        if self.pixel is not None:
+        if self.pixel is not None and perception:
             pairs.append((self.perc_t, self.perc))
             if self.double:
                 pairs.append((self.perc2_t, self.perc2))
         return pairs
 
-    def hard_update(self):
-        for t, s in self.target_pairs():
+    def hard_update(self, perception=True):
+        """ddpg.py:420-428 (the interval update: every target, perception
+        included); perception=False is the constructor's sync (ddpg.py:174-178)"""
+        for t, s in self.target_pairs(perception):
             t.load_state_dict(s.state_dict())
 
     def perception(self, net, obs):                                     # ddpg_net.py:69-79

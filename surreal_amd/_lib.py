@@ -271,9 +271,12 @@ class Context(object):
         check(lib().smi_context_make_current(ctypes.c_void_p(self.handle)), 'smi_context_make_current')
 
     def __del__(self):
+        # no make_current(None) here: the collector may run this on any thread
+        # in the middle of another object's launches; smi_context_destroy
+        # clears only this thread's current context if it is this one, and a
+        # thread still holding it falls back to the default workspace
         h, self.handle = getattr(self, 'handle', None), None
         if h and _lib is not None:
-            _lib.smi_context_make_current(None)
             _lib.smi_context_destroy(ctypes.c_void_p(h))
 
 

@@ -130,9 +130,14 @@ class DDPGAgentBatch(object):
         self.action_dim = ec.action_spec['dim'][0]
         self.device = torch.device(device) if device is not None else torch.device('cuda')
         self._ctx = L.Context(self.device)      # own workspace (re-entrancy)
+        cs = lc.model.get('conv_spec', {})       # the learner's perception (ddpg.py:135-143)
         self.model = DDPGModel(ec.obs_spec, self.action_dim, lc.model.use_layernorm,
                                lc.model.actor_fc_hidden_sizes, lc.model.critic_fc_hidden_sizes,
+                               conv_out_channels=cs.get('out_channels'),
+                               conv_kernel_sizes=cs.get('kernel_sizes'), conv_strides=cs.get('strides'),
+                               conv_hidden_dim=cs.get('hidden_output_dim'),
                                device=self.device, generator=torch.Generator().manual_seed(seed))
+        self.frame_stack_concatenate_on_env = bool(ec.get('frame_stack_concatenate_on_env', True))
         exp = lc.algo.exploration
         if exp.get('param_noise_type') is not None:
             raise NotImplementedError('surreal_amd: DDPG parameter-space noise is not built')
@@ -168,13 +173,41 @@ class DDPGAgentBatch(object):
         self.x_prev = x
         return x
 
+    def _camera(self, frames):
+        """camera0 of N agents -> a uint8 (N, C, H, W) device tensor; a list of
+        per-agent frame lists is concatenated along channels first, as
+        ddpg_agent.py:158-163 does when frames are not stacked by the env"""
+        if not self.frame_stack_concatenate_on_env and isinstance(frames, (list, tuple)):
+            frames = np.stack([np.concatenate(f, axis=0) for f in frames])
+        a = np.asarray(frames)
+        if a.dtype != np.uint8:
+            if not (np.all(a == np.round(a)) and a.min() >= 0 and a.max() <= 255):
+                raise TypeError('DDPG camera observations must hold uint8 pixel values')
+            a = a.astype(np.uint8)
+        return torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+
     def act(self, obs):
-        """obs: (N, D) low-dim observations (or {'low_dim': {key: (N, D)}})."""
+        """obs: (N, D) low-dim observations, or {'low_dim': {key: (N, D)}, 'pixel':
+        {'camera0': (N, C, H, W) uint8}} -- the reference agent's forward_perception
+        then forward_actor (ddpg_agent.py:153-182, ddpg_net.py:69-95), for N agents"""
         self._ctx.make_current()
-        if isinstance(obs, dict):
-            obs = obs['low_dim'][list(obs['low_dim'])[0]]
-        x = torch.from_numpy(np.ascontiguousarray(obs, dtype=np.float32)).to(self.device)
-        a = self.model.forward_actor(x).cpu().numpy().clip(-1, 1)
+        m = self.model
+        if isinstance(obs, dict) and m.is_pixel_input:
+            o = {'pixel': {'camera0': self._camera(obs['pixel']['camera0'])}}
+            if m.low_dim:
+                low = obs['low_dim'][list(obs['low_dim'])[0]]
+                o['low_dim'] = {'flat_inputs': torch.from_numpy(
+                    np.ascontiguousarray(low, dtype=np.float32)).to(self.device)}
+            x = m.forward_perception(o)
+        else:
+            if isinstance(obs, dict):
+                obs = obs['low_dim'][list(obs['low_dim'])[0]]
+            if m.is_pixel_input:
+                raise ValueError('this DDPG model reads camera0: pass {"pixel": {"camera0": ...}, ...}')
+            x = torch.from_numpy(np.ascontiguousarray(obs, dtype=np.float32)).to(self.device)
+        if x.dim() != 2 or x.shape[0] != self.n:
+            raise ValueError(f'expected observations of {self.n} agents, got shape {tuple(x.shape)}')
+        a = m.forward_actor(x).cpu().numpy().clip(-1, 1)
         if self.agent_mode != 'eval_deterministic':
             a += self._noise()
         return a.clip(-1, 1)

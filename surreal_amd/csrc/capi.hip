@@ -55,12 +55,23 @@ void ktime_end(int slot, int cls, double flops, hipStream_t st) {
 // context (smi_context_make_current) serves every workspace request of the
 // launches that thread enqueues; without one, the default context
 // (smi_set_workspace) does.
+// A destroyed context is only marked dead, never freed: another thread may
+// still hold it as its current context (a thread_local this thread cannot
+// clear), and then falls back to the default context instead of reading freed
+// memory.  A context is 24 bytes; the workspace itself belongs to the caller.
 }  // namespace smi
-struct smi_context { void* ws; int64_t bytes; };
+struct smi_context { void* ws; int64_t bytes; std::atomic<bool> alive; };
 namespace smi {
-static smi_context g_default_ctx{nullptr, 0};
+static smi_context g_default_ctx{nullptr, 0, {true}};
+#ifdef SMI_FAULT_INJECTION
+static int g_fault = SMI_FAULT_NONE;
+int fault() { return g_fault; }
+#endif
 static thread_local smi_context* t_ctx = nullptr;
-static smi_context* cur_ctx() { return t_ctx ? t_ctx : &g_default_ctx; }
+static smi_context* cur_ctx() {
+  smi_context* c = t_ctx;
+  return c && c->alive.load(std::memory_order_acquire) ? c : &g_default_ctx;
+}
 int64_t smi_workspace_floats() {
   const smi_context* c = cur_ctx();
   return c->ws ? c->bytes / 4 : 0;
@@ -149,10 +160,12 @@ smi_context* smi_context_create(void* workspace, int64_t bytes) {
     set_error(SMI_E_ARG, "context_create: bad args");
     return nullptr;
   }
-  return new smi_context{workspace, bytes};
+  return new smi_context{workspace, bytes, {true}};
 }
 
 int smi_context_make_current(smi_context* ctx) {
+  REQUIRE(!ctx || ctx->alive.load(std::memory_order_acquire),
+          "context_make_current: the context was destroyed");
   t_ctx = ctx;
   return SMI_OK;
 }
@@ -160,10 +173,21 @@ int smi_context_make_current(smi_context* ctx) {
 int smi_context_destroy(smi_context* ctx) {
   REQUIRE(ctx, "context_destroy: null context");
   if (t_ctx == ctx) t_ctx = nullptr;
-  delete ctx;
+  ctx->alive.store(false, std::memory_order_release);   // not freed: see above
+  ctx->ws = nullptr;
+  ctx->bytes = 0;
   return SMI_OK;
 }
 int64_t smi_workspace_bytes(void) { return (int64_t)128 << 20; }
+
+#ifdef SMI_FAULT_INJECTION
+/* test-only build variant (smi_internal.hpp): select a fault; not declared in
+ * include/surreal_mi.h and absent from the product library */
+int smi_fault_set(int mode) {
+  smi::g_fault = mode;
+  return SMI_OK;
+}
+#endif
 
 /* Per-launch HIP-event timing of the MFMA kernels (GEMM forward / input-grad /
  * weight-grad / split-K reduce, LSTM forward / backward): on != 0 starts a

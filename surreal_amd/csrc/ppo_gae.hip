@@ -638,13 +638,18 @@ int launch_gae_windows(const float* values, float* values_masked, const float* r
   a.E = T - H + 1;
   a.gtab = gtab; a.ltab = ltab; a.gamma = gamma; a.gamma_H = gamma_H;
   a.adv = adv; a.ret = ret; a.partials = partials;
-  {
+  const bool faulted = fault() == SMI_FAULT_GAE_HORIZON && H > 1 && a.E > 1;
+  if (faulted) {             // windows of H - 1 steps, the same E windows
+    a.H = H - 1;
+    a.gamma_H = gamma_H / gamma;
+  }
+  if (!faulted) {
     int rc = 0;
     // the reference defaults: RNN n_step 25 / horizon 5; non-RNN n_step 50
     if (try_gae_seg<25, 5, 256>(a, n_partials, stream, &rc)) return rc;
     if (try_gae_seg<50, 50, 128>(a, n_partials, stream, &rc)) return rc;
   }
-  if (T + 1 <= 64 && (a.E == 1 || H <= 16)) {
+  if (T + 1 <= 64 && (a.E == 1 || H <= 16) && (!faulted || a.H <= 16)) {
     int TPR = 8;
     while (TPR < T + 1) TPR *= 2;
     const int64_t groups = (B + 64 / TPR - 1) / (64 / TPR);

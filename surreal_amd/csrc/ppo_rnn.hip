@@ -1420,6 +1420,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       return check_launch("policy_decide_kernel");
     }
     case SMI_RNN_PH_POLICY_BWD: {
+      if (fault() == SMI_FAULT_POLICY_EPOCH_SHORT && e == a.epoch_policy - 1) return SMI_OK;
       PolRowArgs p = pol_rows(a, d, s);
       // clip: the log_var partials came from POLICY_FWD's fused pass, over its grid
       const int nb = a.mode == 0 ? pol_stats_blocks<true>(d.A, d.NE) : rnn_nblk(d.NE, kRowNT);
@@ -1446,6 +1447,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       return check_launch("logvar_grad_kernel");
     }
     case SMI_RNN_PH_POLICY_APPLY: {
+      if (fault() == SMI_FAULT_POLICY_EPOCH_SHORT && e == a.epoch_policy - 1) return SMI_OK;
       const int64_t n = d.nA_head + d.nS;
       const int g = grid_of(n, 1024);
       const int kt = ktime_begin(st);
@@ -1481,13 +1483,15 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       return stem_backward(a, d, critic, lm, cnn, gC, s, d.nC_head, st, nullptr);
     }
     case SMI_RNN_PH_VALUE_APPLY: {
-      const int64_t n = d.nC_head + d.nS;
+      if (fault() == SMI_FAULT_CRITIC_ADAM_SKIP) return SMI_OK;
+      const int64_t nS = fault() == SMI_FAULT_CRITIC_STEM_OMIT ? 0 : d.nS;
+      const int64_t n = d.nC_head + nS;
       const int g = grid_of(n, 1024);
       const int kt = ktime_begin(st);
       hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gC, n, s.part, nullptr,
                          a.critic_step, nullptr);
       RC(check_launch("sumsq_part_kernel"));
-      AdamSplitArgs aa{a.critic, d.nC_head, a.lstm, d.nS, gC, a.critic_m, a.critic_v,
+      AdamSplitArgs aa{a.critic, d.nC_head, a.lstm, nS, gC, a.critic_m, a.critic_v,
                        a.critic_step, a.hyper + SMI_HYP_LR_CRITIC, a.beta1, a.beta2, a.adam_eps,
                        a.critic_wd, a.clip_critic_grad ? a.critic_max_norm : 0.f, s.part, g,
                        nullptr, a.clip_critic_grad ? a.stats + SMI_ST_GRAD_NORM_CRITIC : nullptr,

@@ -46,6 +46,21 @@ int dw_group_begin();
 int dw_group_flush(hipStream_t st);
 int check_launch(const char* what);
 
+// Test-only fault injection (build variant 'fault', -DSMI_FAULT_INJECTION;
+// tests/negative_controls.py): deliberate departures from the reference the
+// parity checks must catch.  The product library has no such state: fault()
+// is the constant 0 there and every branch on it compiles away.
+enum { SMI_FAULT_NONE = 0,
+       SMI_FAULT_CRITIC_ADAM_SKIP = 1,     // value phases never apply Adam
+       SMI_FAULT_CRITIC_STEM_OMIT = 2,     // the stems left out of the critic optimizer
+       SMI_FAULT_POLICY_EPOCH_SHORT = 3,   // the last policy epoch's update skipped
+       SMI_FAULT_GAE_HORIZON = 4 };        // GAE windows one step shorter than the horizon
+#ifdef SMI_FAULT_INJECTION
+int fault();
+#else
+constexpr int fault() { return SMI_FAULT_NONE; }
+#endif
+
 #define RC_CHECK(x) do { const int rc_ = (x); if (rc_) return rc_; } while (0)
 
 // ---- pixel stem (CNNStemNetwork, builders.py:8-33) -------------------------

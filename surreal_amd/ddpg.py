@@ -30,6 +30,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
+from .session import LearnerHooks
 from .config import Config, ConfigError
 from .model import CNNStemNetwork, _FlatViews, _LinearView
 
@@ -190,6 +191,15 @@ def _p(t):
     return L.ptr(t)
 
 
+def _check_rows(x, rows, width, what):
+    """x must be a [>= rows][width] fp32 device matrix with unit column stride
+    (the kernels read rows x width through its row stride)"""
+    if (x.dim() != 2 or x.shape[0] < rows or x.shape[1] != width or x.stride(1) != 1
+            or x.dtype != torch.float32):
+        raise ValueError(f'{what} input: expected a float32 [{rows}][{width}] matrix, got '
+                         f'{x.dtype} {tuple(x.shape)}')
+
+
 class _Net(object):
     """Launch helpers over a DDPGModel's flat buffers."""
 
@@ -266,6 +276,7 @@ class _Net(object):
     def actor_fwd(self, obs, rows, store='a', actor=None):
         actor = actor if actor is not None else self.m.actor
         D, h1, h2, A = actor.dims
+        _check_rows(obs, rows, D, 'actor')
         pre = store or 'tmp'
         H1 = self.buf(pre + '_h1', (rows, h1))
         H2 = self.buf(pre + '_h2', (rows, h2))
@@ -286,6 +297,8 @@ class _Net(object):
 
     def critic_fwd(self, critic, obs, act, rows, store):
         D, c1, c2, A = critic.dims
+        _check_rows(obs, rows, D, 'critic')
+        _check_rows(act, rows, A, 'critic action')
         pre = store or 'ctmp'
         CAT = self.buf(pre + '_cat', (rows, c1 + A))
         H2 = self.buf(pre + '_h2', (rows, c2))
@@ -307,11 +320,13 @@ class _Net(object):
         return Q if store else Q.clone()
 
 
-class DDPGLearner(object):
-    """ddpg.py:12-440 on MI355X (low-dim observations; optional layernorm)."""
+class DDPGLearner(LearnerHooks):
+    """ddpg.py:12-440 on MI355X (low-dim or pixel observations; optional
+    layernorm, TD3 options)."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
-                 device=None, seed=0, use_graph=False, dp=None, checkpoint_full_state=False):
+                 device=None, seed=0, use_graph=False, dp=None, checkpoint_full_state=False,
+                 checkpoint=None):
         """dp: None (one GPU) or a data-parallel group exposing `world_size`,
         `rank` and `allreduce_(tensor)` (in-place SUM, stream-ordered), e.g.
         learner.TorchDistAllReduce() over RCCL (SURVEY §8(e) DDPG row).  Each rank
@@ -319,14 +334,17 @@ class DDPGLearner(object):
         the ranks before clip + Adam, which equals the reference's mean loss on
         the concatenated global batch (equal shards).  Initial weights are
         broadcast from rank 0 (learner.replicate_from_rank0), so parameters stay
-        replicated whatever seed each rank passes."""
+        replicated whatever seed each rank passes.
+        metrics / checkpoint: as PPOLearner's (session.py): learn() reports the
+        statistics and calls periodic_checkpoint(global_steps=
+        current_iteration) as ddpg.py:371-376 does."""
         L.require_gpu()
         self.checkpoint_full_state = bool(checkpoint_full_state)
         self.dp = dp if dp is not None and dp.world_size > 1 else None
         self.learner_config = lc = learner_config if isinstance(learner_config, Config) else Config(learner_config)
         self.env_config = ec = env_config if isinstance(env_config, Config) else Config(env_config)
         self.session_config = session_config
-        self.metrics = metrics
+        self._init_hooks(metrics, checkpoint)
         self.device = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
         L.ensure_workspace(self.device)
@@ -379,8 +397,15 @@ class DDPGLearner(object):
             flats.append(self.model.perception.flat)
             if self.use_double_critic:
                 flats.append(self.model2.perception.flat)
+        if self.is_pixel_input:        # the target perceptions keep their own init (below)
+            flats.append(self.model_target.perception.flat)
+            if self.use_double_critic:
+                flats.append(self.model_target2.perception.flat)
         replicate_from_rank0(self.dp, flats)
-        self._hard_update()
+        # ddpg.py:174-178: the constructor hard-syncs the target actor and
+        # critic(s) only; a target perception keeps its own random init until
+        # the first target update
+        self._hard_update(perception=False)
         dev = self.device
         self.opt = {}
         groups = [('critic', self.model.critic.flat, net.lr_critic, net.critic_regularization),
@@ -420,21 +445,21 @@ class DDPGLearner(object):
         self._gin = None
 
     # ------------------------------------------------------------ helpers
-    def _target_pairs(self):
+    def _target_pairs(self, perception=True):
         """(target, source) flat buffers of the target update (ddpg.py:409-428)"""
         pairs = [(self.model_target.actor.flat, self.model.actor.flat),
                  (self.model_target.critic.flat, self.model.critic.flat)]
         if self.use_double_critic:
             pairs.append((self.model_target2.critic.flat, self.model2.critic.flat))
-            if self.is_pixel_input:
+            if self.is_pixel_input and perception:
                 pairs.append((self.model_target2.perception.flat, self.model2.perception.flat))
-        if self.is_pixel_input:
+        if self.is_pixel_input and perception:
             pairs.append((self.model_target.perception.flat, self.model.perception.flat))
         return pairs
 
-    def _hard_update(self):
+    def _hard_update(self, perception=True):
         with torch.no_grad():
-            for t, s_ in self._target_pairs():
+            for t, s_ in self._target_pairs(perception):
                 t.copy_(s_)
 
     def _dp_mean_(self, t):
@@ -696,8 +721,8 @@ class DDPGLearner(object):
             self._optimize_graphed(*ins)
         else:
             self._optimize(*ins)
-        if self.metrics is not None:
-            self.metrics(self.last_stats(), self.current_iteration)
+        self._report_metrics(self.current_iteration)                     # ddpg.py:371
+        self.periodic_checkpoint(global_steps=self.current_iteration, score=None)
 
     def _optimize_graphed(self, obs, actions, rewards, obs_next, done):
         """One _optimize as a hipGraph replay (the step is ~40 small launches at
@@ -713,7 +738,7 @@ class DDPGLearner(object):
             self._gin = [torch.zeros(tuple(t.shape), dtype=torch.float32, device=self.device)
                          for t in ins]
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode='thread_local'):
                 self._optimize(*self._gin, target_update=False)
             self._graph = g
             return
@@ -729,8 +754,13 @@ class DDPGLearner(object):
         return None if self._gin is None else dict(zip(
             ('obs', 'actions', 'rewards', 'obs_next', 'dones'), self._gin))
 
+    def _host_scalars(self):
+        return {}
+
     def last_stats(self):
-        v = self.stats_buf.cpu().numpy()
+        return self._stats_dict(self.stats_buf.cpu().numpy(), {})
+
+    def _stats_dict(self, v, host):
         out = {'actor_loss': float(v[0]), 'critic_loss': float(v[1]), 'action_norm': float(v[2]),
                'rewards': float(v[3]), 'Q_target': float(v[4]), 'Q_policy': float(v[5])}
         if self.use_double_critic:

@@ -27,6 +27,7 @@ from . import _lib as L
 from .aggregator import MultistepAggregatorWithInfo, SSARAggregator, StagingArena
 from .config import Config, ConfigError
 from .model import DiagGauss, PPOModel, RewardFilter
+from .session import LearnerHooks
 
 
 def _as_config(c):
@@ -115,13 +116,14 @@ _RNN_PHASE_NAMES = {0: 'rnn_gae', 1: 'rnn_prep', 2: 'rnn_policy_fwd', 3: 'rnn_po
                     7: 'rnn_zstats', 8: 'rnn_zapply', 9: 'rnn_policy_decide'}
 
 
-class PPOLearner(object):
+class PPOLearner(LearnerHooks):
     """ppo.py:12-682 on MI355X.  Same constructor, learn/module_dict/
-    publish_parameter/checkpoint_attributes/preprocess/_prefetcher_preprocess."""
+    publish_parameter/checkpoint_attributes/preprocess/_prefetcher_preprocess/
+    periodic_checkpoint."""
 
     def __init__(self, learner_config, env_config, session_config=None, metrics=None,
                  publisher=None, device=None, seed=0, dp=None, checkpoint_full_state=False,
-                 use_graph=False):
+                 use_graph=False, checkpoint=None):
         """dp: None (one GPU) or a data-parallel group exposing `world_size` and
         `allreduce_(tensor)` (in-place SUM, stream-ordered), e.g.
         TorchDistAllReduce() over RCCL.  Each rank passes its own shard of
@@ -135,14 +137,22 @@ class PPOLearner(object):
         use_graph (one GPU): learn() replays a hipGraph of the whole device
         sequence (preprocess, GAE, the epochs, z_update) captured after the
         first call, with the batch copied into static buffers when it lives
-        elsewhere; bit-identical to eager learn() (test_ppo_graph_replay_bit_exact)."""
+        elsewhere; bit-identical to eager learn() (test_ppo_graph_replay_bit_exact).
+        metrics: callable(stats, global_step) called after every learn() (one
+        device read each), or a throttled sink with due() (session.
+        TimeThrottledMetrics, tracker.py:81-104): statistics accumulate on the
+        device and are read, averaged, only when it is due.
+        checkpoint: what learn() hands periodic_checkpoint(global_steps=
+        current_iteration) to (ppo.py:606-609): a PeriodicCheckpoint-like
+        object (the reference's own, or session.PeriodicCheckpoint) or a
+        callable(global_steps=, score=)."""
         L.require_gpu()
         self.dp = dp
         self.checkpoint_full_state = bool(checkpoint_full_state)
         self.learner_config = lc = _as_config(learner_config)
         self.env_config = ec = _as_config(env_config)
         self.session_config = _as_config(session_config)
-        self.metrics = metrics
+        self._init_hooks(metrics, checkpoint)
         self.publisher = publisher
         self.device = torch.device(device) if device is not None else \
             torch.device('cuda', torch.cuda.current_device())
@@ -669,8 +679,11 @@ class PPOLearner(object):
             yield from self._device_phases(batch, preprocessed=True)
         else:
             yield from self._device_phases(batch)
-        if self.metrics is not None:
-            self.metrics(self.last_stats(), self.global_step)
+        self._learn_epilogue()
+
+    def _learn_epilogue(self):                                # ppo.py:606-613
+        self.periodic_checkpoint(global_steps=self.current_iteration, score=None)
+        self._report_metrics(self.global_step)
         self.exp_counter += self.batch_size * (self.dp.world_size if self.dp is not None else 1)
         self.global_step += 1
 
@@ -719,7 +732,11 @@ class PPOLearner(object):
         if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
             batch = self._arena.stage(batch)
         leaves, build = self._leaves(batch)
-        key = tuple((tuple(t.shape), t.dtype) for t in leaves)
+        # the host switches read while the launches are issued are part of
+        # what a captured graph bakes in (export pointers, the side stream,
+        # the epoch counts and the device the phases run on)
+        key = (tuple((tuple(t.shape), t.dtype) for t in leaves), bool(self.export_advantages),
+               bool(self.prep_side_stream), self.epoch_policy, self.epoch_baseline)
         self.current_iteration += 1
         self._ctx.make_current()
         if self._hyper_values() != self._hyper_key:
@@ -729,9 +746,15 @@ class PPOLearner(object):
                 pass
             self._gin = [t.detach().clone() for t in leaves]
             static = build(self._gin)
+            # quiesce the parameter publisher (its worker thread synchronizes
+            # events and launches copies on its own stream) before capturing,
+            # and capture in thread-local mode so another thread's CUDA calls
+            # cannot invalidate the capture
+            if self.publisher is not None and hasattr(self.publisher, 'flush'):
+                self.publisher.flush()
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode='thread_local'):
                 self._ctx.make_current()
                 for _ in self._device_phases(static):
                     pass
@@ -742,24 +765,34 @@ class PPOLearner(object):
                 if s_.data_ptr() != t.data_ptr():
                     s_.copy_(t)
             self._graph.replay()
-        if self.metrics is not None:
-            self.metrics(self.last_stats(), self.global_step)
-        self.exp_counter += self.batch_size
-        self.global_step += 1
+        self._learn_epilogue()
+
+    def _host_scalars(self):
+        """host-side entries of the statistics (averaged by a throttled sink)"""
+        out = {'_lr': self.actor_lr_scheduler.get_lr()[0]}
+        if self.ppo_mode == 'clip':
+            out['_clip_epsilon'] = self.clip_epsilon
+        else:
+            out['_beta'] = self.beta
+        return out
 
     def last_stats(self):
         """Statistics dict of the last learn() (ppo.py:219-224,278-284,328-331,555,571-582).
         Synchronises with the device."""
-        v = self.stats_buf.cpu().numpy()
+        return self._stats_dict(self.stats_buf.cpu().numpy(), self._host_scalars())
+
+    def _stats_dict(self, v, host):
+        """the reference's statistics dict from a host copy of the device
+        statistics vector v and the host scalars (_lr, _clip_epsilon / _beta)"""
         s = {}
         if self.ppo_mode == 'clip':
             for k in ('_surr_loss', '_clip_surr_loss', '_entropy'):
                 s[k] = float(v[L.ST[k]])
-            s['_clip_epsilon'] = self.clip_epsilon
+            s['_clip_epsilon'] = host['_clip_epsilon']
         else:
             for k in ('_kl_loss_adapt', '_surr_loss', '_entropy'):
                 s[k] = float(v[L.ST[k]])
-            s['_beta'] = self.beta
+            s['_beta'] = host['_beta']
         s['_pol_kl'] = float(v[L.ST['_pol_kl']])
         if self.clip_actor_gradient:
             s['grad_norm_actor'] = float(v[L.ST['grad_norm_actor']])
@@ -768,8 +801,9 @@ class PPOLearner(object):
             s[k] = float(v[L.ST[k]])
         if self.clip_critic_gradient:
             s['grad_norm_critic'] = float(v[L.ST['grad_norm_critic']])
-        s['_lr'] = self.actor_lr_scheduler.get_lr()[0]
-        s['epochs_run'] = int(v[L.ST['epochs_run']])
+        s['_lr'] = host['_lr']
+        er = float(v[L.ST['epochs_run']])              # (an average over a throttled window)
+        s['epochs_run'] = int(er) if er == int(er) else er
         if self.use_z_filter:
             zf = self.model.z_filter
             s['obs_running_mean'] = float(np.mean(zf.running_mean()))

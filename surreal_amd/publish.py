@@ -81,13 +81,22 @@ class Snapshot(object):
         self.iteration, self.message = iteration, message
         self.time = time.time()
 
+    def _commit_if_pending(self):
+        """a deferred snapshot whose D2H nobody issued yet: issue it now (from
+        whichever thread asks), so waiting on it cannot block forever"""
+        pub = getattr(self, '_pub', None)
+        if pub is not None and not self._event.is_set():
+            pub._commit(self)
+
     def ready(self):
+        self._commit_if_pending()
         return self._event.is_set()
 
     def numpy_dict(self, copy=True):
         """{module name: {state_dict key: ndarray}} as ModuleDict.dumps builds it.
         copy=False returns views of the pinned slot (valid until the slot is
         reused: the publisher's worker serializes from them, then frees it)."""
+        self._commit_if_pending()
         self._event.wait()
         raw = self._host.numpy()
         out = {}
@@ -126,6 +135,7 @@ class DeviceParameterPublisher(object):
             sl['free'].set()
         self.next = 0
         self._pending = None
+        self._pending_lock = threading.Lock()
         self.last = None
         self.published = 0
         self._q = queue.Queue()
@@ -159,8 +169,10 @@ class DeviceParameterPublisher(object):
         snap._taken = taken
         snap._done = None
         snap._issued = threading.Event()
+        snap._pub = self
         if defer:
-            self._pending = snap
+            with self._pending_lock:
+                self._pending = snap
         else:
             snap._issued.set()                # the worker issues the D2H
         # neither half of the slot is rewritten before the worker has serialized
@@ -182,9 +194,19 @@ class DeviceParameterPublisher(object):
         snap._done = done
 
     def commit(self):
-        """Issue the D2H of the last snapshot(defer=True) (learner thread)."""
-        snap, self._pending = self._pending, None
-        if snap is not None:
+        """Issue the D2H of the last snapshot(defer=True).  The learner calls it
+        after its post-publish host reads; Snapshot.numpy_dict()/ready() and
+        flush() call it too, from any thread, so a deferred snapshot is never
+        waited on unissued."""
+        self._commit(None)
+
+    def _commit(self, want):
+        """issue the pending snapshot (if want is given: only if it is that one)"""
+        with self._pending_lock:
+            snap = self._pending
+            if snap is None or (want is not None and snap is not want):
+                return
+            self._pending = None
             self._issue(snap)
             snap._issued.set()
 

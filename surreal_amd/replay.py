@@ -106,14 +106,28 @@ class UniformReplay(object):
             self._idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
         return self.rng.randint_device(len(self), batch_size, self._idx)
 
-    def sample(self, batch_size, out=None):
-        """Returns (indices, rows[batch, W]) on device; rows gathered by kernel."""
+    def sample(self, batch_size, out=None, rank=0, world=1):
+        """Returns (indices, rows[batch, W]) on device; rows gathered by kernel.
+
+        Data parallel (world > 1, SURVEY §8(e) DDPG row): every rank holds the
+        same replicated ring and the same MT19937 state (same seed, same
+        inserts), so all ranks draw the SAME `batch_size` global indices -- the
+        one CPython-exact stream a single learner draws
+        (uniform_replay.py:43-47) -- and gather only their own slice of
+        batch_size / world rows: the sampling stays bit-exact and the shards
+        concatenate to the single learner's batch."""
+        if world < 1 or not 0 <= rank < world or batch_size % world:
+            raise ValueError(f'batch_size {batch_size} must split evenly over {world} ranks')
         idx = self.sample_indices(batch_size)
+        n = batch_size // world
+        mine = idx[rank * n:(rank + 1) * n]
         if out is None:
-            out = torch.empty(batch_size, self.width, dtype=torch.float32, device=self.device)
-        L.call('smi_gather_rows', L.ptr(self.table), self.width, L.ptr(idx), batch_size, L.ptr(out),
+            out = torch.empty(n, self.width, dtype=torch.float32, device=self.device)
+        if tuple(out.shape) != (n, self.width) or not out.is_contiguous():
+            raise ValueError(f'out must be a contiguous ({n}, {self.width}) tensor')
+        L.call('smi_gather_rows', L.ptr(self.table), self.width, L.ptr(mine), n, L.ptr(out),
                L.stream(self.device))
-        return idx, out
+        return mine, out
 
     def split(self, rows):
         D, A = self.obs_dim, self.act_dim

@@ -40,7 +40,7 @@ def make(case):
     r64, vs = P.envelope(st, lc, D, A, pixel, c['n_ulp'], c['orders'])
     meta = {'case': case, 'init_digest': P.digest([st[k] for k in sorted(st)]),
             'batch_digest': [], 'epochs_run': [], 'width': {}, 'scale': {},
-            'variants': len(vs), 'torch': torch.__version__}
+            'variants': len(vs), 'torch': torch.__version__, 'update': {}}
     arrays = {}
     na = lc.algo.network
     for it in range(len(c['batch_seeds'])):
@@ -80,6 +80,21 @@ def make(case):
             key = f'{name}@{it}'
             w, s = P.width(r, variants)
             meta['width'][key], meta['scale'][key] = w, s
+            if name in st:            # parameters: the envelope of the update measures
+                st0 = np.asarray(st[name], dtype=np.float64)
+                u64 = np.asarray(r, np.float64) - st0
+                uvs = [np.asarray(v, np.float64) - st0 for v in variants]
+                # the mask: entries the fp64 update moved by more than thr,
+                # from half an Adam step up -- the first threshold at which the
+                # envelope is informative (parity.py UPDATE_MASK_STEPS)
+                for mult in P.UPDATE_MASK_STEPS:
+                    thr = mult * P.update_thr(lc, name)
+                    w_rel, w_cos, n = P.update_widths(u64, uvs, thr)
+                    if 2.0 * w_rel + P.UPDATE_SLACK < P.UPDATE_TARGET_BAR:
+                        break
+                meta['update'][key] = [w_rel, w_cos, thr, n]
+                print(f'  {key}: update relL2 width {w_rel:.3e}, 1-cos width {w_cos:.3e}, '
+                      f'{n} entries moved > {thr:.1e} ({mult} x lr/2)', flush=True)
             r = np.asarray(r, dtype=np.float64)
             if name in st:            # parameters: fp32 difference from the initial state
                 r = r - np.asarray(st[name], dtype=np.float64)

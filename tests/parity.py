@@ -45,6 +45,18 @@ Three pieces, shared by the GPU tests and by tests/golden/make_envelopes.py:
    relative to the mean magnitude of those terms — the fp32 oracle itself
    lands 2e-4 of the KL away from fp64 (tests/test_cpu_stats_consistency.py);
    the explained variance relative to max(|ev|, |1 - ev|).
+
+4. UPDATE MEASURES.  At full size the max-abs bar of item 1 on a post-step
+   parameter tensor can exceed the tensor's whole movement (entries whose
+   gradient cancels to rounding noise take Adam's sign-normalised step either
+   way), so a learner that never updated it would pass.  Every post-step
+   tensor is therefore also checked on its UPDATE u = params - init against
+   the fp64 update u64: the relative L2 error over the entries u64 moved by
+   more than a threshold (from half an Adam step up, UPDATE_MASK_STEPS) and
+   1 - cos(u, u64) over all entries, each within 2 x the envelope's (+1e-4).
+   Both bars must stay under UPDATE_MAX_BAR = 0.3 or the check fails as
+   uninformative: a frozen tensor scores 1.0 on both.  tests/negative_controls.py
+   shows the checks failing on deliberately faulty learners.
 """
 import hashlib
 import json
@@ -298,11 +310,97 @@ def check(name, got, r64, env, scale, report, slack=SLACK, factor=2.0):
         report.setdefault('_fail', []).append(name)
 
 
-def print_report(report):
+def update_metrics(u, u64, thr):
+    """How far an update u (post-step parameters minus the initial ones) lands
+    from the fp64 update u64: (relative L2 error over the entries u64 moved by
+    more than thr, 1 - cosine of the whole update vectors, entries moved).
+    Unlike max|GPU - fp64|, whose bar at full size is set by entries whose
+    gradient cancels to rounding noise (Adam's sign-normalised step moves them
+    a full lr either way), both measures are relative to the movement itself:
+    a learner that never applied an update scores 1.0 on each."""
+    u = np.asarray(u, dtype=np.float64).reshape(-1)
+    u64 = np.asarray(u64, dtype=np.float64).reshape(-1)
+    m = np.abs(u64) > thr
+    n = int(m.sum())
+    ref = float(np.linalg.norm(u64[m])) if n else 0.0
+    rel = float(np.linalg.norm(u[m] - u64[m])) / ref if ref > 0 else 0.0
+    nu, n64 = float(np.linalg.norm(u)), float(np.linalg.norm(u64))
+    cos = float(np.dot(u, u64)) / (nu * n64) if nu > 0 and n64 > 0 else 0.0
+    return rel, 1.0 - cos, n
+
+
+def update_thr(lc, name):
+    """half an Adam step of the tensor's optimizer(s): an entry whose fp64
+    update exceeds it moved by a real step, not by rounding (the stems sit in
+    both optimizers, ppo_net.py:202-224)"""
+    na = lc.algo.network
+    lr = {'actor': na.lr_actor, 'critic': na.lr_critic}.get(name, min(na.lr_actor, na.lr_critic))
+    return 0.5 * float(lr)
+
+
+UPDATE_SLACK = 1e-4      # floor of the update bars (relative L2 / 1 - cos)
+UPDATE_MAX_BAR = 0.3     # a bar above this cannot tell a frozen tensor from a moving one
+# The relative-L2 mask starts at entries moved by more than half an Adam step
+# (thr = lr/2).  Where the trajectory itself is chaotic at that mask -- C5 at
+# 10 + 10 epochs: even the fp64 oracle with 2^-24 input noise lands 15-17 % of
+# the critic update away from fp64 over it -- the generator raises the mask in
+# these multiples of lr/2 to the first at which 2 x width stays under
+# UPDATE_TARGET_BAR: the entries that took many consistent Adam steps, which
+# every valid execution reproduces.  The cosine bar always covers every entry.
+UPDATE_MASK_STEPS = (1, 2, 4, 8, 16)
+UPDATE_TARGET_BAR = 0.25
+
+
+def update_widths(u64, u_variants, thr):
+    """the envelope of the update measures: (max_v rel L2, max_v 1 - cos, entries moved)"""
+    ms = [update_metrics(v, u64, thr) for v in u_variants]
+    n = update_metrics(u64, u64, thr)[2]
+    return max(x[0] for x in ms), max(x[1] for x in ms), n
+
+
+def check_update(name, u, u64, thr, w_rel, w_cos, report, factor=2.0):
+    """relative L2 and 1 - cos of the update within factor x the envelope's
+    (+ UPDATE_SLACK); the bars must themselves stay under UPDATE_MAX_BAR or
+    the check is flagged uninformative (a failure, not a pass)"""
+    rel, omc, n = update_metrics(u, u64, thr)
+    b_rel = factor * w_rel + UPDATE_SLACK
+    b_cos = factor * w_cos + UPDATE_SLACK
+    for tag, e, b in (('relL2', rel, b_rel), ('1-cos', omc, b_cos)):
+        key = f'upd_{tag}:{name}'
+        ok = e <= b and b < UPDATE_MAX_BAR and n > 0
+        report[key] = (e, b, ok)
+        if not ok:
+            report.setdefault('_fail', []).append(key)
+
+
+def report_json(report):
+    """the report as a JSON-able dict: {check: {"gpu": err, "bar": bar, "ok": bool}}"""
+    return {k: {'gpu': float(v[0]), 'bar': float(v[1]), 'ok': bool(v[2])}
+            for k, v in report.items() if k != '_fail'}
+
+
+def save_report(case, report):
+    """append the per-check (GPU err, bar) of a case to $SMI_PARITY_REPORT
+    (a JSON file, one object per case), when set"""
+    path = os.environ.get('SMI_PARITY_REPORT')
+    if not path:
+        return
+    d = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            d = json.load(f)
+    d[case] = report_json(report)
+    with open(path, 'w') as f:
+        json.dump(d, f, indent=1, sort_keys=True)
+
+
+def print_report(report, case=None):
     print('\n(GPU err / scale, envelope err / scale) vs the fp64 oracle:')
     for k, v in report.items():
         if k != '_fail':
             print(f'  {k:30s} gpu {v[0]:.3e}  bar {v[1]:.3e}  {"" if v[2] else "FAIL"}')
+    if case is not None:
+        save_report(case, report)
     assert not report.get('_fail'), report.get('_fail')
 
 

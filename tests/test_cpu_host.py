@@ -200,3 +200,25 @@ def test_context_lifecycle_without_device_work():
     assert lib.smi_context_make_current(None) == 0
     assert lib.smi_context_destroy(ctypes.c_void_p(h)) == 0
     assert lib.smi_context_destroy(None) == -1
+    # a destroyed context cannot be made current again; one still current on
+    # this thread is cleared (the thread falls back to the default workspace)
+    h2 = lib.smi_context_create(fake, 1 << 20)
+    assert lib.smi_context_make_current(ctypes.c_void_p(h2)) == 0
+    assert lib.smi_context_destroy(ctypes.c_void_p(h2)) == 0
+    assert lib.smi_context_make_current(ctypes.c_void_p(h2)) != 0
+    assert b'destroyed' in lib.smi_last_error()
+
+
+def test_fault_injection_only_in_the_test_build():
+    """smi_fault_set (tests/negative_controls.py) exists only in the
+    fault-injection variant, never in the product library"""
+    import subprocess
+    prod = os.path.join(ROOT, 'surreal_amd', 'libsurreal_mi.so')
+    syms = subprocess.run(['nm', '-D', '--defined-only', prod], capture_output=True, text=True,
+                          check=True).stdout
+    assert 'smi_fault_set' not in syms and 'fault' not in syms
+    var = os.path.join(ROOT, 'surreal_amd', 'libsurreal_mi_fault.so')
+    if os.path.exists(var):
+        syms = subprocess.run(['nm', '-D', '--defined-only', var], capture_output=True, text=True,
+                              check=True).stdout
+        assert 'smi_fault_set' in syms

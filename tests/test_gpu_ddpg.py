@@ -212,7 +212,13 @@ def _load_ddpg(ref, init, noisy=None):
         R.load_flat(list(ref.perc.parameters()), f(init['perc']))
     if 'perc2' in init:
         R.load_flat(list(ref.perc2.parameters()), f(init['perc2']))
-    ref.hard_update()
+    # the constructor syncs actor / critic(s) only (ddpg.py:174-178); the target
+    # perceptions keep their own init, taken from the learner
+    ref.hard_update(perception=False)
+    if 'perc_t' in init:
+        R.load_flat(list(ref.perc_t.parameters()), f(init['perc_t']))
+    if 'perc2_t' in init:
+        R.load_flat(list(ref.perc2_t.parameters()), f(init['perc2_t']))
 
 
 def _ddpg_state(learner):
@@ -228,6 +234,7 @@ def _ddpg_state(learner):
         out['perc_t'] = learner.model_target.perception.flat.detach().cpu().clone()
         if learner.use_double_critic:
             out['perc2'] = learner.model2.perception.flat.detach().cpu().clone()
+            out['perc2_t'] = learner.model_target2.perception.flat.detach().cpu().clone()
     return out
 
 
@@ -242,6 +249,7 @@ def _ddpg_ref_state(ref):
         out['perc_t'] = R.flat_of(list(ref.perc_t.parameters()))
         if ref.double:
             out['perc2'] = R.flat_of(list(ref.perc2.parameters()))
+            out['perc2_t'] = R.flat_of(list(ref.perc2_t.parameters()))
     return {k: v.double().numpy() for k, v in out.items()}
 
 
@@ -251,20 +259,44 @@ def ddpg_envelope_run(lc, D, A, iters=3, batches=None, n_ulp=6, learn_input=None
     steps.  batches: list of numpy dicts (obs, actions, rewards (B,1),
     obs_next, dones (B,1)); learn_input(learner, it) -> what learner.learn()
     gets (default: the batch on the device)."""
-    from tests import parity as P
     B = lc.replay.batch_size
     from surreal_amd.config import pixel_env_config
     ec = pixel_env_config(D, A, pixel) if pixel is not None else gym_env_config(D, A)
     learner = DDPGLearner(lc, ec, seed=seed)
     init = {k: v for k, v in _ddpg_state(learner).items()
-            if k in ('actor', 'critic', 'critic2', 'perc', 'perc2')}
+            if k in ('actor', 'critic', 'critic2', 'perc', 'perc2', 'perc_t', 'perc2_t')}
+    if batches is None:
+        batches = [{k: v.numpy() for k, v in synthetic.ddpg_batch(B, D, A, seed=it).items()}
+                   for it in range(iters)]
+    gpu = []
+    for it, b in enumerate(batches):
+        np.random.seed(100 + it)                    # the TD3 smoothing noise's stream
+        if learn_input is None and pixel is not None:
+            dev = {k: torch.as_tensor(b[k], dtype=torch.float32).cuda()
+                   for k in ('actions', 'rewards', 'dones')}
+            for k, pk in (('obs', 'pix'), ('obs_next', 'pix_next')):
+                dev[k] = {'low_dim': {'flat_inputs': torch.as_tensor(b[k], dtype=torch.float32).cuda()},
+                          'pixel': {'camera0': torch.as_tensor(b[pk]).cuda()}}
+            learner.learn(dev)
+        elif learn_input is None:
+            learner.learn({k: torch.as_tensor(v, dtype=torch.float32).cuda() for k, v in b.items()})
+        else:
+            learner.learn(learn_input(learner, it))
+        gpu.append((_ddpg_state(learner), learner.last_stats()))
+    ddpg_envelope_check(lc, D, A, init, batches, gpu, n_ulp=n_ulp, pixel=pixel)
+    return learner
+
+
+def ddpg_envelope_check(lc, D, A, init, batches, gpu, n_ulp=6, pixel=None, tag=''):
+    """gpu[it] = (_ddpg_state, last_stats()) of a HIP learner after step it
+    (started from `init`, np.random seeded 100 + it before each step) against
+    the fp64 oracle's optimize() over the same batches, within the envelope of
+    equally valid fp32 executions (tests/parity.py)."""
+    from tests import parity as P
     r64 = R.DDPGLearnerRef(lc, D, A, dtype=torch.float64, pixel=pixel)
     _load_ddpg(r64, init)
     vs = [_DVariant('order', k, lc, D, A, init, pixel) for k in DDPG_ORDERS]
     vs += [_DVariant('ulp', k, lc, D, A, init, pixel) for k in range(1, n_ulp + 1)]
-    if batches is None:
-        batches = [{k: v.numpy() for k, v in synthetic.ddpg_batch(B, D, A, seed=it).items()}
-                   for it in range(iters)]
     report = {}
     for it, b in enumerate(batches):
         np.random.seed(100 + it)
@@ -277,33 +309,21 @@ def ddpg_envelope_run(lc, D, A, iters=3, batches=None, n_ulp=6, learn_input=None
         for v in vs:
             np.random.seed(100 + it)
             svs.append(v.optimize(b, it))
-        np.random.seed(100 + it)
-        if learn_input is None and pixel is not None:
-            dev = {k: torch.as_tensor(b[k], dtype=torch.float32).cuda()
-                   for k in ('actions', 'rewards', 'dones')}
-            for k, pk in (('obs', 'pix'), ('obs_next', 'pix_next')):
-                dev[k] = {'low_dim': {'flat_inputs': torch.as_tensor(b[k], dtype=torch.float32).cuda()},
-                          'pixel': {'camera0': torch.as_tensor(b[pk]).cuda()}}
-            learner.learn(dev)
-        elif learn_input is None:
-            learner.learn({k: torch.as_tensor(v, dtype=torch.float32).cuda() for k, v in b.items()})
-        else:
-            learner.learn(learn_input(learner, it))
-        s = learner.last_stats()
-        got, p64 = _ddpg_state(learner), _ddpg_ref_state(r64)
+        got, s = gpu[it]
+        p64 = _ddpg_ref_state(r64)
         pvs = [_ddpg_ref_state(v.ref) for v in vs]
         for k in p64:
             w, sc = P.width(p64[k], [x[k] for x in pvs])
-            P.check(f'{k}@{it}', got[k], p64[k], w, sc, report)
+            P.check(f'{k}{tag}@{it}', got[k], p64[k], w, sc, report)
         for k in s64:
             w = max(abs(x[k] - s64[k]) for x in svs)
             e, sc = abs(s[k] - s64[k]), max(abs(s64[k]), 1e-30)
             ok = e <= 2 * w + 1e-6 * sc or e <= 1e-5 * sc
-            report[f'stat:{k}@{it}'] = (e / sc, max(w / sc, 1e-5), ok)
+            report[f'stat{tag}:{k}@{it}'] = (e / sc, max(w / sc, 1e-5), ok)
             if not ok:
-                report.setdefault('_fail', []).append(f'stat:{k}@{it}')
+                report.setdefault('_fail', []).append(f'stat{tag}:{k}@{it}')
     P.print_report(report)
-    return learner
+    return report
 
 
 @pytest.mark.parametrize('target,clip_critic,layernorm', [('hard', False, False), ('soft', True, False),

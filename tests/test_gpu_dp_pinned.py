@@ -104,4 +104,4 @@ def test_dp_two_ranks_match_global_fixture(case):
                                 adv, ret, r0['stats']['epochs_run'])
         P.check_stats(r0['stats'], rec, report, tag=f'_dp@{it}')
         assert r0['stats'] == r1['stats']
-    P.print_report(report)
+    P.print_report(report, f'{case}_dp2')

@@ -220,6 +220,13 @@ def check_fixture_state(meta, fx, st, it, fin, adv, ret, zf, report, tag=''):
         if f'{k}@{it}' in fx:
             r, w, sc = P.truth(meta, fx, k, it, st)
             P.check(f'{k}{tag}@{it}', fin[k], r, w, sc, report)
+            # the update itself (GPU - init vs fp64 - init): relative L2 over the
+            # entries the fp64 update moved and the cosine, on bars that a frozen
+            # or mis-stepped tensor cannot meet (tests/parity.py update_metrics)
+            w_rel, w_cos, thr, _ = meta['update'][f'{k}@{it}']
+            st0 = np.asarray(st[k], dtype=np.float64)
+            P.check_update(f'{k}{tag}@{it}', np.asarray(fin[k], np.float64) - st0,
+                           fx[f'{k}@{it}'].astype(np.float64), thr, w_rel, w_cos, report)
     for b, v in zip(('running_sum', 'running_sumsq'), zf[:2]):
         r, w, sc = P.truth(meta, fx, f'zf_{b}', it, st)
         P.check(f'zf_{b}{tag}@{it}', v, r, w, sc, report)
@@ -239,7 +246,7 @@ def pinned_fixture(case):
         check_fixture_state(meta, fx, st, it, cap['final'], adv, ret, cap['final']['zf'], report)
         _check_stats(lc, c['D'], c['A'], c['pixel'], oracle_batch(batch), cap, learner, report,
                      f'@{it}')
-    P.print_report(report)
+    P.print_report(report, case)
 
 
 @pytest.mark.timeout(300)
@@ -301,7 +308,7 @@ def test_pinned_first_step_gradients(case):
     for k, v in got.items():
         r, w, sc = P.truth(meta, fx, f'grad_{k}', 0, st)
         P.check(f'grad_{k}', v, r, w, sc, report)
-    P.print_report(report)
+    P.print_report(report, case)
 
 
 # ------------------------------------------------------ staging (a2 / f2)
