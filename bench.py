@@ -454,8 +454,9 @@ def main():
                     help='strong (default for c3/c5): the workload\'s global batch split over '
                          'the ranks; weak (c2, c4): the per-GPU batch fixed')
     ap.add_argument('--graph', choices=['on', 'off'], default='on',
-                    help='one GPU: learn() as a hipGraph replay of its device sequence '
-                         '(PPOLearner(use_graph=True), bit-identical to eager); ranks > 1 run eager')
+                    help='learn() as a hipGraph replay of its device sequence '
+                         '(PPOLearner(use_graph=True), bit-identical to eager); with ranks > 1 '
+                         'over RCCL the all-reduces are captured too (gloo runs eager)')
     args = ap.parse_args()
 
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:

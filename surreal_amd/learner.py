@@ -77,6 +77,11 @@ class TorchDistAllReduce(object):
         # optional: a list receiving (start, end, bytes) event pairs of every
         # all-reduce, recorded on the caller's stream (bench.py instrumentation)
         self.timing = None
+        # RCCL collectives are enqueued on the caller's stream and can be
+        # captured into a hipGraph with the learner's kernels (a PPOLearner
+        # with use_graph=True then replays the whole data-parallel learn(),
+        # all-reduces included); gloo's run on the host and cannot
+        self.capturable = dist.get_backend(group) == 'nccl'
 
     def allreduce_(self, t):
         if self.timing is not None and t.is_cuda:
@@ -266,7 +271,12 @@ class PPOLearner(LearnerHooks):
         # optional export of the advantages as the policy epochs use them (and
         # the RNN window returns) into self._bufs['adv_used'] / ['ret_used']
         self.export_advantages = False
-        self.use_graph = bool(use_graph) and dp is None
+        # hipGraph replay: one GPU, or data parallel over a capturable group
+        # (RCCL: the all-reduces are captured with the kernels).  The data-
+        # parallel RewardFilter commits host-side state between its exchange and
+        # the GAE, so that combination stays eager.
+        self.use_graph = bool(use_graph) and (
+            dp is None or (getattr(dp, 'capturable', False) and not self.use_r_filter))
         self._graph = None
         self._gin = None
         # LSTM / pixel phases: ref_pol on a second stream beside the GAE pass
@@ -741,9 +751,11 @@ class PPOLearner(LearnerHooks):
         self._ctx.make_current()
         if self._hyper_values() != self._hyper_key:
             self._write_hyper()
+        dp = self.dp
         if self._graph is None or self._graph_key != key:
-            for _ in self._device_phases(batch):
-                pass
+            for buf in self._device_phases(batch):
+                if dp is not None:
+                    dp.allreduce_(buf)
             self._gin = [t.detach().clone() for t in leaves]
             static = build(self._gin)
             # quiesce the parameter publisher (its worker thread synchronizes
@@ -754,10 +766,24 @@ class PPOLearner(LearnerHooks):
                 self.publisher.flush()
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode='thread_local'):
+            try:
+                with torch.cuda.graph(g, capture_error_mode='thread_local'):
+                    self._ctx.make_current()
+                    for buf in self._device_phases(static):
+                        if dp is not None:            # RCCL all-reduce, captured
+                            dp.allreduce_(buf)
+            except RuntimeError as e:
+                if dp is None:
+                    raise
+                # a collective library that refuses capture: this learner stays
+                # eager (this call's update already ran above)
+                import warnings
+                warnings.warn(f'data-parallel learn() could not be captured ({e}); eager launches')
+                self.use_graph = False
+                self._graph = None
                 self._ctx.make_current()
-                for _ in self._device_phases(static):
-                    pass
+                self._learn_epilogue()
+                return
             self._ctx.make_current()
             self._graph, self._graph_key = g, key
         else:

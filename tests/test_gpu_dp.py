@@ -141,3 +141,53 @@ def test_dp_world1_matches_fused_path():
         assert sf['epochs_run'] == sp['epochs_run']
         assert max_rel_err(phased.model.actor.flat.cpu(), fused.model.actor.flat.cpu()) < 1e-4
         assert max_rel_err(phased.model.critic.flat.cpu(), fused.model.critic.flat.cpu()) < 1e-4
+
+
+def _capture_worker(rank, port, outdir):
+    import os
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1)
+    from surreal_amd.learner import TorchDistAllReduce
+    from tests.test_gpu_boundary import _same, _state
+    dp = TorchDistAllReduce()
+    lc = ppo_config(B=128, T=25, mode='adapt', use_z_filter=True, hidden=(300, 200), lam=1.0,
+                    epochs=(4, 4), rnn=True, rnn_hidden=100, horizon=5)
+    lc.parameter_publish.exp_interval = 2 * lc.replay.batch_size
+    ec = env_config(42, 8)
+    eager = PPOLearner(lc, ec, seed=4, dp=dp)
+    graph = PPOLearner(lc, ec, seed=4, dp=dp, use_graph=True)
+    same = []
+    for it in range(5):
+        b = synthetic.to_device(synthetic.ppo_batch(128, 25, 42, 8, seed=70 + it, rnn_hidden=100), 'cuda')
+        eager.learn(b)
+        graph.learn(b)
+        eager.publish_parameter(it)
+        graph.publish_parameter(it)
+        torch.cuda.synchronize()
+        ok = _same(_state(eager), _state(graph)) and eager.last_stats() == graph.last_stats()
+        ok = ok and all(torch.equal(v, graph.optimizer_state()[k]) for k, v in eager.optimizer_state().items())
+        same.append(bool(ok))
+    torch.save({'capturable': dp.capturable, 'captured': graph._graph is not None, 'same': same},
+               os.path.join(outdir, 'res.pt'))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_learn_captured_with_rccl_allreduce_bit_exact():
+    """A data-parallel learner over RCCL (backend 'nccl', world 1 on this one-GPU
+    box) replays learn() as ONE hipGraph with the all-reduces captured between
+    its launches: bit-identical to the same data-parallel learner run eagerly,
+    over several learns with a publish between them (a rank of a
+    strong-scaled job issues ~400 launches and 33 collectives per learn)."""
+    import os
+    import tempfile
+    import torch.multiprocessing as mp
+    from tests.test_gpu_dp_procs import _free_port
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_capture_worker, args=(_free_port(), d), nprocs=1, join=True)
+        res = torch.load(os.path.join(d, 'res.pt'), weights_only=True)
+    assert res['capturable'] and res['captured'], res
+    assert all(res['same']), res

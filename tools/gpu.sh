@@ -9,6 +9,7 @@
 #   bash tools/gpu.sh <tag> kt <name> [bench.py args...]    rocprofv3 kernel-trace --stats of a bench command
 #   bash tools/gpu.sh <tag> pmc <name> [bench.py args...]   FETCH_SIZE / WRITE_SIZE passes (separate runs)
 #   bash tools/gpu.sh <tag> final                           tests + smoke + the round's bench lines + kt + pmc
+#   bash tools/gpu.sh <tag> run <name> <timeout> cmd...     any command -> <name>.log (A/B arms: VAR=x env ...)
 #
 # Outputs go to gpurun_out/<tag>/ (copied back by gpurun); the parity report
 # of the tests step is gpurun_out/<tag>/parity_report.json.
@@ -60,8 +61,15 @@ pmc() {  # name args...: one counter group per run (gfx950: FETCH_SIZE x2 = byte
   echo "pmc $n done"
 }
 
+run() {  # name timeout cmd...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$OUT/$n.log" 2>&1 || { tail -30 "$OUT/$n.log"; die "run $n"; }
+  tail -5 "$OUT/$n.log"
+}
+
 case "$what" in
   tests) tests "$@" ;;
+  run) run "$@" ;;
   smoke) smoke ;;
   bench) bench "$@" ;;
   kt) kt "$@" ;;
