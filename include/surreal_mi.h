@@ -586,6 +586,13 @@ int smi_layernorm_backward(const float* dy, int64_t ldg, const float* x, int64_t
  * `stream` (the publisher's side stream), so the caller's thread never waits
  * in a DMA copy call.  Fails when host_dst is not pinned, mapped memory. */
 int smi_copy_to_host(void* host_dst, const void* src, int64_t nbytes, void* stream);
+/* The publisher's snapshot (module_dict.py:22-35: every state_dict tensor of
+ * the published modules): n device segments srcs[i] (16-byte aligned, nbytes[i]
+ * a multiple of 4) copied to dst + dst_offsets[i] (16-byte aligned) in one
+ * launch per 16 segments on `stream` (the learner's, stream-ordered after the
+ * last update).  srcs / dst_offsets / nbytes are host arrays. */
+int smi_copy_gather(void* dst, const void* const* srcs, const int64_t* dst_offsets,
+                    const int64_t* nbytes, int n, void* stream);
 /* target <- tau*src + (1-tau)*target (soft target update, ddpg.py:409-417) */
 int smi_soft_update(float* target, const float* src, int64_t n, float tau, void* stream);
 /* action_norm, rewards, Q_target, Q_policy means of ddpg.py:335-345 -> stats4 */

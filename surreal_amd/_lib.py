@@ -162,6 +162,7 @@ _SIGS = {
     'smi_tanh_backward': (c_int, [P, c_i64, P, c_i64, c_i64, c_int, P, c_i64, P]),
     'smi_copy_cols': (c_int, [P, c_i64, c_i64, c_int, P, c_i64, P]),
     'smi_copy_to_host': (c_int, [P, P, c_i64, P]),
+    'smi_copy_gather': (c_int, [P, P, P, P, c_int, P]),
     'smi_head_forward': (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_i64, c_i64, P, P, P, P,
                                  P]),
     'smi_head_backward_input': (c_int, [P, c_int, c_int, c_int, c_int, P, P, c_i64, P, P, P, P,

@@ -21,6 +21,16 @@ HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 CXXFLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-mcode-object-version=5',
             '-Wall', '-Wno-unused-function']
+# Compilation units: (object, source, extra flags).  lstm_kernels.hip is
+# compiled twice: the MFMA forms + launchers, and the VALU recurrence with
+# -fno-slp-vectorize (its fmaf chains stay scalar v_fmac_f32: the SLP
+# vectorizer packs them into v_pk_fma_f32 + operand moves; measured at 128
+# segments, one MI355X: lstm_fwd 43.0 -> 40.9 us, lstm_bwd 34.5 -> 27.0 us per
+# launch, learn 3.48 -> 3.29 ms; the flag on the MFMA forms changed their
+# rounding)
+UNITS = [(s.replace('.hip', '.o'), s, []) for s in SOURCES if s != 'lstm_kernels.hip'] + [
+    ('lstm_kernels.o', 'lstm_kernels.hip', ['-DSMI_LSTM_PART=1']),
+    ('lstm_valu.o', 'lstm_kernels.hip', ['-DSMI_LSTM_PART=2', '-fno-slp-vectorize'])]
 
 
 def torch_lib_dir():
@@ -71,12 +81,12 @@ def build(verbose=False, force=False, variant=None):
     deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'surreal_mi.h')]
     dep_t = max(_mtime(d) for d in deps)
     objs, cmds = [], []
-    for src in SOURCES:
+    for obj, src, extra in UNITS:
         sp = os.path.join(CSRC, src)
-        op = os.path.join(build_dir, src.replace('.hip', '.o'))
+        op = os.path.join(build_dir, obj)
         objs.append(op)
-        if force or _mtime(op) < max(_mtime(sp), dep_t):
-            cmds.append([HIPCC] + CXXFLAGS + VARIANTS[variant] + ['-c', sp, '-o', op])
+        if force or _mtime(op) < max(_mtime(sp), dep_t, _mtime(__file__)):
+            cmds.append([HIPCC] + CXXFLAGS + extra + VARIANTS[variant] + ['-c', sp, '-o', op])
     # one hipcc per source, run side by side (each is single-threaded)
     from concurrent.futures import ThreadPoolExecutor
     jobs = max(1, min(len(cmds), int(os.environ.get('MAX_JOBS', os.cpu_count() or 1))))

@@ -110,13 +110,15 @@ int launch_tanh_backward(const float*, int64_t, const float*, int64_t, int64_t, 
 int launch_copy_cols(const float*, int64_t, int64_t, int, float*, int64_t, hipStream_t);
 int launch_soft_update(float*, const float*, int64_t, float, hipStream_t);
 int launch_copy_bytes16(const void*, void*, int64_t, hipStream_t);
+int launch_copy_gather(void*, const void* const*, const int64_t*, const int64_t*, int, hipStream_t);
 bool head_fused_ok(int in, int64_t ldx, int h1, int h2, int out, const float* X,
                    const float* W1, const float* W2, const float* W3);
 int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
                           const float* b1, int h1, const float* W2, const float* b2, int h2,
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
-                          hipStream_t st, const int* skip);
+                          hipStream_t st, const int* skip, const float* vret = nullptr,
+                          float* vgrad = nullptr, float vscale = 0.f);
 int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
                           const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
@@ -506,6 +508,18 @@ int smi_copy_to_host(void* host_dst, const void* src, int64_t nbytes, void* stre
   if (hipHostGetDevicePointer(&dev, host_dst, 0) != hipSuccess || !dev)
     return set_error(SMI_E_ARG, "copy_to_host: destination is not pinned (mapped) host memory");
   return launch_copy_bytes16(src, dev, nbytes / 16, SMI_STREAM(stream));
+}
+
+int smi_copy_gather(void* dst, const void* const* srcs, const int64_t* dst_offsets,
+                    const int64_t* nbytes, int n, void* stream) {
+  REQUIRE(dst && n >= 0 && (n == 0 || (srcs && dst_offsets && nbytes)), "copy_gather: bad args");
+  for (int i = 0; i < n; ++i)
+    REQUIRE(srcs[i] && nbytes[i] >= 0 && nbytes[i] % 4 == 0 && dst_offsets[i] % 16 == 0 &&
+                (reinterpret_cast<uintptr_t>(srcs[i]) & 15) == 0,
+            "copy_gather: 16-byte aligned segments of a multiple of 4 bytes required");
+  REQUIRE((reinterpret_cast<uintptr_t>(dst) & 15) == 0, "copy_gather: 16-byte aligned destination");
+  if (n == 0) return SMI_OK;
+  return launch_copy_gather(dst, srcs, dst_offsets, nbytes, n, SMI_STREAM(stream));
 }
 
 int smi_soft_update(float* target, const float* src, int64_t n, float tau, void* stream) {

@@ -16,6 +16,8 @@
 
 namespace smi {
 
+constexpr int kGatherMax = 16;      // segments per copy_gather launch
+
 __global__ void __launch_bounds__(kWG)
 mse_grad_kernel(const float* __restrict__ q, int64_t qs, const float* __restrict__ y, int64_t n,
                 float* __restrict__ dq, float* loss) {
@@ -75,6 +77,25 @@ __global__ void __launch_bounds__(kWG)
 copy_bytes16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16) {
   for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kWG)
     dst[i] = src[i];
+}
+
+// up to kGatherMax device segments into one destination (the publisher's
+// snapshot arena): blockIdx.y = segment, 16-byte body + 4-byte tail
+struct GatherArgs {
+  const char* src[kGatherMax]; int64_t off[kGatherMax]; int64_t nbytes[kGatherMax];
+  char* dst;
+};
+__global__ void __launch_bounds__(kWG)
+copy_gather_kernel(GatherArgs a) {
+  const int s = blockIdx.y;
+  const char* __restrict__ src = a.src[s];
+  char* __restrict__ dst = a.dst + a.off[s];
+  const int64_t n = a.nbytes[s], n16 = n >> 4;
+  const int64_t t0 = (int64_t)blockIdx.x * kWG + threadIdx.x, ts = (int64_t)gridDim.x * kWG;
+  for (int64_t i = t0; i < n16; i += ts)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  for (int64_t i = (n16 << 2) + t0; i < (n >> 2); i += ts)
+    reinterpret_cast<float*>(dst)[i] = reinterpret_cast<const float*>(src)[i];
 }
 
 __global__ void __launch_bounds__(kWG)
@@ -259,6 +280,27 @@ int launch_copy_bytes16(const void* src, void* dst, int64_t n16, hipStream_t st)
   hipLaunchKernelGGL(copy_bytes16_kernel, dim3((unsigned)g), dim3(kWG), 0, st,
                      reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16);
   return check_launch("copy_bytes16_kernel");
+}
+int launch_copy_gather(void* dst, const void* const* srcs, const int64_t* offs,
+                       const int64_t* nbytes, int n, hipStream_t st) {
+  for (int b = 0; b < n; b += kGatherMax) {
+    GatherArgs a{};
+    a.dst = static_cast<char*>(dst);
+    const int m = n - b < kGatherMax ? n - b : kGatherMax;
+    int64_t mx = 0;
+    for (int i = 0; i < m; ++i) {
+      a.src[i] = static_cast<const char*>(srcs[b + i]);
+      a.off[i] = offs[b + i];
+      a.nbytes[i] = nbytes[b + i];
+      mx = nbytes[b + i] > mx ? nbytes[b + i] : mx;
+    }
+    int64_t g = (mx / 16 + kWG - 1) / kWG;
+    g = g < 1 ? 1 : (g > 64 ? 64 : g);
+    hipLaunchKernelGGL(copy_gather_kernel, dim3((unsigned)g, (unsigned)m), dim3(kWG), 0, st, a);
+    const int rc = check_launch("copy_gather_kernel");
+    if (rc) return rc;
+  }
+  return SMI_OK;
 }
 int launch_soft_update(float* t, const float* s, int64_t n, float tau, hipStream_t st) {
   hipLaunchKernelGGL(soft_update_kernel, dim3(grid_of(n)), dim3(kWG), 0, st, t, s, n, tau);

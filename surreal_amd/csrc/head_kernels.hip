@@ -54,6 +54,10 @@ struct HeadFwdArgs {
   float* W1T; float* W2T;                // optional: [K0][h1], [h1][h2] for the backward
   int64_t rows; const int* skip;
   int ld0, ld1, ld2;                     // LDS leading dims (floats)
+  // optional value-loss epilogue (out == 1, ppo.py:311-331): vgrad[r] =
+  // vscale * (Y[r] - vret[r]), the MSE gradient the learner's value_rows pass
+  // would compute from Y (same fp32 ops), written by the forward itself
+  const float* vret; float* vgrad; float vscale;
 };
 
 struct HeadBwdArgs {
@@ -69,6 +73,34 @@ struct HeadBwdArgs {
   int64_t rows; const int* skip;
   int ld2, ld1;                          // LDS leading dims
 };
+
+// Developer phase timer (build variant 'prof', -DSMI_PROF): thread 0 of every
+// workgroup adds its wall-clock ticks (100 MHz) per phase into g_head_ticks
+// (vector atomics), [8] counts the workgroups; forward and backward each own
+// 10 slots (smi_head_phase_ticks, tools/head_ticks.py)
+#ifdef SMI_PROF
+__device__ unsigned long long g_head_ticks[2][10];
+#define HEAD_T0() unsigned long long h_t0_ = wall_clock64(), h_prev_ = h_t0_
+#define HEAD_TICK(k, id)                                                   \
+  do {                                                                      \
+    if (threadIdx.x == 0) {                                                 \
+      const unsigned long long n_ = wall_clock64();                         \
+      atomicAdd(&g_head_ticks[k][id], n_ - h_prev_);                        \
+      h_prev_ = n_;                                                         \
+    }                                                                       \
+  } while (0)
+#define HEAD_END(k)                                                        \
+  do {                                                                      \
+    if (threadIdx.x == 0) {                                                 \
+      atomicAdd(&g_head_ticks[k][8], 1ull);                                 \
+      atomicAdd(&g_head_ticks[k][9], wall_clock64() - h_t0_);               \
+    }                                                                       \
+  } while (0)
+#else
+#define HEAD_T0() (void)0
+#define HEAD_TICK(k, id) (void)0
+#define HEAD_END(k) (void)0
+#endif
 
 // LDS leading dim of a K-wide activation tile: K rounded up to the 16-k chunk,
 // + 4 (an odd multiple of 4 floats: the 16 rows of a chunk read land on 16
@@ -323,6 +355,7 @@ head_fwd_kernel(HeadFwdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
   const int64_t r0 = (int64_t)blockIdx.x * R;
+  HEAD_T0();
   if (r0 < a.rows) {
     // layer 1's weight stream and bias first: in flight while X arrives
     HcStream<NT1> S1;
@@ -339,25 +372,31 @@ head_fwd_kernel(HeadFwdArgs a) {
       *reinterpret_cast<float4*>(s0 + r * a.ld0 + 4 * q) = v;
     }
     __syncthreads();
+    HEAD_TICK(0, 0);                              // X staged
     HcStream<NT2> S2;
     float e2[RT][NT2][4];
     {   // layer 1: HA1 = relu(X W1^T + b1)
       f32x4 acc[RT][NT1];
       hc_run<NT1, RT>(S1, s0, a.ld0, acc);
+      HEAD_TICK(0, 1);                            // layer 1 k loop
       S2.init(a.W2, a.h1, a.h1, a.h2, wave, 4, 0, 1);     // layer 2's stream, in flight
       hc_epi_load<NT2, 0, RT>(wave, a.h2, a.b2, nullptr, r0, a.rows, e2);
       hc_store<NT1, 0, RT>(acc, e1, wave, a.h1, s1, a.ld1);
     }
     hc_sync();
+    HEAD_TICK(0, 2);                              // epilogue 1 + barrier
     hc_copy_out<RT>(s1, a.ld1, a.h1, a.HA1, r0, a.rows);
+    HEAD_TICK(0, 3);                              // HA1 copy-out issue
     HcStream<1> S3;
     {   // layer 2: HA2 = relu(HA1 W2^T + b2)
       f32x4 acc[RT][NT2];
       hc_run<NT2, RT>(S2, s1, a.ld1, acc);
+      HEAD_TICK(0, 4);                            // layer 2 k loop
       S3.init(a.W3, a.h2, a.h2, a.out, 0, 1, wave, 4);    // layer 3's stream
       hc_store<NT2, 0, RT>(acc, e2, wave, a.h2, s2, a.ld2);
     }
     hc_sync();
+    HEAD_TICK(0, 5);                              // epilogue 2 + barrier
     hc_copy_out<RT>(s2, a.ld2, a.h2, a.HA2, r0, a.rows);
     {   // layer 3 (out <= 16): the waves split the k chunks, fixed-order sum
       const float bn = a.b3[li < a.out ? li : a.out - 1];
@@ -377,11 +416,14 @@ head_fwd_kernel(HeadFwdArgs a) {
             if (r0 + r >= a.rows) continue;
             const float v = ((sR[((0 * RT + rt) * 64 + lane) * 4 + i] + sR[((1 * RT + rt) * 64 + lane) * 4 + i]) +
                              (sR[((2 * RT + rt) * 64 + lane) * 4 + i] + sR[((3 * RT + rt) * 64 + lane) * 4 + i])) + bn;
-            a.Y[(r0 + r) * a.ldy + li] = a.tanh_out ? tanhf(v) : v;
+            const float y = a.tanh_out ? tanhf(v) : v;
+            a.Y[(r0 + r) * a.ldy + li] = y;
+            if (a.vgrad) a.vgrad[r0 + r] = a.vscale * (y - a.vret[r0 + r]);
           }
       }
     }
   }
+  HEAD_TICK(0, 6);                                // HA2 copy-out + layer 3
   // side job for the backward of the same phase: W1^T, W2^T
   if (a.W1T) {
     const int t1 = ((a.h1 + 31) >> 5) * ((a.K0 + 31) >> 5);
@@ -391,6 +433,8 @@ head_fwd_kernel(HeadFwdArgs a) {
       else hc_transpose_tile(a.W2, a.h2, a.h1, a.W2T, tix - t1, sR);
     }
   }
+  HEAD_TICK(0, 7);                                // transposes
+  HEAD_END(0);
 }
 
 template <int NTA, int NTB, int RT>
@@ -406,6 +450,7 @@ head_bwd_kernel(HeadBwdArgs a) {
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int out = a.out;
+  HEAD_T0();
   // dZ rows (zero past out: the dH2 pass runs whole groups of 4 k), loaded
   // first; dH1's weight stream (W2^T) and its masks are issued behind them and
   // stay in flight through the dZ W3 pass
@@ -473,20 +518,25 @@ head_bwd_kernel(HeadBwdArgs a) {
   float eA[RT][NTA][4];
   hc_epi_load<NTA, 1, RT>(wave, a.h1, nullptr, a.HA1, r0, a.rows, eA);
   hc_sync();
+  HEAD_TICK(1, 0);                                // dZ W3 pass
   HcStream<NTB> SB;
   {   // dH1 = (dH2 W2) * [HA1 > 0] = dH2 (W2^T)^T
     f32x4 acc[RT][NTA];
     hc_run<NTA, RT>(SA, s2, a.ld2, acc);
+    HEAD_TICK(1, 1);                              // dH1 k loop
     if (a.dxn > 0)      // dX's weight stream (rows dx0.. of W1^T), in flight
       SB.init(a.W1T + (int64_t)a.dx0 * a.h1, a.h1, a.h1, a.dxn, wave, 4, 0, 1);
     hc_store<NTA, 1, RT>(acc, eA, wave, a.h1, s1, a.ld1);
   }
   hc_sync();
+  HEAD_TICK(1, 2);                                // epilogue + barrier
   hc_copy_out<RT>(s1, a.ld1, a.h1, a.dH1, r0, a.rows);
-  if (a.dxn <= 0) return;
+  HEAD_TICK(1, 3);                                // dH1 copy-out issue
+  if (a.dxn <= 0) { HEAD_END(1); return; }
   {   // dX = dH1 W1[:, dx0 : dx0 + dxn]
     f32x4 acc[RT][NTB];
     hc_run<NTB, RT>(SB, s1, a.ld1, acc);
+    HEAD_TICK(1, 4);                              // dX k loop
     const int CT = (a.dxn + 15) >> 4;
 #pragma unroll
     for (int t = 0; t < NTB; ++t) {
@@ -506,7 +556,19 @@ head_bwd_kernel(HeadBwdArgs a) {
         }
     }
   }
+  HEAD_TICK(1, 5);                                // dX epilogue
+  HEAD_END(1);
 }
+
+#ifdef SMI_PROF
+extern "C" int smi_head_phase_ticks(unsigned long long* out /* [2][10] */) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_head_ticks), sizeof(g_head_ticks)) != hipSuccess)
+    return SMI_E_LAUNCH;
+  static const unsigned long long zero[20] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_head_ticks), zero, sizeof(zero)) == hipSuccess ? SMI_OK
+                                                                                        : SMI_E_LAUNCH;
+}
+#endif
 
 // ------------------------------------------------------------------ host side
 static int use_head_fused() {
@@ -552,10 +614,12 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
                           const float* b1, int h1, const float* W2, const float* b2, int h2,
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
-                          hipStream_t st, const int* skip) {
+                          hipStream_t st, const int* skip, const float* vret, float* vgrad,
+                          float vscale) {
   if (rows <= 0) return SMI_OK;
+  if (vgrad && (out != 1 || !vret)) return set_error(SMI_E_ARG, "head_forward: value epilogue needs out == 1");
   HeadFwdArgs a{X, ldx, in, W1, b1, W2, b2, W3, b3, h1, h2, out, tanh_out, HA1, HA2, Y, ldy,
-                W1T, W2T, rows, skip, hc_ld(in), hc_ld(h1), hc_ld(h2)};
+                W1T, W2T, rows, skip, hc_ld(in), hc_ld(h1), hc_ld(h2), vret, vgrad, vscale};
   const int rt = hc_rt(rows);
   const int R = HC_R * rt;
   const size_t lds = (size_t)(R * ((a.ld0 > a.ld2 ? a.ld0 : a.ld2) + a.ld1) + hc_sr(rt)) * 4;

@@ -21,9 +21,22 @@
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
 
+// The file is compiled twice (build.py): SMI_LSTM_PART 1 = the MFMA forms and
+// the launchers, SMI_LSTM_PART 2 = the VALU recurrence (lstm_fwd_v_kernel /
+// lstm_bwd_v_kernel) with -fno-slp-vectorize.  The VALU recurrence's fmaf
+// chains must stay scalar v_fmac_f32 (the SLP vectorizer packs them into
+// v_pk_fma_f32 + operand moves: same sums, slower); the flag on the MFMA forms
+// changed their rounding, so it is applied to the VALU half only.
+// 0 (default) = both halves in one object.
+#ifndef SMI_LSTM_PART
+#define SMI_LSTM_PART 0
+#endif
+#define SMI_LSTM_MFMA (SMI_LSTM_PART != 2)
+#define SMI_LSTM_VALU_HALF (SMI_LSTM_PART != 1)
+
 namespace smi {
 
-constexpr int LR = 16;   // segments per workgroup
+[[maybe_unused]] constexpr int LR = 16;   // segments per workgroup
 
 // Developer phase timer (build variant 'prof', -DSMI_PROF): workgroup 0, wave
 // 0 accumulates wall-clock ticks (100 MHz) per step phase:
@@ -107,6 +120,17 @@ struct LstmFwdArgs {
   const float* b_ih;      // [4H]
 };
 
+struct LstmBwdArgs {
+  const float* dh;        // [S][B][H]  dL/dh_t from the heads
+  const float* gates;     // [S][B][4H] activated (i, f, g, o)
+  const float* cbuf;      // [S+1][B][H]
+  const float* w_hh;      // [4H][H]
+  int S, B, H;
+  float* dgates;          // [S][B][4H] dL/d(pre-activation gates)
+  const int* skip;
+};
+
+#if SMI_LSTM_MFMA
 template <int MAXUT>
 __global__ void __launch_bounds__(kWG)
 lstm_fwd_kernel(LstmFwdArgs a) {
@@ -242,15 +266,7 @@ lstm_fwd_kernel(LstmFwdArgs a) {
   }
 }
 
-struct LstmBwdArgs {
-  const float* dh;        // [S][B][H]  dL/dh_t from the heads
-  const float* gates;     // [S][B][4H] activated (i, f, g, o)
-  const float* cbuf;      // [S+1][B][H]
-  const float* w_hh;      // [4H][H]
-  int S, B, H;
-  float* dgates;          // [S][B][4H] dL/d(pre-activation gates)
-  const int* skip;
-};
+
 
 template <int MAXUT>
 __global__ void __launch_bounds__(kWG)
@@ -872,6 +888,9 @@ lstm_bwd_r4_kernel(LstmBwdArgs a) {
 // Backward: thread (u, q) holds column u of W_hh restricted to gate q's rows,
 // dh_rec[u] = sum_q sum_j dgates[q*H + j] W_hh[q*H + j][u] is a per-lane
 // partial over gate q plus a fixed-order quad sum.
+#endif  // SMI_LSTM_MFMA
+
+#if SMI_LSTM_VALU_HALF
 template <int K>
 __device__ __forceinline__ float quad_bcast(float v) {      // lane K of each quad
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), K * 0x55, 0xF, 0xF, false));
@@ -1183,6 +1202,8 @@ lstm_bwd_v_kernel(LstmBwdArgs a) {
   }
 }
 
+#endif  // SMI_LSTM_VALU_HALF
+
 // VALU recurrence selection: SMI_LSTM_VALU = 0 (never), 1 (always when the
 // shape fits), unset: when the batch leaves at least one segment group per CU
 // idle under the MFMA forms (B <= 2 x CUs, i.e. R <= 2)
@@ -1226,10 +1247,11 @@ static int lstm_valu_r(int B, int H) {
 
 // LDS of the staged x sequence and the precomputed x parts (KX > 0); the fused
 // form is used up to kVxMax (S <= 52 steps at H = 100, x width <= 64)
-constexpr size_t kVxMax = 120 * 1024;
+[[maybe_unused]] constexpr size_t kVxMax = 120 * 1024;
 static size_t lstm_fwd_v_lds(int S, int R, int KX, int blk) {
   return ((((size_t)S * R * KX + 3) & ~(size_t)3) + (size_t)S * R * blk) * 4;
 }
+#if SMI_LSTM_VALU_HALF
 template <int R, int KX>
 static void fwd_v_dispatch_kp(const LstmFwdArgs& a, hipStream_t st) {
   const dim3 grid((a.B + R - 1) / R), blk((4 * a.H + 63) & ~63);
@@ -1260,6 +1282,36 @@ static void bwd_v_dispatch_kp(const LstmBwdArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((lstm_bwd_v_kernel<R, 128>), grid, blk, 0, st, a);
 }
 
+// the VALU forms' entry points for the launchers (the other half of the file
+// when it is compiled in two parts): kx 0 = xproj input, else the fused x
+// projection at R = 1 with x widths <= kx (48 / 64)
+void lstm_v_fwd(const LstmFwdArgs& a, int R, int kx, hipStream_t st) {
+  if (kx == 0) fwd_v_dispatch(a, R, st);
+  else if (kx <= 48) fwd_v_dispatch_kp<1, 48>(a, st);
+  else fwd_v_dispatch_kp<1, 64>(a, st);
+}
+void lstm_v_bwd(const LstmBwdArgs& a, int R, hipStream_t st) {
+  if (R == 1) bwd_v_dispatch_kp<1>(a, st);
+  else if (R == 2) bwd_v_dispatch_kp<2>(a, st);
+  else bwd_v_dispatch_kp<4>(a, st);
+}
+#ifdef SMI_PROF
+// the VALU half's phase ticks (its own copy of g_lstm_ticks when the file is
+// compiled in two parts)
+extern "C" int smi_lstm_v_phase_ticks(unsigned long long* out /* [8] */) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_ticks), sizeof(g_lstm_ticks)) != hipSuccess)
+    return SMI_E_LAUNCH;
+  static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_lstm_ticks), zero, sizeof(zero)) == hipSuccess ? SMI_OK
+                                                                                        : SMI_E_LAUNCH;
+}
+#endif
+#else
+void lstm_v_fwd(const LstmFwdArgs& a, int R, int kx, hipStream_t st);
+void lstm_v_bwd(const LstmBwdArgs& a, int R, hipStream_t st);
+#endif  // SMI_LSTM_VALU_HALF
+
+#if SMI_LSTM_MFMA
 static int use_r4() {
   static int u = -1;
   if (u < 0) {
@@ -1293,7 +1345,7 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
   struct End { int s; hipStream_t st; double f;
                ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{kslot, st, 8.0 * B * H * (double)H * S};
   if (const int R = lstm_valu_r(B, H)) {
-    fwd_v_dispatch(a, R, st);
+    lstm_v_fwd(a, R, 0, st);
     return check_launch("lstm_fwd_v_kernel");
   }
   if (H <= 128 && use_r4()) {
@@ -1351,8 +1403,7 @@ int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, c
                ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{
       kslot, st, 8.0 * B * H * (double)(H + din) * S};
   if (R == 1) {
-    if (din <= 48) fwd_v_dispatch_kp<1, 48>(a, st);
-    else fwd_v_dispatch_kp<1, 64>(a, st);
+    lstm_v_fwd(a, 1, din <= 48 ? 48 : 64, st);
     return check_launch("lstm_fwd_v_kernel");
   }
   const dim3 g4((B + LR4 - 1) / LR4);
@@ -1376,9 +1427,7 @@ int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, cons
                ~End() { ktime_end(s, KT_LSTM_BWD, f, st); } } end_{kslot, st,
                                                                  8.0 * B * H * (double)H * (S - 1)};
   if (const int R = lstm_valu_r(B, H)) {
-    if (R == 1) bwd_v_dispatch_kp<1>(a, st);
-    else if (R == 2) bwd_v_dispatch_kp<2>(a, st);
-    else bwd_v_dispatch_kp<4>(a, st);
+    lstm_v_bwd(a, R, st);
     return check_launch("lstm_bwd_v_kernel");
   }
   if (H <= 128 && use_r4()) {
@@ -1417,5 +1466,7 @@ int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, cons
   }
   return check_launch("lstm_bwd_kernel");
 }
+
+#endif  // SMI_LSTM_MFMA
 
 }  // namespace smi

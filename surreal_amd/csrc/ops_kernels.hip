@@ -512,12 +512,33 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 
 // torch.optim.Adam (single-tensor path) on a flat buffer, after the optional
 // clip_grad_norm_ coefficient.  HBM-bound: 28 B per parameter, 16-byte loads
-// and stores of p, g, m, v.
+// and stores of p, g, m, v.  NT bit 0: nontemporal stores of p, m, v; bit 1:
+// nontemporal loads (streams touched once per launch at sweep sizes).
+template <typename T>
+__device__ __forceinline__ T adam_ld(const T* p, int nt) {
+  return nt ? __builtin_nontemporal_load(p) : *p;
+}
+template <typename T>
+__device__ __forceinline__ void adam_st(T* p, T v, int nt) {
+  if (nt) __builtin_nontemporal_store(v, p); else *p = v;
+}
+__device__ __forceinline__ float4 adam_ld4(const float4* p, int nt) {
+  if (!nt) return *p;
+  const f32x4 u = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return float4{u[0], u[1], u[2], u[3]};
+}
+__device__ __forceinline__ void adam_st4(float4* p, float4 v, int nt) {
+  if (!nt) { *p = v; return; }
+  __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
+}
+
+template <int NT>
 __global__ void __launch_bounds__(kWG)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, int64_t n, int* step, const float* lr_ptr, float beta1,
             float beta2, float eps, float wd, float max_norm, float clip_value, const double* part,
             int np, const int* skip, float* norm_out) {
+  constexpr int NS = NT & 1, NL = (NT >> 1) & 1;
   if (skip && skip[0] != 0) return;
   __shared__ float s_coef;
   __shared__ int s_t;
@@ -557,18 +578,18 @@ adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restric
   float4* v4 = reinterpret_cast<float4*>(v);
   int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
   for (; i < n4; i += stride) {
-    float4 pp = p4[i], mm = m4[i], vv = v4[i];
-    const float4 gg = g4[i];
+    float4 pp = adam_ld4(p4 + i, NL), mm = adam_ld4(m4 + i, NL), vv = adam_ld4(v4 + i, NL);
+    const float4 gg = adam_ld4(g4 + i, NL);
     adam_elem(pp.x, gg.x, mm.x, vv.x, k);
     adam_elem(pp.y, gg.y, mm.y, vv.y, k);
     adam_elem(pp.z, gg.z, mm.z, vv.z, k);
     adam_elem(pp.w, gg.w, mm.w, vv.w, k);
-    p4[i] = pp; m4[i] = mm; v4[i] = vv;
+    adam_st4(p4 + i, pp, NS); adam_st4(m4 + i, mm, NS); adam_st4(v4 + i, vv, NS);
   }
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += stride) {
-    float pi = p[i], mi = m[i], vi = v[i];
-    adam_elem(pi, g[i], mi, vi, k);
-    p[i] = pi; m[i] = mi; v[i] = vi;
+    float pi = adam_ld(p + i, NL), mi = adam_ld(m + i, NL), vi = adam_ld(v + i, NL);
+    adam_elem(pi, adam_ld(g + i, NL), mi, vi, k);
+    adam_st(p + i, pi, NS); adam_st(m + i, mi, NS); adam_st(v + i, vi, NS);
   }
 }
 
@@ -721,7 +742,8 @@ int launch_moments(const float* x, int64_t n, const double* part, int np, double
 int launch_adam_clip(float* p, const float* g, float* m, float* v, int64_t n, int* step,
                      const float* lr, float b1, float b2, float eps, float wd, float max_norm,
                      float clip_value, const int* skip, float* norm_out, hipStream_t st) {
-  const int grid = grid_for((n + 3) / 4, 2048);
+  static const int gcap = [] { const char* e = getenv("SMI_ADAM_GRID"); return e ? atoi(e) : 2048; }();
+  const int grid = grid_for((n + 3) / 4, gcap > 0 && gcap <= 2048 ? gcap : 2048);
   const bool need_norm = max_norm > 0.f || norm_out != nullptr;
   double* part = nullptr;
   if (need_norm) {
@@ -731,7 +753,18 @@ int launch_adam_clip(float* p, const float* g, float* m, float* v, int64_t n, in
     const int rc0 = check_launch("sumsq_partial_kernel");
     if (rc0) return rc0;
   }
-  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kWG), 0, st, p, g, m, v, n, step, lr, b1, b2,
+  // nontemporal loads and stores of p, g, m, v from SMI_ADAM_NT_MIN (2^24)
+  // parameters: streams read and written once per launch, past the caches.
+  // Measured (67 M parameters, tools/bench_hbm.py, one MI355X): plain 0.61 /
+  // 0.61 of HBM (clip / no clip), nontemporal stores 0.62 / 0.62, both 0.75 /
+  // 0.67.  A/B knob SMI_ADAM_NT: 0 plain, 1 stores, 2 loads, 3 both (default).
+  static const int nt_v = [] { const char* e = getenv("SMI_ADAM_NT"); return e ? atoi(e) & 3 : 3; }();
+  static const int64_t nt_min = [] {
+    const char* e = getenv("SMI_ADAM_NT_MIN"); return e ? (int64_t)atoll(e) : (int64_t)1 << 24; }();
+  const int ntv = n >= nt_min ? nt_v : 0;
+  auto kfn = ntv == 1 ? adam_kernel<1> : ntv == 2 ? adam_kernel<2> : ntv == 3 ? adam_kernel<3>
+                                                                    : adam_kernel<0>;
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(kWG), 0, st, p, g, m, v, n, step, lr, b1, b2,
                      eps, wd, max_norm, clip_value, part, need_norm ? grid : 0, skip, norm_out);
   int rc = check_launch("adam_kernel");
   if (rc) return rc;

@@ -461,19 +461,54 @@ __device__ __forceinline__ float row_kl(const float* mu0, const float* sd0, cons
   return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
 }
 
+// row_loglik with the std's reciprocal: (a - mu) * (1 / sd) instead of the
+// IEEE divide (one rounding more, within the parity envelope): the learner's
+// std is a per-column constant (reciprocal hoisted out of the row loop), the
+// behaviour policy's is per row (one v_rcp_f32 shared by every term of the
+// row that divides by it)
+template <int AT>
+__device__ __forceinline__ float row_loglik_r(const float* act, const float* mu, const float* isd,
+                                              const float* logsd, int A, float c_ll) {
+  float s = 0.f, l = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    const float u = (act[j] - mu[j]) * isd[j];
+    s += u * u;
+    l += logsd[j];
+  }
+  return (-0.5f * s - c_ll) - l;
+}
+
 // row_kl with BOTH distributions' stds fixed per column (the reference policy
 // against the learner: log(sd1 / sd0), sd0^2 and 2 sd1^2 are hoisted out of the
 // row loop as lkl, s02, den2 — the same operations in the same order, computed
 // once per workgroup instead of once per row)
 template <int AT>
 __device__ __forceinline__ float row_kl_cc(const float* mu0, const float* mu1, const float* lkl,
-                                           const float* s02, const float* den2, int A) {
+                                           const float* s02, const float* iden2, int A) {
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
     s1 += lkl[j];
     const float d = mu0[j] - mu1[j];
-    s2 += (s02[j] + d * d) / den2[j];
+    s2 += (s02[j] + d * d) * iden2[j];
+  }
+  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
+}
+
+// KL(reference || behaviour) of a row: the reference std per column (its
+// log and square hoisted), the behaviour std per row through its log (already
+// formed for the log-likelihood) and reciprocal
+template <int AT>
+__device__ __forceinline__ float row_kl_rb(const float* mu0, const float* lsd0, const float* s02,
+                                           const float* mu1, const float* lsd1, const float* isd1,
+                                           int A) {
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    s1 += lsd1[j] - lsd0[j];
+    const float d = mu0[j] - mu1[j];
+    s2 += (s02[j] + d * d) * (0.5f * (isd1[j] * isd1[j]));
   }
   return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
 }
@@ -521,13 +556,20 @@ policy_rows_stats_kernel(PolRowArgs a) {
     srsig[j] = expf(a.ref_lv[j]);
   }
   __syncthreads();
-  float sig[AM], lsig[AM], rsig[AM], lkl[AM], s02[AM], den2[AM];
+  // per-column terms of the learner std (log-likelihood, KL(ref || learner))
+  // and the reference std (KL(ref || behaviour)), hoisted out of the row loop;
+  // divisions by them become multiplications by hoisted reciprocals (one
+  // rounding more per term: row_loglik_r)
+  float sig[AM], isig[AM], lsig[AM], lkl[AM], s02[AM], iden2[AM], lrsig[AM];
 #pragma unroll
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    sig[j] = ssig[j]; lsig[j] = slsig[j]; rsig[j] = srsig[j];
-    lkl[j] = logf(sig[j] / rsig[j]);            // row_kl(rm, rsig, m, sig)'s per-column terms
-    s02[j] = rsig[j] * rsig[j];
-    den2[j] = 2.f * (sig[j] * sig[j]);
+    sig[j] = ssig[j]; lsig[j] = slsig[j];
+    const float rsig = srsig[j];
+    isig[j] = 1.f / sig[j];
+    lkl[j] = logf(sig[j] / rsig);               // row_kl(rm, rsig, m, sig)'s per-column terms
+    s02[j] = rsig * rsig;
+    iden2[j] = 1.f / (2.f * (sig[j] * sig[j]));
+    lrsig[j] = logf(rsig);
   }
   const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   double acc[PS_N];
@@ -548,12 +590,16 @@ policy_rows_stats_kernel(PolRowArgs a) {
     ld_row<AT>(bmu, rw + A, A);
     ld_row<AT>(bsd, rw + 2 * A, A);
     const float av = norm_adv_of(a, rw[3 * A]);
-    const float ex = expf(row_loglik<AT>(ac, m, sig, lsig, A, a.c_ll));
+    const float ex = expf(row_loglik_r<AT>(ac, m, isig, lsig, A, a.c_ll));
     const float lp = fmaxf(ex, 1e-5f);
+    float ibsd[AM];
 #pragma unroll
-    for (int j = 0; j < (AT > 0 ? AT : A); ++j) blsd[j] = logf(bsd[j]);
-    const float bl = fmaxf(expf(row_loglik<AT>(ac, bmu, bsd, blsd, A, a.c_ll)), 1e-5f);
-    acc[PS_KL] += (double)row_kl_cc<AT>(rm, m, lkl, s02, den2, A);
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+      blsd[j] = logf(bsd[j]);
+      ibsd[j] = __builtin_amdgcn_rcpf(bsd[j]);
+    }
+    const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
+    acc[PS_KL] += (double)row_kl_cc<AT>(rm, m, lkl, s02, iden2, A);
     if (a.mode == 0) {
       const float ratio = lp / bl;
       const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
@@ -565,7 +611,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
     }
     acc[PS_ISW] += (double)(lp / (bl + 1e-4f));
     acc[PS_BL] += (double)bl;
-    acc[PS_RBD] += (double)row_kl<AT>(rm, rsig, bmu, bsd, A);
+    acc[PS_RBD] += (double)row_kl_rb<AT>(rm, lrsig, s02, bmu, blsd, ibsd, A);
     acc[PS_RET] += (double)a.ret_tm[n];
     if constexpr (FUSE) {          // policy_rows_grad_kernel's clip branch, weight a.invN
       const float ratio = lp / bl;
@@ -576,10 +622,10 @@ policy_rows_stats_kernel(PolRowArgs a) {
       float dz[AM];
 #pragma unroll
       for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-        const float s1 = sig[j];
-        const float u = (ac[j] - m[j]) / s1;
-        const float gmu = g_ll * (u / s1);
-        const float gsd = g_ll * (u * u / s1 - 1.f / s1);
+        const float i1 = isig[j];
+        const float u = (ac[j] - m[j]) * i1;
+        const float gmu = g_ll * (u * i1);
+        const float gsd = g_ll * (u * u * i1 - i1);
         glv[j] += gsd;
         dz[j] = gmu * (1.f - m[j] * m[j]);
       }
@@ -635,15 +681,17 @@ policy_rows_grad_kernel(PolRowArgs a) {
     srsig[j] = expf(a.ref_lv[j]);
   }
   __syncthreads();
-  float sig[AM], lsig[AM], rsig[AM], inv1[AM], s1sq[AM], s1cu[AM], rs2[AM];
+  // per-column factors of the row loop, hoisted; divisions by them become
+  // multiplications by their reciprocals (as in policy_rows_stats_kernel)
+  float lsig[AM], inv1[AM], is1sq[AM], is1cu[AM], rs2[AM];
 #pragma unroll
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    sig[j] = ssig[j]; lsig[j] = slsig[j]; rsig[j] = srsig[j];
-    // per-column factors of the row loop, hoisted (same operations, same order)
-    inv1[j] = 1.f / sig[j];
-    s1sq[j] = sig[j] * sig[j];
-    s1cu[j] = sig[j] * sig[j] * sig[j];
-    rs2[j] = rsig[j] * rsig[j];
+    const float sg = ssig[j], rsig = srsig[j];
+    lsig[j] = slsig[j];
+    inv1[j] = 1.f / sg;
+    is1sq[j] = 1.f / (sg * sg);
+    is1cu[j] = 1.f / (sg * sg * sg);
+    rs2[j] = rsig * rsig;
   }
   const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   const float wsurr = a.cf[CF_SURRW], wkl = a.cf[CF_KLCOEF];
@@ -660,12 +708,16 @@ policy_rows_grad_kernel(PolRowArgs a) {
     ld_row<AT>(bmu, rw + A, A);
     ld_row<AT>(bsd, rw + 2 * A, A);
     const float av = norm_adv_of(a, rw[3 * A]);
-    const float ll = row_loglik<AT>(ac, m, sig, lsig, A, a.c_ll);
+    const float ll = row_loglik_r<AT>(ac, m, inv1, lsig, A, a.c_ll);
     const float ex = expf(ll);
     const float lp = fmaxf(ex, 1e-5f);
+    float ibsd[AM];
 #pragma unroll
-    for (int j = 0; j < (AT > 0 ? AT : A); ++j) blsd[j] = logf(bsd[j]);
-    const float bl = fmaxf(expf(row_loglik<AT>(ac, bmu, bsd, blsd, A, a.c_ll)), 1e-5f);
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+      blsd[j] = logf(bsd[j]);
+      ibsd[j] = __builtin_amdgcn_rcpf(bsd[j]);
+    }
+    const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
     float g_lp;
     if (a.mode == 0) {
       const float ratio = lp / bl;
@@ -680,14 +732,14 @@ policy_rows_grad_kernel(PolRowArgs a) {
     const float g_ll = (ex >= 1e-5f) ? g_lp * ex : 0.f;    // clamp + exp backward
 #pragma unroll
     for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-      const float s1 = sig[j];
-      const float u = (ac[j] - m[j]) / s1;
-      float gmu = g_ll * (u / s1);
-      float gsd = g_ll * (u * u / s1 - inv1[j]);
+      const float i1 = inv1[j];
+      const float u = (ac[j] - m[j]) * i1;
+      float gmu = g_ll * (u * i1);
+      float gsd = g_ll * (u * u * i1 - i1);
       if (wkl != 0.f) {
         const float d = rm[j] - m[j];
-        gmu += wkl * (-d / s1sq[j]);
-        gsd += wkl * (inv1[j] - (rs2[j] + d * d) / s1cu[j]);
+        gmu += wkl * (-d * is1sq[j]);
+        gsd += wkl * (i1 - (rs2[j] + d * d) * is1cu[j]);
       }
       glv[j] += gsd;
       dz[j] = gmu * (1.f - m[j] * m[j]);                    // tanh backward
@@ -1062,7 +1114,8 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
                           const float* b1, int h1, const float* W2, const float* b2, int h2,
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
-                          hipStream_t st, const int* skip);
+                          hipStream_t st, const int* skip, const float* vret = nullptr,
+                          float* vgrad = nullptr, float vscale = 0.f);
 int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
                           const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
@@ -1077,14 +1130,22 @@ static bool head_fused(const Head& h, const float* X, int64_t ldx) {
 // forward: X[rows][ldx] -> HA1 -> HA2 -> Y ([rows][out]); one fused launch
 // (head_kernels.hip) when the shapes allow, which with wT also writes W1^T | W2^T
 // for a fused backward of the same parameters
+// vret / vgrad / vscale: the value-loss gradient written by the fused forward
+// (out == 1); *vdone tells whether it was (the layer-GEMM path does not)
 static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, float* HA1,
-                    float* HA2, float* Y, hipStream_t st, const int* skip, float* wT = nullptr) {
+                    float* HA2, float* Y, hipStream_t st, const int* skip, float* wT = nullptr,
+                    const float* vret = nullptr, float* vgrad = nullptr, float vscale = 0.f,
+                    bool* vdone = nullptr) {
   const MlpLayout& L = h.L;
-  if (head_fused(h, X, ldx))
+  if (vdone) *vdone = false;
+  if (head_fused(h, X, ldx)) {
+    const bool ve = vgrad && h.out == 1;
+    if (vdone) *vdone = ve;
     return launch_head_fwd_fused(X, ldx, rows, h.in, h.P + L.fW1, h.P + L.fb1, h.h1, h.P + L.fW2,
                                  h.P + L.fb2, h.h2, h.P + L.fW3, h.P + L.fb3, h.out, h.tanh_out,
                                  HA1, HA2, Y, h.out, wT, wT ? wT + (int64_t)h.in * h.h1 : nullptr,
-                                 st, skip);
+                                 st, skip, ve ? vret : nullptr, ve ? vgrad : nullptr, vscale);
+  }
   const int M = (int)rows;
   RC(launch_linear_fwd(X, ldx, M, h.in, h.P + h.L.fW1, h.in, h.P + h.L.fb1, h.h1, ACT_RELU, HA1,
                        h.h1, st, skip));
@@ -1466,15 +1527,22 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_VALUE_GRAD: {
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
       if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, nullptr));
-      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr,
-                  s.wT));
-      const int nb = rnn_nblk((d.NE + 3) / 4, kRowNT);     // 4 rows per thread
+      // dV = 2 (V - R) / N: written by the head forward's epilogue, except in
+      // the last epoch, whose value_rows pass also sums the statistics of
+      // ppo.py:324-331 (and on the layer-GEMM path)
       const bool last = e == a.epoch_baseline - 1;
-      const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(value_rows_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, s.OUT, s.ret_tm, d.B, d.E,
-                         (float)(2.0 / (double)NEg), s.dOUT, last ? s.part : nullptr);
-      ktime_end(kt, KT_VALUE_ROWS, 12.0 * (double)d.NE, st);     // V, R read, dV written
-      RC(check_launch("value_rows_kernel"));
+      const float vscale = (float)(2.0 / (double)NEg);
+      bool vdone = false;
+      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr,
+                  s.wT, last ? nullptr : s.ret_tm, last ? nullptr : s.dOUT, vscale, &vdone));
+      const int nb = rnn_nblk((d.NE + 3) / 4, kRowNT);     // 4 rows per thread
+      if (!vdone) {
+        const int kt = ktime_begin(st);
+        hipLaunchKernelGGL(value_rows_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, s.OUT, s.ret_tm, d.B,
+                           d.E, vscale, s.dOUT, last ? s.part : nullptr);
+        ktime_end(kt, KT_VALUE_ROWS, 12.0 * (double)d.NE, st);     // V, R read, dV written
+        RC(check_launch("value_rows_kernel"));
+      }
       if (last) {
         hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, 5,
                            a.zbuf, nullptr);

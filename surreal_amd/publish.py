@@ -8,8 +8,10 @@ parameter_server.py:40-55).  Agents consume it with ModuleDict.load, so the
 state_dict keys and shapes are the wire format.
 
 MI355X side: the learner's parameters live in a handful of flat device
-buffers (model.py), so a snapshot is a few device-to-device copies into a
-snapshot arena, enqueued on the learner's stream right after the last
+buffers (model.py), so a snapshot is ONE gather-copy launch of those buffers
+into a snapshot arena (smi_copy_gather; one ctypes call instead of a torch
+copy per buffer: the learner thread's issue time is the eager learner's
+critical path), enqueued on the learner's stream right after the last
 learn() (stream-ordered: no host wait), followed by ONE device-to-host copy of
 the arena into pinned memory on a side stream, issued by the learner thread once
 its own post-publish host reads are done (commit()).  The D2H is a copy KERNEL
@@ -21,7 +23,8 @@ the copy because the copy reads the arena, not the parameters.  A background
 thread waits for the copy and hands the numpy dict — views of the pinned
 arena reshaped to the state_dict shapes — to the serializer, then frees the
 slot (no host-side copies: the worker holds the GIL as briefly as possible,
-since any Python it runs delays the learner thread's launches).
+since any Python it runs delays the learner thread's launches: the views of
+each slot are built once, at construction).
 """
 import base64
 import ctypes
@@ -71,6 +74,20 @@ class _Layout(object):
                 self.keys.append((name, key, boff, tuple(t.shape),
                                   torch.empty(0, dtype=t.dtype).numpy().dtype))
         self.nbytes = max(off, 256)
+        # the snapshot's gather copy, as ctypes arrays built once
+        n = len(self.storages)
+        self.c_n = n
+        self.c_src = (ctypes.c_void_p * n)(*[v.data_ptr() for v, _, _ in self.storages])
+        self.c_off = (ctypes.c_int64 * n)(*[o for _, o, _ in self.storages])
+        self.c_len = (ctypes.c_int64 * n)(*[b for _, _, b in self.storages])
+
+    def views(self, raw):
+        """{module name: {state_dict key: ndarray view}} of an arena image"""
+        out = {}
+        for name, key, boff, shape, dt in self.keys:
+            n = int(np.prod(shape)) * dt.itemsize
+            out.setdefault(name, {})[key] = raw[boff:boff + n].view(dt).reshape(shape)
+        return out
 
 
 class Snapshot(object):
@@ -98,13 +115,12 @@ class Snapshot(object):
         reused: the publisher's worker serializes from them, then frees it)."""
         self._commit_if_pending()
         self._event.wait()
-        raw = self._host.numpy()
-        out = {}
-        for name, key, boff, shape, dt in self._layout.keys:
-            n = int(np.prod(shape)) * dt.itemsize
-            v = raw[boff:boff + n].view(dt).reshape(shape)
-            out.setdefault(name, {})[key] = v.copy() if copy else v
-        return out
+        if not copy and self._slot is not None:
+            return self._slot['views']
+        views = self._layout.views(self._host.numpy())
+        if not copy:
+            return views
+        return {name: {k: v.copy() for k, v in d.items()} for name, d in views.items()}
 
 
 class DeviceParameterPublisher(object):
@@ -133,6 +149,7 @@ class DeviceParameterPublisher(object):
                        'free': threading.Event()} for _ in range(slots)]
         for sl in self.slots:
             sl['free'].set()
+            sl['views'] = self.layout.views(sl['host'].numpy())
         self.next = 0
         self._pending = None
         self._pending_lock = threading.Lock()
@@ -158,8 +175,9 @@ class DeviceParameterPublisher(object):
         slot['free'].wait()                   # the worker has copied this slot's last snapshot out
         slot['free'].clear()
         cur = torch.cuda.current_stream(self.device)
-        for view, off, nbytes in self.layout.storages:        # D2D, stream-ordered after learn()
-            slot['dev'][off:off + nbytes].copy_(view, non_blocking=True)
+        lay = self.layout                                      # D2D, stream-ordered after learn()
+        L.call('smi_copy_gather', ctypes.c_void_p(slot['dev'].data_ptr()), lay.c_src, lay.c_off,
+               lay.c_len, lay.c_n, ctypes.c_void_p(cur.cuda_stream))
         taken = torch.cuda.Event()
         taken.record(cur)
         # the D2H is issued by the worker once the snapshot's D2D has run (it

@@ -178,7 +178,8 @@ def test_publish_snapshot_bytes_match_state_dict(rnn):
     pub.close()
 
 
-def test_publish_snapshot_does_not_serialize_learn():
+@pytest.mark.parametrize('use_graph', [True, False], ids=['graph', 'eager'])
+def test_publish_snapshot_does_not_serialize_learn(use_graph):
     """The snapshot's D2D copy is stream-ordered and its D2H runs on a side
     stream, so learn() + publish with a pending snapshot costs what learn() +
     publish without a publisher costs (both run _post_publish, ppo.py:637-666,
@@ -189,17 +190,18 @@ def test_publish_snapshot_does_not_serialize_learn():
     must still beat the reference's synchronous ModuleDict.dumps in the
     learner loop (state_dict -> cpu().numpy() -> serialize, module_dict.py:
     22-35, parameter_server.py:40-55).  learn() runs as the bench runs it, one
-    hipGraph replay: an eager learn() at this batch is bound by the host issue
-    of its ~400 launches, so the publish's host bookkeeping (an event, one
-    ctypes call) lands on its critical path — 3-5 % there against 2-3 % with
-    the replay (tools/diag_publish.py, profiles/r03/ab/diag_publish_*.json)."""
+    hipGraph replay, and eager (a data-parallel rank's configuration before
+    round 4): an eager learn() at this batch is bound by the host issue of its
+    ~400 launches, so the publish's host work lands on its critical path (it is
+    one gather launch, one event and one ctypes call for the D2H; the worker's
+    views are built once per slot)."""
     import time
     from surreal_amd.publish import binary_hash
     lc = ppo_config(B=256, T=25, mode='adapt', use_z_filter=True, hidden=(300, 200), lam=1.0,
                     rnn=True, rnn_hidden=100, horizon=5)
     lc.parameter_publish.exp_interval = lc.replay.batch_size      # publish after every learn()
     D, A, Hd = 42, 8, 100
-    learner = PPOLearner(lc, env_config(D, A), seed=1, use_graph=True)
+    learner = PPOLearner(lc, env_config(D, A), seed=1, use_graph=use_graph)
     batch = synthetic.to_device(synthetic.ppo_batch(256, 25, D, A, seed=3, rnn_hidden=Hd), DEV)
     got = []
     fast = DeviceParameterPublisher(learner.module_dict(), sink=lambda b, i: got.append(i['hash']),

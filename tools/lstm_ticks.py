@@ -28,15 +28,21 @@ def main():
     learner = PPOLearner(lc, env_config(D, A), seed=1, device='cuda')
     batch = synthetic.to_device(synthetic.ppo_batch(B, T, D, A, seed=0, rnn_hidden=100), 'cuda')
     lib = L.lib()
-    lib.smi_lstm_phase_ticks.argtypes = [ctypes.c_void_p]
-    buf = (ctypes.c_ulonglong * 8)()
+    # the MFMA forms' and the VALU recurrence's ticks (two objects: build.py UNITS)
+    fns = [lib.smi_lstm_phase_ticks, lib.smi_lstm_v_phase_ticks]
+    for f in fns:
+        f.argtypes = [ctypes.c_void_p]
+    bufs = [(ctypes.c_ulonglong * 8)() for _ in fns]
     learner.learn(batch)
     torch.cuda.synchronize()
-    lib.smi_lstm_phase_ticks(ctypes.cast(buf, ctypes.c_void_p))      # reset
+    for f, b in zip(fns, bufs):
+        f(ctypes.cast(b, ctypes.c_void_p))      # reset
     for _ in range(K):
         learner.learn(batch)
     torch.cuda.synchronize()
-    lib.smi_lstm_phase_ticks(ctypes.cast(buf, ctypes.c_void_p))
+    for f, b in zip(fns, bufs):
+        f(ctypes.cast(b, ctypes.c_void_p))
+    buf = [bufs[0][i] + bufs[1][i] for i in range(8)]
     E = T - 5 + 1
     runs = learner.last_stats()['epochs_run']
     fwd_steps = K * ((T + 1) + E + (runs + 1) * E + 10 * E)
