@@ -382,23 +382,30 @@ struct PolRowArgs {
   float invN;
 };
 
-__device__ inline float norm_adv_of(const PolRowArgs& a, float raw) {
-  if (!a.norm_adv || !a.moments) return raw;
-  // ppo.py:402-405: (adv - mean) / max(std, 1e-4), std unbiased over all B*E
-  const double n = a.moments[2];
-  const double mean = a.moments[0] / n;
-  const double var = (a.moments[1] - n * mean * mean) / (n - 1.0);
-  const float sd = (float)sqrt(var > 0.0 ? var : 0.0);
-  return (raw - (float)mean) / fmaxf(sd, 1e-4f);
-}
+// ppo.py:402-405: (adv - mean) / max(std, 1e-4), std unbiased over all B*E;
+// the fp64 moments are turned into (mean_f, max(std_f, 1e-4)) once per thread
+// (AdvNorm), outside the row loops: per row only the fp32 subtract and divide
+struct AdvNorm {
+  bool on; float mean, den;
+  __device__ explicit AdvNorm(const PolRowArgs& a) : on(a.norm_adv && a.moments), mean(0.f), den(1.f) {
+    if (!on) return;
+    const double n = a.moments[2];
+    const double m = a.moments[0] / n;
+    const double var = (a.moments[1] - n * m * m) / (n - 1.0);
+    mean = (float)m;
+    den = fmaxf((float)sqrt(var > 0.0 ? var : 0.0), 1e-4f);
+  }
+  __device__ float operator()(float raw) const { return on ? (raw - mean) / den : raw; }
+};
 
 // optional export of the advantages as the epochs use them and the returns,
 // both [B][E] batch-major (smi_ppo_rnn_args.adv_out / ret_out)
 __global__ void __launch_bounds__(kWG)
 adv_export_kernel(PolRowArgs a, float* __restrict__ adv_out, float* __restrict__ ret_out) {
   const int64_t n = (int64_t)a.B * a.E;
+  const AdvNorm nadv(a);
   for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < n; e += (int64_t)gridDim.x * kWG) {
-    if (adv_out) adv_out[e] = norm_adv_of(a, a.adv[e]);
+    if (adv_out) adv_out[e] = nadv(a.adv[e]);
     if (ret_out) ret_out[e] = a.ret[e];
   }
 }
@@ -581,6 +588,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
     for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
   }
   const int64_t N = (int64_t)a.E * a.B;
+  const AdvNorm nadv(a);
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
     float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM];
     ld_row<AT>(m, a.mu + n * A, A);
@@ -589,7 +597,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
     ld_row<AT>(ac, rw, A);
     ld_row<AT>(bmu, rw + A, A);
     ld_row<AT>(bsd, rw + 2 * A, A);
-    const float av = norm_adv_of(a, rw[3 * A]);
+    const float av = nadv(rw[3 * A]);
     const float ex = expf(row_loglik_r<AT>(ac, m, isig, lsig, A, a.c_ll));
     const float lp = fmaxf(ex, 1e-5f);
     float ibsd[AM];
@@ -699,6 +707,7 @@ policy_rows_grad_kernel(PolRowArgs a) {
 #pragma unroll
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
   const int64_t N = (int64_t)a.E * a.B;
+  const AdvNorm nadv(a);
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
     float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM], dz[AM];
     ld_row<AT>(m, a.mu + n * A, A);
@@ -707,7 +716,7 @@ policy_rows_grad_kernel(PolRowArgs a) {
     ld_row<AT>(ac, rw, A);
     ld_row<AT>(bmu, rw + A, A);
     ld_row<AT>(bsd, rw + 2 * A, A);
-    const float av = norm_adv_of(a, rw[3 * A]);
+    const float av = nadv(rw[3 * A]);
     const float ll = row_loglik_r<AT>(ac, m, inv1, lsig, A, a.c_ll);
     const float ex = expf(ll);
     const float lp = fmaxf(ex, 1e-5f);
