@@ -93,9 +93,9 @@ struct RnnScratch {
   // W1^T | W2^T of the head a phase's fused forward wrote for its backward
   float *wT;
   float *values, *adv, *ret, *refmu, *lvpart;
-  // time-major per-row inputs of the row kernels, packed once per learn:
-  // rowin[n] = {actions (A) | behave mu, sigma (2A) | raw advantage | pad},
-  // n = t*B + b, stride row_w(A); ret_tm[n] the window return
+  // time-major per-row inputs of the row kernels, packed once per learn,
+  // FIELD-major: rowin[f * NE + n], f = {actions (A) | behave mu, sigma (2A) |
+  // raw advantage}, n = t*B + b; ret_tm[n] the window return
   float *rowin, *ret_tm;
   float *A1, *A2, *dA2, *dF, *cpart;        // pixel stem (empty without one)
   double *part, *gaepart;
@@ -104,8 +104,8 @@ struct RnnScratch {
 };
 
 static inline int64_t al64(int64_t n) { return (n + 63) & ~(int64_t)63; }
-// packed row width: 3A + 1 floats rounded up to 16 bytes
-__host__ __device__ inline int row_w(int A) { return (3 * A + 1 + 3) & ~3; }
+// fields of a packed row: A actions, 2A behaviour parameters, the advantage
+__host__ __device__ inline int row_w(int A) { return 3 * A + 1; }
 
 __host__ __device__ inline int rnn_nblk(int64_t rows, int nt = kWG) {
   // at most 1024 four-wave blocks' worth of waves (4096 one-wave blocks)
@@ -367,7 +367,7 @@ struct PolRowArgs {
   const float* behave;    // [B][T][2A]
   const float* adv;       // [B][E] raw
   const float* ret;       // [B][E]
-  const float* rowin;     // [NE][row_w(A)] time-major {actions | behave | raw adv}
+  const float* rowin;     // [row_w(A)][NE] field-major {actions | behave | raw adv}
   const float* ret_tm;    // [NE] time-major returns
   const double* moments;  // [3] global (sum, sumsq, n) of adv, or null (no norm)
   int norm_adv;
@@ -520,25 +520,33 @@ __device__ __forceinline__ float row_kl_rb(const float* mu0, const float* lsd0, 
   return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
 }
 
-// rowin / ret_tm from the batch-major inputs (once per learn): the per-row
-// kernels of every epoch then read whole rows in time-major order (coalesced)
-// instead of A- and E-strided gathers from [B][T][.] / [B][E]
+// rowin / ret_tm from the batch-major inputs (once per learn), field-major:
+// the per-row kernels of every epoch give a thread one row, so lane i reads
+// field f of row n0 + i and one load instruction covers 64 consecutive floats
+// (a row-major 100-byte row per lane made every load instruction touch ~56
+// cache lines: the row kernels waited on the texture addresser, PMC TA_BUSY)
 __global__ void __launch_bounds__(kWG)
 row_pack_kernel(PolRowArgs a, float* __restrict__ rowin, float* __restrict__ ret_tm) {
-  const int A = a.A, RW = row_w(A);
-  const int N = a.E * a.B;
-  for (int n = blockIdx.x * kWG + threadIdx.x; n < N; n += gridDim.x * kWG) {
-    const int t = n / a.B, b = n - t * a.B;
+  const int A = a.A;
+  const int64_t N = (int64_t)a.E * a.B;
+  for (int64_t n = (int64_t)blockIdx.x * kWG + threadIdx.x; n < N; n += (int64_t)gridDim.x * kWG) {
+    const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
     const int64_t src = (int64_t)b * a.T + t;
-    float* o = rowin + (int64_t)n * RW;
     const float* ac = a.actions + src * A;
     const float* bh = a.behave + src * 2 * A;
-    for (int j = 0; j < A; ++j) o[j] = ac[j];
-    for (int j = 0; j < 2 * A; ++j) o[A + j] = bh[j];
-    o[3 * A] = a.adv[(int64_t)b * a.E + t];
-    for (int j = 3 * A + 1; j < RW; ++j) o[j] = 0.f;
+    for (int j = 0; j < A; ++j) rowin[j * N + n] = ac[j];
+    for (int j = 0; j < 2 * A; ++j) rowin[(A + j) * N + n] = bh[j];
+    rowin[3 * A * N + n] = a.adv[(int64_t)b * a.E + t];
     ret_tm[n] = a.ret[(int64_t)b * a.E + t];
   }
+}
+
+// field j .. j + AT - 1 of row n from the field-major rowin
+template <int AT>
+__device__ __forceinline__ void ld_fields(float* dst, const float* __restrict__ rowin, int64_t N,
+                                          int64_t n, int f0, int A) {
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) dst[j] = rowin[(int64_t)(f0 + j) * N + n];
 }
 
 // forward statistics of the policy over the E*B rows (ppo.py:203-224,
@@ -556,7 +564,6 @@ policy_rows_stats_kernel(PolRowArgs a) {
   __shared__ double scr[NT / 64][PS_N];
   __shared__ float gls[FUSE ? NT / 64 : 1][32];
   const int A = AT > 0 ? AT : a.A;
-  const int RW = row_w(A);
   for (int j = threadIdx.x; j < A; j += NT) {
     ssig[j] = expf(a.lv[j]);                 // builders.py:127 std = exp(log_var)
     slsig[j] = logf(ssig[j]);                // std0.log() of ppo_net.py:40
@@ -593,11 +600,10 @@ policy_rows_stats_kernel(PolRowArgs a) {
     float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM];
     ld_row<AT>(m, a.mu + n * A, A);
     ld_row<AT>(rm, a.refmu + n * A, A);
-    const float* rw = a.rowin + n * RW;
-    ld_row<AT>(ac, rw, A);
-    ld_row<AT>(bmu, rw + A, A);
-    ld_row<AT>(bsd, rw + 2 * A, A);
-    const float av = nadv(rw[3 * A]);
+    ld_fields<AT>(ac, a.rowin, N, n, 0, A);
+    ld_fields<AT>(bmu, a.rowin, N, n, A, A);
+    ld_fields<AT>(bsd, a.rowin, N, n, 2 * A, A);
+    const float av = nadv(a.rowin[(int64_t)(3 * A) * N + n]);
     const float ex = expf(row_loglik_r<AT>(ac, m, isig, lsig, A, a.c_ll));
     const float lp = fmaxf(ex, 1e-5f);
     float ibsd[AM];
@@ -682,7 +688,6 @@ policy_rows_grad_kernel(PolRowArgs a) {
   __shared__ float ssig[32], slsig[32], srsig[32];
   __shared__ float gls[NT / 64][32];
   const int A = AT > 0 ? AT : a.A;
-  const int RW = row_w(A);
   for (int j = threadIdx.x; j < A; j += NT) {
     ssig[j] = expf(a.lv[j]);
     slsig[j] = logf(ssig[j]);
@@ -712,11 +717,10 @@ policy_rows_grad_kernel(PolRowArgs a) {
     float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM], dz[AM];
     ld_row<AT>(m, a.mu + n * A, A);
     ld_row<AT>(rm, a.refmu + n * A, A);
-    const float* rw = a.rowin + n * RW;
-    ld_row<AT>(ac, rw, A);
-    ld_row<AT>(bmu, rw + A, A);
-    ld_row<AT>(bsd, rw + 2 * A, A);
-    const float av = nadv(rw[3 * A]);
+    ld_fields<AT>(ac, a.rowin, N, n, 0, A);
+    ld_fields<AT>(bmu, a.rowin, N, n, A, A);
+    ld_fields<AT>(bsd, a.rowin, N, n, 2 * A, A);
+    const float av = nadv(a.rowin[(int64_t)(3 * A) * N + n]);
     const float ll = row_loglik_r<AT>(ac, m, inv1, lsig, A, a.c_ll);
     const float ex = expf(ll);
     const float lp = fmaxf(ex, 1e-5f);
