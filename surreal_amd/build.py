@@ -64,7 +64,7 @@ VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             # MFMAs without the operand stream / the stream without the MFMAs
             'dwdiag_mfma': ['-DSMI_DWD_DIAG=1'], 'dwdiag_load': ['-DSMI_DWD_DIAG=2'],
             # per-workgroup start / end clock of the grouped dW launch (product results)
-            'dwtrace': ['-DSMI_DWD_DIAG=3'],
+            'dwtrace': ['-DSMI_DWD_DIAG=3'], 'dwtrace_mfma': ['-DSMI_DWD_DIAG=1', '-DSMI_DWD_TRACE=1'],
             # test-only fault injection (tests/negative_controls.py): the parity
             # checks must FAIL on this build's deliberate departures
             'fault': ['-DSMI_FAULT_INJECTION']}

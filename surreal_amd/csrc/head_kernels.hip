@@ -377,6 +377,13 @@ head_fwd_kernel(HeadFwdArgs a) {
     float e2[RT][NT2][4];
     {   // layer 1: HA1 = relu(X W1^T + b1)
       f32x4 acc[RT][NT1];
+      // every load before this point has landed (the X rows went through
+      // registers into LDS), but on the path where this thread staged no X
+      // the waitcnt pass still counts the stream's first chunks and the bias
+      // loads in flight, and that merged state set the k loop's header waits
+      // to vmcnt(4) / vmcnt(1) instead of the ring depth (vmcnt(9..5)): an
+      // explicit vmcnt(0) (expcnt / lgkmcnt left at their maxima) clears it
+      __builtin_amdgcn_s_waitcnt(0x0F70);
       hc_run<NT1, RT>(S1, s0, a.ld0, acc);
       HEAD_TICK(0, 1);                            // layer 1 k loop
       S2.init(a.W2, a.h1, a.h1, a.h2, wave, 4, 0, 1);     // layer 2's stream, in flight

@@ -631,6 +631,11 @@ gemm_dw128_kernel(GemmArgs g) {
 #ifndef SMI_DWD_DIAG
 #define SMI_DWD_DIAG 0
 #endif
+// per-workgroup clock trace of the grouped launch (bench_dwgroup only; the
+// `dwtrace` builds), independent of the DIAG mode
+#ifndef SMI_DWD_TRACE
+#define SMI_DWD_TRACE (SMI_DWD_DIAG == 3)
+#endif
 #ifndef SMI_DWD_P
 #define SMI_DWD_P 4
 #endif
@@ -730,13 +735,19 @@ __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nst
     }
   }
   float4 av[DWD_P], bv[DWD_P][NH];
+  // global (addrspace 1) loads spelled out: with the prologue pinned below the
+  // compiler no longer infers the address space and emits flat loads, which
+  // also count against lgkmcnt
+  using gf4 = const __attribute__((address_space(1))) f32x4;
+  using gf1 = const __attribute__((address_space(1))) float;
+  auto f4 = [](const f32x4 x) { return float4{x[0], x[1], x[2], x[3]}; };
   auto load = [&](int p) {
-    if constexpr (MT == 4) av[p] = *reinterpret_cast<const float4*>(pa);
-    else av[p].x = *pa;
+    if constexpr (MT == 4) av[p] = f4(*(gf4*)pa);
+    else av[p].x = *(gf1*)pa;
     pa += sa;
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
-      bv[p][h] = *reinterpret_cast<const float4*>(pb[h]);
+      bv[p][h] = f4(*(gf4*)pb[h]);
       pb[h] += sb[h];
     }
   };
@@ -757,8 +768,15 @@ __device__ __forceinline__ void dwd_main_fast(const GemmArgs& g, int rw, int nst
     }
 #endif
   };
+  // the prologue's loads are pinned in step order too: the loop header's
+  // vmcnt is the merge of the preheader and the back edge, so one prologue
+  // load issued out of order (the scheduler put b0 seventh of eight) made
+  // every iteration wait at vmcnt(1), i.e. on the loads just issued
 #pragma unroll
-  for (int p = 0; p < DWD_P; ++p) load(p);
+  for (int p = 0; p < DWD_P; ++p) {
+    load(p);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // sched_barrier pins each refill right behind the MFMAs of the step it
   // replaces: without it the scheduler sinks all DWD_P refills to the end of
   // the unrolled body and the next iteration waits on them (vmcnt(9..0)), i.e.
@@ -968,34 +986,39 @@ struct DwGroup {
 #endif
 constexpr int DWG_NT = SMI_DWG_NT;
 
-#if SMI_DWD_DIAG == 3
+#if SMI_DWD_TRACE
 // diagnostic (bench_dwgroup only): per-workgroup {start, end, HW_ID, XCC_ID |
-// group << 8} in 100 MHz wall-clock ticks, read back by smi_diag_dw_trace
+// group << 8} in 100 MHz wall-clock ticks plus {start, end} of the shader
+// clock (clock64: the in-kernel clock is its delta over the wall delta),
+// read back by smi_diag_dw_trace
 constexpr int kDwTraceMax = 8192;
-__device__ unsigned long long g_dw_trace[kDwTraceMax][4];
+__device__ unsigned long long g_dw_trace[kDwTraceMax][6];
 extern "C" int smi_diag_dw_trace(void* dst, int n) {
   if (n > kDwTraceMax) n = kDwTraceMax;
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dw_trace), (size_t)n * 32, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dw_trace), (size_t)n * 48, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
 }
 #endif
 
 template <int WV>
 __global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWG_OCC : 1)
 gemm_dwd_group_kernel(DwGroup G) {
-#if SMI_DWD_DIAG == 3
-  const unsigned long long t_start = wall_clock64();
+#if SMI_DWD_TRACE
+  const unsigned long long t_start = wall_clock64(), c_start = clock64();
   struct TraceEnd {
-    unsigned long long t0; int gi = 0;
+    unsigned long long t0, c0; int gi = 0, rows = 0;
     __device__ ~TraceEnd() {
       __syncthreads();
       if (threadIdx.x == 0 && blockIdx.x < kDwTraceMax) {
         g_dw_trace[blockIdx.x][0] = t0;
         g_dw_trace[blockIdx.x][1] = wall_clock64();
         g_dw_trace[blockIdx.x][2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        g_dw_trace[blockIdx.x][3] = __builtin_amdgcn_s_getreg((31 << 11) | 20) | (gi << 8);
+        g_dw_trace[blockIdx.x][3] = __builtin_amdgcn_s_getreg((31 << 11) | 20) | (gi << 8) |
+                                    ((unsigned long long)rows << 16);
+        g_dw_trace[blockIdx.x][4] = c0;
+        g_dw_trace[blockIdx.x][5] = clock64();
       }
     }
-  } trace_end{t_start};
+  } trace_end{t_start, c_start};
 #endif
   extern __shared__ float4 dwd_red[];
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -1007,7 +1030,7 @@ gemm_dwd_group_kernel(DwGroup G) {
   int gi = 0;
   while (gi + 1 < G.n && w >= G.wg0[gi + 1]) ++gi;
   const GemmArgs& g = G.g[gi];
-#if SMI_DWD_DIAG == 3
+#if SMI_DWD_TRACE
   trace_end.gi = gi;
 #endif
   if (g.skip && g.skip[0] != 0) return;
@@ -1016,6 +1039,10 @@ gemm_dwd_group_kernel(DwGroup G) {
   ti.nt = local % gn;
   ti.mt = (local / gn) % gm;
   ti.z = local / (gn * gm);
+#if SMI_DWD_TRACE
+  trace_end.rows = (min(g.K, (ti.z + 1) * g.kchunk) - ti.z * g.kchunk) |
+                   ((G.narrow[gi] && ti.mt == gm - 1) << 16) | (G.vec[gi] << 17);
+#endif
   if (G.narrow[gi] && ti.mt == gm - 1) {
     // a tail of <= 16 gradient rows (M 8 / 200 / 400 at C3) on one 16-wide
     // m sub-tile instead of a 64-wide tile that is >= 75 % padding
@@ -1468,8 +1495,15 @@ int dw_group_flush(hipStream_t st) {
   double r0 = work / target;                        // cost-rows per workgroup
   int64_t need = 0;
   int64_t kcs[kDwGroupMax];
-  for (int pass = 0; pass < 8; ++pass) {            // grow the slabs until the partials fit
+  // slab lengths are rounded up to whole prefetch windows, so the workgroup
+  // count can land a few above the target; in whole rounds every extra
+  // workgroup is a second round of its own (the C3 launch was 769 for 768
+  // slots: the last workgroup started at 59 us and set the span), so the
+  // cost-rows per workgroup grow in small steps until the count fits
+  const bool rounds_fit = !fixed_target && target >= slots;
+  for (int pass = 0; pass < 400; ++pass) {
     need = 0;
+    int64_t wgs = 0;
     for (int i = 0; i < G.n; ++i) {
       const GemmArgs& g = G.g[i];
       int64_t S = (int64_t)(g.K * cost[i] / r0 + 0.5);
@@ -1478,10 +1512,13 @@ int dw_group_flush(hipStream_t st) {
       if (kc < 2 * rs) kc = 2 * rs;                 // >= 8 MFMA steps per wave
       if (kc >= g.K) kc = ((int64_t)g.K + rs - 1) / rs * rs;
       kcs[i] = kc;
-      need += (int64_t)((g.K + kc - 1) / kc) * g.M * g.N;
+      const int64_t s_i = (g.K + kc - 1) / kc;
+      need += s_i * g.M * g.N;
+      wgs += s_i * tiles[i];
     }
-    if (need <= cap) break;
-    r0 *= 2.0;
+    if (need > cap) { r0 *= 2.0; continue; }         // grow the slabs until the partials fit
+    if (rounds_fit && wgs > target && wgs <= 2 * target) { r0 *= 1.005; continue; }
+    break;
   }
   float* base = workspace_f32(need);
   if (!base) return set_error(SMI_E_ARG, "gemm: workspace too small for the grouped dW partials");

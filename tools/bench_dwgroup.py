@@ -75,25 +75,46 @@ def main():
     torch.cuda.synchronize()
     t = sorted(s.elapsed_time(e) for s, e in ev)
     ms = t[len(t) // 2]
-    if os.environ.get('SMI_LIB_VARIANT') == 'dwtrace':
+    if (os.environ.get('SMI_LIB_VARIANT') or '').startswith('dwtrace'):
         # one more phase, then the per-workgroup clock trace of its dW launch
         import ctypes
         import numpy as np
         phase()
         torch.cuda.synchronize()
-        buf = np.zeros((8192, 4), dtype=np.uint64)
+        buf = np.zeros((8192, 6), dtype=np.uint64)
         n = L.lib().smi_diag_dw_trace(ctypes.c_void_p(buf.ctypes.data), 8192)
         tr = buf[:n]
         tr = tr[tr[:, 1] > 0]
         t0 = tr[:, 0].min()
         st_, en = (tr[:, 0] - t0) / 100.0, (tr[:, 1] - t0) / 100.0      # us (100 MHz)
         dur = en - st_
-        gi = (tr[:, 3] >> 8).astype(int)
+        gi = ((tr[:, 3] >> 8) & 0xFF).astype(int)
+        rows = ((tr[:, 3] >> 16) & 0xFFFF).astype(int)
+        narrow = ((tr[:, 3] >> 32) & 1).astype(int)
+        vec = ((tr[:, 3] >> 33) & 3).astype(int)
         xcc = (tr[:, 3] & 0xF).astype(int)
         cu = ((tr[:, 2] >> 8) & 0xF).astype(int) + 16 * ((tr[:, 2] >> 13) & 0x7).astype(int)
         grid = np.arange(0.0, float(en.max()) + 1.0, 1.0)
         conc = [int(((st_ <= x) & (en > x)).sum()) for x in grid]
-        out = {'trace_wgs': int(len(tr)), 'span_us': round(float(en.max()), 1),
+        clk = (tr[:, 5] - tr[:, 4]).astype(np.float64) / np.maximum(dur, 1e-3) / 1e3   # GHz
+        # residency: workgroups per CU at 20 us, and durations by that count
+        key = xcc * 64 + cu
+        at = (st_ <= 20.0) & (en > 20.0)
+        per_cu = np.bincount(key[at], minlength=512)
+        cnt = per_cu[key]
+        # work per workgroup in full-tile rows (narrow tiles at 0.4), and us per 1000 of them
+        work = rows * np.where(narrow == 1, 0.4, 1.0)
+        out_extra = {
+            'wgs_per_cu_at_20us_hist': {int(k): int(v) for k, v in enumerate(np.bincount(per_cu[per_cu > 0]))},
+            'dur_med_by_cu_count': {int(k): round(float(np.median(dur[at & (cnt == k)])), 1)
+                                    for k in np.unique(cnt[at])},
+            'slab_rows_by_group': {int(k): sorted(set(int(r) for r in rows[gi == k]))[:4] for k in np.unique(gi)},
+            'us_per_krow_p10_50_90': [round(float(np.percentile(1e3 * dur / np.maximum(work, 1), q)), 2)
+                                      for q in (10, 50, 90)],
+            'vec_by_group': {int(k): int(np.median(vec[gi == k])) for k in np.unique(gi)},
+            'narrow_wgs': int(narrow.sum())}
+        out = {**out_extra, 'clock_ghz_p10_50_90': [round(float(np.percentile(clk, q)), 3) for q in (10, 50, 90)],
+               'trace_wgs': int(len(tr)), 'span_us': round(float(en.max()), 1),
                'dur_us_p10_50_90_max': [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90, 100)],
                'start_us_p50_90_max': [round(float(np.percentile(st_, q)), 1) for q in (50, 90, 100)],
                'per_group_dur_med': {int(k): round(float(np.median(dur[gi == k])), 1) for k in np.unique(gi)},
