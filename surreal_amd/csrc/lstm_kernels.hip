@@ -591,6 +591,10 @@ lstm_bwd_reg_kernel(LstmBwdArgs a) {
 // (ceil(H/64) groups of 64) and K = 4H split over the waves of a group; the
 // partial sums meet in LDS and are added in a fixed order by the cell threads.
 constexpr int LR4 = 4;
+#ifndef SMI_LSTM_HQ
+#define SMI_LSTM_HQ 4
+#endif
+constexpr int LSTM_HQ = SMI_LSTM_HQ;    // h float4 LDS reads in flight (forward r4)
 
 __device__ __forceinline__ f32x4 mfma4x64(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 4, 0, 0);
@@ -637,13 +641,14 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
   const bool xown = KX > 0 && tid < LR4 * KXS;
   const int64_t xoff0 = (int64_t)min(r0 + xr, B - 1) * a.ldx + min(xk, a.din - 1);
   const bool xval = xk < a.din;
-  auto xload = [&](int t) -> float {
-    const float v = a.x[(int64_t)t * B * a.ldx + xoff0];
-    return xval ? v : 0.f;
-  };
+  // the raw value (clamped address): the zero for k >= din is selected when it
+  // is written to LDS a step later, so the load stays in flight across the
+  // step (a select right after the load made the compiler wait vmcnt(0) on it
+  // in every step, the x fetch latency on the recurrence's critical path)
+  auto xload = [&](int t) -> float { return a.x[(int64_t)t * B * a.ldx + xoff0]; };
   float xnext = 0.f;
   if constexpr (KX > 0) {
-    if (xown && a.S > 0) xS[0][xr * KXS + xk] = xload(0);
+    if (xown && a.S > 0) xS[0][xr * KXS + xk] = xval ? xload(0) : 0.f;
     if (xown && a.S > 1) xnext = xload(1);
   }
   // cell owned by this thread: (crow, cunit)
@@ -706,17 +711,32 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
     float* hn = hS[(t + 1) & 1];
     if (cact) {
       const float4* hr = reinterpret_cast<const float4*>(hp + (lane & 3) * KP);
+      // h_{t-1} through a ring of LSTM_HQ float4 LDS reads in flight (the
+      // compiler's own schedule kept one read ahead, so every 4 MFMAs (32
+      // cycles) waited out an LDS round trip); the same MFMAs per accumulator
+      // in the same k order: float4 j feeds acc[4 (j & 1) .. + 3]
+      constexpr int NQ = KP / 4;
+      float4 q[LSTM_HQ];
 #pragma unroll
-      for (int k8 = 0; k8 < KP / 8; ++k8) {
-        const float4 u = hr[2 * k8], v = hr[2 * k8 + 1];
-        acc[0] = mfma4x64(u.x, w[8 * k8 + 0], acc[0]);
-        acc[1] = mfma4x64(u.y, w[8 * k8 + 1], acc[1]);
-        acc[2] = mfma4x64(u.z, w[8 * k8 + 2], acc[2]);
-        acc[3] = mfma4x64(u.w, w[8 * k8 + 3], acc[3]);
-        acc[4] = mfma4x64(v.x, w[8 * k8 + 4], acc[4]);
-        acc[5] = mfma4x64(v.y, w[8 * k8 + 5], acc[5]);
-        acc[6] = mfma4x64(v.z, w[8 * k8 + 6], acc[6]);
-        acc[7] = mfma4x64(v.w, w[8 * k8 + 7], acc[7]);
+      for (int j = 0; j < LSTM_HQ; ++j) q[j] = hr[j];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const float4 u = q[j % LSTM_HQ];
+        const int ab = (j & 1) * 4;
+        acc[ab + 0] = mfma4x64(u.x, w[4 * j + 0], acc[ab + 0]);
+        acc[ab + 1] = mfma4x64(u.y, w[4 * j + 1], acc[ab + 1]);
+        acc[ab + 2] = mfma4x64(u.z, w[4 * j + 2], acc[ab + 2]);
+        acc[ab + 3] = mfma4x64(u.w, w[4 * j + 3], acc[ab + 3]);
+        if (j + LSTM_HQ < NQ) q[j % LSTM_HQ] = hr[j + LSTM_HQ];
+      }
+      // pin that schedule (left alone, the scheduler shrinks the ring back to
+      // one read for register pressure): the ring's first reads, then per
+      // float4 its 4 MFMAs and the read that refills its slot
+      __builtin_amdgcn_sched_group_barrier(0x100, LSTM_HQ, 0);
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        if (j + LSTM_HQ < NQ) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
       const f32x4 sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
                         ((acc[4] + acc[5]) + (acc[6] + acc[7]));
@@ -730,7 +750,7 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
       }
     }
     if constexpr (KX > 0) {   // x_{t+1} into the other buffer, x_{t+2} in flight
-      if (xown && t + 1 < a.S) xS[(t + 1) & 1][xr * KXS + xk] = xnext;
+      if (xown && t + 1 < a.S) xS[(t + 1) & 1][xr * KXS + xk] = xval ? xnext : 0.f;
       if (xown && t + 2 < a.S) xnext = xload(t + 2);
     }
     LSTM_TICK(0);
