@@ -55,7 +55,7 @@ VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             # fused-head weight ring depth A/B (product: 2)
             'hcd3': ['-DSMI_HC_DEPTH=3'], 'hcd4': ['-DSMI_HC_DEPTH=4'],
             # grouped dW tile A/B: 64 x 128 tiles at 2 waves per SIMD (round 2)
-            'dwg8': ['-DSMI_DWG_NT=8'], 'dwgocc4': ['-DSMI_DWG_OCC=4'],   # (occupancy 4: 122 us)
+            'dwg8': ['-DSMI_DWG_NT=8'], 'dwgocc4': ['-DSMI_DWG_OCC=4'], 'dwgocc2': ['-DSMI_DWG_OCC=2'],   # (occupancy 4: 122 us)
             # VALU recurrence: LDS reads per pipelined chunk (product: 4)
             'vc2': ['-DSMI_LSTM_VC=2'], 'vc8': ['-DSMI_LSTM_VC=8'],
             # VALU recurrence dot products on v_pk_fma_f32 (product: scalar FMAs)

@@ -54,6 +54,18 @@ __host__ __device__ inline int64_t lds_img_bytes(const CnnGeom& g) { return (g.i
 // waves at 176: 132 vs 143 us per 2688-image forward (tools/bench_cnn.py).
 // Three stacked RGB frames (C = 9, DDPG's frame_stacks = 3, ddpg_configs.py:
 // 114): the 144 conv-1 weight registers need one wave per SIMD.
+// per-thread 16-byte chunk counts of an 84 x 84 frame's staging (image, A1,
+// dA2), register arrays of the forward's batched image loads and the
+// backward's next-image prefetch (larger frames: a tail loop / PF off)
+#ifndef SMI_CNN_FWD_KB
+#define SMI_CNN_FWD_KB 6
+#endif
+template <int C> struct CnnPf {
+  static constexpr int KI = C <= 3 ? 6 : 16;     // uint4 of the uint8 image
+  static constexpr int KA = 7;                   // float4 of A1 (16 x P1)
+  static constexpr int KD = 3;                   // float4 of dA2 (flat)
+};
+
 template <int C>
 __global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(C <= 3 ? 3 : 1, C <= 3 ? 3 : 1)))
 cnn_fwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t rows,
@@ -83,11 +95,23 @@ cnn_fwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
   const int HW = H * W;
 
   for (int64_t n = blockIdx.x; n < rows; n += gridDim.x) {
-    {
-      const uint4* src = reinterpret_cast<const uint4*>(pix_of(pr, n));
-      uint4* dst = reinterpret_cast<uint4*>(img);
+    {   // all of a thread's image loads first, then its LDS stores: one
+        // memory round trip per image instead of one per 16-byte chunk
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      // (batches of KB chunks: the RGB kernel's 3-waves/SIMD register budget
+      // spills weights with more staging registers live)
+      constexpr int KB = SMI_CNN_FWD_KB;
+      const u32x4* src = reinterpret_cast<const u32x4*>(pix_of(pr, n));
+      u32x4* dst = reinterpret_cast<u32x4*>(img);
       const int nv = (int)(g.img >> 4);
-      for (int i = tid; i < nv; i += kWG) dst[i] = src[i];
+      for (int i0 = tid; i0 < nv; i0 += KB * kWG) {
+        u32x4 v[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) v[k] = src[min(i0 + k * kWG, nv - 1)];
+#pragma unroll
+        for (int k = 0; k < KB; ++k)
+          if (i0 + k * kWG < nv) dst[i0 + k * kWG] = v[k];
+      }
     }
     __syncthreads();
     // ---- conv 1: two pixel tiles (two independent MFMA chains) per pass
@@ -174,8 +198,15 @@ cnn_fwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
 //       (y % 2, x % 2) = (w >> 1, w & 1); its taps ky = py + {0,2},
 //       kx = px + {0,2} are all dense: M = positions, N = 16, K = 32 x 4 taps
 //   (d) dW1[co][k] += sum_p dA1[co][p] * col(img/255)[p][k]  M=16 N=64C K=P1
-template <int C>
-__global__ void __launch_bounds__(kWG)
+// Next-image prefetch (PF): the image, A1 and dA2 of the workgroup's next
+// image are loaded into registers (clamped addresses, unconditional loads)
+// right after this image's staging barrier and written to LDS at the top of
+// the next iteration, so their latency hides behind this image's three MFMA
+// passes instead of ~14 serialized load -> LDS-store round trips per image.
+// Per-thread register counts for 84 x 84 frames (host-checked, else PF off).
+
+template <int C, bool PF>
+__global__ void __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(1, PF ? 2 : 4)))
 cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t rows,
                const float* __restrict__ A1g, const float* __restrict__ dA2g,
                float* __restrict__ part, const int* skip) {
@@ -230,20 +261,48 @@ cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
   for (int t = 0; t < C; ++t) acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db2p = 0.f, db1p = 0.f;
 
+  const int nvi = (int)(g.img >> 4), nva = 4 * g.P1, nvd = g.flat >> 2;
+  constexpr int KI = PF ? CnnPf<C>::KI : 1, KA = PF ? CnnPf<C>::KA : 1, KD = PF ? CnnPf<C>::KD : 1;
+  // ext-vector element types (the HIP vector structs kept these arrays in
+  // scratch: SROA does not split them)
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 pfi[KI];
+  f32x4 pfa[KA], pfd[KD];
+#define SMI_CNN_FETCH(n_)                                                                   \
+  do {                                                                                      \
+    const int64_t nn_ = (n_);                                                               \
+    const u32x4* si_ = reinterpret_cast<const u32x4*>(pix_of(pr, nn_));                     \
+    const f32x4* s1_ = reinterpret_cast<const f32x4*>(A1g + nn_ * (int64_t)(16 * g.P1));    \
+    const f32x4* s2_ = reinterpret_cast<const f32x4*>(dA2g + nn_ * (int64_t)g.flat);        \
+    _Pragma("unroll") for (int k = 0; k < KI; ++k) pfi[k] = si_[min(tid + k * kWG, nvi - 1)]; \
+    _Pragma("unroll") for (int k = 0; k < KA; ++k) pfa[k] = s1_[min(tid + k * kWG, nva - 1)]; \
+    _Pragma("unroll") for (int k = 0; k < KD; ++k) pfd[k] = s2_[min(tid + k * kWG, nvd - 1)]; \
+  } while (0)
+  if (PF && (int64_t)blockIdx.x < rows) SMI_CNN_FETCH(blockIdx.x);
   for (int64_t n = blockIdx.x; n < rows; n += gridDim.x) {
-    {
+    if constexpr (PF) {
+      u32x4* dst = reinterpret_cast<u32x4*>(img);
+      f32x4* d1 = reinterpret_cast<f32x4*>(a1);
+      f32x4* d2 = reinterpret_cast<f32x4*>(da2);
+#pragma unroll
+      for (int k = 0; k < KI; ++k) if (tid + k * kWG < nvi) dst[tid + k * kWG] = pfi[k];
+#pragma unroll
+      for (int k = 0; k < KA; ++k) if (tid + k * kWG < nva) d1[tid + k * kWG] = pfa[k];
+#pragma unroll
+      for (int k = 0; k < KD; ++k) if (tid + k * kWG < nvd) d2[tid + k * kWG] = pfd[k];
+    } else {
       const uint4* src = reinterpret_cast<const uint4*>(pix_of(pr, n));
       uint4* dst = reinterpret_cast<uint4*>(img);
-      const int nv = (int)(g.img >> 4);
-      for (int i = tid; i < nv; i += kWG) dst[i] = src[i];
+      for (int i = tid; i < nvi; i += kWG) dst[i] = src[i];
       const float4* s1 = reinterpret_cast<const float4*>(A1g + n * (int64_t)(16 * g.P1));
       float4* d1 = reinterpret_cast<float4*>(a1);
-      for (int i = tid; i < 4 * g.P1; i += kWG) d1[i] = s1[i];
+      for (int i = tid; i < nva; i += kWG) d1[i] = s1[i];
       const float4* s2 = reinterpret_cast<const float4*>(dA2g + n * (int64_t)g.flat);
       float4* d2 = reinterpret_cast<float4*>(da2);
-      for (int i = tid; i < (g.flat >> 2); i += kWG) d2[i] = s2[i];
+      for (int i = tid; i < nvd; i += kWG) d2[i] = s2[i];
     }
     __syncthreads();
+    if (PF && n + gridDim.x < rows) SMI_CNN_FETCH(n + gridDim.x);
     // ---- (b) conv-2 weight gradient
     for (int j = 0; j < (g.P2 + 3) >> 2; ++j) {
       const int p = 4 * j + lg;
@@ -348,6 +407,7 @@ cnn_bwd_kernel(const float* __restrict__ prm, PixRows pr, int H, int W, int64_t 
     out[g.ob1 + tid] = s;
   }
 }
+#undef SMI_CNN_FETCH
 
 // ------------------------------------------------------------------- host
 static int cnn_check(const CnnGeom& g) {
@@ -403,7 +463,15 @@ int cnn_backward(const float* prm, const PixRows& pr, int C, int H, int W, int F
   RC_CHECK(launch_linear_bwd_dx(dz, lddz, (int)rows, F, prm + g.oWf, g.flat, g.flat, A2, g.flat,
                                 dA2, g.flat, st, skip));
   const size_t lds = cnn_bwd_lds(g);
-  auto k = C == 9 ? cnn_bwd_kernel<9> : cnn_bwd_kernel<3>;
+  // next-image prefetch when the frame fits its register arrays (84 x 84 does)
+  static const bool pf_on = [] { const char* e = getenv("SMI_CNN_PF"); return !(e && e[0] == '0'); }();
+  auto fits = [&](auto pf) {
+    using P = decltype(pf);
+    return (g.img >> 4) <= (int64_t)P::KI * kWG && 4 * g.P1 <= P::KA * kWG && (g.flat >> 2) <= P::KD * kWG;
+  };
+  const bool pf = pf_on && (C == 9 ? fits(CnnPf<9>{}) : fits(CnnPf<3>{}));
+  auto k = C == 9 ? (pf ? cnn_bwd_kernel<9, true> : cnn_bwd_kernel<9, false>)
+                  : (pf ? cnn_bwd_kernel<3, true> : cnn_bwd_kernel<3, false>);
   allow_lds(k, lds);
   const int grid = cnn_bwd_grid(rows);
   const int kt = ktime_begin(st);
