@@ -130,6 +130,11 @@ __device__ __forceinline__ void hc_sync() {
 // trials): 2 -> 8.45 ms, 3 -> 8.59, 4 -> 8.67 per learn: the deeper rings cost
 // occupancy (124 -> 184 VGPRs) and gain nothing
 constexpr int HC_D = SMI_HC_DEPTH;
+// 16-byte X loads per thread in flight while staging the forward's input rows
+#ifndef SMI_HC_XB
+#define SMI_HC_XB 4
+#endif
+constexpr int HC_XB = SMI_HC_XB;
 static_assert(HC_D >= 2, "ring of at least two chunks");
 template <int NT>
 struct HcStream {
@@ -362,14 +367,28 @@ head_fwd_kernel(HeadFwdArgs a) {
     S1.init(a.W1, a.K0, a.K0, a.h1, wave, 4, 0, 1);
     float e1[RT][NT1][4];
     hc_epi_load<NT1, 0, RT>(wave, a.h1, a.b1, nullptr, r0, a.rows, e1);
-    // X rows into LDS (columns K0 .. ld0 - 4 zero: the last chunk's padding)
+    // X rows into LDS (columns K0 .. ld0 - 4 zero: the last chunk's padding),
+    // HC_XB 16-byte loads per thread in flight before their LDS stores (one
+    // memory round trip per batch instead of one per float4; addresses
+    // clamped, the padding zeroed at the store)
     const int q0 = (a.ld0 - 4) >> 2;
-    for (int e = threadIdx.x; e < R * q0; e += kWG) {
-      const int r = e / q0, q = e - r * q0;
-      const int64_t rr = r0 + r < a.rows ? r0 + r : a.rows - 1;
-      float4 v = {0.f, 0.f, 0.f, 0.f};
-      if (4 * q < a.K0) v = *reinterpret_cast<const float4*>(a.X + rr * a.ldx + 4 * q);
-      *reinterpret_cast<float4*>(s0 + r * a.ld0 + 4 * q) = v;
+    for (int e0 = threadIdx.x; e0 < R * q0; e0 += HC_XB * kWG) {
+      f32x4 v[HC_XB];
+#pragma unroll
+      for (int k = 0; k < HC_XB; ++k) {
+        const int e = min(e0 + k * kWG, R * q0 - 1);
+        const int r = e / q0, q = e - r * q0;
+        const int64_t rr = r0 + r < a.rows ? r0 + r : a.rows - 1;
+        v[k] = *reinterpret_cast<const f32x4*>(a.X + rr * a.ldx + min(4 * q, a.K0 - 4));
+      }
+#pragma unroll
+      for (int k = 0; k < HC_XB; ++k) {
+        const int e = e0 + k * kWG;
+        if (e >= R * q0) break;
+        const int r = e / q0, q = e - r * q0;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(s0 + r * a.ld0 + 4 * q) = 4 * q < a.K0 ? v[k] : z;
+      }
     }
     __syncthreads();
     HEAD_TICK(0, 0);                              // X staged
@@ -477,45 +496,57 @@ head_bwd_kernel(HeadBwdArgs a) {
     s2[r * a.ld2 + a.h2 + c] = 0.f;
   }
   __syncthreads();
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    // dH2 = (dZ W3) * [HA2 > 0], K = out: lane = a 4-column group, wave = 4
-    // rows of row tile rt; the k-ordered fmaf chain from 0 (steps k >= out add 0 * w)
-    const int nq = a.h2 >> 2;            // <= 128: at most two passes, unrolled (a loop
+  // dH2 = (dZ W3) * [HA2 > 0], K = out: lane = a 4-column group, wave = 4
+  // rows of each row tile; the k-ordered fmaf chain from 0 (steps k >= out add
+  // 0 * w).  Per column pass, every W3 row group (out <= 16: <= 4 groups) and
+  // the HA2 masks of all row tiles are loaded before the first FMA: one memory
+  // round trip per pass instead of one per (row tile, k group) — the same FMAs
+  // in the same order
+  const int nq = a.h2 >> 2;              // <= 128: at most two passes, unrolled (a loop
 #pragma unroll                           // header made the first pass drain every load
-    for (int q0 = 0; q0 < 128; q0 += 64) {  // in flight, the weight prefetch included)
-      if (q0 >= nq) break;
-      const bool qv = q0 + lane < nq;
-      const int q = qv ? q0 + lane : nq - 1;
-      float4 m[4], v[4];
+  for (int q0 = 0; q0 < 128; q0 += 64) {  // in flight, the weight prefetch included)
+    if (q0 >= nq) break;
+    const bool qv = q0 + lane < nq;
+    const int q = qv ? q0 + lane : nq - 1;
+    constexpr int KGM = 4;               // k groups of 4 (out <= 16)
+    f32x4 w[KGM][4], m[RT][4];
+#pragma unroll
+    for (int g = 0; g < KGM; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[g][j] = *reinterpret_cast<const f32x4*>(a.W3 + (int64_t)min(4 * g + j, out - 1) * a.h2 + 4 * q);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t rr = min(r0 + 16 * rt + 4 * wave + i, a.rows - 1);
-        m[i] = *reinterpret_cast<const float4*>(a.HA2 + rr * a.h2 + 4 * q);
-        v[i] = float4{0.f, 0.f, 0.f, 0.f};
+        m[rt][i] = *reinterpret_cast<const f32x4*>(a.HA2 + rr * a.h2 + 4 * q);
       }
-      for (int kg = 0; kg < out; kg += 4) {
-        float4 w[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          w[j] = *reinterpret_cast<const float4*>(a.W3 + (int64_t)min(kg + j, out - 1) * a.h2 + 4 * q);
+    for (int rt = 0; rt < RT; ++rt) {
+      f32x4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < KGM; ++g) {
+        if (4 * g >= out) break;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float z = sZ[(16 * rt + 4 * wave + i) * 16 + kg + j];
-            v[i].x = fmaf(z, w[j].x, v[i].x); v[i].y = fmaf(z, w[j].y, v[i].y);
-            v[i].z = fmaf(z, w[j].z, v[i].z); v[i].w = fmaf(z, w[j].w, v[i].w);
+            const float z = sZ[(16 * rt + 4 * wave + i) * 16 + 4 * g + j];
+            v[i][0] = fmaf(z, w[g][j][0], v[i][0]); v[i][1] = fmaf(z, w[g][j][1], v[i][1]);
+            v[i][2] = fmaf(z, w[g][j][2], v[i][2]); v[i][3] = fmaf(z, w[g][j][3], v[i][3]);
           }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 16 * rt + 4 * wave + i;
-        const float4 o = {m[i].x > 0.f ? v[i].x : 0.f, m[i].y > 0.f ? v[i].y : 0.f,
-                          m[i].z > 0.f ? v[i].z : 0.f, m[i].w > 0.f ? v[i].w : 0.f};
+        const f32x4 o = {m[rt][i][0] > 0.f ? v[i][0] : 0.f, m[rt][i][1] > 0.f ? v[i][1] : 0.f,
+                         m[rt][i][2] > 0.f ? v[i][2] : 0.f, m[rt][i][3] > 0.f ? v[i][3] : 0.f};
         if (qv) {
-          *reinterpret_cast<float4*>(s2 + r * a.ld2 + 4 * q) = o;
-          if (r0 + r < a.rows) *reinterpret_cast<float4*>(a.dH2 + (r0 + r) * a.h2 + 4 * q) = o;
+          *reinterpret_cast<f32x4*>(s2 + r * a.ld2 + 4 * q) = o;
+          if (r0 + r < a.rows) *reinterpret_cast<f32x4*>(a.dH2 + (r0 + r) * a.h2 + 4 * q) = o;
         }
       }
     }
