@@ -426,6 +426,16 @@ head_fwd_kernel(HeadFwdArgs a) {
     hc_copy_out<RT>(s2, a.ld2, a.h2, a.HA2, r0, a.rows);
     {   // layer 3 (out <= 16): the waves split the k chunks, fixed-order sum
       const float bn = a.b3[li < a.out ? li : a.out - 1];
+      // the value targets of the lane's rows (value-gradient epilogue), in
+      // flight through layer 3
+      float vr[RT][4];
+      if (a.vgrad) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            vr[rt][i] = a.vret[min(r0 + 16 * rt + 4 * lk + i, a.rows - 1)];
+      }
       f32x4 acc[RT][1];
       hc_run<1, RT>(S3, s2, a.ld2, acc);
 #pragma unroll
@@ -434,6 +444,11 @@ head_fwd_kernel(HeadFwdArgs a) {
             float4{acc[rt][0][0], acc[rt][0][1], acc[rt][0][2], acc[rt][0][3]};
       hc_sync();
       if (wave == 0 && li < a.out) {
+        // one wait for the bias / target loads (and the HA2 copy-out stores
+        // issued before them): without it the waitcnt pass, unsure of the bias
+        // register across the row branches, waited vmcnt(0) in every row —
+        // on the previous row's Y store
+        __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -444,7 +459,7 @@ head_fwd_kernel(HeadFwdArgs a) {
                              (sR[((2 * RT + rt) * 64 + lane) * 4 + i] + sR[((3 * RT + rt) * 64 + lane) * 4 + i])) + bn;
             const float y = a.tanh_out ? tanhf(v) : v;
             a.Y[(r0 + r) * a.ldy + li] = y;
-            if (a.vgrad) a.vgrad[r0 + r] = a.vscale * (y - a.vret[r0 + r]);
+            if (a.vgrad) a.vgrad[r0 + r] = a.vscale * (y - vr[rt][i]);
           }
       }
     }

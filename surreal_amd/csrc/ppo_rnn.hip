@@ -556,7 +556,7 @@ __device__ __forceinline__ void ld_fields(float* dst, const float* __restrict__ 
 // epoch (the clip surrogate's gradient needs no global statistic: weight 1/N,
 // no KL term), bit-identically, so the gradient phase skips its row pass
 template <int NT, int AT, bool FUSE>
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, AT > 0 ? 3 : 8)))
 policy_rows_stats_kernel(PolRowArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   constexpr int AM = AT > 0 ? AT : 32;
@@ -596,14 +596,28 @@ policy_rows_stats_kernel(PolRowArgs a) {
   }
   const int64_t N = (int64_t)a.E * a.B;
   const AdvNorm nadv(a);
-  for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
-    float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM];
-    ld_row<AT>(m, a.mu + n * A, A);
-    ld_row<AT>(rm, a.refmu + n * A, A);
-    ld_fields<AT>(ac, a.rowin, N, n, 0, A);
-    ld_fields<AT>(bmu, a.rowin, N, n, A, A);
-    ld_fields<AT>(bsd, a.rowin, N, n, 2 * A, A);
-    const float av = nadv(a.rowin[(int64_t)(3 * A) * N + n]);
+  // one row's inputs; with a compile-time action width the row loop runs two
+  // alternating register sets, the next row's loads in flight behind this
+  // row's arithmetic (clamped row index: always issued, so the waitcnt pass
+  // waits for exactly the set it consumes)
+  struct RowIn { float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], adv, ret; };
+  auto load_row = [&](RowIn& x, int64_t n) {
+    ld_row<AT>(x.m, a.mu + n * A, A);
+    ld_row<AT>(x.rm, a.refmu + n * A, A);
+    ld_fields<AT>(x.ac, a.rowin, N, n, 0, A);
+    ld_fields<AT>(x.bmu, a.rowin, N, n, A, A);
+    ld_fields<AT>(x.bsd, a.rowin, N, n, 2 * A, A);
+    x.adv = a.rowin[(int64_t)(3 * A) * N + n];
+    x.ret = a.ret_tm[n];
+  };
+  auto row = [&](const RowIn& x, int64_t n) {
+    const float* m = x.m;
+    const float* rm = x.rm;
+    const float* ac = x.ac;
+    const float* bmu = x.bmu;
+    const float* bsd = x.bsd;
+    float blsd[AM];
+    const float av = nadv(x.adv);
     const float ex = expf(row_loglik_r<AT>(ac, m, isig, lsig, A, a.c_ll));
     const float lp = fmaxf(ex, 1e-5f);
     float ibsd[AM];
@@ -614,19 +628,25 @@ policy_rows_stats_kernel(PolRowArgs a) {
     }
     const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
     acc[PS_KL] += (double)row_kl_cc<AT>(rm, m, lkl, s02, iden2, A);
+    // both modes add into fixed accumulators (adapt adds an exact 0 to the
+    // clip sum): merged branches had indexed acc[] by mode, i.e. from scratch
+    float t_surr, t_clip;
     if (a.mode == 0) {
       const float ratio = lp / bl;
       const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
       const float surr = -ratio * av, csur = -cr * av;
-      acc[PS_SURR] += (double)surr;
-      acc[PS_CLIP] += (double)fmaxf(surr, csur);
+      t_surr = surr;
+      t_clip = fmaxf(surr, csur);
     } else {
-      acc[PS_SURR] += (double)(av * (lp / fmaxf(bl, 1e-2f)));
+      t_surr = av * (lp / fmaxf(bl, 1e-2f));
+      t_clip = 0.f;
     }
+    acc[PS_SURR] += (double)t_surr;
+    acc[PS_CLIP] += (double)t_clip;
     acc[PS_ISW] += (double)(lp / (bl + 1e-4f));
     acc[PS_BL] += (double)bl;
     acc[PS_RBD] += (double)row_kl_rb<AT>(rm, lrsig, s02, bmu, blsd, ibsd, A);
-    acc[PS_RET] += (double)a.ret_tm[n];
+    acc[PS_RET] += (double)x.ret;
     if constexpr (FUSE) {          // policy_rows_grad_kernel's clip branch, weight a.invN
       const float ratio = lp / bl;
       const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
@@ -644,6 +664,24 @@ policy_rows_stats_kernel(PolRowArgs a) {
         dz[j] = gmu * (1.f - m[j] * m[j]);
       }
       st_row<AT>(a.dz + n * A, dz, A);
+    }
+  };
+  const int64_t n0 = (int64_t)blockIdx.x * NT + threadIdx.x, ns = (int64_t)gridDim.x * NT;
+  if constexpr (AT > 0) {
+    RowIn X0, X1;
+    if (n0 < N) load_row(X0, n0);
+    for (int64_t n = n0; n < N; n += 2 * ns) {
+      load_row(X1, min(n + ns, N - 1));
+      row(X0, n);
+      if (n + ns >= N) break;
+      load_row(X0, min(n + 2 * ns, N - 1));
+      row(X1, n + ns);
+    }
+  } else {
+    for (int64_t n = n0; n < N; n += ns) {
+      RowIn X;
+      load_row(X, n);
+      row(X, n);
     }
   }
   if constexpr (FUSE) {            // block partials of sum_rows d/dstd, as the grad kernel
