@@ -94,8 +94,9 @@ struct RnnScratch {
   float *wT;
   float *values, *adv, *ret, *refmu, *lvpart;
   // time-major per-row inputs of the row kernels, packed once per learn,
-  // FIELD-major: rowin[f * NE + n], f = {actions (A) | behave mu, sigma (2A) |
-  // raw advantage}, n = t*B + b; ret_tm[n] the window return
+  // field-major within blocks of 64 rows: rowin[rin_idx(W, n, f)], f =
+  // {actions (A) | behave mu, sigma (2A) | raw advantage}, n = t*B + b;
+  // ret_tm[n] the window return
   float *rowin, *ret_tm;
   float *A1, *A2, *dA2, *dF, *cpart;        // pixel stem (empty without one)
   double *part, *gaepart;
@@ -106,6 +107,13 @@ struct RnnScratch {
 static inline int64_t al64(int64_t n) { return (n + 63) & ~(int64_t)63; }
 // fields of a packed row: A actions, 2A behaviour parameters, the advantage
 __host__ __device__ inline int row_w(int A) { return 3 * A + 1; }
+// rowin is blocked by 64 rows: block b holds field f of rows 64b .. 64b + 63
+// as 64 consecutive floats, the block's fields back to back, so one wave's
+// row loads read one contiguous ~5 KB run (a field-major [W][NE] layout made
+// every wave touch W DRAM pages per row batch)
+__host__ __device__ inline int64_t rin_idx(int W, int64_t n, int f) {
+  return (n >> 6) * ((int64_t)W << 6) + ((int64_t)f << 6) + (n & 63);
+}
 
 __host__ __device__ inline int rnn_nblk(int64_t rows, int nt = kWG) {
   // at most 1024 four-wave blocks' worth of waves (4096 one-wave blocks)
@@ -142,7 +150,7 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   s.adv = take(d.NE);
   s.ret = take(d.NE);
   s.refmu = take(d.NE * d.A);
-  s.rowin = take(d.NE * row_w(d.A));
+  s.rowin = take(((d.NE + 63) & ~(int64_t)63) * row_w(d.A));
   s.ret_tm = take(d.NE);
   s.lvpart = take((int64_t)4096 * d.A);
   const bool px = d.F > 0;
@@ -367,7 +375,7 @@ struct PolRowArgs {
   const float* behave;    // [B][T][2A]
   const float* adv;       // [B][E] raw
   const float* ret;       // [B][E]
-  const float* rowin;     // [row_w(A)][NE] field-major {actions | behave | raw adv}
+  const float* rowin;     // {actions | behave | raw adv} blocked by 64 rows (rin_idx)
   const float* ret_tm;    // [NE] time-major returns
   const double* moments;  // [3] global (sum, sumsq, n) of adv, or null (no norm)
   int norm_adv;
@@ -520,9 +528,10 @@ __device__ __forceinline__ float row_kl_rb(const float* mu0, const float* lsd0, 
   return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
 }
 
-// rowin / ret_tm from the batch-major inputs (once per learn), field-major:
-// the per-row kernels of every epoch give a thread one row, so lane i reads
-// field f of row n0 + i and one load instruction covers 64 consecutive floats
+// rowin / ret_tm from the batch-major inputs (once per learn), field-major in
+// 64-row blocks: the per-row kernels of every epoch give a thread one row, so
+// lane i reads field f of row n0 + i and one load instruction covers 64
+// consecutive floats
 // (a row-major 100-byte row per lane made every load instruction touch ~56
 // cache lines: the row kernels waited on the texture addresser, PMC TA_BUSY)
 __global__ void __launch_bounds__(kWG)
@@ -534,19 +543,21 @@ row_pack_kernel(PolRowArgs a, float* __restrict__ rowin, float* __restrict__ ret
     const int64_t src = (int64_t)b * a.T + t;
     const float* ac = a.actions + src * A;
     const float* bh = a.behave + src * 2 * A;
-    for (int j = 0; j < A; ++j) rowin[j * N + n] = ac[j];
-    for (int j = 0; j < 2 * A; ++j) rowin[(A + j) * N + n] = bh[j];
-    rowin[3 * A * N + n] = a.adv[(int64_t)b * a.E + t];
+    const int W = row_w(A);
+    for (int j = 0; j < A; ++j) rowin[rin_idx(W, n, j)] = ac[j];
+    for (int j = 0; j < 2 * A; ++j) rowin[rin_idx(W, n, A + j)] = bh[j];
+    rowin[rin_idx(W, n, 3 * A)] = a.adv[(int64_t)b * a.E + t];
     ret_tm[n] = a.ret[(int64_t)b * a.E + t];
   }
 }
 
-// field j .. j + AT - 1 of row n from the field-major rowin
+// field j .. j + AT - 1 of row n from the blocked rowin
 template <int AT>
-__device__ __forceinline__ void ld_fields(float* dst, const float* __restrict__ rowin, int64_t N,
+__device__ __forceinline__ void ld_fields(float* dst, const float* __restrict__ rowin, int64_t /*N*/,
                                           int64_t n, int f0, int A) {
+  const int W = row_w(AT > 0 ? AT : A);
 #pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) dst[j] = rowin[(int64_t)(f0 + j) * N + n];
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) dst[j] = rowin[rin_idx(W, n, f0 + j)];
 }
 
 // forward statistics of the policy over the E*B rows (ppo.py:203-224,
@@ -607,7 +618,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
     ld_fields<AT>(x.ac, a.rowin, N, n, 0, A);
     ld_fields<AT>(x.bmu, a.rowin, N, n, A, A);
     ld_fields<AT>(x.bsd, a.rowin, N, n, 2 * A, A);
-    x.adv = a.rowin[(int64_t)(3 * A) * N + n];
+    x.adv = a.rowin[rin_idx(row_w(A), n, 3 * A)];
     x.ret = a.ret_tm[n];
   };
   auto row = [&](const RowIn& x, int64_t n) {
@@ -758,7 +769,7 @@ policy_rows_grad_kernel(PolRowArgs a) {
     ld_fields<AT>(ac, a.rowin, N, n, 0, A);
     ld_fields<AT>(bmu, a.rowin, N, n, A, A);
     ld_fields<AT>(bsd, a.rowin, N, n, 2 * A, A);
-    const float av = nadv(a.rowin[(int64_t)(3 * A) * N + n]);
+    const float av = nadv(a.rowin[rin_idx(row_w(A), n, 3 * A)]);
     const float ll = row_loglik_r<AT>(ac, m, inv1, lsig, A, a.c_ll);
     const float ex = expf(ll);
     const float lp = fmaxf(ex, 1e-5f);
