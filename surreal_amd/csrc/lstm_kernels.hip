@@ -690,18 +690,28 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
   for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto x_part = [&](int tt) {
     if constexpr (KX > 0) {
+      // the same LDS read ring as the h part below: the wave issues these
+      // MFMAs ahead of its cell update, so LDS round trips here delay the cell
       const float4* xr4 = reinterpret_cast<const float4*>(xS[tt & 1] + (lane & 3) * KXS);
+      constexpr int NQX = KX / 4;
+      float4 q[LSTM_HQ];
 #pragma unroll
-      for (int k8 = 0; k8 < KX / 8; ++k8) {
-        const float4 u = xr4[2 * k8], v = xr4[2 * k8 + 1];
-        acc[0] = mfma4x64(u.x, wx[8 * k8 + 0], acc[0]);
-        acc[1] = mfma4x64(u.y, wx[8 * k8 + 1], acc[1]);
-        acc[2] = mfma4x64(u.z, wx[8 * k8 + 2], acc[2]);
-        acc[3] = mfma4x64(u.w, wx[8 * k8 + 3], acc[3]);
-        acc[4] = mfma4x64(v.x, wx[8 * k8 + 4], acc[4]);
-        acc[5] = mfma4x64(v.y, wx[8 * k8 + 5], acc[5]);
-        acc[6] = mfma4x64(v.z, wx[8 * k8 + 6], acc[6]);
-        acc[7] = mfma4x64(v.w, wx[8 * k8 + 7], acc[7]);
+      for (int j = 0; j < LSTM_HQ && j < NQX; ++j) q[j] = xr4[j];
+#pragma unroll
+      for (int j = 0; j < NQX; ++j) {
+        const float4 u = q[j % LSTM_HQ];
+        const int ab = (j & 1) * 4;
+        acc[ab + 0] = mfma4x64(u.x, wx[4 * j + 0], acc[ab + 0]);
+        acc[ab + 1] = mfma4x64(u.y, wx[4 * j + 1], acc[ab + 1]);
+        acc[ab + 2] = mfma4x64(u.z, wx[4 * j + 2], acc[ab + 2]);
+        acc[ab + 3] = mfma4x64(u.w, wx[4 * j + 3], acc[ab + 3]);
+        if (j + LSTM_HQ < NQX) q[j % LSTM_HQ] = xr4[j + LSTM_HQ];
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, LSTM_HQ < NQX ? LSTM_HQ : NQX, 0);
+#pragma unroll
+      for (int j = 0; j < NQX; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        if (j + LSTM_HQ < NQX) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
     }
   };
