@@ -188,11 +188,15 @@ def roofline_hbm(kt, n_inst):
     tot_b = sum(kt[n][2] for n in rows)
     tot_ms = sum(kt[n][1] for n in rows)
     agg = tot_b / (tot_ms * 1e-3) / 1e9
+    # the largest per-launch working set against the 256 MB MALL: below it the
+    # streams are (partly) cache-resident and the fraction is launch latency
+    big = max(r['bytes_per_launch'] for r in rows.values())
+    where = ('cache-resident at these batch sizes (largest launch %.1f MB <= 256 MB MALL)' % (big / 1e6)
+             if big <= 256e6 else 'largest launch %.0f MB > 256 MB MALL: HBM-resident streams' % (big / 1e6))
     return {'kernels': rows, 'aggregate': {'achieved': round(agg, 1), 'unit': 'GB/s',
                                            'frac': round(agg / HBM_PEAK_GBS, 4),
                                            'ms_per_step': round(tot_ms / n_inst, 4)},
-            'note': 'in-workload (cache-resident at these batch sizes); > 256 MB sweeps: '
-                    'tools/bench_hbm.py, profiles/'}
+            'note': f'in-workload ({where}); > 256 MB sweeps: tools/bench_hbm.py, profiles/'}
 
 
 def mlp_flops_per_row(d, h1, h2, o):
@@ -472,6 +476,8 @@ def main():
     ap.add_argument('--scaling', choices=['strong', 'weak'], default=None,
                     help='strong (default for c3/c5): the workload\'s global batch split over '
                          'the ranks; weak (c2, c4): the per-GPU batch fixed')
+    ap.add_argument('--no-host-batch', action='store_true',
+                    help='skip the host-fed line (numpy batches through the StagingArena)')
     ap.add_argument('--graph', choices=['on', 'off'], default='on',
                     help='learn() as a hipGraph replay of its device sequence '
                          '(PPOLearner(use_graph=True), bit-identical to eager); with ranks > 1 '
@@ -531,6 +537,30 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     epochs_run = learner.last_stats()['epochs_run']
+    host_fed = None
+    if not args.no_host_batch:
+        # the same learns fed as the reference's learn() is fed: numpy batches
+        # (the aggregator's output) staged by the learner itself -- one pinned
+        # buffer, one H2D per batch (StagingArena, ppo.py:420-484) -- timed like
+        # the headline; reported beside it, never as `value`
+        hpool = [synthetic.ppo_batch(B, T, D, A, seed=rank * 1000 + i, rnn_hidden=dims['rnn_hidden'],
+                                     pixel=dims.get('pixel')) for i in range(4)]
+        for i in range(2):
+            learner.learn(hpool[i % len(hpool)])
+        barrier()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            learner.learn(hpool[k % len(hpool)])
+        barrier()
+        he = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([he], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            he = float(t.item())
+        host_fed = {'value': round(world * B * T * args.steps / he, 1), 'unit': 'env-steps/s',
+                    'ms_per_step': round(he / args.steps * 1e3, 4),
+                    'note': 'numpy batches -> StagingArena (every array packed into one pinned '
+                            'buffer, one async H2D) -> learn(): PCIe-inclusive, not the headline'}
     # instrumented pass (separate, after the timed region): per-launch HIP
     # events of the MFMA kernels recorded by the library on the learner's
     # stream, and per-phase torch events -> roofline / kernels / phases
@@ -638,6 +668,8 @@ def main():
         out['roofline_hbm'] = rhbm
     if allreduce is not None:
         out['allreduce'] = allreduce
+    if host_fed is not None:
+        out['host_fed'] = host_fed
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(args.config, make_config(args.config)[0], dims,
                                            args.cpu_budget)

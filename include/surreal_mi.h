@@ -57,8 +57,12 @@ typedef struct smi_context smi_context;
 smi_context* smi_context_create(void* workspace, int64_t bytes);   /* NULL on bad args */
 int          smi_context_make_current(smi_context* ctx);            /* this thread; NULL = default */
 /* Marks ctx dead (its 24-byte handle is kept, never freed): a thread that
- * still has it current falls back to the default workspace; making a dead
- * context current is an error.  The workspace may be freed afterwards. */
+ * still has it current falls back to the default workspace for its LATER
+ * launches; making a dead context current is an error.  A launch that another
+ * thread is issuing on ctx concurrently with the destroy may still use its
+ * workspace: free the workspace only after every thread that had ctx current
+ * has finished issuing launches with it (the Python owner keeps it alive for
+ * as long as any thread holds the context). */
 int          smi_context_destroy(smi_context* ctx);
 
 /* Measurement only (not part of the reference API): per-launch HIP-event

@@ -8,6 +8,9 @@ One-agent-at-a-time restatement of the reference actors' act():
   DDPGAgent.act    surreal/agent/ddpg_agent.py:153-182 (actor forward, clip,
                    exploration noise, clip)
   NormalActionNoise / OrnsteinUhlenbeckActionNoise   surreal/agent/action_noise.py:9-40
+  NormalParameterNoise / AdaptiveNormalParameterNoise surreal/agent/param_noise.py:9-72,
+                   applied on parameter fetch and (adaptive) measured in act()
+                   (ddpg_agent.py:134-151, 172-173)
 Random draws come from numpy's global RNG in the reference's order.
 """
 import numpy as np
@@ -77,13 +80,67 @@ class OUNoiseRef(object):
         return x
 
 
+class NormalParameterNoiseRef(object):
+    """param_noise.py:9-24: every array of the fetched params + N(0, sigma)"""
+
+    def __init__(self, sigma):
+        self.sigma = sigma
+
+    def apply(self, params):
+        for key in params:
+            for k in params[key]:
+                p = params[key][k]
+                params[key][k] = p + np.random.normal(0, self.sigma, size=tuple(p.shape))
+        return params
+
+
+class AdaptiveNormalParameterNoiseRef(object):
+    """param_noise.py:29-72.  original_actor(obs) is the unperturbed actor
+    (the reference's original_model forward with calculate_value=False)"""
+
+    def __init__(self, original_actor, load_original, target_stddev, compute_dist_interval=10,
+                 alpha=1.04, sigma=0.01):
+        self.sigma, self.target_stddev = sigma, target_stddev
+        self.compute_dist_interval, self.alpha = compute_dist_interval, alpha
+        self.original_actor, self.load_original = original_actor, load_original
+        self.i = 0
+        self.total_action_distance = 0.0
+
+    def compute_action_distance(self, obs, modified_model_action):
+        if self.i % self.compute_dist_interval == 0:
+            with torch.no_grad():
+                a0 = self.original_actor(obs)
+            # assigned, not accumulated (param_noise.py:44)
+            self.total_action_distance = float((((a0 - modified_model_action) ** 2).sum()) ** 0.5)
+        self.i += 1
+
+    def apply(self, params):
+        if self.i > 0:
+            mean_action_dist = self.total_action_distance / self.i
+            if mean_action_dist > self.target_stddev:
+                self.sigma /= self.alpha
+            else:
+                self.sigma *= self.alpha
+        self.i = 0
+        self.load_original({k: {kk: np.array(vv) for kk, vv in v.items()} for k, v in params.items()})
+        for key in params:
+            for k in params[key]:
+                p = params[key][k]
+                params[key][k] = p + np.random.normal(0, self.sigma, size=tuple(p.shape))
+        return params
+
+
 class DDPGAgentRef(object):
-    def __init__(self, actor, noise=None, agent_mode='training'):
+    def __init__(self, actor, noise=None, agent_mode='training', param_noise=None):
         self.actor, self.noise, self.agent_mode = actor, noise, agent_mode
+        self.param_noise = param_noise
 
     def act(self, obs):
+        x = torch.as_tensor(obs, dtype=torch.float32).unsqueeze(0)
         with torch.no_grad():
-            a = self.actor(torch.as_tensor(obs, dtype=torch.float32).unsqueeze(0))
+            a = self.actor(x)
+        if isinstance(self.param_noise, AdaptiveNormalParameterNoiseRef):
+            self.param_noise.compute_action_distance(x, a)
         a = a.numpy()[0].clip(-1, 1)
         if self.agent_mode != 'eval_deterministic':
             a += self.noise()

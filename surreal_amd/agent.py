@@ -114,7 +114,16 @@ class PPOAgentBatch(object):
 
 class DDPGAgentBatch(object):
     """N DDPG actors with their own exploration noise processes
-    (ddpg_agent.py:103-182; action_noise.py:9-40)."""
+    (ddpg_agent.py:103-182; action_noise.py:9-40) and, when configured, their
+    own parameter-space noise (param_noise.py:9-72, ddpg_agent.py:134-151,172-173):
+    every fetched parameter set is perturbed once per agent (numpy's global
+    RNG, agents in order, each agent's state_dict keys in order), so each
+    agent acts with its own perturbed perception + actor.  'adaptive_normal'
+    keeps the unperturbed parameters, measures every compute_dist_interval-th
+    act the distance between the unperturbed and perturbed actions, and scales
+    each agent's sigma by alpha at the next fetch."""
+
+    PN_DIST_INTERVAL = 10                     # AdaptiveNormalParameterNoise default
 
     def __init__(self, learner_config, env_config, n_agents, agent_mode='training', device=None,
                  seed=0, agent_ids=None, num_agents=None):
@@ -139,8 +148,19 @@ class DDPGAgentBatch(object):
                                device=self.device, generator=torch.Generator().manual_seed(seed))
         self.frame_stack_concatenate_on_env = bool(ec.get('frame_stack_concatenate_on_env', True))
         exp = lc.algo.exploration
-        if exp.get('param_noise_type') is not None:
-            raise NotImplementedError('surreal_amd: DDPG parameter-space noise is not built')
+        self.param_noise_type = exp.get('param_noise_type')
+        if self.param_noise_type not in (None, 'normal', 'adaptive_normal'):
+            raise ValueError('Param noise type {} undefined.'.format(self.param_noise_type))
+        if agent_mode == 'eval_deterministic':   # _init_noise returns early (ddpg_agent.py:121-122)
+            self.param_noise_type = None
+        if self.param_noise_type is not None:
+            self.pn_sigma = np.full(self.n, float(exp.get('param_noise_sigma', 0.05)))
+            self.pn_alpha = float(exp.get('param_noise_alpha', 1.15))
+            self.pn_target = float(exp.get('param_noise_target_stddev', 0.005))
+            self.pn_i = np.zeros(self.n, dtype=np.int64)        # acts since the last fetch
+            self.pn_dist = [0.0] * self.n                      # total_action_distance
+            self._pn_flats = None      # per agent: perturbed [perception | actor] device images
+            self._pn_orig = None       # the fetched (unperturbed) images
         if exp.noise_type not in ('normal', 'ou_noise'):
             raise ValueError('Noise type {} undefined.'.format(exp.noise_type))
         self.noise_type = exp.noise_type
@@ -156,7 +176,43 @@ class DDPGAgentBatch(object):
         self.model.load_state_dict(module_dict['ddpg'].state_dict())
 
     def load_numpy(self, numpy_dict):
-        self.model.load_state_dict(_np_state_to_torch(numpy_dict['ddpg']))
+        """on_parameter_fetched (ddpg_agent.py:134-137): the published numpy
+        parameters, perturbed per agent when parameter noise is configured"""
+        if self.param_noise_type is None:
+            self.model.load_state_dict(_np_state_to_torch(numpy_dict['ddpg']))
+            return
+        self._apply_param_noise(numpy_dict)
+
+    def _acting_flats(self):
+        m = self.model
+        return [x.flat for x in (m.perception, m.actor) if x is not None]
+
+    def _apply_param_noise(self, numpy_dict):
+        sd = numpy_dict['ddpg']
+        # the unperturbed set (AdaptiveNormalParameterNoise.original_model)
+        self.model.load_state_dict(_np_state_to_torch(sd))
+        self._pn_orig = [f.detach().clone() for f in self._acting_flats()]
+        self._pn_flats = []
+        for i in range(self.n):
+            if self.param_noise_type == 'adaptive_normal':
+                if self.pn_i[i] > 0:                            # param_noise.py:53-60
+                    mean_dist = self.pn_dist[i] / self.pn_i[i]
+                    if mean_dist > self.pn_target:
+                        self.pn_sigma[i] /= self.pn_alpha
+                    else:
+                        self.pn_sigma[i] *= self.pn_alpha
+                self.pn_i[i] = 0
+            noisy = {}
+            for k, v in sd.items():                             # param_noise.py:17-24 / 63-70
+                v = np.asarray(v)
+                noisy[k] = v + np.random.normal(0, self.pn_sigma[i], size=tuple(v.shape))
+            self.model.load_state_dict(_np_state_to_torch(noisy))
+            self._pn_flats.append([f.detach().clone() for f in self._acting_flats()])
+        self._set_flats(self._pn_orig)
+
+    def _set_flats(self, imgs):
+        for f, img in zip(self._acting_flats(), imgs):
+            f.copy_(img)
 
     def reset(self, agents=None):
         idx = slice(None) if agents is None else list(agents)
@@ -172,6 +228,36 @@ class DDPGAgentBatch(object):
             (self.sigma[:, None] * np.sqrt(self.dt)) * np.random.normal(size=(self.n, A))
         self.x_prev = x
         return x
+
+    def _act_param_noise(self, obs, x):
+        """each agent's action from its own perturbed perception + actor (one
+        forward per agent); adaptive: every PN_DIST_INTERVAL-th call the
+        unperturbed model's actions give total_action_distance
+        (param_noise.py:41-46: assigned, not accumulated, as the reference does)"""
+        m = self.model
+        rows = []
+        for i in range(self.n):
+            self._set_flats(self._pn_flats[i])
+            xi = self._perceive_row(obs, i) if m.is_pixel_input else x[i:i + 1]
+            rows.append(m.forward_actor(xi))
+        a = torch.cat(rows, 0)
+        self._set_flats(self._pn_orig)
+        if self.param_noise_type == 'adaptive_normal':
+            due = [i for i in range(self.n) if self.pn_i[i] % self.PN_DIST_INTERVAL == 0]
+            if due:
+                a0 = m.forward_actor(x)                # x: the unperturbed perception
+                for i in due:
+                    self.pn_dist[i] = float(((a0[i] - a[i]) ** 2).sum() ** 0.5)
+            self.pn_i += 1
+        return a
+
+    def _perceive_row(self, obs, i):
+        o = {'pixel': {'camera0': self._camera(obs['pixel']['camera0'])[i:i + 1]}}
+        if self.model.low_dim:
+            low = obs['low_dim'][list(obs['low_dim'])[0]]
+            o['low_dim'] = {'flat_inputs': torch.from_numpy(
+                np.ascontiguousarray(low, dtype=np.float32)[i:i + 1]).to(self.device)}
+        return self.model.forward_perception(o)
 
     def _camera(self, frames):
         """camera0 of N agents -> a uint8 (N, C, H, W) device tensor; a list of
@@ -207,7 +293,10 @@ class DDPGAgentBatch(object):
             x = torch.from_numpy(np.ascontiguousarray(obs, dtype=np.float32)).to(self.device)
         if x.dim() != 2 or x.shape[0] != self.n:
             raise ValueError(f'expected observations of {self.n} agents, got shape {tuple(x.shape)}')
-        a = m.forward_actor(x).cpu().numpy().clip(-1, 1)
+        if self.param_noise_type is not None and self._pn_flats is not None:
+            a = self._act_param_noise(obs, x).cpu().numpy().clip(-1, 1)
+        else:
+            a = m.forward_actor(x).cpu().numpy().clip(-1, 1)
         if self.agent_mode != 'eval_deterministic':
             a += self._noise()
         return a.clip(-1, 1)

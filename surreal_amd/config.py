@@ -155,9 +155,12 @@ DDPG_DEFAULT_LEARNER_CONFIG = Config({
             'use_double_critic': False,
             'target_update': {'type': 'hard', 'interval': 500},
         },
-        # agent-side exploration (ddpg_configs.py:63-86); parameter noise is not built
+        # agent-side exploration (ddpg_configs.py:63-86)
         'exploration': {
-            'param_noise_type': None,
+            'param_noise_type': None,          # None | 'normal' | 'adaptive_normal'
+            'param_noise_sigma': 0.05,
+            'param_noise_alpha': 1.15,
+            'param_noise_target_stddev': 0.005,
             'noise_type': 'normal',
             'max_sigma': 1.0,
             'theta': 0.15,

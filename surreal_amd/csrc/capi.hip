@@ -175,9 +175,12 @@ int smi_context_make_current(smi_context* ctx) {
 int smi_context_destroy(smi_context* ctx) {
   REQUIRE(ctx, "context_destroy: null context");
   if (t_ctx == ctx) t_ctx = nullptr;
+  // ws / bytes are never written after create (no race with a reader that
+  // passed the alive check): a launch another thread is issuing on this
+  // context right now still targets its workspace, which is why the caller
+  // frees the workspace only once no thread issues launches with it
+  // (include/surreal_mi.h)
   ctx->alive.store(false, std::memory_order_release);   // not freed: see above
-  ctx->ws = nullptr;
-  ctx->bytes = 0;
   return SMI_OK;
 }
 int64_t smi_workspace_bytes(void) { return (int64_t)128 << 20; }

@@ -61,18 +61,27 @@ struct GemmArgs {
 };
 
 // where output (m, n) of a weight gradient goes (bias column, the second
-// destination of a two-source B, padding)
-__device__ __forceinline__ void dw_put(const GemmArgs& g, int m, int n, float v) {
+// destination of a two-source B, padding); returns the sum of squares of the
+// values it stored (each destination element once: b_ih and b_hh both hold the
+// bias gradient, so it counts twice, as in clip_grad_norm_ over both)
+__device__ __forceinline__ float dw_put(const GemmArgs& g, int m, int n, float v) {
   if (n == g.ones_col) {
-    g.bias_out[m] = g.accumulate ? g.bias_out[m] + v : v;
-    if (g.bias_out2) g.bias_out2[m] = g.accumulate ? g.bias_out2[m] + v : v;
-    return;
+    const float b = g.accumulate ? g.bias_out[m] + v : v;
+    g.bias_out[m] = b;
+    if (g.bias_out2) {
+      const float b2 = g.accumulate ? g.bias_out2[m] + v : v;
+      g.bias_out2[m] = b2;
+      return b * b + b2 * b2;
+    }
+    return b * b;
   }
   float* dst;
   if (g.B2 && n >= g.split_col) dst = g.C2 + (int64_t)m * g.ldc2 + (n - g.split_col);
-  else if (g.B2 && n >= g.c1_real) return;                   // padding column
+  else if (g.B2 && n >= g.c1_real) return 0.f;               // padding column
   else dst = g.C + (int64_t)m * g.ldc + n;
-  *dst = g.accumulate ? *dst + v : v;
+  const float r = g.accumulate ? *dst + v : v;
+  *dst = r;
+  return r * r;
 }
 
 // Operand loader: one 64 (rows) x 32 (k) tile, 2048 elements, 8 per thread
@@ -961,6 +970,7 @@ gemm_dwd_kernel(GemmArgs g) {
 // (and no side stream): the ~20 us fixed cost of a dW launch is paid once.
 constexpr int kDwGroupMax = 6;
 struct DwGroup {
+  DwEpilogue x;                  // optional epilogue task of the reducer (smi_internal.hpp)
   GemmArgs g[kDwGroupMax];
   int wg0[kDwGroupMax + 1];      // workgroup prefix
   int rb0[kDwGroupMax + 1];      // reducer-block prefix
@@ -1060,11 +1070,54 @@ gemm_dwd_group_kernel(DwGroup G) {
 }
 
 // the partials of every GEMM of a group, each element summed over its slabs in
-// the fixed order of gemm_splitk_reduce_kernel
+// the fixed order of gemm_splitk_reduce_kernel.  With an epilogue task
+// (G.x.on): every block also writes the fp64 sum of squares of the values it
+// stored to x.sq[block] (fixed order: lane values, wave butterfly, waves in
+// order), and one more block (the last) runs the task itself: the log_var
+// gradient from its row partials, that block's sum of squares, the partial
+// count and the optimizer step bump (what sumsq_part_kernel and
+// logvar_grad_kernel did as launches of their own)
+__device__ void dw_epilogue_block(const DwEpilogue& x, int nsq) {
+  __shared__ double red[kWG / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float q = 0.f;
+  if (x.lvpart) {
+    // d log_var[j] = std_j * sum_blocks lvpart[.][j] (logvar_grad_kernel's order)
+    for (int j = wave; j < x.lv_A; j += kWG / 64) {
+      float t = 0.f;
+      for (int i = lane; i < x.lv_nb; i += 64) t += x.lvpart[(int64_t)i * x.lv_A + j];
+      t = wave_sum(t);
+      const float gv = t * expf(x.lv[j]);
+      if (lane == 0) {
+        x.lv_out[j] = gv;
+        q += gv * gv;
+      }
+    }
+  }
+  if (!x.sq) {
+    if (threadIdx.x == 0 && x.step) x.step[0] += 1;
+    if (threadIdx.x == 0 && x.runs) x.runs[0] += 1;
+    return;
+  }
+  const double t = block_sum_d((double)q, red);
+  if (threadIdx.x == 0) {
+    x.sq[nsq] = t;
+    x.np[0] = nsq + 1;
+    if (x.step) x.step[0] += 1;
+    if (x.runs) x.runs[0] += 1;
+  }
+}
+
 __global__ void __launch_bounds__(kWG)
 gemm_group_reduce_kernel(DwGroup G) {
   __shared__ float red[4][64];
+  __shared__ double sqr[kWG / 64];
   const int b = blockIdx.x;
+  if (b >= G.rb0[G.n]) {                          // the epilogue task's block
+    if (G.x.skip && G.x.skip[0] != 0) return;
+    dw_epilogue_block(G.x, G.rb0[G.n]);
+    return;
+  }
   int gi = 0;
   while (gi + 1 < G.n && b >= G.rb0[gi + 1]) ++gi;
   const GemmArgs& g = G.g[gi];
@@ -1086,10 +1139,15 @@ gemm_group_reduce_kernel(DwGroup G) {
   for (; z < S; z += 4) s0 += part[(int64_t)z * MN + ec];
   red[zl][el] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (zl != 0 || e >= MN) return;
-  const float v = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
-  const int m = (int)(e / g.N), n = (int)(e - (int64_t)m * g.N);
-  dw_put(g, m, n, v);
+  float q = 0.f;
+  if (zl == 0 && e < MN) {
+    const float v = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+    const int m = (int)(e / g.N), n = (int)(e - (int64_t)m * g.N);
+    q = dw_put(g, m, n, v);
+  }
+  if (!G.x.sq) return;
+  const double t = block_sum_d((double)q, sqr);
+  if (threadIdx.x == 0) G.x.sq[b] = t;
 }
 
 
@@ -1336,12 +1394,28 @@ static thread_local double g_grp_flops = 0.0;
 int dw_group_begin() {
   g_grp_on = true;
   g_grp.n = 0;
+  g_grp.x = DwEpilogue{};
   g_grp_flops = 0.0;
   return SMI_OK;
 }
 
+// the reducer's epilogue task of the open group (dw_group_flush launches one
+// more reducer block for it); with x.sq every weight gradient of the bracket
+// must join the group (the fused sum of squares covers only the group)
+int dw_group_epilogue(const DwEpilogue& x) {
+  if (!g_grp_on) return set_error(SMI_E_ARG, "dw group: no open group for the epilogue");
+  g_grp.x = x;
+  g_grp.x.on = 1;
+  return SMI_OK;
+}
+
+static thread_local bool g_grp_overflow = false;
 static bool dw_group_add(const GemmArgs& g) {
-  if (!g_grp_on || g_grp.n >= kDwGroupMax) return false;
+  if (!g_grp_on) return false;
+  if (g_grp.n >= kDwGroupMax) {
+    g_grp_overflow = true;
+    return false;
+  }
   auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
   const bool va = al16(g.A) && g.M >= 4 && g.M % 4 == 0 && g.a_cs % 4 == 0;
@@ -1412,7 +1486,17 @@ static int dwd_group_slots(size_t lds) {
 int dw_group_flush(hipStream_t st) {
   g_grp_on = false;
   DwGroup& G = g_grp;
-  if (G.n == 0) return SMI_OK;
+  const bool overflow = g_grp_overflow;
+  g_grp_overflow = false;
+  if (G.x.on && G.x.sq && overflow)
+    return set_error(SMI_E_ARG, "dw group: a fused sum of squares needs every dW GEMM in the group");
+  if (G.n == 0) {
+    if (!G.x.on) return SMI_OK;
+    if (G.x.sq) return set_error(SMI_E_ARG, "dw group: fused sum of squares over an empty group");
+    G.rb0[0] = 0;                                   // the epilogue task alone
+    hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(1), dim3(kWG), 0, st, G);
+    return check_launch("gemm_group_reduce_kernel");
+  }
   constexpr int MT = 4, NT = DWG_NT;
   const size_t lds = (size_t)2 * MT * NT * 64 * sizeof(float4);
   const int rs = 4 * dwd_waves() * DWD_P;           // rows per prefetch window
@@ -1542,7 +1626,8 @@ int dw_group_flush(hipStream_t st) {
   ktime_end(kslot, KT_GEMM_DW, g_grp_flops, st);
   RC_CHECK(check_launch("gemm_dwd_group_kernel"));
   const int rslot = ktime_begin(st);
-  hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(G.rb0[G.n]), dim3(kWG), 0, st, G);
+  hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(G.rb0[G.n] + (G.x.on ? 1 : 0)), dim3(kWG), 0,
+                     st, G);
   ktime_end(rslot, KT_GEMM_REDUCE, (double)need, st);
   return check_launch("gemm_group_reduce_kernel");
 }

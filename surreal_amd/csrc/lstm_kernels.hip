@@ -118,6 +118,10 @@ struct LstmFwdArgs {
   int din;
   const float* w_ih;      // [4H][din]
   const float* b_ih;      // [4H]
+  // cbuf / gates are stored for steps t < keep only (0: all S steps): a forward
+  // over more steps than a backward needs (the GAE critic pass over T + 1
+  // steps serves as the first policy forward over its first E steps)
+  int keep;
 };
 
 struct LstmBwdArgs {
@@ -135,6 +139,7 @@ template <int MAXUT>
 __global__ void __launch_bounds__(kWG)
 lstm_fwd_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  const int keepS = a.keep > 0 ? a.keep : a.S;     // steps whose c / gates are stored
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int H = a.H, B = a.B, G4 = 4 * H;
   const int LDH = lstm_ld(4 * lstm_q(H));
@@ -254,8 +259,8 @@ lstm_fwd_kernel(LstmFwdArgs a) {
         if (unit < H) hn[row * LDH + unit] = ok ? h : 0.f;
         if (ok) {
           a.hbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = h;
-          if (a.cbuf) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = c;
-          if (a.gates) {
+          if (a.cbuf && t < keepS) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = c;
+          if (a.gates && t < keepS) {
             float* gp = a.gates + ((int64_t)t * B + gr) * G4 + unit;
             gp[0] = ig; gp[H] = fg; gp[2 * H] = cg; gp[3 * H] = og;
           }
@@ -376,6 +381,7 @@ template <int KS>
 __global__ void __launch_bounds__(kWG8)
 lstm_fwd_reg_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  const int keepS = a.keep > 0 ? a.keep : a.S;     // steps whose c / gates are stored
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int H = a.H, B = a.B, G4 = 4 * H;
   const int LDH = lstm_ld(4 * KS);
@@ -461,8 +467,8 @@ lstm_fwd_reg_kernel(LstmFwdArgs a) {
         if (unit < H) hn[row * LDH + unit] = ok ? h : 0.f;
         if (ok) {
           a.hbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = h;
-          if (a.cbuf) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = c;
-          if (a.gates) {
+          if (a.cbuf && t < keepS) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)gr * H + unit] = c;
+          if (a.gates && t < keepS) {
             float* gp = a.gates + ((int64_t)t * B + gr) * G4 + unit;
             gp[0] = ig; gp[H] = fg; gp[2 * H] = cg; gp[3 * H] = og;
           }
@@ -609,6 +615,7 @@ template <int KP, int KX>
 __global__ void __launch_bounds__(kWG8)
 lstm_fwd_r4_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  const int keepS = a.keep > 0 ? a.keep : a.S;     // steps whose c / gates are stored
   constexpr int KXS = KX > 0 ? KX : 8;
   __shared__ __attribute__((aligned(16))) float hS[2][LR4 * KP];
   __shared__ __attribute__((aligned(16))) float xS[2][LR4 * KXS];
@@ -779,8 +786,8 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
       hn[crow * KP + cunit] = cok ? h : 0.f;
       if (cok) {
         a.hbuf[(int64_t)(t + 1) * BH + (int64_t)cgr * H + cunit] = h;
-        if (a.cbuf) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)cgr * H + cunit] = c;
-        if (a.gates) {
+        if (a.cbuf && t < keepS) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)cgr * H + cunit] = c;
+        if (a.gates && t < keepS) {
           float* gp = a.gates + ((int64_t)t * B + cgr) * G4 + cunit;
           gp[0] = ig; gp[H] = fg; gp[2 * H] = cg; gp[3 * H] = og;
         }
@@ -988,6 +995,7 @@ template <int R, int KP, int KX>
 __global__ void __launch_bounds__(kVT)
 lstm_fwd_v_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  const int keepS = a.keep > 0 ? a.keep : a.S;     // steps whose c / gates are stored
   constexpr int KXS = KX > 0 ? KX : 4;
   __shared__ __attribute__((aligned(16))) float hS[2][R * KP];
   // KX > 0: the segment rows' x for EVERY step, staged once before the
@@ -1129,9 +1137,9 @@ lstm_fwd_v_kernel(LstmFwdArgs a) {
         if (q == 0) {
           hn[r * KP + u] = h;
           a.hbuf[(int64_t)(t + 1) * BH + (int64_t)b * H + u] = h;
-          if (a.cbuf) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)b * H + u] = c;
+          if (a.cbuf && t < keepS) a.cbuf[(int64_t)(t + 1) * BH + (int64_t)b * H + u] = c;
         }
-        if (a.gates) a.gates[((int64_t)t * B + b) * G4 + g] = av;
+        if (a.gates && t < keepS) a.gates[((int64_t)t * B + b) * G4 + g] = av;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1232,6 +1240,311 @@ lstm_bwd_v_kernel(LstmBwdArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// One segment per workgroup with the recurrent product's K split over the
+// lane quad (round 5; R = 1 — a rank's share of a strong-scaled job).  The
+// R-segment kernels above give thread (u, q) a whole W_hh row, so every
+// thread reads all of h_{t-1} each step (26 ds_read_b128 per wave at H = 100:
+// 728 LDS cycles per CU per step) and runs one 104-long FMA stream.  Here
+// thread (u, q) = (tid >> 2, tid & 3) holds the FOUR gate rows j*H + u of
+// unit u over its quarter k in [q*KQ, (q+1)*KQ) as (k, k+1) pairs:
+//   forward  p_j = sum_k h_{t-1}[k] W_hh[j*H + u][k] on v_pk_fma_f32 (KQ/2
+//            packed FMAs per gate over 2-float LDS reads: 13 ds_read_b64 per
+//            wave), the four lanes' partials summed by two quad DPP adds
+//            (l ^ 1, then l ^ 2: every lane of the quad ends with the same
+//            four sums); lane q then finishes gate q exactly as the R forms
+//            do (activation, quad broadcast, the cell computed alike in the
+//            four lanes).  The x part is precomputed with the same K split of
+//            W_ih over the staged x sequence (XQ > 0), or read from xproj
+//            (XQ == 0) one step ahead.  W_hh is loaded while the x parts are
+//            formed; the step's hbuf / cbuf / gates stores are issued after
+//            the barrier, behind the next step's LDS reads.
+//   BPTT     thread (ug, rr) = (tid >> 4, tid & 15) holds W_hh[r][4ug..4ug+3]
+//            for the rows r in [rr*BR, rr*BR + BR) (BR = ceil(H / 4)), reads
+//            those BR dgates of the step (a [16][BRP] padded LDS image: b128
+//            reads, 64 distinct banks) and sums its four units on packed
+//            FMAs; the 16 partials of a unit meet through four DPP adds
+//            (quad l ^ 1, l ^ 2, row half-mirror, row rotate 8: identical
+//            sums in all 16 lanes), and the cell backward keeps the (u, q)
+//            mapping (unit u's sum sits in its own 16-lane row).
+// Measured (tools/exp/lstm_v_exp.hip, 128 segments, H 100, one MI355X): see
+// DESIGN.md §9.  Sums are fixed-order (deterministic); their association
+// differs from the R forms' (fp32 rounding only).
+__device__ __forceinline__ float dpp_x1(float v) {            // quad lane l ^ 1
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_x2(float v) {            // quad lane l ^ 2
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_hmirror(float v) {       // row_half_mirror
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_ror8(float v) {          // row_ror:8
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));
+}
+
+template <int KQ, int XQ>
+__global__ void __launch_bounds__(kVT)
+lstm_fwd_q_kernel(LstmFwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  const int keepS = a.keep > 0 ? a.keep : a.S;
+  static_assert(KQ % 2 == 0 && XQ % 4 == 0, "K split: pairs of h, float4 runs of x");
+  constexpr int KX = 4 * XQ, KXS = XQ > 0 ? KX : 4;
+  __shared__ __attribute__((aligned(16))) float hS[2][4 * KQ];
+  extern __shared__ __attribute__((aligned(16))) float xS[];    // [S][KXS] x, then [S][blockDim] x parts
+  float* xP = xS + (((int64_t)a.S * KXS + 3) & ~3);
+  const int H = a.H, B = a.B, G4 = 4 * H, NT = blockDim.x;
+  const int tid = threadIdx.x, u = tid >> 2, q = tid & 3;
+  const bool act = u < H;
+  const int uc = act ? u : H - 1;
+  const int g = q * H + uc;
+  const int b = blockIdx.x;
+  const int64_t BH = (int64_t)B * H;
+  float bh = a.b_hh[g];
+  // x staging, c0 / h0 (every load issued before W_hh's)
+  if constexpr (XQ > 0) {
+    bh += a.b_ih[g];
+    for (int e = tid; e < a.S * KX; e += NT) {
+      const int t = e / KX, k = e - t * KX;
+      xS[e] = k < a.din ? a.x[((int64_t)t * B + b) * a.ldx + k] : 0.f;
+    }
+  }
+  float creg = a.c0[(int64_t)b * H + uc];
+  if (act && q == 0 && a.cbuf) a.cbuf[(int64_t)b * H + u] = creg;
+  for (int e = tid; e < 4 * KQ; e += NT) {
+    const float v = e < H ? a.h0[(int64_t)b * H + e] : 0.f;
+    hS[0][e] = v;
+    hS[1][e] = 0.f;
+    if (e < H) a.hbuf[(int64_t)b * H + e] = v;
+  }
+  __syncthreads();
+  // W_hh rows j*H + u over k in [q*KQ, q*KQ + KQ): in flight during the x parts
+  vf2 wv[4][KQ / 2];
+  {
+    const bool vec = (H & 1) == 0 && (reinterpret_cast<uintptr_t>(a.w_hh) & 7) == 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* r = a.w_hh + (int64_t)(j * H + uc) * H;
+#pragma unroll
+      for (int i = 0; i < KQ / 2; ++i) {
+        const int k = q * KQ + 2 * i;
+        vf2 v;
+        if (vec) {
+          const float2 t2 = k + 1 < H ? *reinterpret_cast<const float2*>(r + k) : float2{0.f, 0.f};
+          v = vf2{t2.x, t2.y};
+        } else {
+          v = vf2{k < H ? r[k] : 0.f, k + 1 < H ? r[k + 1] : 0.f};
+        }
+        wv[j][i] = v;
+      }
+    }
+  }
+  if constexpr (XQ > 0) {
+    // x parts of every step: W_ih rows j*H + u over x columns [q*XQ, q*XQ + XQ)
+    float wx[4][XQ];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* r = a.w_ih + (int64_t)(j * H + uc) * a.din;
+#pragma unroll
+      for (int kk = 0; kk < XQ; ++kk) {
+        const int k = q * XQ + kk;
+        wx[j][kk] = k < a.din ? r[k] : 0.f;
+      }
+    }
+    for (int t = 0; t < a.S; ++t) {
+      const float4* xp = reinterpret_cast<const float4*>(xS + t * KX + q * XQ);
+      float pj[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k4 = 0; k4 < XQ / 4; ++k4) {
+        const float4 v = xp[k4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pj[j] = fmaf(v.x, wx[j][4 * k4], pj[j]);
+          pj[j] = fmaf(v.y, wx[j][4 * k4 + 1], pj[j]);
+          pj[j] = fmaf(v.z, wx[j][4 * k4 + 2], pj[j]);
+          pj[j] = fmaf(v.w, wx[j][4 * k4 + 3], pj[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pj[j] += dpp_x1(pj[j]);
+        pj[j] += dpp_x2(pj[j]);
+      }
+      const float mine = q == 0 ? pj[0] : q == 1 ? pj[1] : q == 2 ? pj[2] : pj[3];
+      xP[(int64_t)t * NT + tid] = mine + bh;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): W_hh (and xproj of step 0) landed
+  float* hb = a.hbuf + BH + (int64_t)b * H + uc;
+  float* cb = a.cbuf ? a.cbuf + BH + (int64_t)b * H + uc : nullptr;
+  float* gp = a.gates ? a.gates + (int64_t)b * G4 + g : nullptr;
+  const int64_t gstep = (int64_t)B * G4;
+  float xnext = 0.f;
+  if constexpr (XQ == 0) {
+    if (a.S > 0) xnext = a.xproj[(int64_t)b * G4 + g];
+  }
+  float ph = 0.f, pc = 0.f, pav = 0.f;
+  for (int t = 0; t < a.S; ++t) {
+    const float* hp = hS[t & 1] + q * KQ;
+    float* hn = hS[(t + 1) & 1];
+    float xacc;
+    if constexpr (XQ > 0) {
+      xacc = xP[(int64_t)t * NT + tid];
+    } else {
+      xacc = xnext + bh;
+    }
+    const float2* h2 = reinterpret_cast<const float2*>(hp);
+    float2 hv[KQ / 2];
+#pragma unroll
+    for (int i = 0; i < KQ / 2; ++i) hv[i] = h2[i];
+    if constexpr (XQ == 0) {          // xproj of step t + 1, in flight through the step
+      if (t + 1 < a.S) xnext = a.xproj[((int64_t)(t + 1) * B + b) * G4 + g];
+    }
+    // the previous step's stores, behind this step's LDS reads
+    if (t > 0 && act) {
+      if (q == 0) {
+        hb[0] = ph;
+        hb += BH;
+        if (cb && t - 1 < keepS) cb[0] = pc;
+        if (cb) cb += BH;
+      }
+      if (gp && t - 1 < keepS) gp[0] = pav;
+      if (gp) gp += gstep;
+    }
+    vf2 pp[4] = {vf2{0.f, 0.f}, vf2{0.f, 0.f}, vf2{0.f, 0.f}, vf2{0.f, 0.f}};
+#pragma unroll
+    for (int i = 0; i < KQ / 2; ++i) {
+      const vf2 h2v = vf2{hv[i].x, hv[i].y};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pp[j] = __builtin_elementwise_fma(h2v, wv[j][i], pp[j]);
+    }
+    float pj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pj[j] = pp[j].x + pp[j].y;
+      pj[j] += dpp_x1(pj[j]);
+      pj[j] += dpp_x2(pj[j]);
+    }
+    const float mine = q == 0 ? pj[0] : q == 1 ? pj[1] : q == 2 ? pj[2] : pj[3];
+    const float pre = xacc + mine;
+    const float av = q == 2 ? ftanh(pre) : sigm(pre);
+    const float ig = quad_bcast<0>(av), fg = quad_bcast<1>(av);
+    const float cg = quad_bcast<2>(av), og = quad_bcast<3>(av);
+    const float c = fg * creg + ig * cg;
+    const float h = og * ftanh(c);
+    creg = c;
+    if (act && q == 0) hn[u] = h;
+    ph = h; pc = c; pav = av;
+    __syncthreads();
+  }
+  if (a.S > 0 && act) {
+    if (q == 0) {
+      hb[0] = ph;
+      if (cb && a.S - 1 < keepS) cb[0] = pc;
+    }
+    if (gp && a.S - 1 < keepS) gp[0] = pav;
+  }
+}
+
+// BR: rows of W_hh per lane of a 16-lane row (16 BR >= 4H), BRP its padding to
+// whole b128 reads
+template <int BR>
+__global__ void __launch_bounds__(kVT)
+lstm_bwd_q_kernel(LstmBwdArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  constexpr int BRP = (BR + 3) & ~3;
+  __shared__ __attribute__((aligned(16))) float dG[2][16 * BRP];
+  const int H = a.H, B = a.B, G4 = 4 * H;
+  const int tid = threadIdx.x, u = tid >> 2, q = tid & 3;
+  const bool act = u < H;
+  const int uc = act ? u : H - 1;
+  const int g = q * H + uc;
+  const int b = blockIdx.x;
+  const int64_t BH = (int64_t)B * H;
+  const int ug = tid >> 4, rr = tid & 15;
+  for (int e = tid; e < 2 * 16 * BRP; e += blockDim.x) (&dG[0][0])[e] = 0.f;
+  // W_hh[r][4ug + i], r in [rr*BR, rr*BR + BR) (rows past 4H and units past H read as 0)
+  vf2 w01[BR], w23[BR];
+  {
+    const bool vec = (H & 3) == 0 && (reinterpret_cast<uintptr_t>(a.w_hh) & 15) == 0 && 4 * ug + 3 < H;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int r = rr * BR + i;
+      const bool rok = r < G4;
+      const float* row = a.w_hh + (int64_t)(rok ? r : 0) * H;
+      if (vec) {
+        const float4 v = rok ? *reinterpret_cast<const float4*>(row + 4 * ug) : float4{0.f, 0.f, 0.f, 0.f};
+        w01[i] = vf2{v.x, v.y};
+        w23[i] = vf2{v.z, v.w};
+      } else {
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = rok && 4 * ug + k < H ? row[4 * ug + k] : 0.f;
+        w01[i] = vf2{v[0], v[1]};
+        w23[i] = vf2{v[2], v[3]};
+      }
+    }
+  }
+  const int dgi = (g / BR) * BRP + g % BR;        // this lane's dgate in the padded image
+  float gq, ct, ctm, dho, gqn, ctn, ctmn, dhon;
+  auto fetch = [&](int t, float& G, float& C, float& CM, float& DH) {
+    G = a.gates[((int64_t)t * B + b) * G4 + g];
+    C = a.cbuf[(int64_t)(t + 1) * BH + (int64_t)b * H + uc];
+    CM = a.cbuf[(int64_t)t * BH + (int64_t)b * H + uc];
+    DH = a.dh[(int64_t)t * BH + (int64_t)b * H + uc];
+  };
+  if (a.S <= 0) return;
+  fetch(a.S - 1, gq, ct, ctm, dho);
+  fetch(a.S >= 2 ? a.S - 2 : 0, gqn, ctn, ctmn, dhon);
+  float dcreg = 0.f, dhr = 0.f;
+  __syncthreads();
+  for (int t = a.S - 1; t >= 0; --t) {
+    float* dgw = dG[t & 1];
+    const float ig = quad_bcast<0>(gq), fg = quad_bcast<1>(gq);
+    const float cg = quad_bcast<2>(gq), og = quad_bcast<3>(gq);
+    const float dh = dho + dhr;
+    const float tc = ftanh(ct);
+    const float dc = dh * og * (1.f - tc * tc) + dcreg;
+    const float d_o = (dh * tc) * (og * (1.f - og));
+    const float d_i = (dc * cg) * (ig * (1.f - ig));
+    const float d_g = (dc * ig) * (1.f - cg * cg);
+    const float d_f = (dc * ctm) * (fg * (1.f - fg));
+    dcreg = act ? dc * fg : 0.f;
+    float dq = q == 0 ? d_i : q == 1 ? d_f : q == 2 ? d_g : d_o;
+    dq = act ? dq : 0.f;
+    if (act) {
+      dgw[dgi] = dq;
+      a.dgates[((int64_t)t * B + b) * G4 + g] = dq;
+    }
+    gq = gqn; ct = ctn; ctm = ctmn; dho = dhon;
+    fetch(t >= 2 ? t - 2 : 0, gqn, ctn, ctmn, dhon);
+    __syncthreads();
+    if (t == 0) break;
+    const float4* dp = reinterpret_cast<const float4*>(dgw + rr * BRP);
+    float4 dv[BRP / 4];
+#pragma unroll
+    for (int i = 0; i < BRP / 4; ++i) dv[i] = dp[i];
+    vf2 p01 = {0.f, 0.f}, p23 = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const float d = (i & 3) == 0 ? dv[i >> 2].x : (i & 3) == 1 ? dv[i >> 2].y
+                    : (i & 3) == 2 ? dv[i >> 2].z : dv[i >> 2].w;
+      p01 = __builtin_elementwise_fma(vf2{d, d}, w01[i], p01);
+      p23 = __builtin_elementwise_fma(vf2{d, d}, w23[i], p23);
+    }
+    float pu[4] = {p01.x, p01.y, p23.x, p23.y};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pu[k] += dpp_x1(pu[k]);
+      pu[k] += dpp_x2(pu[k]);
+      pu[k] += dpp_hmirror(pu[k]);
+      pu[k] += dpp_ror8(pu[k]);
+    }
+    const int k = u & 3;                           // unit u = 4 ug + k
+    dhr = k == 0 ? pu[0] : k == 1 ? pu[1] : k == 2 ? pu[2] : pu[3];
+  }
+}
 #endif  // SMI_LSTM_VALU_HALF
 
 // VALU recurrence selection: SMI_LSTM_VALU = 0 (never), 1 (always when the
@@ -1315,12 +1628,45 @@ static void bwd_v_dispatch_kp(const LstmBwdArgs& a, hipStream_t st) {
 // the VALU forms' entry points for the launchers (the other half of the file
 // when it is compiled in two parts): kx 0 = xproj input, else the fused x
 // projection at R = 1 with x widths <= kx (48 / 64)
+// the K-split forms at one segment per workgroup (SMI_LSTM_Q=0: the R = 1
+// row forms instead; A/B knob)
+static bool use_q() {
+  static const bool on = [] { const char* e = getenv("SMI_LSTM_Q"); return !(e && e[0] == '0'); }();
+  return on;
+}
+template <int XQ>
+static void fwd_q_dispatch(const LstmFwdArgs& a, hipStream_t st) {
+  const dim3 grid(a.B), blk((4 * a.H + 63) & ~63);
+  const size_t lds = XQ > 0 ? lstm_fwd_v_lds(a.S, 1, 4 * XQ, blk.x) : 0;
+#define SMI_FQ(KQ)                                                                 \
+  do {                                                                             \
+    allow_lds(lstm_fwd_q_kernel<KQ, XQ>, lds);                                     \
+    hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ>), grid, blk, lds, st, a);        \
+  } while (0)
+  if (a.H <= 64) SMI_FQ(16);
+  else if (a.H <= 104) SMI_FQ(26);
+  else SMI_FQ(32);
+#undef SMI_FQ
+}
 void lstm_v_fwd(const LstmFwdArgs& a, int R, int kx, hipStream_t st) {
+  if (R == 1 && use_q()) {
+    if (kx == 0) fwd_q_dispatch<0>(a, st);
+    else if (kx <= 48) fwd_q_dispatch<12>(a, st);
+    else fwd_q_dispatch<16>(a, st);
+    return;
+  }
   if (kx == 0) fwd_v_dispatch(a, R, st);
   else if (kx <= 48) fwd_v_dispatch_kp<1, 48>(a, st);
   else fwd_v_dispatch_kp<1, 64>(a, st);
 }
 void lstm_v_bwd(const LstmBwdArgs& a, int R, hipStream_t st) {
+  if (R == 1 && use_q()) {
+    const dim3 grid(a.B), blk((4 * a.H + 63) & ~63);
+    if (a.H <= 64) hipLaunchKernelGGL(lstm_bwd_q_kernel<16>, grid, blk, 0, st, a);
+    else if (a.H <= 100) hipLaunchKernelGGL(lstm_bwd_q_kernel<25>, grid, blk, 0, st, a);
+    else hipLaunchKernelGGL(lstm_bwd_q_kernel<32>, grid, blk, 0, st, a);
+    return;
+  }
   if (R == 1) bwd_v_dispatch_kp<1>(a, st);
   else if (R == 2) bwd_v_dispatch_kp<2>(a, st);
   else bwd_v_dispatch_kp<4>(a, st);
@@ -1366,10 +1712,11 @@ int64_t lstm_bwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * H) * 4; }
 
 int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
                     const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,
-                    hipStream_t st, const int* skip) {
+                    hipStream_t st, const int* skip, int keep) {
   if (B <= 0 || S < 0) return SMI_OK;
   if (H < 1 || H > 256) return set_error(SMI_E_ARG, "lstm: hidden size must be in [1, 256]");
   LstmFwdArgs a{xproj, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates, skip};
+  a.keep = keep;
   const int kslot = ktime_begin(st);
   // algorithmic flops: the recurrent GEMM h W_hh^T of every step
   struct End { int s; hipStream_t st; double f;
@@ -1419,7 +1766,7 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
 int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, const float* b_ih,
                       const float* w_hh, const float* b_hh, const float* h0, const float* c0,
                       int S, int B, int H, float* hbuf, float* cbuf, float* gates,
-                      hipStream_t st, const int* skip) {
+                      hipStream_t st, const int* skip, int keep) {
   if (!use_r4() || din < 1 || din > 64 || H < 1 || H > 104) return SMI_E_NOFIT;
   if (B <= 0 || S < 0) return SMI_OK;
   const int R = lstm_valu_r(B, H);
@@ -1427,7 +1774,7 @@ int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, c
   if (R == 1 && lstm_fwd_v_lds(S, 1, din <= 48 ? 48 : 64, (4 * H + 63) & ~63) > kVxMax)
     return SMI_E_NOFIT;                            // staged x + x parts > the LDS budget
   LstmFwdArgs a{nullptr, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates, skip,
-                x, ldx, din, w_ih, b_ih};
+                x, ldx, din, w_ih, b_ih, keep};
   const int kslot = ktime_begin(st);
   struct End { int s; hipStream_t st; double f;
                ~End() { ktime_end(s, KT_LSTM_FWD, f, st); } } end_{

@@ -14,9 +14,6 @@
 
 namespace smi {
 
-int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
-                    const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,
-                    hipStream_t st, const int* skip);
 int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
                     int S, int B, int H, float* dgates, hipStream_t st, const int* skip);
 int launch_gae_windows(const float* values, float* values_masked, const float* rewards,
@@ -41,7 +38,7 @@ enum {
 enum { FS_SE = 0, FS_D, FS_D2, FS_R, FS_R2, FS_Z = 5 };
 
 // device control block (int / float scratch)
-enum { CI_STOP = 0, CI_RUNS, CI_NG, CI_COUNT = 8 };
+enum { CI_STOP = 0, CI_RUNS, CI_NG, CI_NP, CI_COUNT = 8 };
 enum { CF_KLCOEF = 0, CF_SURRW, CF_COUNT = 8 };
 
 struct RnnDims {
@@ -342,7 +339,12 @@ zf_tile_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next
 
 // values[b][t] = vt[t*B + b]
 __global__ void __launch_bounds__(kWG)
-tmajor_to_bmajor_kernel(const float* __restrict__ vt, int S, int B, float* __restrict__ v) {
+tmajor_to_bmajor_kernel(const float* __restrict__ vt, int S, int B, float* __restrict__ v,
+                        int* ci, float* cf) {
+  // the learn()'s device control state starts at zero (was rnn_init_kernel,
+  // a launch of its own): nothing before this point of the GAE phase reads it
+  if (blockIdx.x == 0 && ci && threadIdx.x < CI_COUNT) ci[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && cf && threadIdx.x < CF_COUNT) cf[threadIdx.x] = 0.f;
   const int64_t n = (int64_t)S * B;
   for (int64_t e = (int64_t)blockIdx.x * kWG + threadIdx.x; e < n; e += (int64_t)gridDim.x * kWG) {
     const int b = (int)(e / S), t = (int)(e - (int64_t)b * S);
@@ -350,20 +352,34 @@ tmajor_to_bmajor_kernel(const float* __restrict__ vt, int S, int B, float* __res
   }
 }
 
-// fixed-order reduction of [nb][w] double partials -> out[w] (one workgroup)
+// fixed-order reduction of [nb][w] double partials -> out[w] (one workgroup).
+// Column j is summed by a group of L lanes (L the largest power of two <= 64
+// with w * L <= kWG, so a group never straddles a wave): lane l of the group
+// adds partials l, l + L, ... in order, then a butterfly over the group.  (One
+// wave per column left a 2 x 42-column ZFilter reduction 21 serial
+// butterflies deep per wave: 29 us for 21.5 K doubles.)  cnt != null: also
+// out[w] = n (the advantage count of the GAE moments)
 __global__ void __launch_bounds__(kWG)
 reduce_partials_kernel(const double* __restrict__ part, int nb, int w, double* out,
-                       const int* skip) {
+                       const int* skip, double* cnt, double n) {
   if (skip && skip[0] != 0) return;
-  // one wave per column (fixed lane-strided order + butterfly): no barriers
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int j = wave; j < w; j += kNW) {
+  if (cnt && threadIdx.x == 0) cnt[0] = n;
+  int L = 64;
+  while (L > 1 && w * L > kWG) L >>= 1;
+  const int j = threadIdx.x / L, l = threadIdx.x - j * L;
+  for (int jj = j; jj < w; jj += kWG / L) {
     double s = 0.0;
-    for (int i = lane; i < nb; i += 64) s += part[(int64_t)i * w + j];
-    s = wave_sum_d(s);
-    if (lane == 0) out[j] = s;
+    for (int i = l; i < nb; i += L) s += part[(int64_t)i * w + jj];
+    for (int o = L >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (l == 0) out[jj] = s;
   }
 }
+
+struct DecideArgs {
+  const double* ps; int e, Ep, mode; double kl_target; float eta; int64_t N;
+  const float* hyper; const float* lv; int A; float c_ent;
+  int* ci; float* cf; float* stats;
+};
 
 struct PolRowArgs {
   int B, T, E, A, mode;
@@ -388,6 +404,12 @@ struct PolRowArgs {
   float* lvpart;          // [nblk][A] (grad pass)
   const float* cf;        // device coefficients (grad pass)
   float invN;
+  // grad pass, single rank: the statistics pass's partials ([dec_nb][PS_N]) and
+  // the decision's arguments; each block reduces them itself (the order of
+  // reduce_decide_kernel) and decides, block 0 writes the decision's outputs
+  // (one launch fewer per epoch than reduce_decide_kernel + this pass)
+  const double* dec_part; int dec_nb;
+  DecideArgs dec;
 };
 
 // ppo.py:402-405: (adv - mean) / max(std, 1e-4), std unbiased over all B*E;
@@ -479,8 +501,10 @@ __device__ __forceinline__ float row_kl(const float* mu0, const float* sd0, cons
 // row_loglik with the std's reciprocal: (a - mu) * (1 / sd) instead of the
 // IEEE divide (one rounding more, within the parity envelope): the learner's
 // std is a per-column constant (reciprocal hoisted out of the row loop), the
-// behaviour policy's is per row (one v_rcp_f32 shared by every term of the
-// row that divides by it)
+// behaviour policy's is per row (one IEEE-rounded 1.f / sd per row element,
+// shared by every term of the row that divides by it; not the approximate
+// v_rcp_f32, whose ~1 ulp error and denormal flush the learner-std path does
+// not have either)
 template <int AT>
 __device__ __forceinline__ float row_loglik_r(const float* act, const float* mu, const float* isd,
                                               const float* logsd, int A, float c_ll) {
@@ -635,7 +659,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
 #pragma unroll
     for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
       blsd[j] = logf(bsd[j]);
-      ibsd[j] = __builtin_amdgcn_rcpf(bsd[j]);
+      ibsd[j] = 1.f / bsd[j];
     }
     const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
     acc[PS_KL] += (double)row_kl_cc<AT>(rm, m, lkl, s02, iden2, A);
@@ -725,6 +749,73 @@ policy_rows_stats_kernel(PolRowArgs a) {
   }
 }
 
+// After the (all-reduced) policy sums of POLICY_FWD(e): early stop, adapt
+// coefficient and statistics (ppo.py:265-284, 541-557, 568-575).  ps = the
+// sums; write = store the decision (stats, stop flag, coefficients), else only
+// return it (the blocks of a fused gradient pass other than block 0)
+struct Decision { int stop; float surrw, klcoef; };
+__device__ Decision policy_decide_body(const DecideArgs& a, const double* ps, bool write) {
+  Decision r{1, 0.f, 0.f};
+  if (a.ci[CI_STOP]) return r;
+  const double n = (double)a.N;
+  const float kl = (float)(ps[PS_KL] / n);
+  // statistics of the forward with the current parameters (curr_pol after the
+  // previous update, or ref/behave terms before any)
+  if (write) {
+    a.stats[SMI_ST_AVG_IS_WEIGHT] = (float)(ps[PS_ISW] / n);
+    a.stats[SMI_ST_AVG_BEHAVE_LIK] = (float)(ps[PS_BL] / n);
+    a.stats[SMI_ST_REF_BEHAVE_DIFF] = (float)(ps[PS_RBD] / n);
+    a.stats[SMI_ST_AVG_RETURN] = (float)(ps[PS_RET] / n);
+  }
+  if (a.e >= 1) {
+    if (write) a.stats[SMI_ST_POL_KL] = kl;                 // ppo.py:555
+    if ((double)kl > a.kl_target * 4.0) {                    // ppo.py:556
+      if (write) a.ci[CI_STOP] = 1;
+      return r;
+    }
+  }
+  if (a.e >= a.Ep) {
+    if (write) a.ci[CI_STOP] = 1;                            // loop finished
+    return r;
+  }
+  r.stop = 0;
+  // loss statistics of update e
+  r.surrw = (float)(1.0 / n);
+  if (write) {
+    float ent = 0.f;
+    for (int j = 0; j < a.A; ++j) ent += logf(expf(a.lv[j]));
+    ent = 0.5f * ent + a.c_ent;
+    a.stats[SMI_ST_ENTROPY] = ent;
+    a.cf[CF_SURRW] = r.surrw;
+  }
+  if (a.mode == 0) {
+    if (write) {
+      a.stats[SMI_ST_SURR_LOSS] = (float)(ps[PS_SURR] / n);
+      a.stats[SMI_ST_CLIP_SURR_LOSS] = (float)(ps[PS_CLIP] / n);
+      a.cf[CF_KLCOEF] = 0.f;
+    }
+  } else {
+    const float beta = a.hyper[SMI_HYP_BETA];
+    const float surr = -(float)(ps[PS_SURR] / n);
+    float loss = surr + beta * kl;
+    float coef = beta;
+    if ((double)kl - 2.0 * a.kl_target > 0.0) {              // ppo.py:275
+      const float d = kl - (float)(2.0 * a.kl_target);
+      loss += a.eta * (d * d);
+      coef += 2.f * a.eta * d;
+    }
+    r.klcoef = (float)(coef / n);
+    if (write) {
+      a.stats[SMI_ST_SURR_LOSS] = surr;
+      a.stats[SMI_ST_KL_LOSS_ADAPT] = loss;
+      a.stats[SMI_ST_POL_KL_ADAPT] = kl;
+      a.stats[SMI_ST_POL_KL] = kl;
+      a.cf[CF_KLCOEF] = r.klcoef;
+    }
+  }
+  return r;
+}
+
 // per-row gradient of the policy loss w.r.t. the tanh pre-activation (dz) and
 // block partials of d loss / d log_var (ppo_net.py:29-72, ppo.py:209-217,
 // 267-277): surrogate weight cf[CF_SURRW] (1/N), KL weight cf[CF_KLCOEF] (adapt:
@@ -756,7 +847,41 @@ policy_rows_grad_kernel(PolRowArgs a) {
     rs2[j] = rsig * rsig;
   }
   const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
-  const float wsurr = a.cf[CF_SURRW], wkl = a.cf[CF_KLCOEF];
+  float wsurr, wkl;
+  if (a.dec_part) {
+    // the statistics pass's sums, reduced as reduce_decide_kernel does (lane
+    // i sums blocks i, i + 64, ... in order, then the wave butterfly): every
+    // block reaches the same sums and the same decision
+    __shared__ double sps[PS_N];
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < 64) {
+      double t[PS_N];
+#pragma unroll
+      for (int j = 0; j < PS_N; ++j) t[j] = 0.0;
+      for (int i = lane; i < a.dec_nb; i += 64) {
+#pragma unroll
+        for (int j = 0; j < PS_N; ++j) t[j] += a.dec_part[(int64_t)i * PS_N + j];
+      }
+#pragma unroll
+      for (int j = 0; j < PS_N; ++j) {
+        const double u = wave_sum_d(t[j]);
+        if (lane == 0) sps[j] = u;
+      }
+    }
+    __syncthreads();
+    const bool wr = blockIdx.x == 0 && threadIdx.x == 0;
+    if (wr) {
+      double* out = const_cast<double*>(a.dec.ps);
+      for (int j = 0; j < PS_N; ++j) out[j] = sps[j];
+    }
+    const Decision dd = policy_decide_body(a.dec, sps, wr);
+    if (dd.stop) return;
+    wsurr = dd.surrw;
+    wkl = dd.klcoef;
+  } else {
+    wsurr = a.cf[CF_SURRW];
+    wkl = a.cf[CF_KLCOEF];
+  }
   float glv[AM];
 #pragma unroll
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
@@ -777,7 +902,7 @@ policy_rows_grad_kernel(PolRowArgs a) {
 #pragma unroll
     for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
       blsd[j] = logf(bsd[j]);
-      ibsd[j] = __builtin_amdgcn_rcpf(bsd[j]);
+      ibsd[j] = 1.f / bsd[j];
     }
     const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
     float g_lp;
@@ -823,79 +948,10 @@ policy_rows_grad_kernel(PolRowArgs a) {
   }
 }
 
-// d log_var[j] = std_j * sum_blocks lvpart[.][j]   (std = exp(log_var) broadcast)
-__global__ void logvar_grad_kernel(const float* __restrict__ lvpart, int nb, int A,
-                                   const float* lv, float* g, const int* skip) {
-  if (skip && skip[0] != 0) return;
-  // one wave per log_var entry (fixed lane-strided order + butterfly)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int j = wave; j < A; j += nw) {
-    float s = 0.f;
-    for (int i = lane; i < nb; i += 64) s += lvpart[(int64_t)i * A + j];
-    s = wave_sum(s);
-    if (lane == 0) g[j] = s * expf(lv[j]);
-  }
-}
-
-// After the (all-reduced) policy sums of POLICY_FWD(e): early stop, adapt
-// coefficient and statistics (ppo.py:265-284, 541-557, 568-575).
-struct DecideArgs {
-  const double* ps; int e, Ep, mode; double kl_target; float eta; int64_t N;
-  const float* hyper; const float* lv; int A; float c_ent;
-  int* ci; float* cf; float* stats;
-};
-__device__ void policy_decide_body(const DecideArgs& a) {
-  if (a.ci[CI_STOP]) return;
-  const double n = (double)a.N;
-  const float kl = (float)(a.ps[PS_KL] / n);
-  // statistics of the forward with the current parameters (curr_pol after the
-  // previous update, or ref/behave terms before any)
-  a.stats[SMI_ST_AVG_IS_WEIGHT] = (float)(a.ps[PS_ISW] / n);
-  a.stats[SMI_ST_AVG_BEHAVE_LIK] = (float)(a.ps[PS_BL] / n);
-  a.stats[SMI_ST_REF_BEHAVE_DIFF] = (float)(a.ps[PS_RBD] / n);
-  a.stats[SMI_ST_AVG_RETURN] = (float)(a.ps[PS_RET] / n);
-  if (a.e >= 1) {
-    a.stats[SMI_ST_POL_KL] = kl;                            // ppo.py:555
-    if ((double)kl > a.kl_target * 4.0) {                    // ppo.py:556
-      a.ci[CI_STOP] = 1;
-      return;
-    }
-  }
-  if (a.e >= a.Ep) {
-    a.ci[CI_STOP] = 1;                                       // loop finished
-    return;
-  }
-  // loss statistics of update e
-  float ent = 0.f;
-  for (int j = 0; j < a.A; ++j) ent += logf(expf(a.lv[j]));
-  ent = 0.5f * ent + a.c_ent;
-  a.stats[SMI_ST_ENTROPY] = ent;
-  a.cf[CF_SURRW] = (float)(1.0 / n);
-  if (a.mode == 0) {
-    a.stats[SMI_ST_SURR_LOSS] = (float)(a.ps[PS_SURR] / n);
-    a.stats[SMI_ST_CLIP_SURR_LOSS] = (float)(a.ps[PS_CLIP] / n);
-    a.cf[CF_KLCOEF] = 0.f;
-  } else {
-    const float beta = a.hyper[SMI_HYP_BETA];
-    const float surr = -(float)(a.ps[PS_SURR] / n);
-    float loss = surr + beta * kl;
-    float coef = beta;
-    if ((double)kl - 2.0 * a.kl_target > 0.0) {              // ppo.py:275
-      const float d = kl - (float)(2.0 * a.kl_target);
-      loss += a.eta * (d * d);
-      coef += 2.f * a.eta * d;
-    }
-    a.stats[SMI_ST_SURR_LOSS] = surr;
-    a.stats[SMI_ST_KL_LOSS_ADAPT] = loss;
-    a.stats[SMI_ST_POL_KL_ADAPT] = kl;
-    a.stats[SMI_ST_POL_KL] = kl;
-    a.cf[CF_KLCOEF] = (float)(coef / n);
-  }
-}
 
 __global__ void policy_decide_kernel(DecideArgs a) {
   if (threadIdx.x != 0) return;
-  policy_decide_body(a);
+  policy_decide_body(a, a.ps, true);
 }
 
 // single rank (no exchange between the two): the pstat reduction and the
@@ -912,7 +968,7 @@ reduce_decide_kernel(const double* __restrict__ part, int nb, DecideArgs a, cons
     if (lane == 0) out[j] = t;
   }
   __syncthreads();
-  if (threadIdx.x == 0) policy_decide_body(a);
+  if (threadIdx.x == 0) policy_decide_body(a, a.ps, true);
 }
 
 // value loss rows: V and the returns, both time-major [NE]; dV = 2 (V - R) / N
@@ -983,6 +1039,7 @@ struct AdamSplitArgs {
   int* step; const float* lr_ptr; float beta1, beta2, eps, wd, max_norm;
   const double* part; int np;
   const int* skip; float* norm_out; int* runs;
+  const int* np_dev;     // non-null: the partial count on the device (a fused sum of squares)
 };
 __global__ void __launch_bounds__(kWG)
 adam_split_kernel(AdamSplitArgs a) {
@@ -990,9 +1047,10 @@ adam_split_kernel(AdamSplitArgs a) {
   __shared__ double red[kNW];
   __shared__ float s_coef;
   double s = 0.0;
-  for (int i = threadIdx.x; i < a.np; i += kWG) s += a.part[i];
+  const int np = a.np_dev ? a.np_dev[0] : a.np;
+  for (int i = threadIdx.x; i < np; i += kWG) s += a.part[i];
   s = block_sum_d(s, red);
-  const int t = a.step[0];      // already bumped by sumsq_part_kernel
+  const int t = a.step[0];      // already bumped (sumsq_part_kernel or the dW reducer's epilogue)
   if (threadIdx.x == 0) {
     const float norm = (float)sqrt(s);
     float coef = 1.f;
@@ -1074,13 +1132,6 @@ __global__ void rnn_final_kernel(FinalArgs a) {
     if (k < a.kl_capacity) a.kl_record[k] = a.stats[SMI_ST_POL_KL];
     a.kl_count[0] = k + 1;
   }
-}
-
-__global__ void set_count_kernel(double* dst, double n) { dst[0] = n; }
-
-__global__ void rnn_init_kernel(int* ci, float* cf) {
-  if (threadIdx.x < CI_COUNT) ci[threadIdx.x] = 0;
-  if (threadIdx.x < CF_COUNT) cf[threadIdx.x] = 0.f;
 }
 
 // ------------------------------------------------------------ host phases
@@ -1289,9 +1340,11 @@ static LstmP lstm_layer(const RnnDims& d, const float* p, int l) {
 // (fused input projection when it fits, else xproj GEMM + recurrence), layer
 // l >= 1 reads layer l-1's outputs hbuf_l-1[1..S]; keep: store the cell states
 // and gate activations of every layer for a backward
+// keep_steps: with keep, the cell states / gates are stored for the first
+// keep_steps steps only (0: all S; the GAE pass over S1 steps keeps E)
 static int lstm_forward(const RnnDims& d, const float* P, const float* X, int S, const float* h0,
                         const float* c0, const RnnScratch& s, bool keep, hipStream_t st,
-                        const int* skip) {
+                        const int* skip, int keep_steps = 0) {
   const int64_t BH = (int64_t)d.B * d.H;
   for (int l = 0; l < d.L; ++l) {
     const LstmP lp = lstm_layer(d, P, l);
@@ -1302,13 +1355,13 @@ static int lstm_forward(const RnnDims& d, const float* P, const float* X, int S,
     float* cb = keep ? cbuf_of(d, s, l) : nullptr;
     float* gt = keep ? gates_of(d, s, l) : nullptr;
     const int rf = launch_lstm_fwd_x(Xl, ldx, din, lp.Wih, lp.bih, lp.Whh, lp.bhh, h0 + l * BH,
-                                     c0 + l * BH, S, d.B, d.H, hb, cb, gt, st, skip);
+                                     c0 + l * BH, S, d.B, d.H, hb, cb, gt, st, skip, keep_steps);
     if (rf == SMI_E_NOFIT) {
       const int64_t rows = (int64_t)S * d.B;
       RC(launch_linear_fwd(Xl, ldx, (int)rows, din, lp.Wih, din, lp.bih, d.G4, ACT_NONE, s.xproj,
                            d.G4, st, skip));
       RC(launch_lstm_fwd(s.xproj, lp.Whh, lp.bhh, h0 + l * BH, c0 + l * BH, S, d.B, d.H, hb, cb, gt,
-                         st, skip));
+                         st, skip, keep_steps));
     } else if (rf) {
       return rf;
     }
@@ -1410,10 +1463,13 @@ static int stem_backward_chain(const smi_ppo_rnn_args& a, const RnnDims& d, cons
 
 // every weight gradient of the phase (head layers + LSTM) queued and run as
 // one grouped launch after the input-gradient chain and BPTT
+// ex: the reducer's epilogue task (the log_var gradient, the clip-norm partials)
 static int stem_backward(const smi_ppo_rnn_args& a, const RnnDims& d, const Head& hd,
                          const LstmP& lm, const float* cnn, float* G, const RnnScratch& s,
-                         int64_t n_head, hipStream_t st, const int* skip) {
+                         int64_t n_head, hipStream_t st, const int* skip,
+                         const DwEpilogue* ex = nullptr) {
   dw_group_begin();
+  if (ex) RC(dw_group_epilogue(*ex));
   const int rc = stem_backward_chain(a, d, hd, lm, cnn, G, s, n_head, st, skip);
   const int rf = dw_group_flush(st);     // always flush: nothing stays queued after an error
   return rc ? rc : rf;
@@ -1442,6 +1498,23 @@ static PolRowArgs pol_rows(const smi_ppo_rnn_args& a, const RnnDims& d, const Rn
   return p;
 }
 
+// One rank with no pixel stem: the optimizer's clip_grad_norm_ partials come
+// from the dW group's reducer (every gradient of [head | lstm] but log_var is a
+// reducer output, log_var is the reducer's epilogue task), so the APPLY phases
+// run Adam alone.  Data parallel: the norm is of the all-reduced gradient, so
+// the sums of squares stay in APPLY (sumsq_part_kernel); with the pixel stem
+// the CNN gradient is not a reducer output.
+static bool fused_clip_norm(const smi_ppo_rnn_args& a, const RnnDims& d) {
+  static const bool off = [] { const char* e = getenv("SMI_FUSED_NORM"); return e && e[0] == '0'; }();
+  return !off && a.B_global == a.B && d.F == 0 && d.L <= 3 && fault() == 0;
+}
+// adapt mode, one rank, a policy epoch that trains: the decision of POLICY_FWD
+// (early stop, KL coefficient, statistics) is taken by the gradient pass of
+// POLICY_BWD itself (policy_rows_grad_kernel, dec_part)
+static bool fused_decide(const smi_ppo_rnn_args& a, int e) {
+  return a.mode != 0 && a.B_global == a.B && e < a.epoch_policy && fault() == 0;
+}
+
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
   const RnnDims d = rnn_dims(a.B, a.T, a.horizon, a.obs_dim, a.rnn_hidden, a.h1, a.h2, a.act_dim,
                              a.critic_h1, a.critic_h2, a.pix_c, a.pix_h, a.pix_w, a.cnn_feat,
@@ -1458,18 +1531,21 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
   const int64_t NEg = (int64_t)d.E * a.B_global;
   switch (phase) {
     case SMI_RNN_PH_GAE: {
-      hipLaunchKernelGGL(rnn_init_kernel, dim3(1), dim3(64), 0, st, s.ci, s.cf);
-      RC(check_launch("rnn_init_kernel"));
       int kt = ktime_begin(st);
       launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum, a.zf_sumsq,
                        a.zf_count, a.zf_eps, s.Xz, d.ldx, st);
       ktime_end(kt, KT_ZF_TMAJOR, 8.0 * (double)d.NG * d.D, st);      // read x, write z(x)
       RC(check_launch("zf_tmajor_kernel"));
       RC(cnn_features(a, d, cnn, d.S1, s.Xz, nullptr, s, st, nullptr));
-      if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.S1, a.h0, a.c0, s, false, st, nullptr));
+      // the critic's LSTM pass over T + 1 steps (ppo.py:385) with the cell
+      // states and gates of its first E steps kept: the first policy forward
+      // (ppo.py:253-262 at epoch 0) is the same recurrence over the same
+      // inputs from the same (h0, c0) with the same parameters, so
+      // POLICY_FWD(0) reads these instead of recomputing them
+      if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.S1, a.h0, a.c0, s, true, st, nullptr, d.E));
       RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
       hipLaunchKernelGGL(tmajor_to_bmajor_kernel, dim3(grid_of(d.NG)), dim3(kWG), 0, st, s.OUT,
-                         d.S1, d.B, s.values);
+                         d.S1, d.B, s.values, s.ci, s.cf);
       RC(check_launch("tmajor_to_bmajor_kernel"));
       int np = 0;
       kt = ktime_begin(st);
@@ -1478,10 +1554,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       // r, d (8 B) + V (4 (T+1)/T B) per env-step, adv + ret (8 B) per window
       ktime_end(kt, KT_GAE, (double)d.B * (8.0 * d.T + 4.0 * d.S1 + 8.0 * d.E), st);
       hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.gaepart, np, 2,
-                         a.moments, nullptr);
-      RC(check_launch("reduce_partials_kernel"));
-      hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(1), 0, st, a.moments + 2, (double)d.NE);
-      return check_launch("set_count_kernel");
+                         a.moments, nullptr, a.moments + 2, (double)d.NE);
+      return check_launch("reduce_partials_kernel");
     }
     case SMI_RNN_PH_PREP: {
       // ref_pol (ppo.py:539): the reference model's forward over obs_iter.
@@ -1512,7 +1586,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
         RC(check_launch("adv_export_kernel"));
       }
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, stop));
-      if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, stop));
+      if (d.H > 0 && e > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, stop));
       RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop, s.wT));
       PolRowArgs p = pol_rows(a, d, s);
       const int nb = a.mode == 0 ? pol_stats_blocks<true>(d.A, d.NE) : pol_stats_blocks<false>(d.A, d.NE);
@@ -1523,6 +1597,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
       ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
       RC(check_launch("policy_rows_stats_kernel"));
+      if (fused_decide(a, e)) return SMI_OK;     // decided by POLICY_BWD's gradient pass
       if (a.B_global == a.B) {         // one rank: nothing to exchange before the decision
         DecideArgs da{a.pstat, e, a.epoch_policy, a.mode,
                       a.kl_target, a.kl_cutoff_coeff, NEg, a.hyper, a.actor + d.LA.flv, d.A,
@@ -1531,7 +1606,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
         return check_launch("reduce_decide_kernel");
       }
       hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, PS_N,
-                         a.pstat, stop);
+                         a.pstat, stop, nullptr, 0.0);
       return check_launch("reduce_partials_kernel");
     }
     case SMI_RNN_PH_POLICY_DECIDE: {   // after the pstat all-reduce
@@ -1547,6 +1622,13 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       PolRowArgs p = pol_rows(a, d, s);
       // clip: the log_var partials came from POLICY_FWD's fused pass, over its grid
       const int nb = a.mode == 0 ? pol_stats_blocks<true>(d.A, d.NE) : rnn_nblk(d.NE, kRowNT);
+      if (fused_decide(a, e)) {
+        p.dec_part = s.part;
+        p.dec_nb = pol_stats_blocks<false>(d.A, d.NE);
+        p.dec = DecideArgs{a.pstat, e, a.epoch_policy, a.mode,
+                           a.kl_target, a.kl_cutoff_coeff, NEg, a.hyper, a.actor + d.LA.flv, d.A,
+                           c_entropy_of(d.A), s.ci, s.cf, a.stats};
+      }
       if (a.mode != 0) {     // clip: dz and the log_var partials came with POLICY_FWD's pass
         const int kt = ktime_begin(st);
         switch (d.A) {   // compile-time action widths 1..8 (registers); others generic
@@ -1564,31 +1646,49 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
         ktime_end(kt, KT_POLICY_GRAD, 4.0 * (double)d.NE * (6 * d.A + 1), st);
         RC(check_launch("policy_rows_grad_kernel"));
       }
-      RC(stem_backward(a, d, actor, lm, cnn, gA, s, d.nA_head, st, stop));
-      hipLaunchKernelGGL(logvar_grad_kernel, dim3(1), dim3(kWG), 0, st, s.lvpart, nb, d.A,
-                         a.actor + d.LA.flv, gA + d.LA.flv, stop);
-      return check_launch("logvar_grad_kernel");
+      // the log_var gradient (and, fused, the clip-norm partials and the step
+      // bump) as the dW reducer's epilogue task
+      const bool fn = fused_clip_norm(a, d);
+      DwEpilogue ex{};
+      ex.lvpart = s.lvpart; ex.lv_nb = nb; ex.lv_A = d.A;
+      ex.lv = a.actor + d.LA.flv; ex.lv_out = gA + d.LA.flv;
+      ex.skip = stop;
+      if (fn) {
+        ex.sq = s.part; ex.np = s.ci + CI_NP;
+        ex.step = a.actor_step; ex.runs = s.ci + CI_RUNS;
+      }
+      return stem_backward(a, d, actor, lm, cnn, gA, s, d.nA_head, st, stop, &ex);
     }
     case SMI_RNN_PH_POLICY_APPLY: {
       if (fault() == SMI_FAULT_POLICY_EPOCH_SHORT && e == a.epoch_policy - 1) return SMI_OK;
       const int64_t n = d.nA_head + d.nS;
       const int g = grid_of(n, 1024);
       const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gA, n, s.part, stop,
-                         a.actor_step, s.ci + CI_RUNS);
-      RC(check_launch("sumsq_part_kernel"));
+      const bool fn = fused_clip_norm(a, d);
+      if (!fn) {
+        hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gA, n, s.part, stop,
+                           a.actor_step, s.ci + CI_RUNS);
+        RC(check_launch("sumsq_part_kernel"));
+      }
       AdamSplitArgs aa{a.actor, d.nA_head, a.lstm, d.nS, gA, a.actor_m, a.actor_v, a.actor_step,
                        a.hyper + SMI_HYP_LR_ACTOR, a.beta1, a.beta2, a.adam_eps, a.actor_wd,
                        a.clip_actor_grad ? a.actor_max_norm : 0.f, s.part, g, stop,
-                       a.clip_actor_grad ? a.stats + SMI_ST_GRAD_NORM_ACTOR : nullptr, nullptr};
+                       a.clip_actor_grad ? a.stats + SMI_ST_GRAD_NORM_ACTOR : nullptr, nullptr,
+                       fn ? s.ci + CI_NP : nullptr};
       hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(kWG), 0, st, aa);
       // grad-norm pass (g: 4 B) + Adam (p, g, m, v read 16 B; p, m, v written 12 B)
       ktime_end(kt, KT_ADAM, 32.0 * (double)n, st);
       return check_launch("adam_split_kernel");
     }
     case SMI_RNN_PH_VALUE_GRAD: {
-      RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
-      if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, nullptr));
+      // value epoch 0: the last policy forward that ran (the KL check after
+      // the last policy update, ppo.py:553-556, or the epoch-0 forward with
+      // no update) left the stem's outputs, cell states, gates and conv
+      // activations of exactly the current parameters: reused, not recomputed
+      if (e > 0) {
+        RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, nullptr));
+        if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, nullptr));
+      }
       // dV = 2 (V - R) / N: written by the head forward's epilogue, except in
       // the last epoch, whose value_rows pass also sums the statistics of
       // ppo.py:324-331 (and on the layer-GEMM path)
@@ -1607,10 +1707,15 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       }
       if (last) {
         hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, s.part, nb, 5,
-                           a.zbuf, nullptr);
+                           a.zbuf, nullptr, nullptr, 0.0);
         RC(check_launch("reduce_partials_kernel"));
       }
-      return stem_backward(a, d, critic, lm, cnn, gC, s, d.nC_head, st, nullptr);
+      if (!fused_clip_norm(a, d))
+        return stem_backward(a, d, critic, lm, cnn, gC, s, d.nC_head, st, nullptr);
+      DwEpilogue ex{};                // the clip-norm partials and the step bump
+      ex.sq = s.part; ex.np = s.ci + CI_NP;
+      ex.step = a.critic_step;
+      return stem_backward(a, d, critic, lm, cnn, gC, s, d.nC_head, st, nullptr, &ex);
     }
     case SMI_RNN_PH_VALUE_APPLY: {
       if (fault() == SMI_FAULT_CRITIC_ADAM_SKIP) return SMI_OK;
@@ -1618,14 +1723,17 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       const int64_t n = d.nC_head + nS;
       const int g = grid_of(n, 1024);
       const int kt = ktime_begin(st);
-      hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gC, n, s.part, nullptr,
-                         a.critic_step, nullptr);
-      RC(check_launch("sumsq_part_kernel"));
+      const bool fn = fused_clip_norm(a, d);
+      if (!fn) {
+        hipLaunchKernelGGL(sumsq_part_kernel, dim3(g), dim3(kWG), 0, st, gC, n, s.part, nullptr,
+                           a.critic_step, nullptr);
+        RC(check_launch("sumsq_part_kernel"));
+      }
       AdamSplitArgs aa{a.critic, d.nC_head, a.lstm, nS, gC, a.critic_m, a.critic_v,
                        a.critic_step, a.hyper + SMI_HYP_LR_CRITIC, a.beta1, a.beta2, a.adam_eps,
                        a.critic_wd, a.clip_critic_grad ? a.critic_max_norm : 0.f, s.part, g,
                        nullptr, a.clip_critic_grad ? a.stats + SMI_ST_GRAD_NORM_CRITIC : nullptr,
-                       nullptr};
+                       nullptr, fn ? s.ci + CI_NP : nullptr};
       hipLaunchKernelGGL(adam_split_kernel, dim3(g), dim3(kWG), 0, st, aa);
       ktime_end(kt, KT_ADAM, 32.0 * (double)n, st);
       return check_launch("adam_split_kernel");
@@ -1640,7 +1748,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                          d.D, part);
       RC(check_launch("obs_iter_colsum_kernel"));
       hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kWG), 0, st, part, nb, 2 * d.D,
-                         a.zbuf + FS_Z, nullptr);
+                         a.zbuf + FS_Z, nullptr, nullptr, 0.0);
       return check_launch("reduce_partials_kernel");
     }
     case SMI_RNN_PH_ZAPPLY: {

@@ -44,6 +44,22 @@ int launch_linear_bwd_dw2(const float* dY, int64_t ldg, int M, int N, const floa
 // stay unchanged until the flush) and then run as ONE launch + ONE reduce
 int dw_group_begin();
 int dw_group_flush(hipStream_t st);
+// Optional epilogue task of an open group's reducer (one more reducer block):
+//   lvpart  (non-null) the PPO log_var gradient lv_out[j] = exp(lv[j]) *
+//           sum_i lvpart[i][j] over lv_nb row-block partials (ppo_net.py:29-46)
+//   sq      (non-null) fp64 sums of squares of every value the reducer stored
+//           (one per reducer block, then the task's own), *np = their count:
+//           the clip_grad_norm_ partials of the optimizer's Adam launch
+//   step / runs  (non-null) incremented once (the optimizer's step counter)
+//   skip    device stop flag (the task is a no-op when set)
+struct DwEpilogue {
+  int on;
+  double* sq; int* np;
+  const float* lvpart; int lv_nb, lv_A; const float* lv; float* lv_out;
+  int* step; int* runs;
+  const int* skip;
+};
+int dw_group_epilogue(const DwEpilogue& x);
 int check_launch(const char* what);
 
 // Test-only fault injection (build variant 'fault', -DSMI_FAULT_INJECTION;
@@ -145,13 +161,14 @@ int launch_ppo_epoch_apply(const smi_ppo_args* args, int epoch, hipStream_t stre
 int64_t ppo_rnn_scratch_bytes(int B, int T, int Hz, int D, int H, int L, int h1, int h2, int A, int c1,
                               int c2, int pc, int ph, int pw, int F);
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st);
+// keep: cbuf / gates stored for steps t < keep only (0: every step)
 int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
                     const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,
-                    hipStream_t st, const int* skip);
+                    hipStream_t st, const int* skip, int keep = 0);
 int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, const float* b_ih,
                       const float* w_hh, const float* b_hh, const float* h0, const float* c0,
                       int S, int B, int H, float* hbuf, float* cbuf, float* gates,
-                      hipStream_t st, const int* skip);
+                      hipStream_t st, const int* skip, int keep = 0);
 int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
                     int S, int B, int H, float* dgates, hipStream_t st, const int* skip);
 

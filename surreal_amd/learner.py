@@ -16,6 +16,7 @@ the Adam step counters stay on the device until something asks for them
 Construction needs no tensorplex/loggerplex/ZMQ: metrics go to an injectable
 `metrics` callable and parameters to an injectable `publisher` callable.
 """
+import ctypes
 import math
 import os
 import time
@@ -119,6 +120,44 @@ def replicate_from_rank0(dp, tensors):
 _RNN_PHASE_NAMES = {0: 'rnn_gae', 1: 'rnn_prep', 2: 'rnn_policy_fwd', 3: 'rnn_policy_bwd',
                     4: 'rnn_policy_apply', 5: 'rnn_value_grad', 6: 'rnn_value_apply',
                     7: 'rnn_zstats', 8: 'rnn_zapply', 9: 'rnn_policy_decide'}
+
+
+class _GraphInputs(object):
+    """The static device inputs of a captured learn(): every batch leaf in ONE
+    arena (256-byte aligned slots), refreshed before each replay by ONE
+    copy-gather launch on the current stream (smi_copy_gather) instead of a
+    copy launch per leaf (~5 us each inside the replayed sequence); leaves that
+    already are the static tensors are skipped, unaligned ones copied by torch."""
+
+    def __init__(self, leaves, device):
+        offs, lens, off = [], [], 0
+        for t in leaves:
+            n = t.numel() * t.element_size()
+            offs.append(off)
+            lens.append(n)
+            off += (n + 255) // 256 * 256
+        self.arena = torch.empty(max(off, 256), dtype=torch.uint8, device=device)
+        self.views = [self.arena[o:o + n].view(t.dtype).view(t.shape)
+                      for o, n, t in zip(offs, lens, leaves)]
+        self.offs, self.lens = offs, lens
+
+    def refresh(self, leaves):
+        idx = [i for i, (v, t) in enumerate(zip(self.views, leaves)) if v.data_ptr() != t.data_ptr()]
+        if not idx:
+            return
+        ok = [i for i in idx if leaves[i].is_contiguous() and leaves[i].data_ptr() % 16 == 0
+              and self.lens[i] % 4 == 0 and self.lens[i] > 0]
+        for i in idx:
+            if i not in ok:
+                self.views[i].copy_(leaves[i])
+        for k in range(0, len(ok), 16):            # one launch per 16 segments
+            part = ok[k:k + 16]
+            n = len(part)
+            src = (ctypes.c_void_p * n)(*[leaves[i].data_ptr() for i in part])
+            off = (ctypes.c_int64 * n)(*[self.offs[i] for i in part])
+            ln = (ctypes.c_int64 * n)(*[self.lens[i] for i in part])
+            L.call('smi_copy_gather', ctypes.c_void_p(self.arena.data_ptr()), src, off, ln, n,
+                   ctypes.c_void_p(torch.cuda.current_stream(self.arena.device).cuda_stream))
 
 
 class PPOLearner(LearnerHooks):
@@ -707,20 +746,23 @@ class PPOLearner(LearnerHooks):
     # ------------------------------------------------------- hipGraph replay
     @staticmethod
     def _leaves(batch):
-        """the batch's tensors in a fixed order, and a function rebuilding the
-        same structure over another list of tensors"""
-        out = []
+        """the batch's tensors in a fixed order, a function rebuilding the same
+        structure over another list of tensors, and the structure's signature
+        (leaf paths: part of the capture key, so a batch whose nesting differs
+        never replays a graph over a mismatched leaf order)"""
+        out, paths = [], []
 
-        def walk(x):
+        def walk(x, path):
             if isinstance(x, dict):
-                return {k: walk(v) for k, v in x.items()}
+                return {k: walk(v, path + (k,)) for k, v in x.items()}
             if isinstance(x, (list, tuple)):
-                return [walk(v) for v in x]
+                return [walk(v, path + (i,)) for i, v in enumerate(x)]
             if x is None:
                 return None
             out.append(x)
+            paths.append(path)
             return len(out) - 1
-        skel = walk(batch)
+        skel = walk(batch, ())
 
         def build(ts):
             def mk(x):
@@ -730,7 +772,7 @@ class PPOLearner(LearnerHooks):
                     return [mk(v) for v in x]
                 return None if x is None else ts[x]
             return mk(skel)
-        return out, build
+        return out, build, tuple(paths)
 
     def _learn_graphed(self, batch):
         """learn() as one hipGraph replay of the device sequence (module
@@ -741,11 +783,11 @@ class PPOLearner(LearnerHooks):
         same launches over static copies of the inputs."""
         if not isinstance(batch['actions'], torch.Tensor) or not batch['actions'].is_cuda:
             batch = self._arena.stage(batch)
-        leaves, build = self._leaves(batch)
+        leaves, build, paths = self._leaves(batch)
         # the host switches read while the launches are issued are part of
         # what a captured graph bakes in (export pointers, the side stream,
         # the epoch counts and the device the phases run on)
-        key = (tuple((tuple(t.shape), t.dtype) for t in leaves), bool(self.export_advantages),
+        key = (paths, tuple((tuple(t.shape), t.dtype) for t in leaves), bool(self.export_advantages),
                bool(self.prep_side_stream), self.epoch_policy, self.epoch_baseline)
         self.current_iteration += 1
         self._ctx.make_current()
@@ -756,8 +798,9 @@ class PPOLearner(LearnerHooks):
             for buf in self._device_phases(batch):
                 if dp is not None:
                     dp.allreduce_(buf)
-            self._gin = [t.detach().clone() for t in leaves]
-            static = build(self._gin)
+            self._gin = _GraphInputs(leaves, self.device)
+            self._gin.refresh(leaves)
+            static = build(self._gin.views)
             # quiesce the parameter publisher (its worker thread synchronizes
             # events and launches copies on its own stream) before capturing,
             # and capture in thread-local mode so another thread's CUDA calls
@@ -766,6 +809,7 @@ class PPOLearner(LearnerHooks):
                 self.publisher.flush()
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
+            err = None
             try:
                 with torch.cuda.graph(g, capture_error_mode='thread_local'):
                     self._ctx.make_current()
@@ -775,10 +819,17 @@ class PPOLearner(LearnerHooks):
             except RuntimeError as e:
                 if dp is None:
                     raise
-                # a collective library that refuses capture: this learner stays
-                # eager (this call's update already ran above)
+                err = e
+            # data parallel: every rank takes the same path, so no rank replays
+            # a graph while another issues eager launches (one flag all-reduced
+            # eagerly, once per capture)
+            if dp is not None and not self._capture_agreed(err is None):
+                # a collective library that refuses capture (on this rank or a
+                # peer): the learners stay eager (this call's update already
+                # ran above)
                 import warnings
-                warnings.warn(f'data-parallel learn() could not be captured ({e}); eager launches')
+                warnings.warn('data-parallel learn() could not be captured '
+                              f'({err if err is not None else "on a peer rank"}); eager launches')
                 self.use_graph = False
                 self._graph = None
                 self._ctx.make_current()
@@ -787,11 +838,16 @@ class PPOLearner(LearnerHooks):
             self._ctx.make_current()
             self._graph, self._graph_key = g, key
         else:
-            for s_, t in zip(self._gin, leaves):
-                if s_.data_ptr() != t.data_ptr():
-                    s_.copy_(t)
+            self._gin.refresh(leaves)
             self._graph.replay()
         self._learn_epilogue()
+
+    def _capture_agreed(self, ok):
+        """True when every rank captured its learn() (one eager all-reduce of
+        a failure count)"""
+        flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float32, device=self.device)
+        self.dp.allreduce_(flag)
+        return float(flag.item()) == 0.0
 
     def _host_scalars(self):
         """host-side entries of the statistics (averaged by a throttled sink)"""
@@ -807,9 +863,23 @@ class PPOLearner(LearnerHooks):
         Synchronises with the device."""
         return self._stats_dict(self.stats_buf.cpu().numpy(), self._host_scalars())
 
+    def _stats_vector(self):
+        """the statistics a throttled sink averages per call: the device vector
+        and, with the z-filter, np.mean of its running mean / square / std
+        (ppo.py:578-582), formed on the device (no host read per learn())"""
+        if not self.use_z_filter:
+            return self.stats_buf
+        zf = self.model.z_filter
+        m = zf.running_sum / zf.count
+        sq = zf.running_sumsq / zf.count
+        zv = torch.stack([m.mean(), sq.mean(), (sq - m * m).pow(0.5).mean()])
+        return torch.cat([self.stats_buf, zv.to(self.stats_buf.dtype)])
+
     def _stats_dict(self, v, host):
         """the reference's statistics dict from a host copy of the device
-        statistics vector v and the host scalars (_lr, _clip_epsilon / _beta)"""
+        statistics vector v and the host scalars (_lr, _clip_epsilon / _beta);
+        v may carry the averaged z-filter means after the L.ST_COUNT entries
+        (_stats_vector)"""
         s = {}
         if self.ppo_mode == 'clip':
             for k in ('_surr_loss', '_clip_surr_loss', '_entropy'):
@@ -831,10 +901,14 @@ class PPOLearner(LearnerHooks):
         er = float(v[L.ST['epochs_run']])              # (an average over a throttled window)
         s['epochs_run'] = int(er) if er == int(er) else er
         if self.use_z_filter:
-            zf = self.model.z_filter
-            s['obs_running_mean'] = float(np.mean(zf.running_mean()))
-            s['obs_running_square'] = float(np.mean(zf.running_square()))
-            s['obs_running_std'] = float(np.mean(zf.running_std()))
+            if len(v) >= L.ST_COUNT + 3:
+                s['obs_running_mean'], s['obs_running_square'], s['obs_running_std'] = (
+                    float(x) for x in v[L.ST_COUNT:L.ST_COUNT + 3])
+            else:
+                zf = self.model.z_filter
+                s['obs_running_mean'] = float(np.mean(zf.running_mean()))
+                s['obs_running_square'] = float(np.mean(zf.running_square()))
+                s['obs_running_std'] = float(np.mean(zf.running_std()))
         if self.use_r_filter:
             s['reward_mean'] = self.reward_filter.reward_mean()
         return s

@@ -74,12 +74,20 @@ class _Layout(object):
                 self.keys.append((name, key, boff, tuple(t.shape),
                                   torch.empty(0, dtype=t.dtype).numpy().dtype))
         self.nbytes = max(off, 256)
-        # the snapshot's gather copy, as ctypes arrays built once
-        n = len(self.storages)
+        # the snapshot's gather copy, as ctypes arrays built once.  The gather
+        # kernel moves 16-byte aligned storages of whole 4-byte words (every
+        # flat parameter buffer; arena offsets are 256-byte aligned); any other
+        # storage (a bool / uint8 buffer of odd size, an unaligned view) is
+        # copied by torch on the same stream instead
+        def gatherable(v, nbytes):
+            return nbytes % 4 == 0 and v.data_ptr() % 16 == 0
+        gs = [(v, o, b) for v, o, b in self.storages if gatherable(v, b)]
+        self.other = [(v, o, b) for v, o, b in self.storages if not gatherable(v, b)]
+        n = len(gs)
         self.c_n = n
-        self.c_src = (ctypes.c_void_p * n)(*[v.data_ptr() for v, _, _ in self.storages])
-        self.c_off = (ctypes.c_int64 * n)(*[o for _, o, _ in self.storages])
-        self.c_len = (ctypes.c_int64 * n)(*[b for _, _, b in self.storages])
+        self.c_src = (ctypes.c_void_p * n)(*[v.data_ptr() for v, _, _ in gs])
+        self.c_off = (ctypes.c_int64 * n)(*[o for _, o, _ in gs])
+        self.c_len = (ctypes.c_int64 * n)(*[b for _, _, b in gs])
 
     def views(self, raw):
         """{module name: {state_dict key: ndarray view}} of an arena image"""
@@ -176,8 +184,11 @@ class DeviceParameterPublisher(object):
         slot['free'].clear()
         cur = torch.cuda.current_stream(self.device)
         lay = self.layout                                      # D2D, stream-ordered after learn()
-        L.call('smi_copy_gather', ctypes.c_void_p(slot['dev'].data_ptr()), lay.c_src, lay.c_off,
-               lay.c_len, lay.c_n, ctypes.c_void_p(cur.cuda_stream))
+        if lay.c_n:
+            L.call('smi_copy_gather', ctypes.c_void_p(slot['dev'].data_ptr()), lay.c_src, lay.c_off,
+                   lay.c_len, lay.c_n, ctypes.c_void_p(cur.cuda_stream))
+        for v, o, b in lay.other:
+            slot['dev'][o:o + b].copy_(v)
         taken = torch.cuda.Event()
         taken.record(cur)
         # the D2H is issued by the worker once the snapshot's D2D has run (it

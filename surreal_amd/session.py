@@ -19,6 +19,8 @@ sink keeps the round-1 behaviour (every call's statistics, one read each).
 """
 import time
 
+import torch
+
 
 class PeriodicCheckpoint(object):
     """utils/checkpoint.py:317-347 over a save function: save() runs
@@ -125,22 +127,36 @@ class LearnerHooks(object):
         if m.due():
             m(self._averaged_stats(), global_step)
 
+    def _stats_vector(self):
+        """this call's device statistics to average (the host class may append
+        entries computed on the device, e.g. the z-filter means)"""
+        return self.stats_buf
+
     def _accumulate_stats(self):
-        if self._stats_acc is None or self._stats_acc.shape != self.stats_buf.shape:
-            self._stats_acc = self.stats_buf.detach().clone().zero_()
-        self._stats_acc.add_(self.stats_buf)          # stream-ordered, no host sync
+        """utils/common.py:606-648 (AverageDictionary of AverageValue): every
+        call adds its values; the device vector is summed stream-ordered (no
+        host sync)"""
+        cur = self._stats_vector().detach()
+        if self._stats_acc is None or self._stats_acc.shape != cur.shape:
+            self._stats_acc = torch.zeros_like(cur)
+            self._stats_n = 0
+            self._host_acc = {}
+        self._stats_acc.add_(cur)
+        self._stats_last = cur.clone()
         self._stats_n += 1
         for k, v in self._host_scalars().items():
-            s, n = self._host_acc.get(k, (0.0, 0))
-            self._host_acc[k] = (s + float(v), n + 1)
+            s, n, _ = self._host_acc.get(k, (0.0, 0, 0.0))
+            self._host_acc[k] = (s + float(v), n + 1, float(v))
 
     def _averaged_stats(self):
-        """the statistics averaged over the calls since the last emit (one
-        device read), then the accumulators restart"""
+        """the statistics averaged over the window (one device read), then each
+        accumulator restarts from the window's LAST value with count 1, as
+        AverageValue.avg(clear=True) does (utils/common.py:620-630): the next
+        window's average includes the value this one ended on"""
         n = max(self._stats_n, 1)
         vec = (self._stats_acc / n).cpu().numpy()
-        host = {k: s / c for k, (s, c) in self._host_acc.items()}
-        self._stats_acc.zero_()
-        self._stats_n = 0
-        self._host_acc = {}
+        host = {k: s / c for k, (s, c, _) in self._host_acc.items()}
+        self._stats_acc.copy_(self._stats_last)
+        self._stats_n = 1
+        self._host_acc = {k: (last, 1, last) for k, (_, _, last) in self._host_acc.items()}
         return self._stats_dict(vec, host)

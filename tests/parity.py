@@ -116,6 +116,10 @@ CASES = {
     # bench.py --config c5 --local-segments 128: C3 + camera0 3x84x84 -> CNN (FC 256)
     'c5': dict(cfg=lambda: c5_cfg(128), D=42, A=8, Hd=100, pixel=(3, 84, 84),
                init_seed=15, batch_seeds=[1500], n_ulp=3, orders=['given', 'reversed']),
+    # the same at 2 + 2 epochs: fewer ReLU-mask flips of the pixel stem and
+    # Adam sign steps compound, so the update bars stay tight at the lr/2 mask
+    'c5_short': dict(cfg=lambda: c5_cfg(128, (2, 2)), D=42, A=8, Hd=100, pixel=(3, 84, 84),
+                     init_seed=19, batch_seeds=[1900], n_ulp=3, orders=['given', 'reversed']),
     'c5_grad_policy': dict(cfg=lambda: c5_cfg(128, (1, 0)), D=42, A=8, Hd=100, pixel=(3, 84, 84),
                            init_seed=16, batch_seeds=[1600], n_ulp=4,
                            orders=['given', 'reversed'], grad='policy'),
@@ -304,8 +308,10 @@ def check(name, got, r64, env, scale, report, slack=SLACK, factor=2.0):
     assert got.shape == r64.shape, (name, got.shape, r64.shape)
     scale = max(float(scale), 1e-30)
     e = float(np.abs(got - r64).max()) if r64.size else 0.0
-    ok = e <= factor * env + slack * scale
-    report[name] = (e / scale, env / scale, ok)
+    bar = factor * env + slack * scale
+    ok = e <= bar
+    # (gpu err, the bar it was held to, ok, envelope width), each / scale
+    report[name] = (e / scale, bar / scale, ok, env / scale)
     if not ok:
         report.setdefault('_fail', []).append(name)
 
@@ -368,15 +374,27 @@ def check_update(name, u, u64, thr, w_rel, w_cos, report, factor=2.0):
     for tag, e, b in (('relL2', rel, b_rel), ('1-cos', omc, b_cos)):
         key = f'upd_{tag}:{name}'
         ok = e <= b and b < UPDATE_MAX_BAR and n > 0
-        report[key] = (e, b, ok)
+        report[key] = (e, b, ok, w_rel if tag == 'relL2' else w_cos)
         if not ok:
             report.setdefault('_fail', []).append(key)
 
 
 def report_json(report):
-    """the report as a JSON-able dict: {check: {"gpu": err, "bar": bar, "ok": bool}}"""
-    return {k: {'gpu': float(v[0]), 'bar': float(v[1]), 'ok': bool(v[2])}
-            for k, v in report.items() if k != '_fail'}
+    """the report as a JSON-able dict: {check: {"gpu": err, "bar": the bar the
+    check applied (factor * envelope + slack for the envelope checks), "env":
+    the envelope width the bar was formed from (where there is one),
+    "gpu_over_bar": gpu / bar (<= 1 passes), "ok": bool}}"""
+    out = {}
+    for k, v in report.items():
+        if k == '_fail':
+            continue
+        d = {'gpu': float(v[0]), 'bar': float(v[1])}
+        if len(v) > 3:
+            d['env'] = float(v[3])
+        d['gpu_over_bar'] = float(v[0]) / float(v[1]) if v[1] > 0 else float('inf')
+        d['ok'] = bool(v[2])
+        out[k] = d
+    return out
 
 
 def save_report(case, report):
@@ -395,10 +413,11 @@ def save_report(case, report):
 
 
 def print_report(report, case=None):
-    print('\n(GPU err / scale, envelope err / scale) vs the fp64 oracle:')
+    print('\n(GPU err, applied bar[, envelope width]) vs the fp64 oracle (per scale):')
     for k, v in report.items():
         if k != '_fail':
-            print(f'  {k:30s} gpu {v[0]:.3e}  bar {v[1]:.3e}  {"" if v[2] else "FAIL"}')
+            env = f'  env {v[3]:.3e}' if len(v) > 3 else ''
+            print(f'  {k:30s} gpu {v[0]:.3e}  bar {v[1]:.3e}{env}  {"" if v[2] else "FAIL"}')
     if case is not None:
         save_report(case, report)
     assert not report.get('_fail'), report.get('_fail')
@@ -532,15 +551,38 @@ def recompute_stats(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run):
     value)}: the same computation in fp32 (the reference's precision) says
     how far fp32 arithmetic itself lands from fp64 at this very state."""
     s64 = _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, torch.float64)
-    s32 = _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, torch.float32)
-    return {k: (v, sc, s32[k][0]) for k, (v, sc) in s64.items()}
+    # several fp32 executions: two segment orders (given, reversed: the row
+    # sums behind a gradient norm round differently) and two with one ulp of
+    # relative noise on the observations and cells (pre-activations within
+    # fp32 noise of 0 then take the other side of a ReLU, as they do between
+    # any two fp32 implementations: tools/exp/critic_grad_check.py showed the
+    # C3 critic gradient's hidden-layer blocks moving by ~1e-3 between valid
+    # fp32 executions, 1.2e-5 in its norm); the farthest sets the bar
+    s32s = [_stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, torch.float32, perm=pm)
+            for pm in (None, 'reversed', ('ulp', 1), ('ulp', 2))]
+    return {k: (v, sc, max((x[k][0] for x in s32s), key=lambda u: abs(u - v)))
+            for k, (v, sc) in s64.items()}
 
 
-def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype):
-    f64 = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32).to(dtype)  # noqa: E731
+def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype, perm=None):
+    """perm: None, 'reversed' (the segment order the rows are summed in; every
+    per-segment input permuted alike) or ('ulp', k) (observations and cells
+    with one ulp of seeded relative noise): the same statistics up to fp32
+    rounding"""
+    B0 = np.asarray(ob['rewards']).shape[0]
+    order = np.arange(B0)[::-1].copy() if perm == 'reversed' else None
+    noise = np.random.RandomState(977 * perm[1]) if isinstance(perm, tuple) else None
+
+    def f64(a, axis=0, noisy=False):
+        a = np.asarray(a)
+        if order is not None and a.ndim > axis and a.shape[axis] == B0:
+            a = np.take(a, order, axis=axis)
+        if noisy and noise is not None:     # one ulp of relative noise, rounded to fp32
+            a = (a.astype(np.float64) * (1.0 + 2.0 ** -24 * noise.standard_normal(a.shape))).astype(np.float32)
+        return torch.as_tensor(a, dtype=torch.float32).to(dtype)
     rnn = bool(lc.algo.rnn.if_rnn_policy)
     E = lc.algo.n_step - lc.algo.rnn.horizon + 1 if rnn else 1
-    obs = None if ob['obs'] is None else f64(ob['obs'])
+    obs = None if ob['obs'] is None else f64(ob['obs'], noisy=True)
     if rnn:
         obs_iter = None if obs is None else obs[:, :E].contiguous()
         actions = f64(ob['actions'])[:, :E].contiguous()
@@ -550,12 +592,13 @@ def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype):
         actions = f64(ob['actions'])[:, 0].contiguous()
         behave = f64(ob['pds'])[:, 0].contiguous()
     if pixel is not None:
-        pix = torch.as_tensor(ob['pixels'])
+        px = np.asarray(ob['pixels'])
+        pix = torch.as_tensor(px if order is None else np.take(px, order, axis=0))
         obs_iter = (obs_iter, pix[:, :E].contiguous() if rnn else pix[:, 0].contiguous())
     cells = None
     if rnn:
-        cells = (f64(ob['onetime'][0]).transpose(0, 1).contiguous(),
-                 f64(ob['onetime'][1]).transpose(0, 1).contiguous())
+        cells = (f64(ob['onetime'][0], noisy=True).transpose(0, 1).contiguous(),
+                 f64(ob['onetime'][1], noisy=True).transpose(0, 1).contiguous())
     adv = f64(adv_used).reshape(-1, 1)
     ret = f64(ret_used)
     if not rnn:

@@ -100,9 +100,11 @@ def test_throttled_metrics_read_only_when_due_and_average():
     # due at t = 1004 (call 4, value 3) and t = 1008 (call 8, value 7)
     assert [s for s, _ in out] == [3, 7]          # global_step before the increment
     assert reads == [4, 8], reads                  # no statistics read on the other calls
-    # averaged over the calls since the last emit: values 0..3, then 4..7
+    # AverageValue (utils/common.py:606-630): the first window averages 0..3;
+    # avg(clear=True) restarts from the last value with count 1, so the second
+    # window averages 3..7, not 4..7
     assert out[0][1]['_surr_loss'] == pytest.approx(1.5)
-    assert out[1][1]['_surr_loss'] == pytest.approx(5.5)
+    assert out[1][1]['_surr_loss'] == pytest.approx(5.0)
     assert out[0][1]['_beta'] == 1.0 and out[0][1]['_lr'] == pytest.approx(3e-4)
     assert sink.emitted == 2
 
@@ -115,3 +117,33 @@ def test_plain_metrics_callable_gets_every_call():
         learn_once(ln, i)
     assert out == [(0, 0.0), (1, 1.0), (2, 2.0)]
     assert reads == [1, 2, 3]
+
+
+def test_throttled_metrics_average_zfilter_entries():
+    """obs_running_* (ppo.py:578-582) go through the same AverageValue as the
+    other scalars: averaged over the window from device-side means, not read
+    at the emit's current state"""
+    import numpy as np
+    clock = Clock()
+    out = []
+    sink = TimeThrottledMetrics(lambda stats, step: out.append(stats), 2.0, clock=clock)
+    ln, _ = shell(metrics=sink)
+    ln.use_z_filter = True
+
+    class ZF(object):
+        pass
+    zf = ZF()
+    zf.count = torch.tensor(1.0)
+    ln.model = ZF()
+    ln.model.z_filter = zf
+    means = []
+    for i in range(4):
+        clock.t += 1.0
+        zf.running_sum = torch.tensor([float(i), float(i) + 2.0])
+        zf.running_sumsq = torch.tensor([float(i * i) + 1.0, (float(i) + 2.0) ** 2 + 4.0])
+        means.append(np.mean([i, i + 2.0]))
+        learn_once(ln, i)
+    # emits at calls 2 and 4: windows {0, 1} and {1, 2, 3}
+    assert out[0]['obs_running_mean'] == pytest.approx(np.mean(means[0:2]))
+    assert out[1]['obs_running_mean'] == pytest.approx(np.mean(means[1:4]))
+    assert out[1]['obs_running_std'] == pytest.approx(1.5)     # mean(sqrt(1), sqrt(4))

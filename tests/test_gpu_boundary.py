@@ -331,6 +331,70 @@ def test_ddpg_agent_batch_matches_sequential_reference_agents(noise):
         assert max_rel_err(a, ra, floor=1e-2) < 1e-5, (step, a, ra)
 
 
+@pytest.mark.parametrize('pn', ['normal', 'adaptive_normal'])
+def test_ddpg_agent_param_noise_matches_reference_agents(pn):
+    """Parameter-space noise (param_noise.py:9-72, ddpg_agent.py:134-151,172-173):
+    each agent perturbs every fetched array with numpy's global RNG (agents in
+    order) and acts with its perturbed actor; adaptive agents measure the
+    unperturbed / perturbed action distance every 10th act and rescale sigma by
+    alpha at the next fetch.  Checked against one oracle agent per actor over
+    three fetches of 12 acts each (the adaptation both ways)."""
+    lc = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
+    ex = lc.algo.exploration
+    ex.noise_type = 'normal'
+    ex.param_noise_type = pn
+    ex.param_noise_sigma, ex.param_noise_alpha, ex.param_noise_target_stddev = 0.05, 1.15, 0.02
+    D, A, N = 17, 6, 3
+    ec = gym_env_config(D, A)
+    agents = DDPGAgentBatch(lc, ec, N, seed=4)
+    keys = list(agents.model.state_dict().keys())
+    akeys = [k for k in keys if k.startswith('actor.')]
+
+    def actor_of(params):
+        actor = DR.ActorX(D, A, lc.model.actor_fc_hidden_sizes)
+        f = np.concatenate([np.asarray(params['ddpg'][k], dtype=np.float32).reshape(-1) for k in akeys])
+        assert f.size == agents.model.actor.flat.numel()
+        DR.load_flat(actor.params(), torch.from_numpy(f))
+        return actor
+    refs = []
+    for i in range(N):
+        sigma = ex.max_sigma * (float(i) / N)
+        nz = AR.NormalActionNoiseRef(np.zeros(A), np.ones(A) * sigma)
+        if pn == 'normal':
+            pnr = AR.NormalParameterNoiseRef(ex.param_noise_sigma)
+        else:
+            orig = DR.ActorX(D, A, lc.model.actor_fc_hidden_sizes)
+
+            def load_original(params, orig=orig):
+                o = actor_of(params)
+                DR.load_flat(orig.params(), torch.cat([q.detach().reshape(-1) for q in o.params()]))
+            pnr = AR.AdaptiveNormalParameterNoiseRef(orig, load_original, ex.param_noise_target_stddev,
+                                                     alpha=ex.param_noise_alpha, sigma=ex.param_noise_sigma)
+        refs.append(AR.DDPGAgentRef(None, nz, param_noise=pnr))
+    rs = np.random.RandomState(11)
+    np.random.seed(13)
+    base = {k: v.detach().cpu().numpy() for k, v in agents.model.state_dict().items()}
+    for fetch in range(3):
+        params = {'ddpg': {k: v + 0.01 * fetch for k, v in base.items()}}
+        state = np.random.get_state()
+        agents.load_numpy(copy.deepcopy(params))
+        np.random.set_state(state)
+        for r in refs:
+            r.actor = actor_of(r.param_noise.apply(copy.deepcopy(params)))
+        if pn == 'adaptive_normal':
+            assert np.allclose(agents.pn_sigma, [r.param_noise.sigma for r in refs], rtol=1e-12)
+        for step in range(12):
+            obs = rs.randn(N, D)
+            state = np.random.get_state()
+            a = agents.act(obs)
+            np.random.set_state(state)
+            ra = np.stack([refs[i].act(obs[i]) for i in range(N)])
+            assert max_rel_err(a, ra, floor=1e-2) < 1e-5, (fetch, step, a, ra)
+    if pn == 'adaptive_normal':
+        # the sigmas moved (one direction or the other) at every fetch after the first
+        assert not np.allclose(agents.pn_sigma, ex.param_noise_sigma)
+
+
 def test_learners_on_two_streams_in_three_threads_match_sequential_runs():
     """Re-entrancy (SURVEY §8(b) Threading): two PPO learners and a DDPG learner
     running at the same time on their own streams in their own threads end

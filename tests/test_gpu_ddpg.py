@@ -318,8 +318,9 @@ def ddpg_envelope_check(lc, D, A, init, batches, gpu, n_ulp=6, pixel=None, tag='
         for k in s64:
             w = max(abs(x[k] - s64[k]) for x in svs)
             e, sc = abs(s[k] - s64[k]), max(abs(s64[k]), 1e-30)
-            ok = e <= 2 * w + 1e-6 * sc or e <= 1e-5 * sc
-            report[f'stat{tag}:{k}@{it}'] = (e / sc, max(w / sc, 1e-5), ok)
+            bar = max(2 * w + 1e-6 * sc, 1e-5 * sc)
+            ok = e <= bar
+            report[f'stat{tag}:{k}@{it}'] = (e / sc, bar / sc, ok, w / sc)
             if not ok:
                 report.setdefault('_fail', []).append(f'stat{tag}:{k}@{it}')
     P.print_report(report)

@@ -12,7 +12,9 @@ global batch (segments sharded on the batch axis).  Required:
   * every statistic is self-consistent in fp64 with the global state.
 Cases: C3 (LSTM 100, heads 300x200, obs 42, act 8, 10 + 10 epochs) as 2 x 512
 segments, adapt over two learns and clip; C5 (C3 + camera stem, FC 256) as
-2 x 64 segments.
+2 x 64 segments; and the strong-scaled compositions of BASELINE configs[2]:
+the c3_adapt fixture as 4 x 256 and 8 x 128 segments (one process per rank, all
+on cuda:0: ranks share the GPU, the exchange is gloo over host memory).
 """
 import os
 import socket
@@ -71,12 +73,12 @@ def _worker(rank, world, port, case, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize('case', ['c3_adapt', 'c3_clip', 'c5'])
-def test_dp_two_ranks_match_global_fixture(case):
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('case,world', [('c3_adapt', 2), ('c3_clip', 2), ('c5', 2),
+                                        ('c3_adapt', 4), ('c3_adapt', 8)])
+def test_dp_ranks_match_global_fixture(case, world):
     from tests import parity as P
     from tests.helpers import oracle_batch
-    world = 2
     with tempfile.TemporaryDirectory() as outdir:
         mp.spawn(_worker, args=(world, _free_port(), case, outdir), nprocs=world, join=True)
         out = [torch.load(os.path.join(outdir, f'rank{r}.pt'), weights_only=True)
@@ -87,21 +89,23 @@ def test_dp_two_ranks_match_global_fixture(case):
     st = P.init_state(case)
     report = {}
     for it in range(len(c['batch_seeds'])):
-        r0, r1 = out[0][it], out[1][it]
+        r0 = out[0][it]
         fin = r0['cap']['final']
-        for k in ('actor', 'critic', 'lstm', 'cnn'):
-            if k in fin:
-                assert torch.equal(fin[k], r1['final'][k]), (it, k)
-        for a, b in zip(fin['zf'], r1['final']['zf']):
-            assert torch.equal(a, b), it
-        assert r0['stats']['epochs_run'] == r1['stats']['epochs_run'] == meta['epochs_run'][it]
-        adv = np.concatenate([r0['adv'].numpy(), r1['adv'].numpy()])
-        ret = np.concatenate([r0['ret'].numpy(), r1['ret'].numpy()])
+        for rk in range(1, world):
+            rr = out[rk][it]
+            for k in ('actor', 'critic', 'lstm', 'cnn'):
+                if k in fin:
+                    assert torch.equal(fin[k], rr['final'][k]), (it, rk, k)
+            for a, b in zip(fin['zf'], rr['final']['zf']):
+                assert torch.equal(a, b), (it, rk)
+            assert rr['stats'] == r0['stats'], (it, rk)
+        assert r0['stats']['epochs_run'] == meta['epochs_run'][it]
+        adv = np.concatenate([out[rk][it]['adv'].numpy() for rk in range(world)])
+        ret = np.concatenate([out[rk][it]['ret'].numpy() for rk in range(world)])
         from tests.test_gpu_parity_pinned import check_fixture_state
         check_fixture_state(meta, fx, st, it, fin, adv, ret, fin['zf'], report, tag='_dp')
         batch = P.case_batch(case, it)
         rec = P.recompute_stats(lc, c['D'], c['A'], c['pixel'], oracle_batch(batch), r0['cap'],
                                 adv, ret, r0['stats']['epochs_run'])
         P.check_stats(r0['stats'], rec, report, tag=f'_dp@{it}')
-        assert r0['stats'] == r1['stats']
-    P.print_report(report, f'{case}_dp2')
+    P.print_report(report, f'{case}_dp{world}')

@@ -273,6 +273,13 @@ def test_pinned_c5_full_batch():
     pinned_fixture('c5')
 
 
+@pytest.mark.timeout(300)
+def test_pinned_c5_short():
+    # C5 at 2 + 2 epochs: the pixel stem's update pinned on tight bars (the
+    # 10 + 10 fixture needs a raised relative-L2 mask, tests/parity.py)
+    pinned_fixture('c5_short')
+
+
 def gpu_first_step_grads(learner, phase):
     """the raw gradient a backward phase left in the exchange buffer:
     [actor head | lstm | cnn] then [critic head | lstm | cnn]"""

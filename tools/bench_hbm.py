@@ -10,9 +10,11 @@ the algorithmic bytes are the §8(d) per-unit figures:
   zfilter_apply (D=42)              8 D B per row (read x, write out)
   zfilter_update (D=42)             4 D B per row (read x; 2D+1 floats written)
   diag_gauss kl+loglik+ent (A=8)    a 4A + p0 8A + p1 8A read, 3 x 4 B written per row
-  adam_clip                         g read by the norm pass 4 B + p,g,m,v read 16 B + p,m,v
-                                    written 12 B per param (clip_grad_norm_ must see all of g
-                                    before the first update: two passes over g)
+  adam_clip                         p,g,m,v read 16 B + p,m,v written 12 B per param: SURVEY
+                                    §8(d)'s 28 B (the norm pass's second read of g, 4 B more
+                                    moved, is NOT counted; frac_moved adds it); g spans 3 x 2^26
+                                    floats (768 MiB, > 2 x the MALL) so that re-read cannot hit
+                                    the Infinity Cache
   adam_noclip                       p,g,m,v read 16 B + p,m,v written 12 B per param
   gather_rows (W=42 floats)         8 idx + 2 x 4 W B per gathered row
   moments                           4 B per element
@@ -126,7 +128,7 @@ def main():
         del a, p0, p1, ll, kl, en
 
     if want('adam_clip'):
-        n = 1 << 26
+        n = 3 << 26
         p = torch.randn(n, device=dev, generator=g)
         gr = torch.randn(n, device=dev, generator=g)
         m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
@@ -135,8 +137,10 @@ def main():
         norm = torch.zeros(1, device=dev)
         fn = lambda: L.call('smi_adam_clip', P(p), P(gr), P(m), P(v), n, P(step), P(lr), 0.9,  # noqa
                             0.999, 1e-8, 0.0, 10.0, 0.0, None, P(norm), st)
-        report('adam_clip', n * 32, timed(fn, args.iters), params=n,
-               note='clip_grad_norm_ (norm pass, 4 B) + Adam (28 B)')
+        ms = timed(fn, args.iters)
+        report('adam_clip', n * 28, ms, params=n,
+               frac_moved=round(n * 32 / (ms * 1e-3) / 1e9 / PEAK, 4),
+               note='28 B/param algorithmic (SURVEY 8(d)); frac_moved counts the norm pass (32 B)')
         fn2 = lambda: L.call('smi_adam_clip', P(p), P(gr), P(m), P(v), n, P(step), P(lr), 0.9,  # noqa
                              0.999, 1e-8, 0.0, 0.0, 0.0, None, None, st)
         report('adam_noclip', n * 28, timed(fn2, args.iters), params=n)
