@@ -368,8 +368,15 @@ reduce_partials_kernel(const double* __restrict__ part, int nb, int w, double* o
   while (L > 1 && w * L > kWG) L >>= 1;
   const int j = threadIdx.x / L, l = threadIdx.x - j * L;
   for (int jj = j; jj < w; jj += kWG / L) {
-    double s = 0.0;
-    for (int i = l; i < nb; i += L) s += part[(int64_t)i * w + jj];
+    // four partials in flight per lane (independent sums, combined in order)
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    int i = l;
+    for (; i + 3 * L < nb; i += 4 * L) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s4[k] += part[(int64_t)(i + k * L) * w + jj];
+    }
+    for (; i < nb; i += L) s4[0] += part[(int64_t)i * w + jj];
+    double s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     for (int o = L >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if (l == 0) out[jj] = s;
   }
@@ -1012,21 +1019,50 @@ value_rows_kernel(const float* __restrict__ V, const float* __restrict__ ret_tm,
 }
 
 // column sums of obs_iter = obs[:, :E, :] (B*E rows) in fp64 -> partials
+// part[gridDim.x][2][D].  Block blk takes a contiguous run of rows; a wave
+// takes every 4th row of the run with lane = column (columns past 64 in a
+// second pass), four rows in flight per wave (independent accumulators,
+// summed in a fixed order), then the four waves meet in LDS in wave order.
+// (A column per thread striding the whole batch issued one dependent load
+// per row: 31 us at C3 for a 3.6 MB read.)
 __global__ void __launch_bounds__(kWG)
 obs_iter_colsum_kernel(const float* __restrict__ obs, int B, int T, int E, int D,
                        double* part) {
-  // part [gridDim.x][2][D]
+  __shared__ double red[kWG / 64][2][64];
   const int64_t N = (int64_t)B * E;
-  for (int c = threadIdx.x; c < D; c += kWG) {
-    double s1 = 0.0, s2 = 0.0;
-    for (int64_t n = blockIdx.x; n < N; n += gridDim.x) {
-      const int b = (int)(n / E), t = (int)(n - (int64_t)b * E);
-      const float v = obs[((int64_t)b * T + t) * D + c];
-      s1 += (double)v;
-      s2 += (double)(v * v);
+  const int64_t per = (N + gridDim.x - 1) / gridDim.x;
+  const int64_t n0 = (int64_t)blockIdx.x * per, n1 = n0 + per < N ? n0 + per : N;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c0 = 0; c0 < D; c0 += 64) {
+    const int c = c0 + lane;
+    const bool ok = c < D;
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t n = n0 + wave; n < n1; n += 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t m = n + 4 * j;
+        if (ok && m < n1) {
+          const int b = (int)(m / E), t = (int)(m - (int64_t)b * E);
+          const float v = obs[((int64_t)b * T + t) * D + c];
+          s1[j] += (double)v;
+          s2[j] += (double)(v * v);
+        }
+      }
     }
-    part[((int64_t)blockIdx.x * 2) * D + c] = s1;
-    part[((int64_t)blockIdx.x * 2 + 1) * D + c] = s2;
+    red[wave][0][lane] = (s1[0] + s1[1]) + (s1[2] + s1[3]);
+    red[wave][1][lane] = (s2[0] + s2[1]) + (s2[2] + s2[3]);
+    __syncthreads();
+    if (wave == 0 && ok) {
+      double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < kWG / 64; ++w) {
+        t1 += red[w][0][lane];
+        t2 += red[w][1][lane];
+      }
+      part[((int64_t)blockIdx.x * 2) * D + c] = t1;
+      part[((int64_t)blockIdx.x * 2 + 1) * D + c] = t2;
+    }
+    __syncthreads();
   }
 }
 
@@ -1046,10 +1082,15 @@ adam_split_kernel(AdamSplitArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   __shared__ double red[kNW];
   __shared__ float s_coef;
-  double s = 0.0;
   const int np = a.np_dev ? a.np_dev[0] : a.np;
-  for (int i = threadIdx.x; i < np; i += kWG) s += a.part[i];
-  s = block_sum_d(s, red);
+  double s4[4] = {0.0, 0.0, 0.0, 0.0};       // four partials in flight per thread
+  int i0 = threadIdx.x;
+  for (; i0 + 3 * kWG < np; i0 += 4 * kWG) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s4[k] += a.part[i0 + k * kWG];
+  }
+  for (; i0 < np; i0 += kWG) s4[0] += a.part[i0];
+  double s = block_sum_d((s4[0] + s4[1]) + (s4[2] + s4[3]), red);
   const int t = a.step[0];      // already bumped (sumsq_part_kernel or the dW reducer's epilogue)
   if (threadIdx.x == 0) {
     const float norm = (float)sqrt(s);
@@ -1741,7 +1782,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     case SMI_RNN_PH_ZSTATS: {
       // zbuf (double) = [value sums (5) | column sums (D) | sums of squares (D)]
       if (!a.use_zf) return SMI_OK;
-      const int nb = 256;
+      // >= 64 rows per block (16 per wave, four in flight), at most 256 blocks
+      const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(256, (d.NE + 63) / 64));
       double* part = s.part;     // [nb][2][D] <= 65536 doubles for D <= 128
       if ((int64_t)nb * 2 * d.D > 4096 * 16) return set_error(SMI_E_ARG, "ppo_rnn: obs_dim too large");
       hipLaunchKernelGGL(obs_iter_colsum_kernel, dim3(nb), dim3(kWG), 0, st, a.obs, d.B, d.T, d.E,

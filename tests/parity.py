@@ -552,14 +552,16 @@ def recompute_stats(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run):
     how far fp32 arithmetic itself lands from fp64 at this very state."""
     s64 = _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, torch.float64)
     # several fp32 executions: two segment orders (given, reversed: the row
-    # sums behind a gradient norm round differently) and two with one ulp of
-    # relative noise on the observations and cells (pre-activations within
-    # fp32 noise of 0 then take the other side of a ReLU, as they do between
-    # any two fp32 implementations: tools/exp/critic_grad_check.py showed the
-    # C3 critic gradient's hidden-layer blocks moving by ~1e-3 between valid
-    # fp32 executions, 1.2e-5 in its norm); the farthest sets the bar
+    # sums behind a gradient norm round differently) and four with a few ulp
+    # of relative noise on the observations, cells and parameters (the
+    # rounding of the products a GEMM's summation order changes):
+    # pre-activations within fp32 noise of 0 then take the other side of a
+    # ReLU, as they do between any two fp32 implementations --
+    # tools/exp/critic_grad_check.py found the C3 critic gradient's hidden
+    # blocks 1e-3 apart between valid fp32 executions (one HA2 mask flip),
+    # 1.2e-5 in its norm.  The farthest execution sets the bar
     s32s = [_stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, torch.float32, perm=pm)
-            for pm in (None, 'reversed', ('ulp', 1), ('ulp', 2))]
+            for pm in (None, 'reversed', ('ulp', 1), ('ulp', 2), ('ulp', 3), ('ulp', 4))]
     return {k: (v, sc, max((x[k][0] for x in s32s), key=lambda u: abs(u - v)))
             for k, (v, sc) in s64.items()}
 
@@ -577,9 +579,17 @@ def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype, p
         a = np.asarray(a)
         if order is not None and a.ndim > axis and a.shape[axis] == B0:
             a = np.take(a, order, axis=axis)
-        if noisy and noise is not None:     # one ulp of relative noise, rounded to fp32
-            a = (a.astype(np.float64) * (1.0 + 2.0 ** -24 * noise.standard_normal(a.shape))).astype(np.float32)
+        if noisy and noise is not None:     # 4 ulp of relative noise, rounded to fp32
+            a = (a.astype(np.float64) * (1.0 + 2.0 ** -22 * noise.standard_normal(a.shape))).astype(np.float32)
         return torch.as_tensor(a, dtype=torch.float32).to(dtype)
+
+    def model(st, zf_):
+        if noise is not None:
+            def pn(v):
+                v = np.asarray(v, dtype=np.float64)
+                return torch.from_numpy((v * (1.0 + 2.0 ** -22 * noise.standard_normal(v.shape))).astype(np.float32))
+            st = {k: (pn(v) if k in ('actor', 'critic', 'lstm', 'cnn') else v) for k, v in st.items()}
+        return _stat_model(lc, D, A, pixel, st, zf_, dtype)
     rnn = bool(lc.algo.rnn.if_rnn_policy)
     E = lc.algo.n_step - lc.algo.rnn.horizon + 1 if rnn else 1
     obs = None if ob['obs'] is None else f64(ob['obs'], noisy=True)
@@ -607,12 +617,12 @@ def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype, p
     zf = cap['zf_epochs']
     out = {}
     pd = R.DiagGaussRef(A)
-    refm = _stat_model(lc, D, A, pixel, cap['ref'], cap['ref'].get('zf'), dtype)
+    refm = model(cap['ref'], cap['ref'].get('zf'))
     with torch.no_grad():
         ref_pol = refm.model.forward_actor(obs_iter, cells)
     # --- the last policy update's loss (ppo.py:194-225, 250-285)
     if epochs_run > 0:
-        m = _stat_model(lc, D, A, pixel, cap['pol_in'][epochs_run - 1], zf, dtype)
+        m = model(cap['pol_in'][epochs_run - 1], zf)
         m.cells, m.beta, m.clip_epsilon = cells, beta, clip_eps
         learn_pol = m.model.forward_actor(obs_iter, cells)
         lp = pd.likelihood(actions, learn_pol)
@@ -645,7 +655,7 @@ def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype, p
             n = float(torch.sqrt(sum((g * g).sum() for g in gs if g is not None)))
             out['grad_norm_actor'] = (n, n)
     # --- after the policy loop (ppo.py:553-575)
-    mf = _stat_model(lc, D, A, pixel, cap['pol_final'], zf, dtype)
+    mf = model(cap['pol_final'], zf)
     with torch.no_grad():
         curr_pol = mf.model.forward_actor(obs_iter, cells)
         kl = pd.kl(ref_pol, curr_pol).mean()
@@ -664,7 +674,7 @@ def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype, p
     # --- the last value update's loss (ppo.py:311-353)
     nv = lc.algo.consts.epoch_baseline
     if nv > 0:
-        mv = _stat_model(lc, D, A, pixel, cap['val_in'][nv - 1], zf, dtype)
+        mv = model(cap['val_in'][nv - 1], zf)
         values = mv.model.forward_critic(obs_iter, cells)
         if values.dim() == 3:
             values = values.squeeze(2)
