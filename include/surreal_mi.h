@@ -483,6 +483,15 @@ int smi_lstm_forward(const float* xproj, const float* w_hh, const float* b_hh,
                      float* hbuf, float* cbuf, float* gates_act, void* stream);
 int smi_lstm_backward(const float* dh, const float* gates_act, const float* cbuf,
                       const float* w_hh, int S, int B, int H, float* dgates, void* stream);
+/* forward over the raw inputs x [S][B] rows of ldx floats (din <= ldx used),
+ * the input projection x W_ih^T + b_ih fused into the recurrence launch where
+ * it fits (din <= 64, H <= 104), else the xproj GEMM and smi_lstm_forward's
+ * recurrence; outputs as smi_lstm_forward.  Same semantics as nn.LSTM's layer
+ * 0 (ppo_net.py:146-149: the policy / critic stem's rnn_stem). */
+int smi_lstm_forward_x(const float* x, int64_t ldx, int din, const float* w_ih,
+                       const float* b_ih, const float* w_hh, const float* b_hh,
+                       const float* h0, const float* c0, int S, int B, int H, float* hbuf,
+                       float* cbuf, float* gates_act, float* xproj_scratch, void* stream);
 
 /* Pixel stem: CNNStemNetwork (builders.py:8-33) on obs/255 (ppo_net.py:368-375)
  *   conv 8x8/4 (C->16) -> ReLU -> conv 4x4/2 (16->32) -> ReLU -> Flatten -> Linear(F) -> ReLU

@@ -187,6 +187,8 @@ _SIGS = {
     'smi_ppo_rnn_phase': (c_int, [ctypes.POINTER(RNNArgs), c_int, c_int, P]),
     'smi_lstm_forward': (c_int, [P, P, P, P, P, c_int, c_int, c_int, P, P, P, P]),
     'smi_lstm_backward': (c_int, [P, P, P, P, c_int, c_int, c_int, P, P]),
+    'smi_lstm_forward_x': (c_int, [P, c_i64, c_int, P, P, P, P, P, P, c_int, c_int, c_int,
+                                   P, P, P, P, P]),
 }
 
 _lib = None

@@ -670,6 +670,24 @@ int smi_lstm_forward(const float* xproj, const float* w_hh, const float* b_hh, c
                          SMI_STREAM(stream), nullptr);
 }
 
+int smi_lstm_forward_x(const float* x, int64_t ldx, int din, const float* w_ih,
+                       const float* b_ih, const float* w_hh, const float* b_hh, const float* h0,
+                       const float* c0, int S, int B, int H, float* hbuf, float* cbuf,
+                       float* gates_act, float* xproj_scratch, void* stream) {
+  REQUIRE(x && w_ih && b_ih && w_hh && b_hh && h0 && c0 && hbuf && S >= 0 && B >= 0 && H >= 1 &&
+          din >= 1 && ldx >= din, "lstm_forward_x: bad args");
+  const hipStream_t st = SMI_STREAM(stream);
+  const int rf = launch_lstm_fwd_x(x, ldx, din, w_ih, b_ih, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf,
+                                   gates_act, st, nullptr, 0);
+  if (rf != SMI_E_NOFIT) return rf;
+  REQUIRE(xproj_scratch, "lstm_forward_x: the unfused form needs xproj_scratch [S][B][4H]");
+  const int rc = launch_linear_fwd(x, ldx, S * B, din, w_ih, din, b_ih, 4 * H, ACT_NONE,
+                                   xproj_scratch, 4 * H, st, nullptr);
+  if (rc) return rc;
+  return launch_lstm_fwd(xproj_scratch, w_hh, b_hh, h0, c0, S, B, H, hbuf, cbuf, gates_act, st,
+                         nullptr);
+}
+
 int smi_lstm_backward(const float* dh, const float* gates_act, const float* cbuf,
                       const float* w_hh, int S, int B, int H, float* dgates, void* stream) {
   REQUIRE(dh && gates_act && cbuf && w_hh && dgates && S >= 0 && B >= 0 && H >= 1,

@@ -1284,9 +1284,10 @@ __device__ __forceinline__ float dpp_ror8(float v) {          // row_ror:8
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));
 }
 
-template <int KQ, int XQ>
+template <int KQ, int XQ, bool XM, int WI>
 __global__ void __launch_bounds__(kVT)
 lstm_fwd_q_kernel(LstmFwdArgs a) {
+  static_assert(WI != 2 || KQ % 4 == 0, "float4 k runs");
   if (a.skip && a.skip[0] != 0) return;
   const int keepS = a.keep > 0 ? a.keep : a.S;
   static_assert(KQ % 2 == 0 && XQ % 4 == 0, "K split: pairs of h, float4 runs of x");
@@ -1318,17 +1319,72 @@ lstm_fwd_q_kernel(LstmFwdArgs a) {
     hS[1][e] = 0.f;
     if (e < H) a.hbuf[(int64_t)b * H + e] = v;
   }
+  // the matrix-core x parts' B operands (W_ih^T, below), issued before W_hh's
+  // so that the x parts wait on them alone: wave w's gate tiles w + ti*NW
+  // (ti < 4 covers ceil(H/4) tiles over ceil(H/16) waves).  The k order is
+  // permuted so a lane's operands are contiguous: MFMA step s of lane l takes
+  // k = 16 (s >> 2) + 4 (l >> 4) + (s & 3) (A from the staged x rows alike), so
+  // the four lane groups of a row read 64 contiguous bytes per k chunk
+  constexpr int XT = 4, KS = KX / 4;
+  constexpr bool XMF = XQ > 0 && XM;
+  float bw[XMF ? XT : 1][XMF ? KS : 1];
+  if constexpr (XMF) {
+    const int lane = tid & 63, wave = tid >> 6, NW = NT >> 6;
+    const bool v2 = (a.din & 1) == 0 && (reinterpret_cast<uintptr_t>(a.w_ih) & 7) == 0;
+#pragma unroll
+    for (int ti = 0; ti < XT; ++ti) {
+      const int gg = (wave + ti * NW) * 16 + (lane & 15);
+      const float* wr = a.w_ih + (int64_t)(gg < G4 ? gg : 0) * a.din;
+#pragma unroll
+      for (int m = 0; m < KS / 4; ++m) {
+        const int k0 = 16 * m + 4 * (lane >> 4);
+        if (gg < G4 && v2 && k0 + 3 < a.din) {
+          const float2 p0 = *reinterpret_cast<const float2*>(wr + k0);
+          const float2 p1 = *reinterpret_cast<const float2*>(wr + k0 + 2);
+          bw[ti][4 * m] = p0.x; bw[ti][4 * m + 1] = p0.y;
+          bw[ti][4 * m + 2] = p1.x; bw[ti][4 * m + 3] = p1.y;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bw[ti][4 * m + i] = (gg < G4 && k0 + i < a.din) ? wr[k0 + i] : 0.f;
+        }
+      }
+    }
+  }
   __syncthreads();
-  // W_hh rows j*H + u over k in [q*KQ, q*KQ + KQ): in flight during the x parts
+  // W_hh rows j*H + u over the k pairs (8i + 2q, 8i + 2q + 1), i < KQ / 2: the
+  // quad's four lanes read 32 contiguous bytes of a row per load (a lane-
+  // contiguous quarter row put every lane of a load on its own cache line: the
+  // prologue re-fetched W_hh from L2 many times over); in flight during the x
+  // parts
   vf2 wv[4][KQ / 2];
-  {
+  if constexpr (WI == 2) {
+    // k runs (16 i + 4q .. + 3): 64 contiguous bytes of a row per quad and load
+    const bool vec = (H & 3) == 0 && (reinterpret_cast<uintptr_t>(a.w_hh) & 15) == 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* r = a.w_hh + (int64_t)(j * H + uc) * H;
+#pragma unroll
+      for (int i = 0; i < KQ / 4; ++i) {
+        const int k = 16 * i + 4 * q;
+        float4 v;
+        if (vec) {
+          v = k + 3 < H ? *reinterpret_cast<const float4*>(r + k) : float4{0.f, 0.f, 0.f, 0.f};
+        } else {
+          v = float4{k < H ? r[k] : 0.f, k + 1 < H ? r[k + 1] : 0.f, k + 2 < H ? r[k + 2] : 0.f,
+                     k + 3 < H ? r[k + 3] : 0.f};
+        }
+        wv[j][2 * i] = vf2{v.x, v.y};
+        wv[j][2 * i + 1] = vf2{v.z, v.w};
+      }
+    }
+  } else {
     const bool vec = (H & 1) == 0 && (reinterpret_cast<uintptr_t>(a.w_hh) & 7) == 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float* r = a.w_hh + (int64_t)(j * H + uc) * H;
 #pragma unroll
       for (int i = 0; i < KQ / 2; ++i) {
-        const int k = q * KQ + 2 * i;
+        const int k = WI ? 8 * i + 2 * q : q * KQ + 2 * i;
         vf2 v;
         if (vec) {
           const float2 t2 = k + 1 < H ? *reinterpret_cast<const float2*>(r + k) : float2{0.f, 0.f};
@@ -1340,7 +1396,43 @@ lstm_fwd_q_kernel(LstmFwdArgs a) {
       }
     }
   }
-  if constexpr (XQ > 0) {
+  if constexpr (XMF) {
+    // x parts of every step on the matrix cores: xP[t][tid(g)] = sum_k x_t[k]
+    // W_ih[g][k] + b_ih[g] + b_hh[g] as v_mfma_f32_16x16x4_f32 tiles of 16 steps
+    // x 16 gate rows (A = the staged x rows, B = W_ih^T, one k-ordered fmaf
+    // chain per element); a tile's B operand stays in registers across the
+    // step tiles
+    const int lane = tid & 63, wave = tid >> 6, NW = NT >> 6;
+    const int nmt = (a.S + 15) >> 4;
+#pragma unroll
+    for (int ti = 0; ti < XT; ++ti) {
+      const int nt = wave + ti * NW;
+      if (nt * 16 >= G4) break;
+      const int gs = nt * 16 + (lane & 15);                 // the D column's gate
+      const float bsum = gs < G4 ? a.b_ih[gs] + a.b_hh[gs] : 0.f;
+      const int dst = gs < G4 ? 4 * (gs % H) + gs / H : 0;
+      for (int mt = 0; mt < nmt; ++mt) {
+        const int r = min(mt * 16 + (lane & 15), a.S - 1);
+        const float4* xr = reinterpret_cast<const float4*>(xS + r * KX + 4 * (lane >> 4));
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < KS / 4; ++m) {
+          if (16 * m >= a.din) break;
+          const float4 xv = xr[4 * m];
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, bw[ti][4 * m], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, bw[ti][4 * m + 1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.z, bw[ti][4 * m + 2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.w, bw[ti][4 * m + 3], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = mt * 16 + 4 * (lane >> 4) + i;
+          if (t < a.S && gs < G4) xP[(int64_t)t * NT + dst] = acc[i] + bsum;
+        }
+      }
+    }
+    __syncthreads();
+  } else if constexpr (XQ > 0) {
     // x parts of every step: W_ih rows j*H + u over x columns [q*XQ, q*XQ + XQ)
     float wx[4][XQ];
 #pragma unroll
@@ -1386,7 +1478,7 @@ lstm_fwd_q_kernel(LstmFwdArgs a) {
   }
   float ph = 0.f, pc = 0.f, pav = 0.f;
   for (int t = 0; t < a.S; ++t) {
-    const float* hp = hS[t & 1] + q * KQ;
+    const float* hp = hS[t & 1] + (WI == 2 ? 4 * q : WI ? 2 * q : q * KQ);
     float* hn = hS[(t + 1) & 1];
     float xacc;
     if constexpr (XQ > 0) {
@@ -1394,10 +1486,20 @@ lstm_fwd_q_kernel(LstmFwdArgs a) {
     } else {
       xacc = xnext + bh;
     }
-    const float2* h2 = reinterpret_cast<const float2*>(hp);
     float2 hv[KQ / 2];
+    if constexpr (WI == 2) {
+      const float4* h4 = reinterpret_cast<const float4*>(hp);
 #pragma unroll
-    for (int i = 0; i < KQ / 2; ++i) hv[i] = h2[i];
+      for (int i = 0; i < KQ / 4; ++i) {
+        const float4 v = h4[4 * i];
+        hv[2 * i] = float2{v.x, v.y};
+        hv[2 * i + 1] = float2{v.z, v.w};
+      }
+    } else {
+      const float2* h2 = reinterpret_cast<const float2*>(hp);
+#pragma unroll
+      for (int i = 0; i < KQ / 2; ++i) hv[i] = h2[WI ? 4 * i : i];
+    }
     if constexpr (XQ == 0) {          // xproj of step t + 1, in flight through the step
       if (t + 1 < a.S) xnext = a.xproj[((int64_t)(t + 1) * B + b) * G4 + g];
     }
@@ -1634,18 +1736,43 @@ static bool use_q() {
   static const bool on = [] { const char* e = getenv("SMI_LSTM_Q"); return !(e && e[0] == '0'); }();
   return on;
 }
+// x parts on the matrix cores (SMI_LSTM_XM=0: the VALU K-split form; A/B knob)
+static bool use_xm() {
+  static const bool on = [] { const char* e = getenv("SMI_LSTM_XM"); return !(e && e[0] == '0'); }();
+  return on;
+}
 template <int XQ>
 static void fwd_q_dispatch(const LstmFwdArgs& a, hipStream_t st) {
   const dim3 grid(a.B), blk((4 * a.H + 63) & ~63);
+  const bool xm = XQ > 0 && use_xm();
+  // W_hh register layout (SMI_LSTM_WI; A/B knob): 0 a contiguous quarter row
+  // per lane, 1 k pairs interleaved over the quad, 2 float4 runs interleaved
+  static const int wi = [] { const char* e = getenv("SMI_LSTM_WI"); return e && e[0] ? atoi(e) : 2; }();
   const size_t lds = XQ > 0 ? lstm_fwd_v_lds(a.S, 1, 4 * XQ, blk.x) : 0;
-#define SMI_FQ(KQ)                                                                 \
+#define SMI_FQ(KQ, W)                                                              \
   do {                                                                             \
-    allow_lds(lstm_fwd_q_kernel<KQ, XQ>, lds);                                     \
-    hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ>), grid, blk, lds, st, a);        \
+    if (xm) {                                                                      \
+      allow_lds(lstm_fwd_q_kernel<KQ, XQ, true, W>, lds);                          \
+      hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ, true, W>), grid, blk, lds, st, a);  \
+    } else {                                                                       \
+      allow_lds(lstm_fwd_q_kernel<KQ, XQ, false, W>, lds);                         \
+      hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ, false, W>), grid, blk, lds, st, a); \
+    }                                                                              \
   } while (0)
-  if (a.H <= 64) SMI_FQ(16);
-  else if (a.H <= 104) SMI_FQ(26);
-  else SMI_FQ(32);
+  if (a.H <= 64) {
+    if (wi == 2) SMI_FQ(16, 2);
+    else if (wi == 1) SMI_FQ(16, 1);
+    else SMI_FQ(16, 0);
+  } else if (a.H <= 112 && wi == 2) {
+    SMI_FQ(28, 2);
+  } else if (a.H <= 104) {
+    if (wi == 1) SMI_FQ(26, 1);
+    else SMI_FQ(26, 0);
+  } else {
+    if (wi == 2) SMI_FQ(32, 2);
+    else if (wi == 1) SMI_FQ(32, 1);
+    else SMI_FQ(32, 0);
+  }
 #undef SMI_FQ
 }
 void lstm_v_fwd(const LstmFwdArgs& a, int R, int kx, hipStream_t st) {

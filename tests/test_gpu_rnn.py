@@ -3,7 +3,8 @@ surreal/model/ppo_net.py:137-152) on the HIP kernels vs the CPU oracle.
 
 * LSTM sequence kernels vs torch.nn.LSTM on CPU (the reference's own module):
   outputs, final cells and the parameter gradients assembled from the kernel's
-  dgates, within the GEMM parity bar of test_gpu_ddpg.py.
+  dgates, within the GEMM parity bar of test_gpu_ddpg.py; the fused-input
+  forward (smi_lstm_forward_x) on the same bar.
 * PPOLearner.learn() with the LSTM stem vs oracle.PPOLearnerRef (which runs
   torch.nn.LSTM): clip and adapt, z-filter, ragged segment counts (B not a
   multiple of 16), and the real C3 layer sizes (D 42, LSTM 100, heads 300x200,
@@ -78,6 +79,16 @@ def test_lstm_kernels_vs_torch_lstm(B, S, D, H):
     _fp32_as_good_as_torch(got, out.detach(), out64.detach(), 2e-6)
     _fp32_as_good_as_torch(cbuf[S].cpu(), cn[0].detach(), cn64[0].detach(), 2e-6)
     assert torch.equal(hbuf[0].cpu(), h0[0])
+    # the fused input projection (smi_lstm_forward_x: x W_ih^T in the recurrence
+    # launch where it fits — matrix-core x parts at one segment per workgroup,
+    # the r4 MFMA form beyond — else the xproj GEMM + recurrence)
+    hbx, cbx = torch.empty_like(hbuf), torch.empty_like(cbuf)
+    gx, xps = torch.empty_like(gates), torch.empty_like(xproj)
+    L.call('smi_lstm_forward_x', L.ptr(xt), D, D, L.ptr(Wih), L.ptr(bih), L.ptr(Whh), L.ptr(bhh),
+           L.ptr(h0d), L.ptr(c0d), S, B, H, L.ptr(hbx), L.ptr(cbx), L.ptr(gx), L.ptr(xps), st)
+    _fp32_as_good_as_torch(hbx[1:].transpose(0, 1).cpu(), out.detach(), out64.detach(), 2e-6)
+    _fp32_as_good_as_torch(cbx[S].cpu(), cn[0].detach(), cn64[0].detach(), 2e-6)
+    torch.testing.assert_close(gx.cpu(), gates.cpu(), rtol=0, atol=2e-5)
     # backward: loss = sum(out * dh)
     dht = dh.transpose(0, 1).contiguous().to(DEV)
     dgates = torch.empty(S, B, 4 * H, device=DEV)

@@ -1465,8 +1465,9 @@ static float runb(BFn k, const BArgs& a, int iters, int nt = NT) {
 
 typedef void (*KFn)(Args);
 
-static float run(KFn k, const Args& a, int iters, int nt = NT) {
-  const size_t lds = ((size_t)((a.S * KX + 3) & ~3) + (size_t)a.S * nt) * 4;
+static float run(KFn k, const Args& a, int iters, int nt = NT, size_t min_lds = 0) {
+  size_t lds = ((size_t)((a.S * KX + 3) & ~3) + (size_t)a.S * nt) * 4;
+  if (lds < min_lds) lds = min_lds;
   CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -1524,6 +1525,20 @@ int main() {
     }
     printf("{\"variant\": \"%s\", \"us_S1\": %.2f, \"us_S21\": %.2f, \"us_S41\": %.2f, \"us_per_step\": %.3f}\n",
            names[v], t[0], t[1], t[2], (t[2] - t[0]) / 40.f);
+  }
+  {   // co-residence: segments per launch 128 / 32 / 1, and 128 with 96 KB of
+      // dynamic LDS (one workgroup per CU)
+    struct Co { int B; size_t lds; } co[4] = {{128, 0}, {32, 0}, {1, 0}, {128, 96 * 1024}};
+    for (int kv = 0; kv < 2; ++kv)
+    for (auto& c : co) {
+      float t[3];
+      for (int si = 0; si < 3; ++si) {
+        Args a{dx, ldx, dwih, dbih, dwhh, dbhh, dh0, dc0, Ss[si], c.B, hb[0], cb[0], gt[0]};
+        t[si] = run(kv ? v4_kernel<false> : v0_kernel, a, 30, NT, c.lds);
+      }
+      printf("{\"coresidence\": \"V%d B=%d lds=%zu\", \"us_S1\": %.2f, \"us_S41\": %.2f, \"us_per_step\": %.3f}\n",
+             kv ? 4 : 0, c.B, c.lds, t[0], t[2], (t[2] - t[0]) / 40.f);
+    }
   }
   {   // phase ticks of V3t at S = 21 (shader cycles per launch, per wave; steps summed)
     Args a{dx, ldx, dwih, dbih, dwhh, dbhh, dh0, dc0, 21, B, hb[1], cb[1], gt[1]};
