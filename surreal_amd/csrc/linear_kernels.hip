@@ -25,6 +25,7 @@
 #include <type_traits>
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
+#include "lstm_cell.hpp"
 
 namespace smi {
 
@@ -968,7 +969,8 @@ gemm_dwd_kernel(GemmArgs g) {
 // writes its own split-K partials, and one grouped reducer finishes them all.
 // One launch and one reduce per phase instead of a launch + reduce per layer
 // (and no side stream): the ~20 us fixed cost of a dW launch is paid once.
-constexpr int kDwGroupMax = 6;
+constexpr int kDwGroupMax = 8;   // entries of one reducer (two launches' worth)
+constexpr int kDwSplitMax = 6;    // entries of one grouped launch after tail splits
 struct DwGroup {
   DwEpilogue x;                  // optional epilogue task of the reducer (smi_internal.hpp)
   GemmArgs g[kDwGroupMax];
@@ -1009,50 +1011,29 @@ extern "C" int smi_diag_dw_trace(void* dst, int n) {
 }
 #endif
 
+// one workgroup of a grouped launch: orig = its index among the launch's nwg
+// dW workgroups (the XCD-contiguous remap, gemm_tile_index, assumes orig and
+// the hardware's blockIdx agree mod 8); gi / rows report the entry and slab
+// length for the clock trace
 template <int WV>
-__global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWG_OCC : 1)
-gemm_dwd_group_kernel(DwGroup G) {
-#if SMI_DWD_TRACE
-  const unsigned long long t_start = wall_clock64(), c_start = clock64();
-  struct TraceEnd {
-    unsigned long long t0, c0; int gi = 0, rows = 0;
-    __device__ ~TraceEnd() {
-      __syncthreads();
-      if (threadIdx.x == 0 && blockIdx.x < kDwTraceMax) {
-        g_dw_trace[blockIdx.x][0] = t0;
-        g_dw_trace[blockIdx.x][1] = wall_clock64();
-        g_dw_trace[blockIdx.x][2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        g_dw_trace[blockIdx.x][3] = __builtin_amdgcn_s_getreg((31 << 11) | 20) | (gi << 8) |
-                                    ((unsigned long long)rows << 16);
-        g_dw_trace[blockIdx.x][4] = c0;
-        g_dw_trace[blockIdx.x][5] = clock64();
-      }
-    }
-  } trace_end{t_start, c_start};
-#endif
-  extern __shared__ float4 dwd_red[];
-  const int nwg = gridDim.x, orig = blockIdx.x;
+__device__ __forceinline__ void dwd_group_run(const DwGroup& G, int orig, int nwg, float4* dwd_red,
+                                              int& gi, int& rows) {
   int w = orig;
   if (nwg > 8) {                                  // XCD-contiguous runs (gemm_tile_index)
     const int x = orig & 7, q = nwg >> 3, r = nwg & 7;
     w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
   }
-  int gi = 0;
+  gi = 0;
   while (gi + 1 < G.n && w >= G.wg0[gi + 1]) ++gi;
   const GemmArgs& g = G.g[gi];
-#if SMI_DWD_TRACE
-  trace_end.gi = gi;
-#endif
   if (g.skip && g.skip[0] != 0) return;
   const int local = w - G.wg0[gi], gn = G.gn[gi], gm = G.gm[gi];
   TileIdx ti;
   ti.nt = local % gn;
   ti.mt = (local / gn) % gm;
   ti.z = local / (gn * gm);
-#if SMI_DWD_TRACE
-  trace_end.rows = (min(g.K, (ti.z + 1) * g.kchunk) - ti.z * g.kchunk) |
-                   ((G.narrow[gi] && ti.mt == gm - 1) << 16) | (G.vec[gi] << 17);
-#endif
+  rows = (min(g.K, (ti.z + 1) * g.kchunk) - ti.z * g.kchunk) |
+         ((G.narrow[gi] && ti.mt == gm - 1) << 16) | (G.vec[gi] << 17);
   if (G.narrow[gi] && ti.mt == gm - 1) {
     // a tail of <= 16 gradient rows (M 8 / 200 / 400 at C3) on one 16-wide
     // m sub-tile instead of a 64-wide tile that is >= 75 % padding
@@ -1067,6 +1048,48 @@ gemm_dwd_group_kernel(DwGroup G) {
     case 1: dwd_tile<4, DWG_NT, false, true, WV>(g, ti, dwd_red); break;
     default: dwd_tile<4, DWG_NT, false, false, WV>(g, ti, dwd_red); break;
   }
+}
+
+template <int WV>
+__global__ void __launch_bounds__(64 * WV, WV == 4 ? SMI_DWG_OCC : 1)
+gemm_dwd_group_kernel(DwGroup G) {
+  extern __shared__ float4 dwd_red[];
+  int gi = 0, rows = 0;
+#if SMI_DWD_TRACE
+  const unsigned long long t_start = wall_clock64(), c_start = clock64();
+#endif
+  dwd_group_run<WV>(G, blockIdx.x, gridDim.x, dwd_red, gi, rows);
+#if SMI_DWD_TRACE
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x < kDwTraceMax) {
+    g_dw_trace[blockIdx.x][0] = t_start;
+    g_dw_trace[blockIdx.x][1] = wall_clock64();
+    g_dw_trace[blockIdx.x][2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    g_dw_trace[blockIdx.x][3] = __builtin_amdgcn_s_getreg((31 << 11) | 20) | (gi << 8) |
+                                ((unsigned long long)rows << 16);
+    g_dw_trace[blockIdx.x][4] = c_start;
+    g_dw_trace[blockIdx.x][5] = clock64();
+  }
+#else
+  (void)gi; (void)rows;
+#endif
+}
+
+// BPTT of the one-segment-per-workgroup VALU form (workgroups < la.B) and
+// the weight gradients already queued in the phase's group (the heads'; the
+// others) in ONE launch: the heads' gradients need nothing from the BPTT, so
+// they run on the CUs the recurrence leaves idle (la.B segments on one CU
+// each) instead of after it
+template <int BR>
+__global__ void __launch_bounds__(kVT, 1)
+lstm_bwd_dw_kernel(LstmBwdArgs la, DwGroup G) {
+  if ((int)blockIdx.x < la.B) {
+    lstm_bwd_q_body<BR>(la, blockIdx.x);
+    return;
+  }
+  extern __shared__ float4 dwd_red[];
+  int gi = 0, rows = 0;
+  dwd_group_run<8>(G, blockIdx.x - la.B, gridDim.x - la.B, dwd_red, gi, rows);
 }
 
 // the partials of every GEMM of a group, each element summed over its slabs in
@@ -1437,6 +1460,10 @@ static bool dw_group_add(const GemmArgs& g) {
 // slabs), 512 -> 48, 256 -> 46: slabs shorter than ~384 rows are all ramp.
 // With the 64 x 64 tiles at 3 waves per SIMD (DWG_NT below): 1024 -> 120.5 us
 // per C3 launch, 1536 -> 110.0 (0.37 of the f32 MFMA peak), 2048 -> 110.5.
+// Round 5, 128 segments (3200 rows): the LSTM's gradient alone (the heads'
+// run with the BPTT) at 128 / 175 (work / 384) / 256 / 384 workgroups: 23.8 /
+// 22.9 / 21.1 / 21.3 us; the whole group at 512 vs 458: 26.5 vs 28.0 us —
+// work / 256.
 static int dw_group_target(double work) {
   static int t = -1;
   if (t < 0) {
@@ -1445,7 +1472,7 @@ static int dw_group_target(double work) {
     if (e && e[0] && t < 64) t = 64;
   }
   if (t > 0) return t;
-  const double w = work / 384.0;
+  const double w = work / 256.0;
   return w >= 1536.0 ? 1536 : w <= 128.0 ? 128 : (int)w;
 }
 
@@ -1483,23 +1510,14 @@ static int dwd_group_slots(size_t lds) {
   return slots;
 }
 
-int dw_group_flush(hipStream_t st) {
-  g_grp_on = false;
-  DwGroup& G = g_grp;
-  const bool overflow = g_grp_overflow;
-  g_grp_overflow = false;
-  if (G.x.on && G.x.sq && overflow)
-    return set_error(SMI_E_ARG, "dw group: a fused sum of squares needs every dW GEMM in the group");
-  if (G.n == 0) {
-    if (!G.x.on) return SMI_OK;
-    if (G.x.sq) return set_error(SMI_E_ARG, "dw group: fused sum of squares over an empty group");
-    G.rb0[0] = 0;                                   // the epilogue task alone
-    hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(1), dim3(kWG), 0, st, G);
-    return check_launch("gemm_group_reduce_kernel");
-  }
+// Tail splits, balanced slabs and the split-K partials of G's entries, placed
+// ws_off floats into the workspace; wv: waves per workgroup of the launch that
+// runs them, slots: its resident workgroups.  Sets G.wg0 / rb0 / S / part and
+// need (floats used from ws_off).
+static int dw_prepare(DwGroup& G, int wv, int slots, int64_t ws_off, int64_t& need,
+                      int target_fixed = 0) {
   constexpr int MT = 4, NT = DWG_NT;
-  const size_t lds = (size_t)2 * MT * NT * 64 * sizeof(float4);
-  const int rs = 4 * dwd_waves() * DWD_P;           // rows per prefetch window
+  const int rs = 4 * wv * DWD_P;                    // rows per prefetch window
   auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   // A GEMM whose last m-tile is a <= 16-row tail (M 8 / 200 / 400 at C3) is
   // split, while the group has room, into its full 64-row tiles and a tail
@@ -1513,7 +1531,7 @@ int dw_group_flush(hipStream_t st) {
       const GemmArgs& g = G.g[i];
       const int tail = g.M % (16 * MT);
       const bool split = use_dwd_narrow() && tail > 0 && tail <= 16 && g.M > 16 * MT &&
-                         g.a_rs == 1 && n + (n0 - i) + 1 <= kDwGroupMax;
+                         g.a_rs == 1 && n + (n0 - i) + 1 <= kDwSplitMax;
       E.g[n] = g;
       E.vec[n] = G.vec[i];
       if (!split) { ++n; continue; }
@@ -1543,7 +1561,6 @@ int dw_group_flush(hipStream_t st) {
   // of a full tile per row).  Below one round every workgroup is resident
   // anyway and the span is the longest slab: equal slab lengths (shorter
   // fp32 chains on the tail tiles).
-  const int slots = dwd_group_slots(lds);
   double cost[kDwGroupMax], work = 0.0, work_u = 0.0;  // tiles x rows (x cost)
   int64_t tiles[kDwGroupMax];
   for (int i = 0; i < G.n; ++i) {
@@ -1557,11 +1574,12 @@ int dw_group_flush(hipStream_t st) {
     work_u += (double)tiles[i] * g.K;
     work += (double)tiles[i] * g.K * cost[i];
   }
-  int target = dw_group_target(work_u);
-  static const bool fixed_target = [] {
+  int target = target_fixed > 0 ? target_fixed : dw_group_target(work_u);
+  static const bool env_target = [] {
     const char* e = getenv("SMI_DWD_GROUP_TARGET");
     return e && e[0];
   }();
+  const bool fixed_target = env_target || target_fixed > 0;
   if (!fixed_target && target >= slots) {
     // whole rounds of at most ~2048 cost-rows per workgroup (SMI_DWD_ROUND_ROWS)
     static const double round_rows = [] {
@@ -1575,9 +1593,8 @@ int dw_group_flush(hipStream_t st) {
     for (int i = 0; i < G.n; ++i) cost[i] = 1.0;
     work = work_u;
   }
-  const int64_t cap = smi_workspace_floats();
+  const int64_t cap = smi_workspace_floats() - ws_off;
   double r0 = work / target;                        // cost-rows per workgroup
-  int64_t need = 0;
   int64_t kcs[kDwGroupMax];
   // slab lengths are rounded up to whole prefetch windows, so the workgroup
   // count can land a few above the target; in whole rounds every extra
@@ -1585,6 +1602,7 @@ int dw_group_flush(hipStream_t st) {
   // slots: the last workgroup started at 59 us and set the span), so the
   // cost-rows per workgroup grow in small steps until the count fits
   const bool rounds_fit = !fixed_target && target >= slots;
+  need = 0;
   for (int pass = 0; pass < 400; ++pass) {
     need = 0;
     int64_t wgs = 0;
@@ -1604,8 +1622,9 @@ int dw_group_flush(hipStream_t st) {
     if (rounds_fit && wgs > target && wgs <= 2 * target) { r0 *= 1.005; continue; }
     break;
   }
-  float* base = workspace_f32(need);
+  float* base = workspace_f32(ws_off + need);
   if (!base) return set_error(SMI_E_ARG, "gemm: workspace too small for the grouped dW partials");
+  base += ws_off;
   int64_t off = 0;
   G.wg0[0] = 0;
   G.rb0[0] = 0;
@@ -1618,18 +1637,113 @@ int dw_group_flush(hipStream_t st) {
     G.wg0[i + 1] = G.wg0[i] + (int)(tiles[i] * G.S[i]);
     G.rb0[i + 1] = G.rb0[i] + (int)(((int64_t)g.M * g.N + 63) / 64);
   }
-  const int kslot = ktime_begin(st);
-  if (dwd_waves() == 8)
-    hipLaunchKernelGGL(gemm_dwd_group_kernel<8>, dim3(G.wg0[G.n]), dim3(512), lds, st, G);
-  else
-    hipLaunchKernelGGL(gemm_dwd_group_kernel<4>, dim3(G.wg0[G.n]), dim3(256), lds, st, G);
-  ktime_end(kslot, KT_GEMM_DW, g_grp_flops, st);
-  RC_CHECK(check_launch("gemm_dwd_group_kernel"));
+  return SMI_OK;
+}
+
+// entries already launched with the BPTT (launch_lstm_bwd_dw) whose partials
+// the group's reducer still sums, and the workspace floats they hold
+static thread_local DwGroup g_pre;
+static thread_local bool g_pre_on = false;
+static thread_local int64_t g_pre_need = 0;
+
+constexpr size_t kDwdLds = (size_t)2 * 4 * DWG_NT * 64 * sizeof(float4);
+
+int dw_group_flush(hipStream_t st) {
+  g_grp_on = false;
+  DwGroup& G = g_grp;
+  const bool overflow = g_grp_overflow;
+  g_grp_overflow = false;
+  const bool pre = g_pre_on;
+  g_pre_on = false;
+  if (G.x.on && G.x.sq && overflow)
+    return set_error(SMI_E_ARG, "dw group: a fused sum of squares needs every dW GEMM in the group");
+  if (G.n == 0 && !pre) {
+    if (!G.x.on) return SMI_OK;
+    if (G.x.sq) return set_error(SMI_E_ARG, "dw group: fused sum of squares over an empty group");
+    G.rb0[0] = 0;                                   // the epilogue task alone
+    hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(1), dim3(kWG), 0, st, G);
+    return check_launch("gemm_group_reduce_kernel");
+  }
+  int64_t need = 0;
+  if (G.n > 0) {
+    RC_CHECK(dw_prepare(G, dwd_waves(), dwd_group_slots(kDwdLds), pre ? g_pre_need : 0, need));
+    const int kslot = ktime_begin(st);
+    if (dwd_waves() == 8)
+      hipLaunchKernelGGL(gemm_dwd_group_kernel<8>, dim3(G.wg0[G.n]), dim3(512), kDwdLds, st, G);
+    else
+      hipLaunchKernelGGL(gemm_dwd_group_kernel<4>, dim3(G.wg0[G.n]), dim3(256), kDwdLds, st, G);
+    ktime_end(kslot, KT_GEMM_DW, g_grp_flops, st);
+    RC_CHECK(check_launch("gemm_dwd_group_kernel"));
+  }
+  // the reducer sums the partials of the entries launched with the BPTT and
+  // of these, in one launch
+  DwGroup R = G;
+  if (pre) {
+    R = g_pre;
+    R.x = G.x;
+    if (R.n + G.n > kDwGroupMax) return set_error(SMI_E_ARG, "dw group: too many entries");
+    for (int i = 0; i < G.n; ++i) {
+      const int j = R.n + i;
+      R.g[j] = G.g[i];
+      R.S[j] = G.S[i];
+      R.rb0[j + 1] = R.rb0[j] + (int)(((int64_t)G.g[i].M * G.g[i].N + 63) / 64);
+    }
+    R.n += G.n;
+    need += g_pre_need;
+  }
   const int rslot = ktime_begin(st);
-  hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(G.rb0[G.n] + (G.x.on ? 1 : 0)), dim3(kWG), 0,
-                     st, G);
+  hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(R.rb0[R.n] + (R.x.on ? 1 : 0)), dim3(kWG), 0,
+                     st, R);
   ktime_end(rslot, KT_GEMM_REDUCE, (double)need, st);
   return check_launch("gemm_group_reduce_kernel");
+}
+
+// SMI_BWD_DW=0: the BPTT and the heads' weight gradients as separate launches
+// (A/B knob); SMI_BWD_DW_EXCL=0: let the two kinds of workgroups share CUs
+static bool use_bwd_dw() {
+  static const bool on = [] { const char* e = getenv("SMI_BWD_DW"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+int launch_lstm_bwd_dw(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
+                       int S, int B, int H, float* dgates, hipStream_t st, const int* skip) {
+  const int br = lstm_bwd_q_form(B, H);
+  if (!use_bwd_dw() || !g_grp_on || g_pre_on || g_grp.n == 0 || br == 0 || S <= 0 || B <= 0)
+    return SMI_E_NOFIT;
+  int cus = 0, dev = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  if (cus - B < 32) return SMI_E_NOFIT;             // too few CUs left beside the recurrence
+  DwGroup Ga = g_grp;
+  int64_t need = 0;
+  // balanced for the CUs the recurrence leaves idle (a fixed one-round target
+  // of cus - B workgroups with equal slabs: 50.6 vs 30.9 us per launch at 128
+  // segments — slab rounding pushed the count past one round)
+  RC_CHECK(dw_prepare(Ga, 8, cus - B, 0, need));
+  // one workgroup per CU (the LDS request): the recurrence's workgroups keep
+  // their CUs to themselves, the weight gradients take the others
+  static const bool excl = [] { const char* e = getenv("SMI_BWD_DW_EXCL"); return !(e && e[0] == '0'); }();
+  const size_t lds = excl ? std::max(kDwdLds, (size_t)84 * 1024) : kDwdLds;
+  LstmBwdArgs la{dh, gates, cbuf, w_hh, S, B, H, dgates, skip};
+  const dim3 grid((unsigned)(B + Ga.wg0[Ga.n]));
+  const int kslot = ktime_begin(st);
+#define SMI_BD(BR_)                                                                  \
+  do {                                                                               \
+    allow_lds(lstm_bwd_dw_kernel<BR_>, lds);                                         \
+    hipLaunchKernelGGL(lstm_bwd_dw_kernel<BR_>, grid, dim3(kVT), lds, st, la, Ga);   \
+  } while (0)
+  if (br == 16) SMI_BD(16);
+  else if (br == 25) SMI_BD(25);
+  else SMI_BD(32);
+#undef SMI_BD
+  ktime_end(kslot, KT_LSTM_BWD, 8.0 * B * H * (double)H * (S - 1), st);
+  RC_CHECK(check_launch("lstm_bwd_dw_kernel"));
+  g_pre = Ga;
+  g_pre_on = true;
+  g_pre_need = need;
+  g_grp.n = 0;                                      // the group queues the rest
+  g_grp_flops = 0.0;                                // (its launch times the rest only)
+  return SMI_OK;
 }
 
 static int use_panel() {

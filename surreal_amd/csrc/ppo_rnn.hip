@@ -1082,6 +1082,18 @@ adam_split_kernel(AdamSplitArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   __shared__ double red[kNW];
   __shared__ float s_coef;
+  const int64_t n = a.n0 + a.n1;
+  // the thread's first element (every one at the launch's grid size) is loaded
+  // before the norm's partials are summed: its memory latency overlaps the sum
+  const int64_t i_first = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  float* pf = i_first < a.n0 ? a.p0 + i_first : a.p1 + (i_first - a.n0);
+  float gf = 0.f, pvf = 0.f, mf = 0.f, vf = 0.f;
+  if (i_first < n) {
+    gf = a.g[i_first];
+    pvf = *pf;
+    mf = a.m[i_first];
+    vf = a.v[i_first];
+  }
   const int np = a.np_dev ? a.np_dev[0] : a.np;
   double s4[4] = {0.0, 0.0, 0.0, 0.0};       // four partials in flight per thread
   int i0 = threadIdx.x;
@@ -1110,13 +1122,13 @@ adam_split_kernel(AdamSplitArgs a) {
   const float bc2_sqrt = (float)sqrt(bc2);
   const float w1 = (float)(1.0 - (double)a.beta1);
   const float w2 = (float)(1.0 - (double)a.beta2);
-  const int64_t n = a.n0 + a.n1;
-  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n; i += (int64_t)gridDim.x * kWG) {
-    float* pp = i < a.n0 ? a.p0 + i : a.p1 + (i - a.n0);
-    float g = a.g[i] * coef;
-    float p = *pp;
+  for (int64_t i = i_first; i < n; i += (int64_t)gridDim.x * kWG) {
+    const bool fst = i == i_first;
+    float* pp = fst ? pf : i < a.n0 ? a.p0 + i : a.p1 + (i - a.n0);
+    float g = (fst ? gf : a.g[i]) * coef;
+    float p = fst ? pvf : *pp;
     if (a.wd != 0.f) g = g + a.wd * p;
-    float mi = a.m[i], vi = a.v[i];
+    float mi = fst ? mf : a.m[i], vi = fst ? vf : a.v[i];
     mi = mi + w1 * (g - mi);
     vi = vi * a.beta2 + (w2 * g) * g;
     const float denom = sqrtf(vi) / bc2_sqrt + a.eps;
@@ -1423,8 +1435,18 @@ static int lstm_backward(const RnnDims& d, const float* P, float* G, const RnnSc
     const LstmP lp = lstm_layer(d, P, l);
     float* dg = dgates_of(d, s, l);
     float* hb = hbuf_of(d, s, l);
-    RC(launch_lstm_bwd(s.dh, gates_of(d, s, l), cbuf_of(d, s, l), lp.Whh, d.E, d.B, d.H, dg, st,
-                       skip));
+    // one layer, no pixel stem: the BPTT shares its launch with the heads'
+    // weight gradients queued so far (nothing between here and the group's
+    // flush uses the workspace that holds their partials)
+    int rb = SMI_E_NOFIT;
+    if (d.L == 1 && d.F == 0)
+      rb = launch_lstm_bwd_dw(s.dh, gates_of(d, s, l), cbuf_of(d, s, l), lp.Whh, d.E, d.B, d.H, dg,
+                              st, skip);
+    if (rb == SMI_E_NOFIT)
+      RC(launch_lstm_bwd(s.dh, gates_of(d, s, l), cbuf_of(d, s, l), lp.Whh, d.E, d.B, d.H, dg, st,
+                         skip));
+    else if (rb)
+      return rb;
     const int din = l == 0 ? d.Din : d.H;
     const float* Xl = l == 0 ? s.Xz : hbuf_of(d, s, l - 1) + BH;
     const int64_t ldx = l == 0 ? d.ldx : d.H;

@@ -60,6 +60,13 @@ struct DwEpilogue {
   const int* skip;
 };
 int dw_group_epilogue(const DwEpilogue& x);
+// BR of the one-segment-per-workgroup BPTT form for (B, H), 0 when another form runs
+int lstm_bwd_q_form(int B, int H);
+// the LSTM BPTT (lstm_bwd_q form) and the weight gradients queued so far in the
+// open dW group in one launch (linear_kernels.hip); SMI_E_NOFIT: run
+// launch_lstm_bwd instead (nothing launched)
+int launch_lstm_bwd_dw(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
+                       int S, int B, int H, float* dgates, hipStream_t st, const int* skip);
 int check_launch(const char* what);
 
 // Test-only fault injection (build variant 'fault', -DSMI_FAULT_INJECTION;

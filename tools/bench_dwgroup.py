@@ -22,6 +22,8 @@ def main():
     ap.add_argument('--iters', type=int, default=50)
     ap.add_argument('--segments', type=int, default=1024)
     ap.add_argument('--steps', type=int, default=21)
+    ap.add_argument('--only', choices=('all', 'head', 'lstm'), default='all',
+                    help='queue only the heads\' or only the LSTM\'s GEMMs')
     args = ap.parse_args()
     R = args.segments * args.steps
     dev = torch.device('cuda', 0)
@@ -50,9 +52,13 @@ def main():
 
     def phase():
         L.call('smi_dw_group_begin')
-        L.call('smi_linear_backward_weight', P(dZ), A, R, A, P(HA2), h2, h2, P(gW3), h2, P(gb3), 0, st)
-        L.call('smi_linear_backward_weight', P(dH2), h2, R, h2, P(HA1), h1, h1, P(gW2), h1, P(gb2), 0, st)
-        L.call('smi_linear_backward_weight', P(dH1), h1, R, h1, P(X0), H, H, P(gW1), H, P(gb1), 0, st)
+        if args.only != 'lstm':
+            L.call('smi_linear_backward_weight', P(dZ), A, R, A, P(HA2), h2, h2, P(gW3), h2, P(gb3), 0, st)
+            L.call('smi_linear_backward_weight', P(dH2), h2, R, h2, P(HA1), h1, h1, P(gW2), h1, P(gb2), 0, st)
+            L.call('smi_linear_backward_weight', P(dH1), h1, R, h1, P(X0), H, H, P(gW1), H, P(gb1), 0, st)
+        if args.only == 'head':
+            L.call('smi_dw_group_flush', st)
+            return
         # the LSTM's W_ih and W_hh as two GEMMs of the group (the learner fuses
         # them over [x_t | h_{t-1}] through the internal two-source form)
         # (x padded to 44 columns as the learner's [x_t | h_{t-1}] form reads it:

@@ -113,6 +113,12 @@ int main() {
     CK(hipMemcpy(B, h.data(), (size_t)R * NB * 4, hipMemcpyHostToDevice));
   }
   // 576-row slabs (36 per tile) as at C3; reps stretch a launch to ~1 ms
+  if (getenv("RATE_SMALL")) {      // a rank's share (3200 rows): 448-row slabs, one pass
+    run<0, 1>(A, B, out, clk, 448, 1); run<1, 1>(A, B, out, clk, 448, 1);
+    run<0, 2>(A, B, out, clk, 448, 1); run<1, 2>(A, B, out, clk, 448, 1);
+    run<1, 1>(A, B, out, clk, 1344, 1); run<1, 1>(A, B, out, clk, 448, 20);
+    return 0;
+  }
   run<1, 2>(A, B, out, clk, 576, 20); run<1, 3>(A, B, out, clk, 576, 14);
   run<0, 3>(A, B, out, clk, 576, 1);  // one pass, the dW launch's size
   run<1, 3>(A, B, out, clk, 576, 1);
