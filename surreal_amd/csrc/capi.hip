@@ -119,11 +119,13 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
                           hipStream_t st, const int* skip, const float* vret = nullptr,
                           float* vgrad = nullptr, float vscale = 0.f);
+struct PolRowArgs;
 int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
                           const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
                           int64_t lddx, const float* mask, int64_t ldm, hipStream_t st,
-                          const int* skip);
+                          const int* skip, const PolRowArgs* pg = nullptr);
+int head_bwd_blocks(int64_t rows);
 int launch_ddpg_stats(const float*, int64_t, int, const float*, int64_t, const float*,
                       const float*, int64_t, int64_t, float*, hipStream_t);
 int launch_ddpg_target(const float*, const float*, const float*, const float*, int64_t, float,

@@ -36,6 +36,7 @@
 // three layers stay in the phase's grouped dW launch (linear_kernels.hip).
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
+#include "pol_rows.hpp"
 
 namespace smi {
 
@@ -72,6 +73,11 @@ struct HeadBwdArgs {
   const float* mask; int64_t ldm;        // optional: dX zero where mask <= 0
   int64_t rows; const int* skip;
   int ld2, ld1;                          // LDS leading dims
+  // policy-gradient prologue (head_bwd_kernel<..., PG>): dZ of the workgroup's
+  // rows computed here from the policy rows (policy_rows_grad_kernel's pass)
+  // instead of read; written to pg.dz for the layer-3 weight gradient, the
+  // rows' d/dstd sums to pg.lvpart[blockIdx.x]
+  PolRowArgs pg;
 };
 
 // Developer phase timer (build variant 'prof', -DSMI_PROF): thread 0 of every
@@ -502,7 +508,9 @@ head_fwd_kernel(HeadFwdArgs a) {
   HEAD_END(0);
 }
 
-template <int NTA, int NTB, int RT>
+// PG: the policy loss gradient of the workgroup's rows as the prologue (the
+// action width is the template's 8: out == 8)
+template <int NTA, int NTB, int RT, bool PG>
 __global__ void __launch_bounds__(kWG, RT == 1 ? 3 : 2)
 head_bwd_kernel(HeadBwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
@@ -520,14 +528,55 @@ head_bwd_kernel(HeadBwdArgs a) {
   // first; dH1's weight stream (W2^T) and its masks are issued behind them and
   // stay in flight through the dZ W3 pass
   const int zr = threadIdx.x >> 4, zk = threadIdx.x & 15;
-  float zv[RT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-    zv[rt] = a.dZ[min(r0 + 16 * rt + zr, a.rows - 1) * out + min(zk, out - 1)];
   HcStream<NTA> SA;
-  SA.init(a.W2T, a.h2, a.h2, a.h1, wave, 4, 0, 1);
+  if constexpr (PG) {
+    // thread t < R: row r0 + t's inputs, then the weight stream, then the
+    // epoch's loss weights (and, one rank, its decision: every load above is
+    // in flight meanwhile), then the row's dz and d/dstd terms (pol_rows.hpp,
+    // the same ops as policy_rows_grad_kernel's row pass)
+    constexpr int AT = 8;
+    __shared__ PolGradShared psh;
+    const int t = threadIdx.x;
+    const int64_t n = r0 + t;
+    const bool own = t < R && n < a.rows;
+    PolGradRow<AT> x;
+    if (own) x.load(a.pg, n, AT);
+    SA.init(a.W2T, a.h2, a.h2, a.h1, wave, 4, 0, 1);
+    float wsurr, wkl;
+    if (pol_grad_weights(a.pg, psh, wsurr, wkl)) return;
+    const PolGradCols<AT> cols(a.pg, psh, AT);
+    const AdvNorm nadv(a.pg);
+    float glv[AT];
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt) sZ[(16 * rt + zr) * 16 + zk] = zk < out ? zv[rt] : 0.f;
+    for (int j = 0; j < AT; ++j) glv[j] = 0.f;
+    if (t < R) {
+      float dz[AT];
+      if (own) {
+        pol_grad_compute<AT>(a.pg, cols, nadv, x, wsurr, wkl, dz, glv);
+        st_row<AT>(a.pg.dz + n * AT, dz, AT);
+      } else {
+#pragma unroll
+        for (int j = 0; j < AT; ++j) dz[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sZ[t * 16 + j] = j < AT ? dz[j] : 0.f;
+    }
+    if (wave == 0) {     // R <= 64: every row on wave 0; fixed butterfly order
+#pragma unroll
+      for (int j = 0; j < AT; ++j) {
+        const float sg = wave_sum(glv[j]);
+        if (lane == 0) a.pg.lvpart[(int64_t)blockIdx.x * AT + j] = sg;
+      }
+    }
+  } else {
+    float zv[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+      zv[rt] = a.dZ[min(r0 + 16 * rt + zr, a.rows - 1) * out + min(zk, out - 1)];
+    SA.init(a.W2T, a.h2, a.h2, a.h1, wave, 4, 0, 1);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) sZ[(16 * rt + zr) * 16 + zk] = zk < out ? zv[rt] : 0.f;
+  }
   // padding columns of dH2 (the next layer's last chunk)
   const int h2p = a.ld2 - 4;
   for (int e = threadIdx.x; e < R * (h2p - a.h2); e += kWG) {
@@ -687,6 +736,13 @@ static int hc_rt(int64_t rows) {
   return rows >= 16384 ? 2 : 1;
 }
 
+// workgroups of a fused head launch over rows (the policy prologue writes one
+// log_var partial per workgroup)
+int head_bwd_blocks(int64_t rows) {
+  const int R = HC_R * hc_rt(rows);
+  return (int)((rows + R - 1) / R);
+}
+
 int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
                           const float* b1, int h1, const float* W2, const float* b2, int h2,
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
@@ -739,10 +795,12 @@ int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
                           const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
                           int64_t lddx, const float* mask, int64_t ldm, hipStream_t st,
-                          const int* skip) {
+                          const int* skip, const PolRowArgs* pg) {
   if (rows <= 0) return SMI_OK;
+  if (pg && out != 8) return set_error(SMI_E_ARG, "head_backward: the policy prologue needs out == 8");
   HeadBwdArgs a{dZ, out, W3, W2T, W1T, h1, h2, dx0, dxn, HA1, HA2, dH2, dH1, dX, lddx, mask, ldm,
                 rows, skip, hc_ld(h2), hc_ld(h1)};
+  if (pg) a.pg = *pg;
   const int rt = hc_rt(rows);
   const int R = HC_R * rt;
   const size_t lds = (size_t)(R * (a.ld2 + a.ld1) + R * 16) * 4;
@@ -751,15 +809,20 @@ int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W
   na = na <= 2 ? 2 : na <= 5 ? 5 : 8;
   nb = nb <= 2 ? 2 : 5;
   const int kslot = ktime_begin(st);
-#define SMI_HB(A, B)                                                                   \
+#define SMI_HB2(A, B, P)                                                               \
   do {                                                                                 \
     if (rt == 2) {                                                                     \
-      allow_lds(head_bwd_kernel<A, B, 2>, lds);                                        \
-      hipLaunchKernelGGL((head_bwd_kernel<A, B, 2>), grid, dim3(kWG), lds, st, a);     \
+      allow_lds(head_bwd_kernel<A, B, 2, P>, lds);                                     \
+      hipLaunchKernelGGL((head_bwd_kernel<A, B, 2, P>), grid, dim3(kWG), lds, st, a);  \
     } else {                                                                           \
-      allow_lds(head_bwd_kernel<A, B, 1>, lds);                                        \
-      hipLaunchKernelGGL((head_bwd_kernel<A, B, 1>), grid, dim3(kWG), lds, st, a);     \
+      allow_lds(head_bwd_kernel<A, B, 1, P>, lds);                                     \
+      hipLaunchKernelGGL((head_bwd_kernel<A, B, 1, P>), grid, dim3(kWG), lds, st, a);  \
     }                                                                                  \
+  } while (0)
+#define SMI_HB(A, B)                                                                   \
+  do {                                                                                 \
+    if (pg) SMI_HB2(A, B, true);                                                       \
+    else SMI_HB2(A, B, false);                                                         \
   } while (0)
   if (na == 2 && nb == 2) SMI_HB(2, 2);
   else if (na == 2) SMI_HB(2, 5);
@@ -768,6 +831,7 @@ int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W
   else if (nb == 2) SMI_HB(8, 2);
   else SMI_HB(8, 5);
 #undef SMI_HB
+#undef SMI_HB2
   ktime_end(kslot, KT_GEMM_DX,
             2.0 * (double)rows * ((double)out * h2 + (double)h2 * h1 + (double)h1 * dxn), st);
   return check_launch("head_bwd_kernel");

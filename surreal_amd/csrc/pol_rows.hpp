@@ -1,0 +1,436 @@
+// pol_rows.hpp — the per-row pieces of the PPO policy loss (ppo.py:203-224,
+// 262-284, 553-575; ppo_net.py:29-72) shared by the row kernels of
+// ppo_rnn.hip and the policy-gradient prologue of the fused head input-gradient
+// chain (head_kernels.hip): the packed row layout, the argument blocks, the
+// DiagGauss row terms and the epoch's early-stop / adapt-coefficient decision.
+#pragma once
+#include "smi_device.hpp"
+#include "smi_internal.hpp"
+
+namespace smi {
+
+// policy sums (pstat, double): one forward over the E*B training rows
+enum {
+  PS_KL = 0,       // sum KL(ref || learn)                       ppo.py:265,553
+  PS_SURR,         // clip: sum -ratio*adv; adapt: sum adv*lik/clamp(lik_b)
+  PS_CLIP,         // clip: sum max(surr, clipped surr)          ppo.py:213
+  PS_ISW,          // sum lik / (lik_b + 1e-4)                   ppo.py:573
+  PS_BL,           // sum lik_b                                  ppo.py:572
+  PS_RBD,          // sum KL(ref || behave)                      ppo.py:574
+  PS_RET,          // sum returns                                ppo.py:570
+  PS_N = 8
+};
+// device control block (int / float scratch)
+enum { CI_STOP = 0, CI_RUNS, CI_NG, CI_NP, CI_COUNT = 8 };
+enum { CF_KLCOEF = 0, CF_SURRW, CF_COUNT = 8 };
+
+// fields of a packed row: A actions, 2A behaviour parameters, the advantage
+__host__ __device__ inline int row_w(int A) { return 3 * A + 1; }
+// rowin is blocked by 64 rows: block b holds field f of rows 64b .. 64b + 63
+// as 64 consecutive floats, the block's fields back to back, so one wave's
+// row loads read one contiguous ~5 KB run (a field-major [W][NE] layout made
+// every wave touch W DRAM pages per row batch)
+__host__ __device__ inline int64_t rin_idx(int W, int64_t n, int f) {
+  return (n >> 6) * ((int64_t)W << 6) + ((int64_t)f << 6) + (n & 63);
+}
+
+struct DecideArgs {
+  const double* ps; int e, Ep, mode; double kl_target; float eta; int64_t N;
+  const float* hyper; const float* lv; int A; float c_ent;
+  int* ci; float* cf; float* stats;
+};
+
+struct PolRowArgs {
+  int B, T, E, A, mode;
+  const float* mu;        // [NE][A] learner means (tanh applied)
+  const float* lv;        // [A] learner log_var
+  const float* refmu;     // [NE][A]
+  const float* ref_lv;    // [A]
+  const float* actions;   // [B][T][A]
+  const float* behave;    // [B][T][2A]
+  const float* adv;       // [B][E] raw
+  const float* ret;       // [B][E]
+  const float* rowin;     // {actions | behave | raw adv} blocked by 64 rows (rin_idx)
+  const float* ret_tm;    // [NE] time-major returns
+  const double* moments;  // [3] global (sum, sumsq, n) of adv, or null (no norm)
+  int norm_adv;
+  float c_ll;
+  const float* hyper;
+  const int* skip;
+  // outputs
+  double* part;           // [nblk][PS_N]
+  float* dz;              // [NE][A]   (grad pass)
+  float* lvpart;          // [nblk][A] (grad pass)
+  const float* cf;        // device coefficients (grad pass)
+  float invN;
+  // grad pass, single rank: the statistics pass's partials ([dec_nb][PS_N]) and
+  // the decision's arguments; each block reduces them itself (the order of
+  // reduce_decide_kernel) and decides, block 0 writes the decision's outputs
+  // (one launch fewer per epoch than reduce_decide_kernel + this pass)
+  const double* dec_part; int dec_nb;
+  DecideArgs dec;
+};
+
+// ppo.py:402-405: (adv - mean) / max(std, 1e-4), std unbiased over all B*E;
+// the fp64 moments are turned into (mean_f, max(std_f, 1e-4)) once per thread
+// (AdvNorm), outside the row loops: per row only the fp32 subtract and divide
+struct AdvNorm {
+  bool on; float mean, den;
+  __device__ explicit AdvNorm(const PolRowArgs& a) : on(a.norm_adv && a.moments), mean(0.f), den(1.f) {
+    if (!on) return;
+    const double n = a.moments[2];
+    const double m = a.moments[0] / n;
+    const double var = (a.moments[1] - n * m * m) / (n - 1.0);
+    mean = (float)m;
+    den = fmaxf((float)sqrt(var > 0.0 ? var : 0.0), 1e-4f);
+  }
+  __device__ float operator()(float raw) const { return on ? (raw - mean) / den : raw; }
+};
+
+// Row access of the per-row loss kernels.  AT > 0: the action width is a
+// compile-time constant (the benched A = 8 and HalfCheetah's 6), so a row's
+// values live in registers (fully unrolled loops) and rows of 4k floats move
+// as float4 (16-byte aligned: row offsets are multiples of 4A bytes); AT == 0:
+// any A <= 32 through runtime loops.
+template <int AT>
+__device__ __forceinline__ void ld_row(float* dst, const float* __restrict__ src, int A) {
+  if constexpr (AT > 0 && AT % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < AT / 4; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(src)[q];
+      dst[4 * q] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
+    }
+  } else if constexpr (AT > 0) {
+#pragma unroll
+    for (int j = 0; j < AT; ++j) dst[j] = src[j];
+  } else {
+    for (int j = 0; j < A; ++j) dst[j] = src[j];
+  }
+}
+template <int AT>
+__device__ __forceinline__ void st_row(float* __restrict__ dst, const float* src, int A) {
+  if constexpr (AT > 0 && AT % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < AT / 4; ++q)
+      reinterpret_cast<float4*>(dst)[q] = float4{src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]};
+  } else if constexpr (AT > 0) {
+#pragma unroll
+    for (int j = 0; j < AT; ++j) dst[j] = src[j];
+  } else {
+    for (int j = 0; j < A; ++j) dst[j] = src[j];
+  }
+}
+template <int AT>
+__device__ __forceinline__ float row_loglik(const float* act, const float* mu, const float* sd,
+                                            const float* logsd, int A, float c_ll) {
+  float s = 0.f, l = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    const float u = (act[j] - mu[j]) / sd[j];
+    s += u * u;
+    l += logsd[j];
+  }
+  return (-0.5f * s - c_ll) - l;
+}
+template <int AT>
+__device__ __forceinline__ float row_kl(const float* mu0, const float* sd0, const float* mu1,
+                                        const float* sd1, int A) {
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    s1 += logf(sd1[j] / sd0[j]);
+    const float d = mu0[j] - mu1[j];
+    s2 += (sd0[j] * sd0[j] + d * d) / (2.f * (sd1[j] * sd1[j]));
+  }
+  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
+}
+
+// row_loglik with the std's reciprocal: (a - mu) * (1 / sd) instead of the
+// IEEE divide (one rounding more, within the parity envelope): the learner's
+// std is a per-column constant (reciprocal hoisted out of the row loop), the
+// behaviour policy's is per row (one IEEE-rounded 1.f / sd per row element,
+// shared by every term of the row that divides by it; not the approximate
+// v_rcp_f32, whose ~1 ulp error and denormal flush the learner-std path does
+// not have either)
+template <int AT>
+__device__ __forceinline__ float row_loglik_r(const float* act, const float* mu, const float* isd,
+                                              const float* logsd, int A, float c_ll) {
+  float s = 0.f, l = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    const float u = (act[j] - mu[j]) * isd[j];
+    s += u * u;
+    l += logsd[j];
+  }
+  return (-0.5f * s - c_ll) - l;
+}
+
+// row_kl with BOTH distributions' stds fixed per column (the reference policy
+// against the learner: log(sd1 / sd0), sd0^2 and 2 sd1^2 are hoisted out of the
+// row loop as lkl, s02, den2 — the same operations in the same order, computed
+// once per workgroup instead of once per row)
+template <int AT>
+__device__ __forceinline__ float row_kl_cc(const float* mu0, const float* mu1, const float* lkl,
+                                           const float* s02, const float* iden2, int A) {
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    s1 += lkl[j];
+    const float d = mu0[j] - mu1[j];
+    s2 += (s02[j] + d * d) * iden2[j];
+  }
+  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
+}
+
+// KL(reference || behaviour) of a row: the reference std per column (its
+// log and square hoisted), the behaviour std per row through its log (already
+// formed for the log-likelihood) and reciprocal
+template <int AT>
+__device__ __forceinline__ float row_kl_rb(const float* mu0, const float* lsd0, const float* s02,
+                                           const float* mu1, const float* lsd1, const float* isd1,
+                                           int A) {
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    s1 += lsd1[j] - lsd0[j];
+    const float d = mu0[j] - mu1[j];
+    s2 += (s02[j] + d * d) * (0.5f * (isd1[j] * isd1[j]));
+  }
+  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
+}
+
+// field j .. j + AT - 1 of row n from the blocked rowin
+template <int AT>
+__device__ __forceinline__ void ld_fields(float* dst, const float* __restrict__ rowin, int64_t /*N*/,
+                                          int64_t n, int f0, int A) {
+  const int W = row_w(AT > 0 ? AT : A);
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) dst[j] = rowin[rin_idx(W, n, f0 + j)];
+}
+
+// After the (all-reduced) policy sums of POLICY_FWD(e): early stop, adapt
+// coefficient and statistics (ppo.py:265-284, 541-557, 568-575).  ps = the
+// sums; write = store the decision (stats, stop flag, coefficients), else only
+// return it (the blocks of a fused gradient pass other than block 0)
+struct Decision { int stop; float surrw, klcoef; };
+__device__ inline Decision policy_decide_body(const DecideArgs& a, const double* ps, bool write) {
+  Decision r{1, 0.f, 0.f};
+  if (a.ci[CI_STOP]) return r;
+  const double n = (double)a.N;
+  const float kl = (float)(ps[PS_KL] / n);
+  // statistics of the forward with the current parameters (curr_pol after the
+  // previous update, or ref/behave terms before any)
+  if (write) {
+    a.stats[SMI_ST_AVG_IS_WEIGHT] = (float)(ps[PS_ISW] / n);
+    a.stats[SMI_ST_AVG_BEHAVE_LIK] = (float)(ps[PS_BL] / n);
+    a.stats[SMI_ST_REF_BEHAVE_DIFF] = (float)(ps[PS_RBD] / n);
+    a.stats[SMI_ST_AVG_RETURN] = (float)(ps[PS_RET] / n);
+  }
+  if (a.e >= 1) {
+    if (write) a.stats[SMI_ST_POL_KL] = kl;                 // ppo.py:555
+    if ((double)kl > a.kl_target * 4.0) {                    // ppo.py:556
+      if (write) a.ci[CI_STOP] = 1;
+      return r;
+    }
+  }
+  if (a.e >= a.Ep) {
+    if (write) a.ci[CI_STOP] = 1;                            // loop finished
+    return r;
+  }
+  r.stop = 0;
+  // loss statistics of update e
+  r.surrw = (float)(1.0 / n);
+  if (write) {
+    float ent = 0.f;
+    for (int j = 0; j < a.A; ++j) ent += logf(expf(a.lv[j]));
+    ent = 0.5f * ent + a.c_ent;
+    a.stats[SMI_ST_ENTROPY] = ent;
+    a.cf[CF_SURRW] = r.surrw;
+  }
+  if (a.mode == 0) {
+    if (write) {
+      a.stats[SMI_ST_SURR_LOSS] = (float)(ps[PS_SURR] / n);
+      a.stats[SMI_ST_CLIP_SURR_LOSS] = (float)(ps[PS_CLIP] / n);
+      a.cf[CF_KLCOEF] = 0.f;
+    }
+  } else {
+    const float beta = a.hyper[SMI_HYP_BETA];
+    const float surr = -(float)(ps[PS_SURR] / n);
+    float loss = surr + beta * kl;
+    float coef = beta;
+    if ((double)kl - 2.0 * a.kl_target > 0.0) {              // ppo.py:275
+      const float d = kl - (float)(2.0 * a.kl_target);
+      loss += a.eta * (d * d);
+      coef += 2.f * a.eta * d;
+    }
+    r.klcoef = (float)(coef / n);
+    if (write) {
+      a.stats[SMI_ST_SURR_LOSS] = surr;
+      a.stats[SMI_ST_KL_LOSS_ADAPT] = loss;
+      a.stats[SMI_ST_POL_KL_ADAPT] = kl;
+      a.stats[SMI_ST_POL_KL] = kl;
+      a.cf[CF_KLCOEF] = r.klcoef;
+    }
+  }
+  return r;
+}
+
+
+// ---- the gradient row pass (policy_rows_grad_kernel; the fused head chain's
+// prologue, head_kernels.hip) ----
+// LDS of the pass: the stds of both policies and the decision's sums
+struct PolGradShared { float sig[32], lsig[32], rsig[32]; double sps[PS_N]; };
+
+// the epoch's loss weights: the surrogate weight (1/N) and the KL weight
+// (adapt: (beta + 2 eta relu(kl - 2kt)) / N; clip: 0), from cf, or, with
+// a.dec_part (one rank), decided here from the statistics pass's partials
+// (reduced in reduce_decide_kernel's order: lane i sums blocks i, i + 64, ...
+// then the wave butterfly, so every workgroup reaches the same decision; block
+// 0 writes it).  Also stages the stds in sh.  Returns true when the epoch does
+// not train (early stop / loop done): the caller returns, uniformly.  Every
+// thread of the workgroup must call it (it has barriers).
+__device__ inline bool pol_grad_weights(const PolRowArgs& a, PolGradShared& sh, float& wsurr,
+                                        float& wkl) {
+  const int A = a.A;
+  for (int j = threadIdx.x; j < A; j += blockDim.x) {
+    sh.sig[j] = expf(a.lv[j]);
+    sh.lsig[j] = logf(sh.sig[j]);
+    sh.rsig[j] = expf(a.ref_lv[j]);
+  }
+  if (a.dec_part) {
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < 64) {
+      double t[PS_N];
+#pragma unroll
+      for (int j = 0; j < PS_N; ++j) t[j] = 0.0;
+      for (int i = lane; i < a.dec_nb; i += 64) {
+#pragma unroll
+        for (int j = 0; j < PS_N; ++j) t[j] += a.dec_part[(int64_t)i * PS_N + j];
+      }
+#pragma unroll
+      for (int j = 0; j < PS_N; ++j) {
+        const double u = wave_sum_d(t[j]);
+        if (lane == 0) sh.sps[j] = u;
+      }
+    }
+    __syncthreads();
+    const bool wr = blockIdx.x == 0 && threadIdx.x == 0;
+    if (wr) {
+      double* out = const_cast<double*>(a.dec.ps);
+      for (int j = 0; j < PS_N; ++j) out[j] = sh.sps[j];
+    }
+    const Decision dd = policy_decide_body(a.dec, sh.sps, wr);
+    wsurr = dd.surrw;
+    wkl = dd.klcoef;
+    return dd.stop != 0;
+  }
+  __syncthreads();
+  wsurr = a.cf[CF_SURRW];
+  wkl = a.cf[CF_KLCOEF];
+  return false;
+}
+
+// per-column factors of the row pass, hoisted; divisions by them become
+// multiplications by their reciprocals (as in policy_rows_stats_kernel)
+template <int AT>
+struct PolGradCols {
+  static constexpr int AM = AT > 0 ? AT : 32;
+  float lsig[AM], inv1[AM], is1sq[AM], is1cu[AM], rs2[AM];
+  float clip_lo, clip_hi;
+  int A;
+  __device__ PolGradCols(const PolRowArgs& a, const PolGradShared& sh, int A_) : A(A_) {
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A_); ++j) {
+      const float sg = sh.sig[j], rsig = sh.rsig[j];
+      lsig[j] = sh.lsig[j];
+      inv1[j] = 1.f / sg;
+      is1sq[j] = 1.f / (sg * sg);
+      is1cu[j] = 1.f / (sg * sg * sg);
+      rs2[j] = rsig * rsig;
+    }
+    clip_lo = a.hyper[SMI_HYPX_CLIP_LO];
+    clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
+  }
+};
+
+// one row's inputs of the gradient pass (loaded before the epoch's weights
+// are known: their latency overlaps the decision)
+template <int AT>
+struct PolGradRow {
+  static constexpr int AM = AT > 0 ? AT : 32;
+  float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], adv;
+  __device__ void load(const PolRowArgs& a, int64_t n, int A) {
+    const int64_t N = (int64_t)a.E * a.B;
+    ld_row<AT>(m, a.mu + n * A, A);
+    ld_row<AT>(rm, a.refmu + n * A, A);
+    ld_fields<AT>(ac, a.rowin, N, n, 0, A);
+    ld_fields<AT>(bmu, a.rowin, N, n, A, A);
+    ld_fields<AT>(bsd, a.rowin, N, n, 2 * A, A);
+    adv = a.rowin[rin_idx(row_w(A), n, 3 * A)];
+  }
+};
+
+// a loaded row's dz (gradient at the tanh pre-activation) and its d/dstd
+// terms added into glv
+template <int AT>
+__device__ __forceinline__ void pol_grad_compute(const PolRowArgs& a, const PolGradCols<AT>& c,
+                                                 const AdvNorm& nadv, const PolGradRow<AT>& x,
+                                                 float wsurr, float wkl, float* dz, float* glv) {
+  constexpr int AM = AT > 0 ? AT : 32;
+  const int A = c.A;
+  const float* m = x.m;
+  const float* rm = x.rm;
+  const float* ac = x.ac;
+  const float* bmu = x.bmu;
+  const float* bsd = x.bsd;
+  float blsd[AM];
+  const float av = nadv(x.adv);
+  const float ll = row_loglik_r<AT>(ac, m, c.inv1, c.lsig, A, a.c_ll);
+  const float ex = expf(ll);
+  const float lp = fmaxf(ex, 1e-5f);
+  float ibsd[AM];
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    blsd[j] = logf(bsd[j]);
+    ibsd[j] = 1.f / bsd[j];
+  }
+  const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
+  float g_lp;
+  if (a.mode == 0) {
+    const float ratio = lp / bl;
+    const float cr = fminf(fmaxf(ratio, c.clip_lo), c.clip_hi);
+    const float surr = -ratio * av, csur = -cr * av;
+    // max() routes to the unclipped term unless the clipped one is strictly
+    // larger (then the ratio is outside the clamp and the gradient is 0)
+    g_lp = ((surr >= csur) ? -(wsurr * av) : 0.f) / bl;
+  } else {
+    g_lp = (-wsurr * av) / fmaxf(bl, 1e-2f);
+  }
+  const float g_ll = (ex >= 1e-5f) ? g_lp * ex : 0.f;    // clamp + exp backward
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    const float i1 = c.inv1[j];
+    const float u = (ac[j] - m[j]) * i1;
+    float gmu = g_ll * (u * i1);
+    float gsd = g_ll * (u * u * i1 - i1);
+    if (wkl != 0.f) {
+      const float d = rm[j] - m[j];
+      gmu += wkl * (-d * c.is1sq[j]);
+      gsd += wkl * (i1 - (c.rs2[j] + d * d) * c.is1cu[j]);
+    }
+    glv[j] += gsd;
+    dz[j] = gmu * (1.f - m[j] * m[j]);                    // tanh backward
+  }
+}
+
+// row n's dz and d/dstd terms (load + compute)
+template <int AT>
+__device__ __forceinline__ void pol_grad_row(const PolRowArgs& a, const PolGradCols<AT>& c,
+                                             const AdvNorm& nadv, int64_t n, float wsurr, float wkl,
+                                             float* dz, float* glv) {
+  PolGradRow<AT> x;
+  x.load(a, n, c.A);
+  pol_grad_compute<AT>(a, c, nadv, x, wsurr, wkl, dz, glv);
+}
+
+}  // namespace smi

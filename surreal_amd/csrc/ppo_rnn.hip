@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
+#include "pol_rows.hpp"
 
 namespace smi {
 
@@ -22,24 +23,9 @@ int launch_gae_windows(const float* values, float* values_masked, const float* r
                        double* partials, int* n_partials, hipStream_t stream);
 
 // ----------------------------------------------------------------- layout
-// policy sums (pstat, double): one forward over the E*B training rows
-enum {
-  PS_KL = 0,       // sum KL(ref || learn)                       ppo.py:265,553
-  PS_SURR,         // clip: sum -ratio*adv; adapt: sum adv*lik/clamp(lik_b)
-  PS_CLIP,         // clip: sum max(surr, clipped surr)          ppo.py:213
-  PS_ISW,          // sum lik / (lik_b + 1e-4)                   ppo.py:573
-  PS_BL,           // sum lik_b                                  ppo.py:572
-  PS_RBD,          // sum KL(ref || behave)                      ppo.py:574
-  PS_RET,          // sum returns                                ppo.py:570
-  PS_N = 8
-};
 // final sums (fstat, double): value statistics of the last value epoch, then
 // the ZFilter column sums of obs_iter
 enum { FS_SE = 0, FS_D, FS_D2, FS_R, FS_R2, FS_Z = 5 };
-
-// device control block (int / float scratch)
-enum { CI_STOP = 0, CI_RUNS, CI_NG, CI_NP, CI_COUNT = 8 };
-enum { CF_KLCOEF = 0, CF_SURRW, CF_COUNT = 8 };
 
 struct RnnDims {
   int B, T, Hz, E, S1, D, H, G4, A, h1, h2, c1, c2;
@@ -102,16 +88,6 @@ struct RnnScratch {
 };
 
 static inline int64_t al64(int64_t n) { return (n + 63) & ~(int64_t)63; }
-// fields of a packed row: A actions, 2A behaviour parameters, the advantage
-__host__ __device__ inline int row_w(int A) { return 3 * A + 1; }
-// rowin is blocked by 64 rows: block b holds field f of rows 64b .. 64b + 63
-// as 64 consecutive floats, the block's fields back to back, so one wave's
-// row loads read one contiguous ~5 KB run (a field-major [W][NE] layout made
-// every wave touch W DRAM pages per row batch)
-__host__ __device__ inline int64_t rin_idx(int W, int64_t n, int f) {
-  return (n >> 6) * ((int64_t)W << 6) + ((int64_t)f << 6) + (n & 63);
-}
-
 __host__ __device__ inline int rnn_nblk(int64_t rows, int nt = kWG) {
   // at most 1024 four-wave blocks' worth of waves (4096 one-wave blocks)
   const int64_t cap = (int64_t)1024 * kWG / nt;
@@ -382,59 +358,6 @@ reduce_partials_kernel(const double* __restrict__ part, int nb, int w, double* o
   }
 }
 
-struct DecideArgs {
-  const double* ps; int e, Ep, mode; double kl_target; float eta; int64_t N;
-  const float* hyper; const float* lv; int A; float c_ent;
-  int* ci; float* cf; float* stats;
-};
-
-struct PolRowArgs {
-  int B, T, E, A, mode;
-  const float* mu;        // [NE][A] learner means (tanh applied)
-  const float* lv;        // [A] learner log_var
-  const float* refmu;     // [NE][A]
-  const float* ref_lv;    // [A]
-  const float* actions;   // [B][T][A]
-  const float* behave;    // [B][T][2A]
-  const float* adv;       // [B][E] raw
-  const float* ret;       // [B][E]
-  const float* rowin;     // {actions | behave | raw adv} blocked by 64 rows (rin_idx)
-  const float* ret_tm;    // [NE] time-major returns
-  const double* moments;  // [3] global (sum, sumsq, n) of adv, or null (no norm)
-  int norm_adv;
-  float c_ll;
-  const float* hyper;
-  const int* skip;
-  // outputs
-  double* part;           // [nblk][PS_N]
-  float* dz;              // [NE][A]   (grad pass)
-  float* lvpart;          // [nblk][A] (grad pass)
-  const float* cf;        // device coefficients (grad pass)
-  float invN;
-  // grad pass, single rank: the statistics pass's partials ([dec_nb][PS_N]) and
-  // the decision's arguments; each block reduces them itself (the order of
-  // reduce_decide_kernel) and decides, block 0 writes the decision's outputs
-  // (one launch fewer per epoch than reduce_decide_kernel + this pass)
-  const double* dec_part; int dec_nb;
-  DecideArgs dec;
-};
-
-// ppo.py:402-405: (adv - mean) / max(std, 1e-4), std unbiased over all B*E;
-// the fp64 moments are turned into (mean_f, max(std_f, 1e-4)) once per thread
-// (AdvNorm), outside the row loops: per row only the fp32 subtract and divide
-struct AdvNorm {
-  bool on; float mean, den;
-  __device__ explicit AdvNorm(const PolRowArgs& a) : on(a.norm_adv && a.moments), mean(0.f), den(1.f) {
-    if (!on) return;
-    const double n = a.moments[2];
-    const double m = a.moments[0] / n;
-    const double var = (a.moments[1] - n * m * m) / (n - 1.0);
-    mean = (float)m;
-    den = fmaxf((float)sqrt(var > 0.0 ? var : 0.0), 1e-4f);
-  }
-  __device__ float operator()(float raw) const { return on ? (raw - mean) / den : raw; }
-};
-
 // optional export of the advantages as the epochs use them and the returns,
 // both [B][E] batch-major (smi_ppo_rnn_args.adv_out / ret_out)
 __global__ void __launch_bounds__(kWG)
@@ -445,118 +368,6 @@ adv_export_kernel(PolRowArgs a, float* __restrict__ adv_out, float* __restrict__
     if (adv_out) adv_out[e] = nadv(a.adv[e]);
     if (ret_out) ret_out[e] = a.ret[e];
   }
-}
-
-// Row access of the per-row loss kernels.  AT > 0: the action width is a
-// compile-time constant (the benched A = 8 and HalfCheetah's 6), so a row's
-// values live in registers (fully unrolled loops) and rows of 4k floats move
-// as float4 (16-byte aligned: row offsets are multiples of 4A bytes); AT == 0:
-// any A <= 32 through runtime loops.
-template <int AT>
-__device__ __forceinline__ void ld_row(float* dst, const float* __restrict__ src, int A) {
-  if constexpr (AT > 0 && AT % 4 == 0) {
-#pragma unroll
-    for (int q = 0; q < AT / 4; ++q) {
-      const float4 v = reinterpret_cast<const float4*>(src)[q];
-      dst[4 * q] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
-    }
-  } else if constexpr (AT > 0) {
-#pragma unroll
-    for (int j = 0; j < AT; ++j) dst[j] = src[j];
-  } else {
-    for (int j = 0; j < A; ++j) dst[j] = src[j];
-  }
-}
-template <int AT>
-__device__ __forceinline__ void st_row(float* __restrict__ dst, const float* src, int A) {
-  if constexpr (AT > 0 && AT % 4 == 0) {
-#pragma unroll
-    for (int q = 0; q < AT / 4; ++q)
-      reinterpret_cast<float4*>(dst)[q] = float4{src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]};
-  } else if constexpr (AT > 0) {
-#pragma unroll
-    for (int j = 0; j < AT; ++j) dst[j] = src[j];
-  } else {
-    for (int j = 0; j < A; ++j) dst[j] = src[j];
-  }
-}
-template <int AT>
-__device__ __forceinline__ float row_loglik(const float* act, const float* mu, const float* sd,
-                                            const float* logsd, int A, float c_ll) {
-  float s = 0.f, l = 0.f;
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    const float u = (act[j] - mu[j]) / sd[j];
-    s += u * u;
-    l += logsd[j];
-  }
-  return (-0.5f * s - c_ll) - l;
-}
-template <int AT>
-__device__ __forceinline__ float row_kl(const float* mu0, const float* sd0, const float* mu1,
-                                        const float* sd1, int A) {
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    s1 += logf(sd1[j] / sd0[j]);
-    const float d = mu0[j] - mu1[j];
-    s2 += (sd0[j] * sd0[j] + d * d) / (2.f * (sd1[j] * sd1[j]));
-  }
-  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
-}
-
-// row_loglik with the std's reciprocal: (a - mu) * (1 / sd) instead of the
-// IEEE divide (one rounding more, within the parity envelope): the learner's
-// std is a per-column constant (reciprocal hoisted out of the row loop), the
-// behaviour policy's is per row (one IEEE-rounded 1.f / sd per row element,
-// shared by every term of the row that divides by it; not the approximate
-// v_rcp_f32, whose ~1 ulp error and denormal flush the learner-std path does
-// not have either)
-template <int AT>
-__device__ __forceinline__ float row_loglik_r(const float* act, const float* mu, const float* isd,
-                                              const float* logsd, int A, float c_ll) {
-  float s = 0.f, l = 0.f;
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    const float u = (act[j] - mu[j]) * isd[j];
-    s += u * u;
-    l += logsd[j];
-  }
-  return (-0.5f * s - c_ll) - l;
-}
-
-// row_kl with BOTH distributions' stds fixed per column (the reference policy
-// against the learner: log(sd1 / sd0), sd0^2 and 2 sd1^2 are hoisted out of the
-// row loop as lkl, s02, den2 — the same operations in the same order, computed
-// once per workgroup instead of once per row)
-template <int AT>
-__device__ __forceinline__ float row_kl_cc(const float* mu0, const float* mu1, const float* lkl,
-                                           const float* s02, const float* iden2, int A) {
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    s1 += lkl[j];
-    const float d = mu0[j] - mu1[j];
-    s2 += (s02[j] + d * d) * iden2[j];
-  }
-  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
-}
-
-// KL(reference || behaviour) of a row: the reference std per column (its
-// log and square hoisted), the behaviour std per row through its log (already
-// formed for the log-likelihood) and reciprocal
-template <int AT>
-__device__ __forceinline__ float row_kl_rb(const float* mu0, const float* lsd0, const float* s02,
-                                           const float* mu1, const float* lsd1, const float* isd1,
-                                           int A) {
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    s1 += lsd1[j] - lsd0[j];
-    const float d = mu0[j] - mu1[j];
-    s2 += (s02[j] + d * d) * (0.5f * (isd1[j] * isd1[j]));
-  }
-  return (s1 + s2) - 0.5f * (float)(AT > 0 ? AT : A);
 }
 
 // rowin / ret_tm from the batch-major inputs (once per learn), field-major in
@@ -580,15 +391,6 @@ row_pack_kernel(PolRowArgs a, float* __restrict__ rowin, float* __restrict__ ret
     rowin[rin_idx(W, n, 3 * A)] = a.adv[(int64_t)b * a.E + t];
     ret_tm[n] = a.ret[(int64_t)b * a.E + t];
   }
-}
-
-// field j .. j + AT - 1 of row n from the blocked rowin
-template <int AT>
-__device__ __forceinline__ void ld_fields(float* dst, const float* __restrict__ rowin, int64_t /*N*/,
-                                          int64_t n, int f0, int A) {
-  const int W = row_w(AT > 0 ? AT : A);
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) dst[j] = rowin[rin_idx(W, n, f0 + j)];
 }
 
 // forward statistics of the policy over the E*B rows (ppo.py:203-224,
@@ -756,188 +558,29 @@ policy_rows_stats_kernel(PolRowArgs a) {
   }
 }
 
-// After the (all-reduced) policy sums of POLICY_FWD(e): early stop, adapt
-// coefficient and statistics (ppo.py:265-284, 541-557, 568-575).  ps = the
-// sums; write = store the decision (stats, stop flag, coefficients), else only
-// return it (the blocks of a fused gradient pass other than block 0)
-struct Decision { int stop; float surrw, klcoef; };
-__device__ Decision policy_decide_body(const DecideArgs& a, const double* ps, bool write) {
-  Decision r{1, 0.f, 0.f};
-  if (a.ci[CI_STOP]) return r;
-  const double n = (double)a.N;
-  const float kl = (float)(ps[PS_KL] / n);
-  // statistics of the forward with the current parameters (curr_pol after the
-  // previous update, or ref/behave terms before any)
-  if (write) {
-    a.stats[SMI_ST_AVG_IS_WEIGHT] = (float)(ps[PS_ISW] / n);
-    a.stats[SMI_ST_AVG_BEHAVE_LIK] = (float)(ps[PS_BL] / n);
-    a.stats[SMI_ST_REF_BEHAVE_DIFF] = (float)(ps[PS_RBD] / n);
-    a.stats[SMI_ST_AVG_RETURN] = (float)(ps[PS_RET] / n);
-  }
-  if (a.e >= 1) {
-    if (write) a.stats[SMI_ST_POL_KL] = kl;                 // ppo.py:555
-    if ((double)kl > a.kl_target * 4.0) {                    // ppo.py:556
-      if (write) a.ci[CI_STOP] = 1;
-      return r;
-    }
-  }
-  if (a.e >= a.Ep) {
-    if (write) a.ci[CI_STOP] = 1;                            // loop finished
-    return r;
-  }
-  r.stop = 0;
-  // loss statistics of update e
-  r.surrw = (float)(1.0 / n);
-  if (write) {
-    float ent = 0.f;
-    for (int j = 0; j < a.A; ++j) ent += logf(expf(a.lv[j]));
-    ent = 0.5f * ent + a.c_ent;
-    a.stats[SMI_ST_ENTROPY] = ent;
-    a.cf[CF_SURRW] = r.surrw;
-  }
-  if (a.mode == 0) {
-    if (write) {
-      a.stats[SMI_ST_SURR_LOSS] = (float)(ps[PS_SURR] / n);
-      a.stats[SMI_ST_CLIP_SURR_LOSS] = (float)(ps[PS_CLIP] / n);
-      a.cf[CF_KLCOEF] = 0.f;
-    }
-  } else {
-    const float beta = a.hyper[SMI_HYP_BETA];
-    const float surr = -(float)(ps[PS_SURR] / n);
-    float loss = surr + beta * kl;
-    float coef = beta;
-    if ((double)kl - 2.0 * a.kl_target > 0.0) {              // ppo.py:275
-      const float d = kl - (float)(2.0 * a.kl_target);
-      loss += a.eta * (d * d);
-      coef += 2.f * a.eta * d;
-    }
-    r.klcoef = (float)(coef / n);
-    if (write) {
-      a.stats[SMI_ST_SURR_LOSS] = surr;
-      a.stats[SMI_ST_KL_LOSS_ADAPT] = loss;
-      a.stats[SMI_ST_POL_KL_ADAPT] = kl;
-      a.stats[SMI_ST_POL_KL] = kl;
-      a.cf[CF_KLCOEF] = r.klcoef;
-    }
-  }
-  return r;
-}
-
 // per-row gradient of the policy loss w.r.t. the tanh pre-activation (dz) and
 // block partials of d loss / d log_var (ppo_net.py:29-72, ppo.py:209-217,
-// 267-277): surrogate weight cf[CF_SURRW] (1/N), KL weight cf[CF_KLCOEF] (adapt:
-// (beta + 2 eta relu(kl - 2kt)) / N, clip: 0)
+// 267-277): the row terms are pol_grad_row (pol_rows.hpp), shared with the
+// fused head input-gradient chain's prologue
 template <int NT, int AT>
 __global__ void __launch_bounds__(NT)
 policy_rows_grad_kernel(PolRowArgs a) {
   if (a.skip && a.skip[0] != 0) return;
   constexpr int AM = AT > 0 ? AT : 32;
-  __shared__ float ssig[32], slsig[32], srsig[32];
+  __shared__ PolGradShared sh;
   __shared__ float gls[NT / 64][32];
   const int A = AT > 0 ? AT : a.A;
-  for (int j = threadIdx.x; j < A; j += NT) {
-    ssig[j] = expf(a.lv[j]);
-    slsig[j] = logf(ssig[j]);
-    srsig[j] = expf(a.ref_lv[j]);
-  }
-  __syncthreads();
-  // per-column factors of the row loop, hoisted; divisions by them become
-  // multiplications by their reciprocals (as in policy_rows_stats_kernel)
-  float lsig[AM], inv1[AM], is1sq[AM], is1cu[AM], rs2[AM];
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    const float sg = ssig[j], rsig = srsig[j];
-    lsig[j] = slsig[j];
-    inv1[j] = 1.f / sg;
-    is1sq[j] = 1.f / (sg * sg);
-    is1cu[j] = 1.f / (sg * sg * sg);
-    rs2[j] = rsig * rsig;
-  }
-  const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   float wsurr, wkl;
-  if (a.dec_part) {
-    // the statistics pass's sums, reduced as reduce_decide_kernel does (lane
-    // i sums blocks i, i + 64, ... in order, then the wave butterfly): every
-    // block reaches the same sums and the same decision
-    __shared__ double sps[PS_N];
-    const int lane = threadIdx.x & 63;
-    if (threadIdx.x < 64) {
-      double t[PS_N];
-#pragma unroll
-      for (int j = 0; j < PS_N; ++j) t[j] = 0.0;
-      for (int i = lane; i < a.dec_nb; i += 64) {
-#pragma unroll
-        for (int j = 0; j < PS_N; ++j) t[j] += a.dec_part[(int64_t)i * PS_N + j];
-      }
-#pragma unroll
-      for (int j = 0; j < PS_N; ++j) {
-        const double u = wave_sum_d(t[j]);
-        if (lane == 0) sps[j] = u;
-      }
-    }
-    __syncthreads();
-    const bool wr = blockIdx.x == 0 && threadIdx.x == 0;
-    if (wr) {
-      double* out = const_cast<double*>(a.dec.ps);
-      for (int j = 0; j < PS_N; ++j) out[j] = sps[j];
-    }
-    const Decision dd = policy_decide_body(a.dec, sps, wr);
-    if (dd.stop) return;
-    wsurr = dd.surrw;
-    wkl = dd.klcoef;
-  } else {
-    wsurr = a.cf[CF_SURRW];
-    wkl = a.cf[CF_KLCOEF];
-  }
+  if (pol_grad_weights(a, sh, wsurr, wkl)) return;
+  const PolGradCols<AT> cols(a, sh, A);
   float glv[AM];
 #pragma unroll
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
   const int64_t N = (int64_t)a.E * a.B;
   const AdvNorm nadv(a);
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
-    float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], blsd[AM], dz[AM];
-    ld_row<AT>(m, a.mu + n * A, A);
-    ld_row<AT>(rm, a.refmu + n * A, A);
-    ld_fields<AT>(ac, a.rowin, N, n, 0, A);
-    ld_fields<AT>(bmu, a.rowin, N, n, A, A);
-    ld_fields<AT>(bsd, a.rowin, N, n, 2 * A, A);
-    const float av = nadv(a.rowin[rin_idx(row_w(A), n, 3 * A)]);
-    const float ll = row_loglik_r<AT>(ac, m, inv1, lsig, A, a.c_ll);
-    const float ex = expf(ll);
-    const float lp = fmaxf(ex, 1e-5f);
-    float ibsd[AM];
-#pragma unroll
-    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-      blsd[j] = logf(bsd[j]);
-      ibsd[j] = 1.f / bsd[j];
-    }
-    const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
-    float g_lp;
-    if (a.mode == 0) {
-      const float ratio = lp / bl;
-      const float cr = fminf(fmaxf(ratio, clip_lo), clip_hi);
-      const float surr = -ratio * av, csur = -cr * av;
-      // max() routes to the unclipped term unless the clipped one is strictly
-      // larger (then the ratio is outside the clamp and the gradient is 0)
-      g_lp = ((surr >= csur) ? -(wsurr * av) : 0.f) / bl;
-    } else {
-      g_lp = (-wsurr * av) / fmaxf(bl, 1e-2f);
-    }
-    const float g_ll = (ex >= 1e-5f) ? g_lp * ex : 0.f;    // clamp + exp backward
-#pragma unroll
-    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-      const float i1 = inv1[j];
-      const float u = (ac[j] - m[j]) * i1;
-      float gmu = g_ll * (u * i1);
-      float gsd = g_ll * (u * u * i1 - i1);
-      if (wkl != 0.f) {
-        const float d = rm[j] - m[j];
-        gmu += wkl * (-d * is1sq[j]);
-        gsd += wkl * (i1 - (rs2[j] + d * d) * is1cu[j]);
-      }
-      glv[j] += gsd;
-      dz[j] = gmu * (1.f - m[j] * m[j]);                    // tanh backward
-    }
+    float dz[AM];
+    pol_grad_row<AT>(a, cols, nadv, n, wsurr, wkl, dz, glv);
     st_row<AT>(a.dz + n * A, dz, A);
   }
   // block partials of sum_rows d/dstd (times std at the reduction: d/dlog_var)
@@ -954,7 +597,6 @@ policy_rows_grad_kernel(PolRowArgs a) {
     a.lvpart[(int64_t)blockIdx.x * A + j] = s;
   }
 }
-
 
 __global__ void policy_decide_kernel(DecideArgs a) {
   if (threadIdx.x != 0) return;
@@ -1286,7 +928,8 @@ int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
                           const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
                           int64_t lddx, const float* mask, int64_t ldm, hipStream_t st,
-                          const int* skip);
+                          const int* skip, const PolRowArgs* pg = nullptr);
+int head_bwd_blocks(int64_t rows);
 
 static bool head_fused(const Head& h, const float* X, int64_t ldx) {
   return head_fused_ok(h.in, ldx, h.h1, h.h2, h.out, X, h.P + h.L.fW1, h.P + h.L.fW2,
@@ -1326,10 +969,13 @@ static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, fl
 // to dXout ([rows][dxn], masked by dxmask > 0 when given; dxn == 0: none).
 // Inside a dW group (stem_backward) the weight gradients are queued and run
 // as one grouped launch at the flush.
+// pg: the policy-gradient prologue (dZ computed from the policy rows by the
+// fused chain itself); only on the fused path (head_bwd_pg_ok)
 static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx, int64_t rows,
                     const float* HA1, const float* HA2, float* dH1, float* dH2, float* G,
                     int dx0, int dxn, const float* dxmask, int64_t ldm, float* dXout,
-                    hipStream_t st, const int* skip, const float* wT = nullptr) {
+                    hipStream_t st, const int* skip, const float* wT = nullptr,
+                    const PolRowArgs* pg = nullptr) {
   const int M = (int)rows;
   const MlpLayout& L = h.L;
   if (wT && dxn <= 320 && head_fused(h, X, ldx)) {
@@ -1337,7 +983,7 @@ static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx,
     // weight gradients (queued into the phase's dW group when one is open)
     RC(launch_head_bwd_fused(dZ, h.out, rows, h.P + L.fW3, wT + (int64_t)h.in * h.h1, wT, h.h1,
                              h.h2, dx0, dxn, HA1, HA2, dH2, dH1, dXout, dxn, dxmask, ldm, st,
-                             skip));
+                             skip, pg));
     RC(launch_linear_bwd_dw(dZ, h.out, M, h.out, HA2, h.h2, h.h2, G + L.fW3, h.h2, G + L.fb3, 0,
                             st, skip));
     RC(launch_linear_bwd_dw(dH2, h.h2, M, h.h2, HA1, h.h1, h.h1, G + L.fW2, h.h1, G + L.fb2, 0,
@@ -1345,6 +991,7 @@ static int head_bwd(const Head& h, const float* dZ, const float* X, int64_t ldx,
     return launch_linear_bwd_dw(dH1, h.h1, M, h.h1, X, ldx, h.in, G + L.fW1, h.in, G + L.fb1, 0,
                                 st, skip);
   }
+  if (pg) return set_error(SMI_E_ARG, "head_backward: the policy prologue needs the fused chain");
   RC(launch_linear_bwd_dw(dZ, h.out, M, h.out, HA2, h.h2, h.h2, G + L.fW3, h.h2, G + L.fb3, 0, st,
                           skip));
   RC(launch_linear_bwd_dx(dZ, h.out, M, h.out, h.P + L.fW3, h.h2, h.h2, HA2, h.h2, dH2, h.h2, st,
@@ -1509,14 +1156,16 @@ static const float* head_in(const RnnDims& d, const RnnScratch& s, const float* 
 // backward of one head into G (+ the stem below it): LSTM BPTT and/or CNN
 static int stem_backward_chain(const smi_ppo_rnn_args& a, const RnnDims& d, const Head& hd,
                                const LstmP& lm, const float* cnn, float* G, const RnnScratch& s,
-                               int64_t n_head, hipStream_t st, const int* skip) {
+                               int64_t n_head, hipStream_t st, const int* skip,
+                               const PolRowArgs* pg) {
   const float* X = head_in(d, s, s.Xz);
   if (d.H > 0) {
     RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, 0, d.H, nullptr, 0,
-                s.dh, st, skip, s.wT));
+                s.dh, st, skip, s.wT, pg));
     RC(lstm_backward(d, a.lstm, G + n_head, s, st, skip));
     return cnn_grad(a, d, lm, cnn, G + n_head + d.nL, s, st, skip);
   }
+  if (pg) return set_error(SMI_E_ARG, "ppo_rnn: the policy prologue needs the LSTM stem");
   // MLP policy: the first head layer's input gradient over the CNN columns only
   RC(head_bwd(hd, s.dOUT, X, d.Hld, d.NE, s.HA1, s.HA2, s.dH1, s.dH2, G, d.D, d.F, s.Xz + d.D,
               d.ldx, s.dF, st, skip, s.wT));
@@ -1530,10 +1179,10 @@ static int stem_backward_chain(const smi_ppo_rnn_args& a, const RnnDims& d, cons
 static int stem_backward(const smi_ppo_rnn_args& a, const RnnDims& d, const Head& hd,
                          const LstmP& lm, const float* cnn, float* G, const RnnScratch& s,
                          int64_t n_head, hipStream_t st, const int* skip,
-                         const DwEpilogue* ex = nullptr) {
+                         const DwEpilogue* ex = nullptr, const PolRowArgs* pg = nullptr) {
   dw_group_begin();
   if (ex) RC(dw_group_epilogue(*ex));
-  const int rc = stem_backward_chain(a, d, hd, lm, cnn, G, s, n_head, st, skip);
+  const int rc = stem_backward_chain(a, d, hd, lm, cnn, G, s, n_head, st, skip, pg);
   const int rf = dw_group_flush(st);     // always flush: nothing stays queued after an error
   return rc ? rc : rf;
 }
@@ -1576,6 +1225,21 @@ static bool fused_clip_norm(const smi_ppo_rnn_args& a, const RnnDims& d) {
 // POLICY_BWD itself (policy_rows_grad_kernel, dec_part)
 static bool fused_decide(const smi_ppo_rnn_args& a, int e) {
   return a.mode != 0 && a.B_global == a.B && e < a.epoch_policy && fault() == 0;
+}
+
+// adapt mode with the LSTM stem, 8 actions and the fused head chain at a
+// rank's batch (< 16384 rows: one row tile per workgroup): the policy-gradient
+// row pass runs as that chain's prologue (head_kernels.hip, pol_rows.hpp;
+// SMI_POL_HEAD=0: its own launch, 1: at any batch; A/B knob); one log_var
+// partial per chain workgroup (<= the 4096 of s.lvpart).  Measured: 128
+// segments 2.947 -> 2.929 ms per learn; 1024 segments 6.98 -> 7.05 ms (the
+// 32-row workgroups' serial prologue costs more than the launch it saves)
+static bool pol_head_grad(const smi_ppo_rnn_args& a, const RnnDims& d, const RnnScratch& s,
+                          const Head& actor) {
+  static const int knob = [] { const char* e = getenv("SMI_POL_HEAD"); return e && e[0] ? atoi(e) : -1; }();
+  if (knob == 0) return false;
+  return a.mode != 0 && d.H > 0 && d.A == 8 && d.H <= 320 && (knob == 1 || d.NE < 16384) &&
+         head_fused(actor, head_in(d, s, s.Xz), d.Hld) && head_bwd_blocks(d.NE) <= 4096;
 }
 
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
@@ -1692,7 +1356,11 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
                            a.kl_target, a.kl_cutoff_coeff, NEg, a.hyper, a.actor + d.LA.flv, d.A,
                            c_entropy_of(d.A), s.ci, s.cf, a.stats};
       }
-      if (a.mode != 0) {     // clip: dz and the log_var partials came with POLICY_FWD's pass
+      // adapt: the gradient row pass as the fused head chain's prologue (one
+      // launch fewer), or its own launch
+      const bool pgh = pol_head_grad(a, d, s, actor);
+      const int nb_pg = pgh ? head_bwd_blocks(d.NE) : nb;
+      if (a.mode != 0 && !pgh) {     // clip: dz and the log_var partials came with POLICY_FWD's pass
         const int kt = ktime_begin(st);
         switch (d.A) {   // compile-time action widths 1..8 (registers); others generic
           case 1: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 1>), dim3(nb), dim3(kRowNT), 0, st, p); break;
@@ -1713,14 +1381,15 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       // bump) as the dW reducer's epilogue task
       const bool fn = fused_clip_norm(a, d);
       DwEpilogue ex{};
-      ex.lvpart = s.lvpart; ex.lv_nb = nb; ex.lv_A = d.A;
+      ex.lvpart = s.lvpart; ex.lv_nb = nb_pg; ex.lv_A = d.A;
       ex.lv = a.actor + d.LA.flv; ex.lv_out = gA + d.LA.flv;
       ex.skip = stop;
       if (fn) {
         ex.sq = s.part; ex.np = s.ci + CI_NP;
         ex.step = a.actor_step; ex.runs = s.ci + CI_RUNS;
       }
-      return stem_backward(a, d, actor, lm, cnn, gA, s, d.nA_head, st, stop, &ex);
+      return stem_backward(a, d, actor, lm, cnn, gA, s, d.nA_head, st, stop, &ex,
+                           pgh ? &p : nullptr);
     }
     case SMI_RNN_PH_POLICY_APPLY: {
       if (fault() == SMI_FAULT_POLICY_EPOCH_SHORT && e == a.epoch_policy - 1) return SMI_OK;
