@@ -553,6 +553,13 @@ int smi_linear_forward(const float* x, int64_t ldx, int rows, int in_dim, const 
 int smi_linear_backward_input(const float* dy, int64_t ldg, int rows, int out_dim,
                               const float* w, int64_t ldw, int in_dim, const float* relu_mask,
                               int64_t ldm, float* dx, int64_t lddx, void* stream);
+/* smi_linear_forward plus y[r][out_dim + j] = s[r*lds + j] for j < s_cols in
+ * the same launch: CriticNetworkX's cat(relu(x W1^T + b1), action) input of
+ * its second layer (ddpg_net's critic, ddpg.py:244-352 callers) written by one
+ * launch instead of a forward and a column copy. */
+int smi_linear_forward_cat(const float* x, int64_t ldx, int rows, int in_dim, const float* w,
+                           int64_t ldw, const float* b, int out_dim, int act, float* y,
+                           int64_t ldy, const float* s, int64_t lds, int s_cols, void* stream);
 int smi_linear_backward_weight(const float* dy, int64_t ldg, int rows, int out_dim,
                                const float* x, int64_t ldx, int in_dim, float* dw, int64_t lddw,
                                float* db, int accumulate, void* stream);

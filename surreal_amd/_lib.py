@@ -153,6 +153,8 @@ _SIGS = {
     'smi_adam_clip': (c_int, [P, P, P, P, c_i64, P, P, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32,
                               P, P, P]),
     'smi_linear_forward': (c_int, [P, c_i64, c_int, c_int, P, c_i64, P, c_int, c_int, P, c_i64, P]),
+    'smi_linear_forward_cat': (c_int, [P, c_i64, c_int, c_int, P, c_i64, P, c_int, c_int, P, c_i64,
+                                       P, c_i64, c_int, P]),
     'smi_linear_backward_input': (c_int, [P, c_i64, c_int, c_int, P, c_i64, c_int, P, c_i64, P,
                                           c_i64, P]),
     'smi_linear_backward_weight': (c_int, [P, c_i64, c_int, c_int, P, c_i64, c_int, P, c_i64, P,

@@ -108,6 +108,8 @@ int launch_neg_mean_grad(const float*, int64_t, int64_t, float*, float*, hipStre
 int launch_tanh_backward(const float*, int64_t, const float*, int64_t, int64_t, int, float*,
                          int64_t, hipStream_t);
 int launch_copy_cols(const float*, int64_t, int64_t, int, float*, int64_t, hipStream_t);
+int launch_linear_fwd_cat(const float*, int64_t, int, int, const float*, int64_t, const float*, int,
+                          int, float*, int64_t, const float*, int64_t, int, hipStream_t);
 int launch_soft_update(float*, const float*, int64_t, float, hipStream_t);
 int launch_copy_bytes16(const void*, void*, int64_t, hipStream_t);
 int launch_copy_gather(void*, const void* const*, const int64_t*, const int64_t*, int, hipStream_t);
@@ -435,6 +437,18 @@ int smi_linear_forward(const float* x, int64_t ldx, int rows, int in_dim, const 
   REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_TANH, "linear_forward: act 0/1/2");
   return launch_linear_fwd(x, ldx, rows, in_dim, w, ldw, b, out_dim, act, y, ldy,
                            SMI_STREAM(stream));
+}
+
+int smi_linear_forward_cat(const float* x, int64_t ldx, int rows, int in_dim, const float* w,
+                           int64_t ldw, const float* b, int out_dim, int act, float* y,
+                           int64_t ldy, const float* s, int64_t lds, int s_cols, void* stream) {
+  REQUIRE(x && w && y && s && rows >= 0 && in_dim > 0 && out_dim > 0 && s_cols > 0 && lds >= s_cols,
+          "linear_forward_cat: bad args");
+  REQUIRE(ldx >= in_dim && ldy >= out_dim + s_cols && ldw >= in_dim,
+          "linear_forward_cat: leading dims too small");
+  REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_TANH, "linear_forward_cat: act 0/1/2");
+  return launch_linear_fwd_cat(x, ldx, rows, in_dim, w, ldw, b, out_dim, act, y, ldy, s, lds, s_cols,
+                               SMI_STREAM(stream));
 }
 
 int smi_linear_backward_input(const float* dy, int64_t ldg, int rows, int out_dim, const float* w,

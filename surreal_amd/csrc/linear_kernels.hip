@@ -59,6 +59,10 @@ struct GemmArgs {
   // bias column (b_ih and b_hh have the same gradient).
   const float* B2; int64_t b2_rs; int split_col, c1_real;
   float* C2; int64_t ldc2; float* bias_out2;
+  // EPI_FWD on the short-batch kernel: also C[m][N + j] = xsrc[m*xlds + j],
+  // j < xcols (CriticNetworkX's cat(h1, action): the action block of the
+  // next layer's input written by the layer that writes h1)
+  const float* xsrc; int64_t xlds; int xcols;
 };
 
 // where output (m, n) of a weight gradient goes (bias column, the second
@@ -1916,12 +1920,102 @@ static int dx_smallk_launch(const GemmArgs& g, hipStream_t st) {
   return check_launch("dx_smallk_kernel");
 }
 
+// Forwards and input gradients of short batches (M <= 4096 rows: DDPG's 512-row
+// layers) in ONE launch without split-K: a workgroup owns one 16 x 16 output
+// tile and its four waves split K (wave w takes the 16-k chunks c = w, w + 4,
+// ...), every chunk's operands loaded up front (one memory round trip), a
+// fixed-order LDS sum of the four waves' accumulators, then the epilogue (bias
+// + activation, or the input gradient's ReLU mask).  Lane (i, q) = (lane & 15,
+// lane >> 4) takes k = 16c + 4q + s at MFMA s of a chunk on both operands (the
+// k order permuted identically: every chunk adds its exact 16-term sum), so a
+// k-contiguous operand is one 16-byte load per chunk.  The split-K form this
+// replaces needed a second launch (the reducer) and ran a 64 x 64 tile's
+// serial K loop per slab.
+constexpr int T16_MAXC = 8;                       // chunks per wave: K <= 4 * 16 * 8 = 512
+template <int EPI>
+__global__ void __launch_bounds__(kWG)
+gemm_t16_kernel(GemmArgs g) {
+  if (g.skip && g.skip[0] != 0) return;
+  __shared__ f32x4 red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int m0 = blockIdx.x * 16, n0 = blockIdx.y * 16;
+  const int ra = min(m0 + i, g.M - 1), cb = min(n0 + i, g.N - 1);
+  const float* Ar = g.A + (int64_t)ra * g.a_rs;
+  const float* Bc = g.B + (int64_t)cb * g.b_cs;
+  const int nch = (g.K + 15) >> 4;
+  // 16-byte k runs only where k is the contiguous direction (avec / bvec are
+  // also set for the other orientation)
+  const bool a4 = g.avec && g.a_cs == 1, b4 = g.bvec && g.b_rs == 1;
+  float av[T16_MAXC][4], bv[T16_MAXC][4];
+#pragma unroll
+  for (int j = 0; j < T16_MAXC; ++j) {
+    const int c = wave + 4 * j;
+    const int k0 = 16 * c + 4 * q;
+    if (c >= nch) break;
+    if (a4 && k0 + 3 < g.K) {
+      const float4 x = *reinterpret_cast<const float4*>(Ar + k0);
+      av[j][0] = x.x; av[j][1] = x.y; av[j][2] = x.z; av[j][3] = x.w;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) av[j][t] = k0 + t < g.K ? Ar[(int64_t)(k0 + t) * g.a_cs] : 0.f;
+    }
+    if (b4 && k0 + 3 < g.K) {
+      const float4 x = *reinterpret_cast<const float4*>(Bc + k0);
+      bv[j][0] = x.x; bv[j][1] = x.y; bv[j][2] = x.z; bv[j][3] = x.w;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bv[j][t] = k0 + t < g.K ? Bc[(int64_t)(k0 + t) * g.b_rs] : 0.f;
+    }
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < T16_MAXC; ++j) {
+    if (wave + 4 * j >= nch) break;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][t], bv[j][t], acc, 0, 0, 0);
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (EPI == EPI_FWD && wave == 1 && blockIdx.y == 0 && g.xsrc) {
+    for (int e = lane; e < 16 * g.xcols; e += 64) {
+      const int r = e / g.xcols, j = e - r * g.xcols;
+      if (m0 + r < g.M) g.C[(int64_t)(m0 + r) * g.ldc + g.N + j] = g.xsrc[(int64_t)(m0 + r) * g.xlds + j];
+    }
+  }
+  if (wave != 0) return;
+  const f32x4 sum = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  // D(row 4q + r, col i)
+  const int n = n0 + i;
+  if (n >= g.N) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + 4 * q + r;
+    if (m >= g.M) continue;
+    float v = sum[r];
+    if constexpr (EPI == EPI_FWD) {
+      if (g.bias) v += g.bias[n];
+      if (g.act == ACT_RELU) v = v > 0.f ? v : 0.f;
+      else if (g.act == ACT_TANH) v = tanhf(v);
+    } else {
+      if (g.mask && !(g.mask[(int64_t)m * g.ldm + n] > 0.f)) v = 0.f;
+    }
+    g.C[(int64_t)m * g.ldc + n] = v;
+  }
+}
+
+// SMI_GEMM_T16=0: the split-K form for short batches instead (A/B knob)
+static bool use_t16() {
+  static const bool on = [] { const char* e = getenv("SMI_GEMM_T16"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return SMI_OK;
   g.part = nullptr;
   if (epi == EPI_DX && use_dx_smallk() && g.K >= 1 && g.K <= 8 && g.a_cs == 1 && g.b_cs == 1)
     return dx_smallk_launch(g, st);
-  if (epi != EPI_DW && panel_ok(epi, g)) return panel_launch(epi, g, st);
+  if (epi != EPI_DW && !g.xsrc && panel_ok(epi, g)) return panel_launch(epi, g, st);
   if (epi == EPI_DW && use_dwd() && g.a_rs == 1 && g.b_cs == 1 && g.K >= 1 &&
       (g.ones_col >= 0 ? g.ones_col : g.N) >= 1 && g.M <= 512 && g.N <= 512)
     return dw_group_add(g) ? SMI_OK : dwd_launch(g, st);
@@ -1955,6 +2049,17 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   }();
   const bool split_fwd = (epi == EPI_FWD || epi == EPI_DX) && gm * gn < 256 &&
                          g.K >= fwd_split_min;
+  // the short-batch kernel for every forward / input gradient whose 64 x 64
+  // tiling leaves the GPU mostly idle (< 256 tiles), split-K or not
+  if ((epi == EPI_FWD || epi == EPI_DX) && gm * gn < 256 && use_t16() && g.M <= 4096 &&
+      g.K <= 4 * 16 * T16_MAXC) {
+    const dim3 grid16((g.M + 15) / 16, (g.N + 15) / 16);
+    const int kslot = ktime_begin(st);
+    if (epi == EPI_FWD) hipLaunchKernelGGL(gemm_t16_kernel<EPI_FWD>, grid16, dim3(kWG), 0, st, g);
+    else hipLaunchKernelGGL(gemm_t16_kernel<EPI_DX>, grid16, dim3(kWG), 0, st, g);
+    ktime_end(kslot, epi == EPI_FWD ? KT_GEMM_FWD : KT_GEMM_DX, 2.0 * g.M * (double)g.N * g.K, st);
+    return check_launch("gemm_t16_kernel");
+  }
   if ((epi == EPI_DW && g.K > 4 * GBK) || split_fwd) {
     const int tiles = gm * gn;
     S = (smi_splitk_target() + tiles - 1) / tiles;    // ~2-4 workgroups per CU
@@ -2023,6 +2128,29 @@ int launch_linear_fwd(const float* X, int64_t ldx, int M, int K, const float* W,
   g.A = X; g.a_rs = ldx; g.a_cs = 1;
   g.B = W; g.b_rs = 1; g.b_cs = ldw;        // B(k,n) = W[n][k]
   g.C = Y; g.ldc = ldy; g.bias = b; g.act = act; g.ones_col = -1; g.skip = skip;
+  return gemm_launch(EPI_FWD, g, st);
+}
+
+// launch_linear_fwd plus Y[:, N : N + xcols] = S[:, :xcols] (one launch on the
+// short-batch kernel, else the forward and a column copy)
+int launch_copy_cols(const float* src, int64_t lds, int64_t rows, int cols, float* dst,
+                     int64_t ldd, hipStream_t st);
+int launch_linear_fwd_cat(const float* X, int64_t ldx, int M, int K, const float* W, int64_t ldw,
+                          const float* b, int N, int act, float* Y, int64_t ldy, const float* S,
+                          int64_t lds, int xcols, hipStream_t st) {
+  const int gm = (M + GBM - 1) / GBM, gn = (N + GBN - 1) / GBN;
+  const bool t16 = !(K >= 1 && K <= 64 && N >= 32 && N <= 512 && M >= 2048) && use_t16() &&
+                   gm * gn < 256 && M <= 4096 && K <= 4 * 16 * T16_MAXC && M > 0;
+  if (!t16) {
+    RC_CHECK(launch_linear_fwd(X, ldx, M, K, W, ldw, b, N, act, Y, ldy, st));
+    return launch_copy_cols(S, lds, M, xcols, Y + N, ldy, st);
+  }
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K;
+  g.A = X; g.a_rs = ldx; g.a_cs = 1;
+  g.B = W; g.b_rs = 1; g.b_cs = ldw;
+  g.C = Y; g.ldc = ldy; g.bias = b; g.act = act; g.ones_col = -1;
+  g.xsrc = S; g.xlds = lds; g.xcols = xcols;
   return gemm_launch(EPI_FWD, g, st);
 }
 

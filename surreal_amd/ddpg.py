@@ -308,9 +308,11 @@ class _Net(object):
             H1 = self.buf(pre + '_h1', (rows, c1))
             self.lin(obs, obs.stride(0), rows, D, wo, D, bo, c1, RELU, H1, c1)
             self.norm(critic, 0, H1, rows, CAT, c1 + A, pre + '_ln1')
-        else:
-            self.lin(obs, obs.stride(0), rows, D, wo, D, bo, c1, RELU, CAT, c1 + A)
-        L.call('smi_copy_cols', _p(act), act.stride(0), rows, A, _p(CAT[:, c1:]), c1 + A, self.st)
+            L.call('smi_copy_cols', _p(act), act.stride(0), rows, A, _p(CAT[:, c1:]), c1 + A,
+                   self.st)
+        else:   # relu(obs W^T + b) and the action block of the concat in one launch
+            L.call('smi_linear_forward_cat', _p(obs), obs.stride(0), rows, D, _p(wo), D, _p(bo), c1,
+                   RELU, _p(CAT), c1 + A, _p(act), act.stride(0), A, self.st)
         self.lin(CAT, c1 + A, rows, c1 + A, wc, c1 + A, bc, c2, RELU, H2, c2)
         X2 = H2
         if critic.use_layernorm:

@@ -34,6 +34,12 @@ from surreal_amd.learner import PPOLearner
 from surreal_amd.publish import DeviceParameterPublisher
 from tests.helpers import env_config, load_lstm_flat, max_rel_err, ppo_config
 
+# agent actions vs the oracle agent (torch CPU fp32): two fp32 evaluations of
+# the 17 -> 300 -> 200 -> 6 actor in different summation orders (the GPU's
+# short-batch GEMM sums 16-k chunks as MFMA chains, then four chunk groups);
+# measured up to 1.3e-5 of max(|a|, 1e-2) through the tanh
+AGENT_BAR = 4e-5
+
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
@@ -328,7 +334,7 @@ def test_ddpg_agent_batch_matches_sequential_reference_agents(noise):
         assert a.shape == (N, A)
         # actions live in [-1, 1]: judge against that scale (floor 1e-2), not
         # against the largest entry of a small OU-noise step
-        assert max_rel_err(a, ra, floor=1e-2) < 1e-5, (step, a, ra)
+        assert max_rel_err(a, ra, floor=1e-2) < AGENT_BAR, (step, a, ra)
 
 
 @pytest.mark.parametrize('pn', ['normal', 'adaptive_normal'])
@@ -389,7 +395,7 @@ def test_ddpg_agent_param_noise_matches_reference_agents(pn):
             a = agents.act(obs)
             np.random.set_state(state)
             ra = np.stack([refs[i].act(obs[i]) for i in range(N)])
-            assert max_rel_err(a, ra, floor=1e-2) < 1e-5, (fetch, step, a, ra)
+            assert max_rel_err(a, ra, floor=1e-2) < AGENT_BAR, (fetch, step, a, ra)
     if pn == 'adaptive_normal':
         # the sigmas moved (one direction or the other) at every fetch after the first
         assert not np.allclose(agents.pn_sigma, ex.param_noise_sigma)
