@@ -1644,6 +1644,72 @@ static int dw_prepare(DwGroup& G, int wv, int slots, int64_t ws_off, int64_t& ne
   return SMI_OK;
 }
 
+// short-batch 16 x 16-tile kernels (gemm_t16_kernel, gemm_dwt16_kernel): 16-k
+// chunks per wave, K <= 4 * 16 * 8 = 512
+constexpr int T16_MAXC = 8;
+// SMI_GEMM_T16=0: the split-K / grouped forms for short batches instead (A/B knob)
+static bool use_t16() {
+  static const bool on = [] { const char* e = getenv("SMI_GEMM_T16"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+// Weight gradients of short batches (K = rows <= 512: DDPG's 512-row
+// updates) without split-K: one 16 x 16 tile of one group entry per
+// workgroup, the four waves splitting the rows in 16-row chunks (c = w, w + 4,
+// ...: every chunk's operands loaded up front), a fixed-order LDS sum of the
+// four waves, then the destination written directly (dw_put: no partials, no
+// reducer launch).  Lane (i, q) reads dY[k][m0 + i] and X[k][n0 + i] for k =
+// 16c + 4q + s: 16 consecutive floats per row on both operands.
+__global__ void __launch_bounds__(kWG)
+gemm_dwt16_kernel(DwGroup G) {
+  __shared__ f32x4 red[4][64];
+  const int b = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < G.n && b >= G.wg0[gi + 1]) ++gi;
+  const GemmArgs& g = G.g[gi];
+  if (g.skip && g.skip[0] != 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int local = b - G.wg0[gi], gn16 = (g.N + 15) >> 4;
+  const int m0 = (local / gn16) * 16, n0 = (local % gn16) * 16;
+  const int mi = min(m0 + i, g.M - 1), ni = n0 + i;
+  const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
+  const float* Ar = g.A + (int64_t)mi * g.a_rs;
+  const bool bval = ni < bdata, bone = ni == g.ones_col;
+  const float* Bc = g.B + (int64_t)(bval ? ni : 0) * g.b_cs;
+  const int nch = (g.K + 15) >> 4;
+  float av[T16_MAXC][4], bv[T16_MAXC][4];
+#pragma unroll
+  for (int j = 0; j < T16_MAXC; ++j) {
+    const int c = wave + 4 * j;
+    if (c >= nch) break;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = 16 * c + 4 * q + t;
+      const bool kv = k < g.K;
+      av[j][t] = kv ? Ar[(int64_t)k * g.a_cs] : 0.f;
+      bv[j][t] = kv ? (bval ? Bc[(int64_t)k * g.b_rs] : (bone ? 1.f : 0.f)) : 0.f;
+    }
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < T16_MAXC; ++j) {
+    if (wave + 4 * j >= nch) break;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][t], bv[j][t], acc, 0, 0, 0);
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0) return;
+  const f32x4 sum = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (ni >= g.N) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + 4 * q + r;
+    if (m < g.M) dw_put(g, m, ni, sum[r]);
+  }
+}
+
 // entries already launched with the BPTT (launch_lstm_bwd_dw) whose partials
 // the group's reducer still sums, and the workspace floats they hold
 static thread_local DwGroup g_pre;
@@ -1667,6 +1733,21 @@ int dw_group_flush(hipStream_t st) {
     G.rb0[0] = 0;                                   // the epilogue task alone
     hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(1), dim3(kWG), 0, st, G);
     return check_launch("gemm_group_reduce_kernel");
+  }
+  // short batches (every entry <= 512 rows, one destination): 16 x 16 tiles
+  // written directly, no partials and no reducer
+  if (!pre && !G.x.on && use_t16()) {
+    bool small = G.n > 0;
+    for (int i = 0; i < G.n; ++i) small = small && G.g[i].K <= 4 * 16 * T16_MAXC && !G.g[i].B2;
+    if (small) {
+      G.wg0[0] = 0;
+      for (int i = 0; i < G.n; ++i)
+        G.wg0[i + 1] = G.wg0[i] + ((G.g[i].M + 15) / 16) * ((G.g[i].N + 15) / 16);
+      const int kslot = ktime_begin(st);
+      hipLaunchKernelGGL(gemm_dwt16_kernel, dim3(G.wg0[G.n]), dim3(kWG), 0, st, G);
+      ktime_end(kslot, KT_GEMM_DW, g_grp_flops, st);
+      return check_launch("gemm_dwt16_kernel");
+    }
   }
   int64_t need = 0;
   if (G.n > 0) {
@@ -1931,7 +2012,6 @@ static int dx_smallk_launch(const GemmArgs& g, hipStream_t st) {
 // k-contiguous operand is one 16-byte load per chunk.  The split-K form this
 // replaces needed a second launch (the reducer) and ran a 64 x 64 tile's
 // serial K loop per slab.
-constexpr int T16_MAXC = 8;                       // chunks per wave: K <= 4 * 16 * 8 = 512
 template <int EPI>
 __global__ void __launch_bounds__(kWG)
 gemm_t16_kernel(GemmArgs g) {
@@ -2004,11 +2084,6 @@ gemm_t16_kernel(GemmArgs g) {
   }
 }
 
-// SMI_GEMM_T16=0: the split-K form for short batches instead (A/B knob)
-static bool use_t16() {
-  static const bool on = [] { const char* e = getenv("SMI_GEMM_T16"); return !(e && e[0] == '0'); }();
-  return on;
-}
 
 static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return SMI_OK;
