@@ -1653,13 +1653,18 @@ static bool use_t16() {
   return on;
 }
 
-// Weight gradients of short batches (K = rows <= 512: DDPG's 512-row
-// updates) without split-K: one 16 x 16 tile of one group entry per
-// workgroup, the four waves splitting the rows in 16-row chunks (c = w, w + 4,
-// ...: every chunk's operands loaded up front), a fixed-order LDS sum of the
-// four waves, then the destination written directly (dw_put: no partials, no
-// reducer launch).  Lane (i, q) reads dY[k][m0 + i] and X[k][n0 + i] for k =
-// 16c + 4q + s: 16 consecutive floats per row on both operands.
+// Weight gradients of short batches without split-K: one 16 x 16 tile of one
+// group entry per workgroup, the four waves splitting the rows in 16-row
+// chunks (wave w takes c = w, w + 4, ...) through a ring of DR chunks in
+// flight, two accumulator chains (even / odd chunk of the wave), a fixed-order
+// LDS sum of the four waves, then the destination written directly (dw_put:
+// no partials, no reducer launch).  Lane (i, q) reads dY[k][m0 + i] and
+// X[k][n0 + i] for k = 16c + 4q + s: 16 consecutive floats per row on both
+// operands.  The two-source B of the LSTM's [x_t | h_{t-1}] (B2) and the
+// bias column are formed per lane.  Measured on the LSTM's gradient at 3200
+// rows (a rank's batch): 28-30 us against 21.6 us on the grouped dW launch
+// (800 scalar operand loads per lane), so only short groups take it.
+constexpr int DWT_DR = 8;   // chunks in flight per wave (the trip's accumulators)
 __global__ void __launch_bounds__(kWG)
 gemm_dwt16_kernel(DwGroup G) {
   __shared__ f32x4 red[4][64];
@@ -1675,30 +1680,50 @@ gemm_dwt16_kernel(DwGroup G) {
   const int mi = min(m0 + i, g.M - 1), ni = n0 + i;
   const int bdata = g.ones_col >= 0 ? g.ones_col : g.N;
   const float* Ar = g.A + (int64_t)mi * g.a_rs;
-  const bool bval = ni < bdata, bone = ni == g.ones_col;
-  const float* Bc = g.B + (int64_t)(bval ? ni : 0) * g.b_cs;
+  // column ni of B: the first source, the second (B2: columns >= split_col),
+  // a padding column (c1_real <= ni < split_col), the bias column or past N
+  const float* Bc = g.B;
+  int64_t bs = g.b_rs;
+  bool bz = false, bone = false;
+  if (ni == g.ones_col) bone = true;
+  else if (ni >= bdata || ni >= g.N) bz = true;
+  else if (g.B2 && ni >= g.split_col) { Bc = g.B2 + (ni - g.split_col); bs = g.b2_rs; }
+  else if (g.B2 && ni >= g.c1_real) bz = true;
+  else Bc = g.B + (int64_t)ni * g.b_cs;
   const int nch = (g.K + 15) >> 4;
-  float av[T16_MAXC][4], bv[T16_MAXC][4];
-#pragma unroll
-  for (int j = 0; j < T16_MAXC; ++j) {
+  const int nw = nch > wave ? (nch - wave + 3) >> 2 : 0;        // this wave's chunks
+  float av[DWT_DR][4], bv[DWT_DR][4];
+  auto ld = [&](int j, int slot) {
     const int c = wave + 4 * j;
-    if (c >= nch) break;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int k = 16 * c + 4 * q + t;
-      const bool kv = k < g.K;
-      av[j][t] = kv ? Ar[(int64_t)k * g.a_cs] : 0.f;
-      bv[j][t] = kv ? (bval ? Bc[(int64_t)k * g.b_rs] : (bone ? 1.f : 0.f)) : 0.f;
+      const bool kv = j < nw && k < g.K;
+      av[slot][t] = kv ? Ar[(int64_t)k * g.a_cs] : 0.f;
+      bv[slot][t] = kv ? (bone ? 1.f : bz ? 0.f : Bc[(int64_t)k * bs]) : 0.f;
     }
-  }
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  };
 #pragma unroll
-  for (int j = 0; j < T16_MAXC; ++j) {
-    if (wave + 4 * j >= nch) break;
+  for (int d = 0; d < DWT_DR; ++d) ld(d, d);
+  // each ring trip: one fresh MFMA chain per slot (16 products), the trip's
+  // four chains summed in a fixed tree into the running total (short fp32
+  // chains: at 3200 rows a single chain per wave was ~2x the oracle's fp32
+  // spread on the C3 rank fixture's update bars)
+  f32x4 tot = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nw; j0 += DWT_DR) {
+    f32x4 acc[DWT_DR];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][t], bv[j][t], acc, 0, 0, 0);
+    for (int d = 0; d < DWT_DR; ++d) {
+      acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (j0 + d < nw) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][t], bv[d][t], acc[d], 0, 0, 0);
+      }
+      ld(j0 + d + DWT_DR, d);
+    }
+    tot += ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   }
-  red[wave][lane] = acc;
+  red[wave][lane] = tot;
   __syncthreads();
   if (wave != 0) return;
   const f32x4 sum = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
@@ -1708,6 +1733,12 @@ gemm_dwt16_kernel(DwGroup G) {
     const int m = m0 + 4 * q + r;
     if (m < g.M) dw_put(g, m, ni, sum[r]);
   }
+}
+
+static void dwt16_prefix(DwGroup& G) {
+  G.wg0[0] = 0;
+  for (int i = 0; i < G.n; ++i)
+    G.wg0[i + 1] = G.wg0[i] + ((G.g[i].M + 15) / 16) * ((G.g[i].N + 15) / 16);
 }
 
 // entries already launched with the BPTT (launch_lstm_bwd_dw) whose partials
@@ -1734,15 +1765,13 @@ int dw_group_flush(hipStream_t st) {
     hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(1), dim3(kWG), 0, st, G);
     return check_launch("gemm_group_reduce_kernel");
   }
-  // short batches (every entry <= 512 rows, one destination): 16 x 16 tiles
-  // written directly, no partials and no reducer
+  // short batches (every entry <= 512 rows, one group, no epilogue task):
+  // 16 x 16 tiles written directly, no partials and no reducer
   if (!pre && !G.x.on && use_t16()) {
     bool small = G.n > 0;
-    for (int i = 0; i < G.n; ++i) small = small && G.g[i].K <= 4 * 16 * T16_MAXC && !G.g[i].B2;
+    for (int i = 0; i < G.n; ++i) small = small && G.g[i].K <= 4 * 16 * T16_MAXC;
     if (small) {
-      G.wg0[0] = 0;
-      for (int i = 0; i < G.n; ++i)
-        G.wg0[i + 1] = G.wg0[i] + ((G.g[i].M + 15) / 16) * ((G.g[i].N + 15) / 16);
+      dwt16_prefix(G);
       const int kslot = ktime_begin(st);
       hipLaunchKernelGGL(gemm_dwt16_kernel, dim3(G.wg0[G.n]), dim3(kWG), 0, st, G);
       ktime_end(kslot, KT_GEMM_DW, g_grp_flops, st);
