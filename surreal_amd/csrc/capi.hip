@@ -115,13 +115,15 @@ int launch_copy_bytes16(const void*, void*, int64_t, hipStream_t);
 int launch_copy_gather(void*, const void* const*, const int64_t*, const int64_t*, int, hipStream_t);
 bool head_fused_ok(int in, int64_t ldx, int h1, int h2, int out, const float* X,
                    const float* W1, const float* W2, const float* W3);
+struct PolRowArgs;
 int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
                           const float* b1, int h1, const float* W2, const float* b2, int h2,
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
                           hipStream_t st, const int* skip, const float* vret = nullptr,
-                          float* vgrad = nullptr, float vscale = 0.f);
-struct PolRowArgs;
+                          float* vgrad = nullptr, float vscale = 0.f,
+                          const PolRowArgs* ps = nullptr);
+bool head_fwd_ps_ok(int h1, int h2, int out);
 int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
                           const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,

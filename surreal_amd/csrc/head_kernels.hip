@@ -59,6 +59,10 @@ struct HeadFwdArgs {
   // vscale * (Y[r] - vret[r]), the MSE gradient the learner's value_rows pass
   // would compute from Y (same fp32 ops), written by the forward itself
   const float* vret; float* vgrad; float vscale;
+  // policy statistics epilogue (head_fwd_kernel<..., PS>, adapt mode, out ==
+  // 8): the rows' sums of policy_rows_stats_kernel's pass from the means the
+  // forward just formed, one PS_N partial per workgroup at ps.part
+  PolRowArgs ps;
 };
 
 struct HeadBwdArgs {
@@ -373,7 +377,7 @@ __device__ __forceinline__ void hc_transpose_tile(const float* __restrict__ W, i
 // LDS floats of the forward's last-layer partials / transpose tile
 __host__ __device__ constexpr int hc_sr(int RT) { return RT * 1024 > HC_SR ? RT * 1024 : HC_SR; }
 
-template <int NT1, int NT2, int RT>
+template <int NT1, int NT2, int RT, bool PS>
 __global__ void __launch_bounds__(kWG)
 head_fwd_kernel(HeadFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
@@ -454,6 +458,24 @@ head_fwd_kernel(HeadFwdArgs a) {
     hc_sync();
     HEAD_TICK(0, 5);                              // epilogue 2 + barrier
     hc_copy_out<RT>(s2, a.ld2, a.h2, a.HA2, r0, a.rows);
+    // PS: thread t < R's row inputs of the statistics pass, in flight through
+    // layer 3
+    constexpr int R_ = HC_R * RT, PA = 8;
+    __shared__ float smu[PS ? R_ * PA : 1];
+    float prm[PS ? PA : 1], pac[PS ? PA : 1], pbm[PS ? PA : 1], pbs[PS ? PA : 1], padv = 0.f, pret = 0.f;
+    const int64_t prow = r0 + threadIdx.x;
+    const bool pown = PS && (int)threadIdx.x < R_ && prow < a.rows;
+    if constexpr (PS) {
+      if (pown) {
+        const int64_t N = (int64_t)a.ps.E * a.ps.B;
+        ld_row<PA>(prm, a.ps.refmu + prow * PA, PA);
+        ld_fields<PA>(pac, a.ps.rowin, N, prow, 0, PA);
+        ld_fields<PA>(pbm, a.ps.rowin, N, prow, PA, PA);
+        ld_fields<PA>(pbs, a.ps.rowin, N, prow, 2 * PA, PA);
+        padv = a.ps.rowin[rin_idx(row_w(PA), prow, 3 * PA)];
+        pret = a.ps.ret_tm[prow];
+      }
+    }
     {   // layer 3 (out <= 16): the waves split the k chunks, fixed-order sum
       const float bn = a.b3[li < a.out ? li : a.out - 1];
       // the value targets of the lane's rows (value-gradient epilogue), in
@@ -490,7 +512,37 @@ head_fwd_kernel(HeadFwdArgs a) {
             const float y = a.tanh_out ? tanhf(v) : v;
             a.Y[(r0 + r) * a.ldy + li] = y;
             if (a.vgrad) a.vgrad[r0 + r] = a.vscale * (y - vr[rt][i]);
+            if constexpr (PS) smu[r * PA + li] = y;
           }
+      }
+    }
+    if constexpr (PS) {
+      // the statistics of the workgroup's rows (pol_rows.hpp: the stats
+      // kernel's adapt-mode ops), summed over the rows on wave 0 in a fixed
+      // butterfly order, one PS_N partial per workgroup
+      hc_sync();
+      double acc[PS_N];
+#pragma unroll
+      for (int k = 0; k < PS_N; ++k) acc[k] = 0.0;
+      if (pown) {
+        float sg[PA], lsg[PA], rsg[PA], mu[PA];
+#pragma unroll
+        for (int j = 0; j < PA; ++j) {
+          sg[j] = expf(a.ps.lv[j]);                // builders.py:127 std = exp(log_var)
+          lsg[j] = logf(sg[j]);
+          rsg[j] = expf(a.ps.ref_lv[j]);
+          mu[j] = smu[threadIdx.x * PA + j];
+        }
+        const PolStatsCols<PA> cols(sg, lsg, rsg, PA);
+        const AdvNorm nadv(a.ps);
+        pol_stats_row_adapt<PA>(a.ps, cols, nadv, mu, prm, pac, pbm, pbs, padv, pret, acc);
+      }
+      if (wave == 0) {
+#pragma unroll
+        for (int k = 0; k < PS_N; ++k) {
+          const double v = wave_sum_d(acc[k]);
+          if (lane == 0) a.ps.part[(int64_t)blockIdx.x * PS_N + k] = v;
+        }
       }
     }
   }
@@ -743,32 +795,44 @@ int head_bwd_blocks(int64_t rows) {
   return (int)((rows + R - 1) / R);
 }
 
+// the statistics epilogue's instantiation (C3 / C5 widths)
+bool head_fwd_ps_ok(int h1, int h2, int out) { return hc_nt(h1) == 5 && hc_nt(h2) == 4 && out == 8; }
+
 int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
                           const float* b1, int h1, const float* W2, const float* b2, int h2,
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
                           hipStream_t st, const int* skip, const float* vret, float* vgrad,
-                          float vscale) {
+                          float vscale, const PolRowArgs* ps) {
   if (rows <= 0) return SMI_OK;
   if (vgrad && (out != 1 || !vret)) return set_error(SMI_E_ARG, "head_forward: value epilogue needs out == 1");
+  if (ps && !head_fwd_ps_ok(h1, h2, out)) return set_error(SMI_E_ARG, "head_forward: statistics epilogue shape");
   HeadFwdArgs a{X, ldx, in, W1, b1, W2, b2, W3, b3, h1, h2, out, tanh_out, HA1, HA2, Y, ldy,
                 W1T, W2T, rows, skip, hc_ld(in), hc_ld(h1), hc_ld(h2), vret, vgrad, vscale};
+  if (ps) a.ps = *ps;
   const int rt = hc_rt(rows);
   const int R = HC_R * rt;
   const size_t lds = (size_t)(R * ((a.ld0 > a.ld2 ? a.ld0 : a.ld2) + a.ld1) + hc_sr(rt)) * 4;
   const dim3 grid((unsigned)((rows + R - 1) / R));
   const int n1 = hc_nt(h1), n2 = hc_nt(h2);
   const int kslot = ktime_begin(st);
-#define SMI_HF(A, B)                                                                    \
+#define SMI_HFP(A, B, P)                                                                \
   do {                                                                                  \
     if (rt == 2) {                                                                      \
-      allow_lds(head_fwd_kernel<A, B, 2>, lds);                                         \
-      hipLaunchKernelGGL((head_fwd_kernel<A, B, 2>), grid, dim3(kWG), lds, st, a);      \
+      allow_lds(head_fwd_kernel<A, B, 2, P>, lds);                                      \
+      hipLaunchKernelGGL((head_fwd_kernel<A, B, 2, P>), grid, dim3(kWG), lds, st, a);   \
     } else {                                                                            \
-      allow_lds(head_fwd_kernel<A, B, 1>, lds);                                         \
-      hipLaunchKernelGGL((head_fwd_kernel<A, B, 1>), grid, dim3(kWG), lds, st, a);      \
+      allow_lds(head_fwd_kernel<A, B, 1, P>, lds);                                      \
+      hipLaunchKernelGGL((head_fwd_kernel<A, B, 1, P>), grid, dim3(kWG), lds, st, a);   \
     }                                                                                   \
   } while (0)
+#define SMI_HF(A, B) SMI_HFP(A, B, false)
+  if (ps) {                        // the statistics epilogue: 300 x 200 heads, 8 actions
+    SMI_HFP(5, 4, true);
+    ktime_end(kslot, KT_GEMM_FWD,
+              2.0 * (double)rows * ((double)in * h1 + (double)h1 * h2 + (double)h2 * out), st);
+    return check_launch("head_fwd_kernel");
+  }
   // layer-1 slots {2, 5, 8} x layer-2 slots {2, 3, 4, 5, 8} (C3 / C5: 300 x 200 -> 5, 4)
   const int m1 = n1 <= 2 ? 2 : n1 <= 5 ? 5 : 8;
 #define SMI_HF2(A)                                        \
@@ -786,6 +850,7 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
   else SMI_HF2(8);
 #undef SMI_HF2
 #undef SMI_HF
+#undef SMI_HFP
   ktime_end(kslot, KT_GEMM_FWD,
             2.0 * (double)rows * ((double)in * h1 + (double)h1 * h2 + (double)h2 * out), st);
   return check_launch("head_fwd_kernel");

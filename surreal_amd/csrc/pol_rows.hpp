@@ -433,4 +433,57 @@ __device__ __forceinline__ void pol_grad_row(const PolRowArgs& a, const PolGradC
   pol_grad_compute<AT>(a, c, nadv, x, wsurr, wkl, dz, glv);
 }
 
+// ---- the statistics row pass (policy_rows_stats_kernel, adapt mode; the
+// fused head forward's epilogue) ----
+// per-column terms of the learner std (log-likelihood, KL(ref || learner))
+// and the reference std (KL(ref || behaviour)), hoisted out of the row loop
+template <int AT>
+struct PolStatsCols {
+  static constexpr int AM = AT > 0 ? AT : 32;
+  float isig[AM], lsig[AM], lkl[AM], s02[AM], iden2[AM], lrsig[AM];
+  int A;
+  // sig / lsig / rsig: exp(lv), log(exp(lv)), exp(ref_lv) per column
+  __device__ PolStatsCols(const float* sig, const float* lsg, const float* rsg, int A_) : A(A_) {
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A_); ++j) {
+      const float sg = sig[j], rsig = rsg[j];
+      lsig[j] = lsg[j];
+      isig[j] = 1.f / sg;
+      lkl[j] = logf(sg / rsig);                // row_kl(rm, rsig, m, sig)'s per-column terms
+      s02[j] = rsig * rsig;
+      iden2[j] = 1.f / (2.f * (sg * sg));
+      lrsig[j] = logf(rsig);
+    }
+  }
+};
+
+// adapt-mode sums of one row into acc[PS_N] (policy_rows_stats_kernel's row
+// pass, FUSE off: the same ops in the same order); m = the row's learner means
+template <int AT>
+__device__ __forceinline__ void pol_stats_row_adapt(const PolRowArgs& a, const PolStatsCols<AT>& c,
+                                                    const AdvNorm& nadv, const float* m,
+                                                    const float* rm, const float* ac,
+                                                    const float* bmu, const float* bsd, float adv,
+                                                    float ret, double* acc) {
+  constexpr int AM = AT > 0 ? AT : 32;
+  const int A = c.A;
+  float blsd[AM], ibsd[AM];
+  const float av = nadv(adv);
+  const float ex = expf(row_loglik_r<AT>(ac, m, c.isig, c.lsig, A, a.c_ll));
+  const float lp = fmaxf(ex, 1e-5f);
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    blsd[j] = logf(bsd[j]);
+    ibsd[j] = 1.f / bsd[j];
+  }
+  const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
+  acc[PS_KL] += (double)row_kl_cc<AT>(rm, m, c.lkl, c.s02, c.iden2, A);
+  acc[PS_SURR] += (double)(av * (lp / fmaxf(bl, 1e-2f)));
+  acc[PS_CLIP] += 0.0;
+  acc[PS_ISW] += (double)(lp / (bl + 1e-4f));
+  acc[PS_BL] += (double)bl;
+  acc[PS_RBD] += (double)row_kl_rb<AT>(rm, c.lrsig, c.s02, bmu, blsd, ibsd, A);
+  acc[PS_RET] += (double)ret;
+}
+
 }  // namespace smi

@@ -923,7 +923,9 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
                           hipStream_t st, const int* skip, const float* vret = nullptr,
-                          float* vgrad = nullptr, float vscale = 0.f);
+                          float* vgrad = nullptr, float vscale = 0.f,
+                          const PolRowArgs* ps = nullptr);
+bool head_fwd_ps_ok(int h1, int h2, int out);
 int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
                           const float* HA1, const float* HA2, float* dH2, float* dH1, float* dX,
@@ -941,10 +943,11 @@ static bool head_fused(const Head& h, const float* X, int64_t ldx) {
 // for a fused backward of the same parameters
 // vret / vgrad / vscale: the value-loss gradient written by the fused forward
 // (out == 1); *vdone tells whether it was (the layer-GEMM path does not)
+// ps: the policy statistics epilogue (the fused path only: head_fwd_ps_ok)
 static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, float* HA1,
                     float* HA2, float* Y, hipStream_t st, const int* skip, float* wT = nullptr,
                     const float* vret = nullptr, float* vgrad = nullptr, float vscale = 0.f,
-                    bool* vdone = nullptr) {
+                    bool* vdone = nullptr, const PolRowArgs* ps = nullptr) {
   const MlpLayout& L = h.L;
   if (vdone) *vdone = false;
   if (head_fused(h, X, ldx)) {
@@ -953,8 +956,9 @@ static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, fl
     return launch_head_fwd_fused(X, ldx, rows, h.in, h.P + L.fW1, h.P + L.fb1, h.h1, h.P + L.fW2,
                                  h.P + L.fb2, h.h2, h.P + L.fW3, h.P + L.fb3, h.out, h.tanh_out,
                                  HA1, HA2, Y, h.out, wT, wT ? wT + (int64_t)h.in * h.h1 : nullptr,
-                                 st, skip, ve ? vret : nullptr, ve ? vgrad : nullptr, vscale);
+                                 st, skip, ve ? vret : nullptr, ve ? vgrad : nullptr, vscale, ps);
   }
+  if (ps) return set_error(SMI_E_ARG, "head_forward: the statistics epilogue needs the fused head");
   const int M = (int)rows;
   RC(launch_linear_fwd(X, ldx, M, h.in, h.P + h.L.fW1, h.in, h.P + h.L.fb1, h.h1, ACT_RELU, HA1,
                        h.h1, st, skip));
@@ -1242,6 +1246,25 @@ static bool pol_head_grad(const smi_ppo_rnn_args& a, const RnnDims& d, const Rnn
          head_fused(actor, head_in(d, s, s.Xz), d.Hld) && head_bwd_blocks(d.NE) <= 4096;
 }
 
+// adapt mode, 8 actions, 300 x 200-class heads on the fused path: the policy
+// statistics row pass as the head forward's epilogue (one launch fewer per
+// policy epoch); one PS_N partial per head workgroup (<= 4096 of them).  Off
+// unless SMI_POL_STATS_HEAD=1 (A/B knob): measured 2.933 vs 2.928 ms at 128
+// segments, 6.986 vs 6.999 ms at C3 — the workgroups' serial row epilogue
+// (+6 / +10 us per forward) costs what the launch it removes did
+static bool pol_head_stats(const smi_ppo_rnn_args& a, const RnnDims& d, const RnnScratch& s,
+                           const Head& actor) {
+  static const bool on = [] { const char* e = getenv("SMI_POL_STATS_HEAD"); return e && e[0] == '1'; }();
+  return on && a.mode != 0 && d.A == 8 && head_fwd_ps_ok(d.h1, d.h2, d.A) &&
+         head_fused(actor, head_in(d, s, s.Xz), d.Hld) && head_bwd_blocks(d.NE) <= 4096;
+}
+// the partials the policy statistics pass wrote (its grid, or the head's)
+static int pol_stats_nb(const smi_ppo_rnn_args& a, const RnnDims& d, const RnnScratch& s,
+                        const Head& actor) {
+  if (a.mode == 0) return pol_stats_blocks<true>(d.A, d.NE);
+  return pol_head_stats(a, d, s, actor) ? head_bwd_blocks(d.NE) : pol_stats_blocks<false>(d.A, d.NE);
+}
+
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
   const RnnDims d = rnn_dims(a.B, a.T, a.horizon, a.obs_dim, a.rnn_hidden, a.h1, a.h2, a.act_dim,
                              a.critic_h1, a.critic_h2, a.pix_c, a.pix_h, a.pix_w, a.cnn_feat,
@@ -1314,16 +1337,20 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       }
       RC(cnn_features(a, d, cnn, d.E, s.Xz, s.A1, s, st, stop));
       if (d.H > 0 && e > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.E, a.h0, a.c0, s, true, st, stop));
-      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop, s.wT));
       PolRowArgs p = pol_rows(a, d, s);
-      const int nb = a.mode == 0 ? pol_stats_blocks<true>(d.A, d.NE) : pol_stats_blocks<false>(d.A, d.NE);
-      const int kt = ktime_begin(st);
       p.invN = (float)(1.0 / (double)NEg);
-      if (a.mode == 0) launch_pol_stats<true>(d.A, nb, p, st);     // + the clip gradient
-      else launch_pol_stats<false>(d.A, nb, p, st);
-      // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
-      ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
-      RC(check_launch("policy_rows_stats_kernel"));
+      const bool hs = pol_head_stats(a, d, s, actor);
+      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop, s.wT,
+                  nullptr, nullptr, 0.f, nullptr, hs ? &p : nullptr));
+      const int nb = pol_stats_nb(a, d, s, actor);
+      if (!hs) {
+        const int kt = ktime_begin(st);
+        if (a.mode == 0) launch_pol_stats<true>(d.A, nb, p, st);     // + the clip gradient
+        else launch_pol_stats<false>(d.A, nb, p, st);
+        // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
+        ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
+        RC(check_launch("policy_rows_stats_kernel"));
+      }
       if (fused_decide(a, e)) return SMI_OK;     // decided by POLICY_BWD's gradient pass
       if (a.B_global == a.B) {         // one rank: nothing to exchange before the decision
         DecideArgs da{a.pstat, e, a.epoch_policy, a.mode,
@@ -1351,7 +1378,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       const int nb = a.mode == 0 ? pol_stats_blocks<true>(d.A, d.NE) : rnn_nblk(d.NE, kRowNT);
       if (fused_decide(a, e)) {
         p.dec_part = s.part;
-        p.dec_nb = pol_stats_blocks<false>(d.A, d.NE);
+        p.dec_nb = pol_stats_nb(a, d, s, actor);
         p.dec = DecideArgs{a.pstat, e, a.epoch_policy, a.mode,
                            a.kl_target, a.kl_cutoff_coeff, NEg, a.hyper, a.actor + d.LA.flv, d.A,
                            c_entropy_of(d.A), s.ci, s.cf, a.stats};
