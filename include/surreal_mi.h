@@ -361,7 +361,10 @@ int smi_ppo_epoch_apply(const smi_ppo_args* args, int epoch, void* stream);
  * in the same order on every rank; between some phases a data-parallel caller
  * all-reduces (SUM) the buffer named in the phase table (include order):
  *   GAE              -> all-reduce moments (double[3], smi_ppo_rnn_args.moments)
- *   PREP             (reference-policy forward)
+ *   PREP             (reference-policy forward; after GAE on the same stream —
+ *                    at one segment per workgroup GAE runs PREP's recurrence
+ *                    in its own launch and PREP only the reference head, unless
+ *                    SMI_PREP_SIDE=1 puts PREP on a second stream)
  *   POLICY_FWD(e)    e = 0..epoch_policy: forward + loss sums -> all-reduce pstat
  *   POLICY_DECIDE(e) KL early stop / adapt coefficient / statistics from pstat
  *                    (with B_global == B, one rank, POLICY_FWD already decides

@@ -1225,10 +1225,16 @@ lstm_bwd_v_kernel(LstmBwdArgs a) {
 // Measured (tools/exp/lstm_v_exp.hip, 128 segments, H 100, one MI355X): see
 // DESIGN.md §9.  Sums are fixed-order (deterministic); their association
 // differs from the R forms' (fp32 rounding only).
+// a1: a second, independent sequence set in the same launch (workgroups >=
+// a0.B: the GAE critic pass and the reference policy's forward, two weight
+// sets over two inputs); single launches pass a0 twice over a0.B workgroups
 template <int KQ, int XQ, bool XM, int WI>
 __global__ void __launch_bounds__(kVT)
-lstm_fwd_q_kernel(LstmFwdArgs a) {
+lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
   static_assert(WI != 2 || KQ % 4 == 0, "float4 k runs");
+  const bool second = (int)blockIdx.x >= a0.B;
+  const LstmFwdArgs& a = second ? a1 : a0;
+  const int b = second ? (int)blockIdx.x - a0.B : (int)blockIdx.x;
   if (a.skip && a.skip[0] != 0) return;
   const int keepS = a.keep > 0 ? a.keep : a.S;
   static_assert(KQ % 2 == 0 && XQ % 4 == 0, "K split: pairs of h, float4 runs of x");
@@ -1241,7 +1247,6 @@ lstm_fwd_q_kernel(LstmFwdArgs a) {
   const bool act = u < H;
   const int uc = act ? u : H - 1;
   const int g = q * H + uc;
-  const int b = blockIdx.x;
   const int64_t BH = (int64_t)B * H;
   float bh = a.b_hh[g];
   // x staging, c0 / h0 (every load issued before W_hh's)
@@ -1593,22 +1598,25 @@ static bool use_xm() {
   static const bool on = [] { const char* e = getenv("SMI_LSTM_XM"); return !(e && e[0] == '0'); }();
   return on;
 }
+// a1 (optional): the second sequence set of a dual launch (same H / x width)
 template <int XQ>
-static void fwd_q_dispatch(const LstmFwdArgs& a, hipStream_t st) {
-  const dim3 grid(a.B), blk((4 * a.H + 63) & ~63);
+static void fwd_q_dispatch(const LstmFwdArgs& a, hipStream_t st, const LstmFwdArgs* a1 = nullptr) {
+  const dim3 grid(a.B + (a1 ? a1->B : 0)), blk((4 * a.H + 63) & ~63);
+  const LstmFwdArgs& a2 = a1 ? *a1 : a;
+  const int smax = a1 && a1->S > a.S ? a1->S : a.S;
   const bool xm = XQ > 0 && use_xm();
   // W_hh register layout (SMI_LSTM_WI; A/B knob): 0 a contiguous quarter row
   // per lane, 1 k pairs interleaved over the quad, 2 float4 runs interleaved
   static const int wi = [] { const char* e = getenv("SMI_LSTM_WI"); return e && e[0] ? atoi(e) : 2; }();
-  const size_t lds = XQ > 0 ? lstm_fwd_v_lds(a.S, 1, 4 * XQ, blk.x) : 0;
+  const size_t lds = XQ > 0 ? lstm_fwd_v_lds(smax, 1, 4 * XQ, blk.x) : 0;
 #define SMI_FQ(KQ, W)                                                              \
   do {                                                                             \
     if (xm) {                                                                      \
       allow_lds(lstm_fwd_q_kernel<KQ, XQ, true, W>, lds);                          \
-      hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ, true, W>), grid, blk, lds, st, a);  \
+      hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ, true, W>), grid, blk, lds, st, a, a2);  \
     } else {                                                                       \
       allow_lds(lstm_fwd_q_kernel<KQ, XQ, false, W>, lds);                         \
-      hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ, false, W>), grid, blk, lds, st, a); \
+      hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ, false, W>), grid, blk, lds, st, a, a2); \
     }                                                                              \
   } while (0)
   if (a.H <= 64) {
@@ -1626,6 +1634,11 @@ static void fwd_q_dispatch(const LstmFwdArgs& a, hipStream_t st) {
     else SMI_FQ(32, 0);
   }
 #undef SMI_FQ
+}
+// two sequence sets in one launch, one segment per workgroup (fused x parts)
+void lstm_q_fwd_dual(const LstmFwdArgs& a, const LstmFwdArgs& a1, int kx, hipStream_t st) {
+  if (kx <= 48) fwd_q_dispatch<12>(a, st, &a1);
+  else fwd_q_dispatch<16>(a, st, &a1);
 }
 void lstm_v_fwd(const LstmFwdArgs& a, int R, int kx, hipStream_t st) {
   if (R == 1 && use_q()) {
@@ -1664,6 +1677,7 @@ extern "C" int smi_lstm_v_phase_ticks(unsigned long long* out /* [8] */) {
 #else
 void lstm_v_fwd(const LstmFwdArgs& a, int R, int kx, hipStream_t st);
 void lstm_v_bwd(const LstmBwdArgs& a, int R, hipStream_t st);
+void lstm_q_fwd_dual(const LstmFwdArgs& a, const LstmFwdArgs& a1, int kx, hipStream_t st);
 #endif  // SMI_LSTM_VALU_HALF
 
 #if SMI_LSTM_MFMA
@@ -1780,6 +1794,30 @@ bool lstm_use_q();
 int lstm_bwd_q_form(int B, int H) {
   if (lstm_valu_r(B, H) != 1 || !lstm_use_q()) return 0;
   return H <= 64 ? 16 : H <= 100 ? 25 : 32;
+}
+
+// two independent fused-input forwards (same H and input width, e.g. the GAE
+// critic pass and the reference policy's forward) in ONE launch at one segment
+// per workgroup (the K-split form): SMI_E_NOFIT when that form does not run
+// for B0 + B1 segments on this device or the widths differ
+bool lstm_fwd_x_dual_fits(int B0, int B1, int S, int H, int din) {
+  if (!use_r4() || !lstm_use_q() || din < 1 || din > 64 || H < 1 || H > 104 || B0 <= 0 || B1 <= 0)
+    return false;
+  if (lstm_valu_r(B0 + B1, H) != 1) return false;
+  return lstm_fwd_v_lds(S, 1, din <= 48 ? 48 : 64, (4 * H + 63) & ~63) <= kVxMax;
+}
+
+int launch_lstm_fwd_x_dual(const LstmFwdArgs& a0, const LstmFwdArgs& a1, hipStream_t st) {
+  const int H = a0.H, din = a0.din;
+  const int smax = a0.S > a1.S ? a0.S : a1.S;
+  if (a0.H != a1.H || a0.din != a1.din || !lstm_fwd_x_dual_fits(a0.B, a1.B, smax, H, din))
+    return SMI_E_NOFIT;
+  const int kx = din <= 48 ? 48 : 64;
+  const int kslot = ktime_begin(st);
+  lstm_q_fwd_dual(a0, a1, kx, st);
+  ktime_end(kslot, KT_LSTM_FWD,
+            8.0 * H * (double)(H + din) * ((double)a0.B * a0.S + (double)a1.B * a1.S), st);
+  return check_launch("lstm_fwd_q_kernel");
 }
 
 int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,

@@ -12,11 +12,14 @@
 #include "smi_device.hpp"
 #include "smi_internal.hpp"
 #include "pol_rows.hpp"
+#include "lstm_cell.hpp"
 
 namespace smi {
 
 int launch_lstm_bwd(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
                     int S, int B, int H, float* dgates, hipStream_t st, const int* skip);
+bool lstm_fwd_x_dual_fits(int B0, int B1, int S, int H, int din);
+int launch_lstm_fwd_x_dual(const LstmFwdArgs& a0, const LstmFwdArgs& a1, hipStream_t st);
 int launch_gae_windows(const float* values, float* values_masked, const float* rewards,
                        const float* dones, int64_t B, int T, int H, const float* gtab,
                        const float* ltab, float gamma, float gamma_H, float* adv, float* ret,
@@ -1231,6 +1234,22 @@ static bool fused_decide(const smi_ppo_rnn_args& a, int e) {
   return a.mode != 0 && a.B_global == a.B && e < a.epoch_policy && fault() == 0;
 }
 
+// the GAE critic pass (T + 1 steps) and PREP's reference-policy forward (E
+// steps) as ONE recurrence launch (two weight sets over two inputs, B
+// workgroups each): one LSTM layer, no pixel stem, the one-segment form for 2B
+// segments, PREP on the learner's stream (SMI_PREP_SIDE unset); GAE then also
+// forms PREP's z-filtered input and PREP runs the reference head only.
+// SMI_GAE_DUAL=0: two launches (A/B knob)
+static bool gae_prep_dual(const RnnDims& d) {
+  static const bool off = [] {
+    const char* e = getenv("SMI_GAE_DUAL");
+    const char* p = getenv("SMI_PREP_SIDE");
+    return (e && e[0] == '0') || (p && p[0] == '1');
+  }();
+  return !off && d.H > 0 && d.L == 1 && d.F == 0 &&
+         lstm_fwd_x_dual_fits(d.B, d.B, d.S1 > d.E ? d.S1 : d.E, d.H, d.Din);
+}
+
 // adapt mode with the LSTM stem, 8 actions and the fused head chain at a
 // rank's batch (< 16384 rows: one row tile per workgroup): the policy-gradient
 // row pass runs as that chain's prologue (head_kernels.hip, pol_rows.hpp;
@@ -1292,7 +1311,23 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       // (ppo.py:253-262 at epoch 0) is the same recurrence over the same
       // inputs from the same (h0, c0) with the same parameters, so
       // POLICY_FWD(0) reads these instead of recomputing them
-      if (d.H > 0) RC(lstm_forward(d, a.lstm, s.Xz, d.S1, a.h0, a.c0, s, true, st, nullptr, d.E));
+      if (gae_prep_dual(d)) {
+        // PREP's input (the reference z-filter over obs_iter), then both
+        // recurrences in one launch: the critic's over T + 1 steps keeping E
+        // steps' cells / gates, the reference policy's over E steps
+        launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
+                         a.rzf_count, a.zf_eps, s.Xr, d.ldx, st);
+        RC(check_launch("zf_tmajor_kernel"));
+        const LstmP lc = lstm_layer(d, a.lstm, 0), lr = lstm_layer(d, a.ref_lstm, 0);
+        LstmFwdArgs g0{nullptr, lc.Whh, lc.bhh, a.h0, a.c0, d.S1, d.B, d.H, hbuf_of(d, s, 0),
+                       cbuf_of(d, s, 0), gates_of(d, s, 0), nullptr, s.Xz, d.ldx, d.Din, lc.Wih,
+                       lc.bih, d.E};
+        LstmFwdArgs g1{nullptr, lr.Whh, lr.bhh, a.h0, a.c0, d.E, d.B, d.H, s.hbufR, nullptr, nullptr,
+                       nullptr, s.Xr, d.ldx, d.Din, lr.Wih, lr.bih, 0};
+        RC(launch_lstm_fwd_x_dual(g0, g1, st));
+      } else if (d.H > 0) {
+        RC(lstm_forward(d, a.lstm, s.Xz, d.S1, a.h0, a.c0, s, true, st, nullptr, d.E));
+      }
       RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
       hipLaunchKernelGGL(tmajor_to_bmajor_kernel, dim3(grid_of(d.NG)), dim3(kWG), 0, st, s.OUT,
                          d.S1, d.B, s.values, s.ci, s.cf);
@@ -1315,11 +1350,13 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       RnnScratch sp = s;
       sp.xproj = s.xprojR; sp.hbuf = s.hbufR; sp.HA1 = s.HA1R; sp.HA2 = s.HA2R; sp.A2 = s.A2R;
       const float* X = s.Xr;
-      launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
-                       a.rzf_count, a.zf_eps, s.Xr, d.ldx, st);
-      RC(check_launch("zf_tmajor_kernel"));
-      RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, sp, st, nullptr));
-      if (d.H > 0) RC(lstm_forward(d, a.ref_lstm, X, d.E, a.h0, a.c0, sp, false, st, nullptr));
+      if (!gae_prep_dual(d)) {      // (else the GAE phase ran this input and recurrence)
+        launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
+                         a.rzf_count, a.zf_eps, s.Xr, d.ldx, st);
+        RC(check_launch("zf_tmajor_kernel"));
+        RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, sp, st, nullptr));
+        if (d.H > 0) RC(lstm_forward(d, a.ref_lstm, X, d.E, a.h0, a.c0, sp, false, st, nullptr));
+      }
       const Head ref{a.ref_actor, d.LA, d.Hin, d.h1, d.h2, d.A, 1};
       return head_fwd(ref, head_in(d, sp, X), d.Hld, d.NE, sp.HA1, sp.HA2, s.refmu, st,
                       nullptr);
