@@ -459,8 +459,28 @@ struct PolStatsCols {
 
 // adapt-mode sums of one row into acc[PS_N] (policy_rows_stats_kernel's row
 // pass, FUSE off: the same ops in the same order); m = the row's learner means
-template <int AT>
-__device__ __forceinline__ void pol_stats_row_adapt(const PolRowArgs& a, const PolStatsCols<AT>& c,
+// the same per-column terms held in LDS (policy_rows_stats_lean_kernel: the
+// row pass's registers left to more waves in flight)
+struct PolStatsColsLds {
+  float isig[32], lsig[32], lkl[32], s02[32], iden2[32], lrsig[32];
+  int A;
+};
+__device__ inline void pol_stats_cols_fill(PolStatsColsLds& c, const float* lv, const float* ref_lv,
+                                           int A) {
+  for (int j = threadIdx.x; j < A; j += blockDim.x) {
+    const float sg = expf(lv[j]), rsig = expf(ref_lv[j]);
+    c.lsig[j] = logf(sg);
+    c.isig[j] = 1.f / sg;
+    c.lkl[j] = logf(sg / rsig);
+    c.s02[j] = rsig * rsig;
+    c.iden2[j] = 1.f / (2.f * (sg * sg));
+    c.lrsig[j] = logf(rsig);
+  }
+  if (threadIdx.x == 0) c.A = A;
+}
+
+template <int AT, class Cols>
+__device__ __forceinline__ void pol_stats_row_adapt(const PolRowArgs& a, const Cols& c,
                                                     const AdvNorm& nadv, const float* m,
                                                     const float* rm, const float* ac,
                                                     const float* bmu, const float* bsd, float adv,

@@ -837,13 +837,63 @@ __global__ void rnn_final_kernel(FinalArgs a) {
 // workgroups of the statistics pass: at most one resident round (its register
 // count leaves 3 one-wave blocks per SIMD, so the 4096-block cap of rnn_nblk
 // ran a second, partly filled round: 0.34 of HBM at 65536 segments)
+// adapt mode, 8 actions: the statistics pass with its per-column terms in
+// LDS and one row in flight per thread (168 -> 118 VGPRs: four waves per SIMD
+// instead of three, to cover the rows' cold HBM reads)
+template <int NT>
+__global__ void __launch_bounds__(NT)
+policy_rows_stats_lean_kernel(PolRowArgs a) {
+  if (a.skip && a.skip[0] != 0) return;
+  constexpr int AT = 8;
+  __shared__ PolStatsColsLds sc;
+  __shared__ double scr[NT / 64][PS_N];
+  pol_stats_cols_fill(sc, a.lv, a.ref_lv, AT);
+  __syncthreads();
+  double acc[PS_N];
+#pragma unroll
+  for (int k = 0; k < PS_N; ++k) acc[k] = 0.0;
+  const int64_t N = (int64_t)a.E * a.B;
+  const AdvNorm nadv(a);
+  for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
+    float m[AT], rm[AT], ac[AT], bmu[AT], bsd[AT];
+    ld_row<AT>(m, a.mu + n * AT, AT);
+    ld_row<AT>(rm, a.refmu + n * AT, AT);
+    ld_fields<AT>(ac, a.rowin, N, n, 0, AT);
+    ld_fields<AT>(bmu, a.rowin, N, n, AT, AT);
+    ld_fields<AT>(bsd, a.rowin, N, n, 2 * AT, AT);
+    const float adv = a.rowin[rin_idx(row_w(AT), n, 3 * AT)];
+    pol_stats_row_adapt<AT>(a, sc, nadv, m, rm, ac, bmu, bsd, adv, a.ret_tm[n], acc);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < PS_N; ++k) {
+    const double v = wave_sum_d(acc[k]);
+    if (lane == 0) scr[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < PS_N) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) t += scr[w][threadIdx.x];
+    a.part[(int64_t)blockIdx.x * PS_N + threadIdx.x] = t;
+  }
+}
+
+// off unless SMI_STATS_LEAN=1: at 65536 segments 0.381 vs 0.377 of HBM (the
+// pass reads its rows cold either way)
+static bool use_stats_lean() {
+  static const bool on = [] { const char* e = getenv("SMI_STATS_LEAN"); return e && e[0] == '1'; }();
+  return on;
+}
+
 template <bool FUSE>
 static int pol_stats_blocks(int A, int64_t rows) {
   static int cap[2][9] = {};
   const int ai = A >= 1 && A <= 8 ? A : 0;
   int& c = cap[FUSE][ai];
   if (!c) {
-    switch (ai) {
+    if (!FUSE && ai == 8 && use_stats_lean()) c = resident_grid(policy_rows_stats_lean_kernel<kRowNT>, kRowNT, 0);
+    else switch (ai) {
       case 1: c = resident_grid(policy_rows_stats_kernel<kRowNT, 1, FUSE>, kRowNT, 0); break;
       case 2: c = resident_grid(policy_rows_stats_kernel<kRowNT, 2, FUSE>, kRowNT, 0); break;
       case 3: c = resident_grid(policy_rows_stats_kernel<kRowNT, 3, FUSE>, kRowNT, 0); break;
@@ -862,6 +912,10 @@ static int pol_stats_blocks(int A, int64_t rows) {
 
 template <bool FUSE>
 static void launch_pol_stats(int A, int nb, const PolRowArgs& p, hipStream_t st) {
+  if (!FUSE && A == 8 && use_stats_lean()) {
+    hipLaunchKernelGGL((policy_rows_stats_lean_kernel<kRowNT>), dim3(nb), dim3(kRowNT), 0, st, p);
+    return;
+  }
   switch (A) {   // compile-time action widths 1..8 (registers); others generic
     case 1: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 1, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
     case 2: hipLaunchKernelGGL((policy_rows_stats_kernel<kRowNT, 2, FUSE>), dim3(nb), dim3(kRowNT), 0, st, p); break;
@@ -1227,12 +1281,6 @@ static bool fused_clip_norm(const smi_ppo_rnn_args& a, const RnnDims& d) {
   static const bool off = [] { const char* e = getenv("SMI_FUSED_NORM"); return e && e[0] == '0'; }();
   return !off && a.B_global == a.B && d.F == 0 && d.L <= 3 && fault() == 0;
 }
-// adapt mode, one rank, a policy epoch that trains: the decision of POLICY_FWD
-// (early stop, KL coefficient, statistics) is taken by the gradient pass of
-// POLICY_BWD itself (policy_rows_grad_kernel, dec_part)
-static bool fused_decide(const smi_ppo_rnn_args& a, int e) {
-  return a.mode != 0 && a.B_global == a.B && e < a.epoch_policy && fault() == 0;
-}
 
 // the GAE critic pass (T + 1 steps) and PREP's reference-policy forward (E
 // steps) as ONE recurrence launch (two weight sets over two inputs, B
@@ -1282,6 +1330,18 @@ static int pol_stats_nb(const smi_ppo_rnn_args& a, const RnnDims& d, const RnnSc
                         const Head& actor) {
   if (a.mode == 0) return pol_stats_blocks<true>(d.A, d.NE);
   return pol_head_stats(a, d, s, actor) ? head_bwd_blocks(d.NE) : pol_stats_blocks<false>(d.A, d.NE);
+}
+
+// adapt mode, one rank, a policy epoch that trains: the decision of POLICY_FWD
+// (early stop, KL coefficient, statistics) is taken by the gradient pass of
+// POLICY_BWD itself (policy_rows_grad_kernel, dec_part)
+static bool fused_decide(const smi_ppo_rnn_args& a, const RnnDims& d, const RnnScratch& s,
+                         const Head& actor, int e) {
+  // every gradient workgroup re-reduces the statistics pass's partials: only
+  // while they are few (at 65536 segments, ~3000 partials per workgroup over
+  // ~4000 workgroups took the gradient pass from 47 to 103 us)
+  return a.mode != 0 && a.B_global == a.B && e < a.epoch_policy && fault() == 0 &&
+         pol_stats_nb(a, d, s, actor) <= 512;
 }
 
 int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
@@ -1388,7 +1448,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
         ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
         RC(check_launch("policy_rows_stats_kernel"));
       }
-      if (fused_decide(a, e)) return SMI_OK;     // decided by POLICY_BWD's gradient pass
+      if (fused_decide(a, d, s, actor, e)) return SMI_OK;     // decided by POLICY_BWD's gradient pass
       if (a.B_global == a.B) {         // one rank: nothing to exchange before the decision
         DecideArgs da{a.pstat, e, a.epoch_policy, a.mode,
                       a.kl_target, a.kl_cutoff_coeff, NEg, a.hyper, a.actor + d.LA.flv, d.A,
@@ -1413,7 +1473,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       PolRowArgs p = pol_rows(a, d, s);
       // clip: the log_var partials came from POLICY_FWD's fused pass, over its grid
       const int nb = a.mode == 0 ? pol_stats_blocks<true>(d.A, d.NE) : rnn_nblk(d.NE, kRowNT);
-      if (fused_decide(a, e)) {
+      if (fused_decide(a, d, s, actor, e)) {
         p.dec_part = s.part;
         p.dec_nb = pol_stats_nb(a, d, s, actor);
         p.dec = DecideArgs{a.pstat, e, a.epoch_policy, a.mode,
