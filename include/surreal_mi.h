@@ -122,6 +122,23 @@ int smi_zfilter_update(const float* x, int64_t rows, int dim, int64_t row_stride
 int smi_zfilter_colstats(const float* x, int64_t rows, int dim, int64_t row_stride,
                          float* out_sum, float* out_sumsq, void* stream);
 
+/* The learner's time-major z-filtered input (ZFilter.forward, z_filter.py:59-79,
+ * as ppo_net.py:146-149 applies it to obs[:, t] before the LSTM, with the
+ * obs_next row appended as ppo.py:385-386 builds the critic's input):
+ *   out[t*B + b][c] = zf(obs[b][t][c])  for t < T,  zf(obs_next[b][c]) for t == T,
+ * for t < S (S <= T + 1), c < D, rows ldo floats apart; zf = the clamp of
+ * smi_zfilter_apply with the (running_sum, running_sumsq, count) stats, or the
+ * identity when use_zf == 0.  form: 0 = the learner's choice, 1 = row kernel,
+ * 2 = float2 tile transpose, 3 = float4 tile transpose, 4 / 5 = form 3
+ * writing whole rows (zeros in columns D..ldo-1; needs ldo == D rounded up to
+ * 4), pipelined over a resident grid / one tile per workgroup.  Forms 2 / 3-5
+ * need 8- / 16-byte aligned pointers (SMI_E_ARG otherwise); columns < D are
+ * bit-identical across forms, and forms 0-3 leave columns D..ldo-1 untouched. */
+int smi_zfilter_tmajor(const float* obs, const float* obs_next, int B, int T, int S, int D,
+                       int use_zf, const float* running_sum, const float* running_sumsq,
+                       const float* count, float eps, float* out, int ldo, int form,
+                       void* stream);
+
 /* Replaces RewardFilter.forward / RewardFilter.update
  * (surreal/model/reward_filter.py:18-56) as used by _preprocess_batch_ppo
  * (ppo.py:452-456): rewards *= reward_scale, then by `mode` bits

@@ -128,6 +128,8 @@ _SIGS = {
     'smi_zfilter_apply': (c_int, [P, P, c_i64, c_int, P, P, P, c_f32, P]),
     'smi_zfilter_update': (c_int, [P, c_i64, c_int, c_i64, P, P, P, P]),
     'smi_zfilter_colstats': (c_int, [P, c_i64, c_int, c_i64, P, P, P]),
+    'smi_zfilter_tmajor': (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, c_f32, P,
+                                   c_int, c_int, P]),
     'smi_reward_filter': (c_int, [P, c_i64, c_f32, c_int, P, P, P, c_f32, P]),
     'smi_reward_filter_partial': (c_int, [P, c_i64, c_f32, c_int, P, P, P, c_f32, P, P]),
     'smi_reward_filter_commit': (c_int, [P, P, P, P, P]),

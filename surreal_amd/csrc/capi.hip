@@ -101,6 +101,8 @@ int launch_mlp_forward(const float*, int, int, int, int, int, int, const float*,
                        int64_t, int, const float*, const float*, const float*, float, float*,
                        hipStream_t);
 int launch_moments(const float*, int64_t, const double*, int, double*, hipStream_t);
+int launch_zfilter_tmajor(const float*, const float*, int, int, int, int, int, const float*,
+                          const float*, const float*, float, float*, int, int, hipStream_t);
 int launch_adam_clip(float*, const float*, float*, float*, int64_t, int*, const float*, float,
                      float, float, float, float, float, const int*, float*, hipStream_t);
 int launch_mse_grad(const float*, int64_t, const float*, int64_t, float*, float*, hipStream_t);
@@ -260,6 +262,20 @@ int smi_zfilter_colstats(const float* x, int64_t rows, int dim, int64_t row_stri
           "zfilter_colstats: bad args");
   return launch_colstats(x, rows, dim, row_stride, 0, out_sum, out_sumsq, nullptr,
                          SMI_STREAM(stream));
+}
+
+
+int smi_zfilter_tmajor(const float* obs, const float* obs_next, int B, int T, int S, int D,
+                       int use_zf, const float* rs, const float* rsq, const float* cnt, float eps,
+                       float* out, int ldo, int form, void* stream) {
+  REQUIRE(obs && out && B >= 0 && T >= 1 && S >= 0 && S <= T + 1 && D >= 1 && ldo >= D &&
+              form >= 0 && form <= 5,
+          "zfilter_tmajor: bad args");
+  REQUIRE(S <= T || obs_next, "zfilter_tmajor: obs_next required when S == T + 1");
+  REQUIRE(!use_zf || (rs && rsq && cnt), "zfilter_tmajor: filter buffers required");
+  if (B == 0 || S == 0) return SMI_OK;
+  return launch_zfilter_tmajor(obs, obs_next ? obs_next : obs, B, T, S, D, use_zf, rs, rsq, cnt,
+                               eps, out, ldo, form, SMI_STREAM(stream));
 }
 
 int smi_reward_filter(float* rewards, int64_t n, float reward_scale, int mode, float* rs,

@@ -316,6 +316,243 @@ zf_tile_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next
   }
 }
 
+// zf_tile_kernel with 16-byte accesses on both sides (16-byte aligned obs,
+// obs_next and out, ldo % 4 == 0): the kZfSeg segments' obs rows are ONE
+// contiguous run, copied to LDS as float4 (the float2 copy above issued half
+// the bytes per load instruction); the output rows of a step are written as
+// float4 column chunks (the last one 1-3 wide when D % 4 != 0), every chunk of
+// every (step, segment) row spread over the workgroup's threads.  Same
+// arithmetic per element as the kernels above.
+__global__ void __launch_bounds__(kWG)
+zf_tile4_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next, int B, int T,
+                int S, int D, int use_zf, const float* zs, const float* zq, const float* zc,
+                float eps, float* __restrict__ out, int ldo, int pad) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* zm = sm;                                  // [round4(D)]
+  float* zd = sm + round4(D);
+  float* tile = sm + 2 * round4(D);                // [kZfSeg][T][D], obs's own layout
+  float* nxt = tile + round4(kZfSeg * T * D);      // [kZfSeg][D], the obs_next rows
+  if (use_zf) zfilter_colstats(zs, zq, zc, eps, D, zm, zd);
+  const int b0 = blockIdx.x * kZfSeg;
+  const int nseg = min(kZfSeg, B - b0);
+  {
+    const int tot = nseg * T * D;                   // floats of the run (all T rows)
+    const int tot4 = tot >> 2;
+    const float4* src = reinterpret_cast<const float4*>(obs + (int64_t)b0 * T * D);
+    float4* dst = reinterpret_cast<float4*>(tile);
+    for (int base = 0; base < tot4; base += 8 * kWG) {
+      float4 r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = src[min(base + k * kWG + (int)threadIdx.x, tot4 - 1)];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = base + k * kWG + threadIdx.x;
+        if (e < tot4) dst[e] = r[k];
+      }
+    }
+    for (int e = (tot4 << 2) + threadIdx.x; e < tot; e += kWG) tile[e] = obs[(int64_t)b0 * T * D + e];
+    if (S > T) {
+      const int tn = nseg * D, tn4 = tn >> 2;
+      const float* nsrc = obs_next + (int64_t)b0 * D;
+      for (int e = threadIdx.x; e < tn4; e += kWG)
+        reinterpret_cast<float4*>(nxt)[e] = reinterpret_cast<const float4*>(nsrc)[e];
+      for (int e = (tn4 << 2) + threadIdx.x; e < tn; e += kWG) nxt[e] = nsrc[e];
+    }
+  }
+  __syncthreads();
+  if (pad) {
+    // ldo == round4(D) and columns D..ldo-1 are padding nobody reads: rows are
+    // written whole, as float4 chunks, zeros in the padding, so a step's
+    // kZfSeg output rows are one run of whole 128-byte lines (a row with an
+    // 8-byte hole made every line a partial write)
+    const int cpr = ldo >> 2, per_t = nseg * cpr;
+    const int groups = kWG / per_t;
+    const int g = threadIdx.x / per_t, r = threadIdx.x - g * per_t;
+    if (g >= groups) return;
+    const int bl = r / cpr, c = 4 * (r - bl * cpr);
+    float zmv[4], zdv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      zmv[j] = use_zf && c + j < D ? zm[c + j] : 0.f;
+      zdv[j] = use_zf && c + j < D ? zd[c + j] : 1.f;
+    }
+    const bool even = (D & 1) == 0;
+    for (int t = g; t < S; t += groups) {
+      const float* sp = t < T ? tile + ((int64_t)bl * T + t) * D + c : nxt + bl * D + c;
+      float v[4];
+      if (even) {
+        const float2 lo = *reinterpret_cast<const float2*>(sp);
+        const float2 hi = c + 2 < D ? *reinterpret_cast<const float2*>(sp + 2) : float2{0.f, 0.f};
+        v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = c + j < D ? sp[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (use_zf && c + j < D) v[j] = fminf(fmaxf((v[j] - zmv[j]) / zdv[j], -5.f), 5.f);
+      *reinterpret_cast<float4*>(out + ((int64_t)t * B + b0 + bl) * ldo + c) =
+          float4{v[0], v[1], v[2], v[3]};
+    }
+    return;
+  }
+  if (D % 2 == 0 && D / 2 * kZfSeg <= kWG) {
+    // even widths: zf_tile_kernel's phase 2 (thread = segment x column pair,
+    // conflict-free 8-byte LDS reads, one float2 store per step)
+    const int D2 = D >> 1;
+    const int bl = threadIdx.x / D2, c2 = threadIdx.x - bl * D2;
+    if (bl >= nseg) return;
+    float2 m = {0.f, 0.f}, dd = {1.f, 1.f};
+    if (use_zf) { m = float2{zm[2 * c2], zm[2 * c2 + 1]}; dd = float2{zd[2 * c2], zd[2 * c2 + 1]}; }
+    const float2* tp = reinterpret_cast<const float2*>(tile + (int64_t)bl * T * D) + c2;
+    float* op = out + (int64_t)(b0 + bl) * ldo + 2 * c2;
+    for (int t = 0; t < S; ++t) {
+      float2 v = t < T ? tp[t * D2] : reinterpret_cast<const float2*>(nxt + bl * D)[c2];
+      if (use_zf) {
+        v.x = fminf(fmaxf((v.x - m.x) / dd.x, -5.f), 5.f);
+        v.y = fminf(fmaxf((v.y - m.y) / dd.y, -5.f), 5.f);
+      }
+      *reinterpret_cast<float2*>(op + (int64_t)t * B * ldo) = v;
+    }
+    return;
+  }
+  const int cpr = (D + 3) >> 2;                    // column chunks per row
+  const int per_t = nseg * cpr;
+  const int tot = S * per_t;
+  for (int e = threadIdx.x; e < tot; e += kWG) {
+    const int t = e / per_t, r = e - t * per_t;
+    const int bl = r / cpr, k = r - bl * cpr;
+    const int c = 4 * k, w = min(4, D - c);
+    const float* sp = t < T ? tile + ((int64_t)bl * T + t) * D + c : nxt + bl * D + c;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = j < w ? sp[j] : 0.f;
+      if (use_zf && j < w) v[j] = fminf(fmaxf((v[j] - zm[c + j]) / zd[c + j], -5.f), 5.f);
+    }
+    float* op = out + ((int64_t)t * B + b0 + bl) * ldo + c;
+    if (w == 4) {
+      *reinterpret_cast<float4*>(op) = float4{v[0], v[1], v[2], v[3]};
+    } else if (w == 2) {
+      *reinterpret_cast<float2*>(op) = float2{v[0], v[1]};
+    } else {
+      for (int j = 0; j < w; ++j) op[j] = v[j];
+    }
+  }
+}
+
+// zf_tile4_kernel's padded-row form as a resident grid looping over tiles,
+// software-pipelined: tile i+1's obs run is loaded into registers (kZfNR
+// float4 per thread) while tile i's rows are written from LDS, then stored to
+// the other LDS buffer, so every workgroup keeps reads and writes in flight at
+// once (the one-shot tile kernel alternated a read phase and a write phase)
+constexpr int kZfNR = 10;
+__global__ void __launch_bounds__(kWG)
+zf_pipe_kernel(const float* __restrict__ obs, const float* __restrict__ obs_next, int B, int T,
+               int S, int D, int use_zf, const float* zs, const float* zq, const float* zc,
+               float eps, float* __restrict__ out, int ldo) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* zm = sm;
+  float* zd = sm + round4(D);
+  const int TD = T * D;
+  const int tile_f = round4(kZfSeg * TD), buf_f = tile_f + round4(kZfSeg * D);
+  float* buf0 = sm + 2 * round4(D);
+  if (use_zf) zfilter_colstats(zs, zq, zc, eps, D, zm, zd);
+  const int ntile = (B + kZfSeg - 1) / kZfSeg;
+  const bool has_next = S > T;
+  float4 r0, r1, r2, r3, r4, r5, r6, r7, r8, r9;   // kZfNR named registers (an
+  float4 rn = {0.f, 0.f, 0.f, 0.f};                // array here went to scratch)
+  static_assert(kZfNR == 10, "zf_pipe_kernel: ten staging registers");
+// registers <- tile TL's obs run (and its obs_next rows)
+#define ZF_LOAD(TL)                                                                          \
+  do {                                                                                       \
+    const int lb0 = (TL) * kZfSeg, lns = min(kZfSeg, B - lb0);                               \
+    const int lt4 = (lns * TD) >> 2;                                                         \
+    const float4* src = reinterpret_cast<const float4*>(obs + (int64_t)lb0 * TD);            \
+    if (lt4 > 0) {                                                                           \
+      const int tx = threadIdx.x, m = lt4 - 1;                                               \
+      r0 = src[min(tx, m)]; r1 = src[min(tx + kWG, m)]; r2 = src[min(tx + 2 * kWG, m)];      \
+      r3 = src[min(tx + 3 * kWG, m)]; r4 = src[min(tx + 4 * kWG, m)];                        \
+      r5 = src[min(tx + 5 * kWG, m)]; r6 = src[min(tx + 6 * kWG, m)];                        \
+      r7 = src[min(tx + 7 * kWG, m)]; r8 = src[min(tx + 8 * kWG, m)];                        \
+      r9 = src[min(tx + 9 * kWG, m)];                                                        \
+    }                                                                                        \
+    const int ln4 = (lns * D) >> 2;                                                          \
+    if (has_next && ln4 > 0)                                                                 \
+      rn = reinterpret_cast<const float4*>(obs_next + (int64_t)lb0 * D)[min((int)threadIdx.x, ln4 - 1)]; \
+  } while (0)
+// registers (+ the few floats past the last whole float4) -> LDS buffer BUF
+#define ZF_STASH(TL, BUF)                                                                    \
+  do {                                                                                       \
+    const int lb0 = (TL) * kZfSeg, lns = min(kZfSeg, B - lb0);                               \
+    const int ltot = lns * TD, lt4 = ltot >> 2;                                              \
+    float4* dst = reinterpret_cast<float4*>(BUF);                                            \
+    const int tx = threadIdx.x;                                                              \
+    if (tx < lt4) dst[tx] = r0;                                                              \
+    if (tx + kWG < lt4) dst[tx + kWG] = r1;                                                  \
+    if (tx + 2 * kWG < lt4) dst[tx + 2 * kWG] = r2;                                          \
+    if (tx + 3 * kWG < lt4) dst[tx + 3 * kWG] = r3;                                          \
+    if (tx + 4 * kWG < lt4) dst[tx + 4 * kWG] = r4;                                          \
+    if (tx + 5 * kWG < lt4) dst[tx + 5 * kWG] = r5;                                          \
+    if (tx + 6 * kWG < lt4) dst[tx + 6 * kWG] = r6;                                          \
+    if (tx + 7 * kWG < lt4) dst[tx + 7 * kWG] = r7;                                          \
+    if (tx + 8 * kWG < lt4) dst[tx + 8 * kWG] = r8;                                          \
+    if (tx + 9 * kWG < lt4) dst[tx + 9 * kWG] = r9;                                          \
+    for (int e = (lt4 << 2) + tx; e < ltot; e += kWG) (BUF)[e] = obs[(int64_t)lb0 * TD + e]; \
+    if (has_next) {                                                                          \
+      float* nb = (BUF) + tile_f;                                                            \
+      const int tn = lns * D, tn4 = tn >> 2;                                                 \
+      if (tx < tn4) reinterpret_cast<float4*>(nb)[tx] = rn;                                  \
+      for (int e = (tn4 << 2) + tx; e < tn; e += kWG) nb[e] = obs_next[(int64_t)lb0 * D + e]; \
+    }                                                                                        \
+  } while (0)
+  const int cpr = ldo >> 2, per_t = kZfSeg * cpr;
+  const int groups = kWG / per_t;
+  const int g = threadIdx.x / per_t, rr = threadIdx.x - g * per_t;
+  const int bl = rr / cpr, c = 4 * (rr - bl * cpr);
+  float zmv[4], zdv[4];
+  __syncthreads();                                 // zm / zd
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    zmv[j] = use_zf && c + j < D ? zm[c + j] : 0.f;
+    zdv[j] = use_zf && c + j < D ? zd[c + j] : 1.f;
+  }
+  const bool even = (D & 1) == 0;
+  int tl = blockIdx.x;
+  if (tl < ntile) { ZF_LOAD(tl); ZF_STASH(tl, buf0); }
+  int cur = 0;
+  for (; tl < ntile; tl += gridDim.x) {
+    __syncthreads();                               // buffer `cur` complete
+    const int nx = tl + gridDim.x;
+    if (nx < ntile) ZF_LOAD(nx);                   // in flight behind the writes below
+    float* buf = buf0 + cur * buf_f;
+    const int b0 = tl * kZfSeg, nseg = min(kZfSeg, B - b0);
+    if (g < groups && bl < nseg) {
+      for (int t = g; t < S; t += groups) {
+        const float* sp = t < T ? buf + (bl * T + t) * D + c : buf + tile_f + bl * D + c;
+        float v[4];
+        if (even) {
+          const float2 lo = *reinterpret_cast<const float2*>(sp);
+          const float2 hi = c + 2 < D ? *reinterpret_cast<const float2*>(sp + 2) : float2{0.f, 0.f};
+          v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = c + j < D ? sp[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (use_zf && c + j < D) v[j] = fminf(fmaxf((v[j] - zmv[j]) / zdv[j], -5.f), 5.f);
+        *reinterpret_cast<float4*>(out + ((int64_t)t * B + b0 + bl) * ldo + c) =
+            float4{v[0], v[1], v[2], v[3]};
+      }
+    }
+    cur ^= 1;
+    if (nx < ntile) ZF_STASH(nx, buf0 + cur * buf_f);
+  }
+#undef ZF_LOAD
+#undef ZF_STASH
+}
+
 // values[b][t] = vt[t*B + b]
 __global__ void __launch_bounds__(kWG)
 tmajor_to_bmajor_kernel(const float* __restrict__ vt, int S, int B, float* __restrict__ v,
@@ -946,27 +1183,84 @@ static int zf_grid(int64_t rows) {
 }
 
 // the time-major z-filtered copy of the batch's low-dim observations: the tile
-// transpose where its shape conditions hold, else the row-per-wave kernel
-static void launch_zf_tmajor(const float* obs, const float* obs_next, int B, int T, int S, int D,
-                             int use_zf, const float* zs, const float* zq, const float* zc,
-                             float eps, float* out, int ldo, hipStream_t st) {
-  if (D <= 0 || S <= 0) return;
+// transpose where its shape conditions hold, else the row-per-wave kernel.
+// form: 0 = that choice, 1 = the row kernel, 2 = the float2 tile, 3 = the
+// float4 tile, 4 = the pipelined float4 tile writing whole padded rows (zeros
+// in columns D..ldo-1; the learner's choice only with pad_ok: nothing else
+// writes there), 5 = the one-shot float4 tile writing whole padded rows
+// (smi_zfilter_tmajor's test / bench selection; a form whose shape conditions
+// fail is SMI_E_ARG)
+static int launch_zf_tmajor(const float* obs, const float* obs_next, int B, int T, int S, int D,
+                            int use_zf, const float* zs, const float* zq, const float* zc,
+                            float eps, float* out, int ldo, hipStream_t st, int form = 0,
+                            bool pad_ok = false) {
+  if (D <= 0 || S <= 0) return SMI_OK;
   auto a8 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; };
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const size_t tl = ((size_t)2 * round4(D) + (size_t)kZfSeg * S * D) * 4;
+  const size_t tl4 = ((size_t)2 * round4(D) + round4(kZfSeg * T * D) + (size_t)kZfSeg * D) * 4;
+  const bool tile_ok = D % 2 == 0 && D <= 128 && ldo % 2 == 0 && a8(obs) && a8(obs_next) &&
+                       a8(out) && D / 2 * kZfSeg <= kWG && tl <= 64 * 1024;
+  const bool tile4_ok = ldo % 4 == 0 && a16(obs) && a16(obs_next) && a16(out) && tl4 <= 64 * 1024;
+  const bool pad4_ok = tile4_ok && ldo == round4(D) && kZfSeg * (ldo / 4) <= kWG;
+  const size_t tlp = ((size_t)2 * round4(D) +
+                      2 * ((size_t)round4(kZfSeg * T * D) + round4(kZfSeg * D))) * 4;
+  const bool pipe_ok = pad4_ok && kZfSeg * T * D <= 4 * kZfNR * kWG && kZfSeg * D <= 4 * kWG &&
+                       tlp <= 150 * 1024;
+  // SMI_ZF_PIPE=0: the one-shot padded-row tile (A/B)
+  static const bool pipe_on = [] { const char* e = getenv("SMI_ZF_PIPE"); return !(e && e[0] == '0'); }();
   static const bool tile_on = [] { const char* e = getenv("SMI_ZF_TILE"); return !(e && e[0] == '0'); }();
   static const bool force = [] { const char* e = getenv("SMI_ZF_TILE_FORCE"); return e && e[0] == '1'; }();
-  // (from 4096 segments: at C3's 1024 the 128 tile workgroups took 14.5 us
-  // against 9.7 for the row kernel; at 65536, 146 against 169 us)
-  if (tile_on && (B >= 4096 || force) && D % 2 == 0 && D <= 128 && ldo % 2 == 0 && a8(obs) && a8(obs_next) && a8(out) &&
-      D / 2 * kZfSeg <= kWG && tl <= 64 * 1024) {
-    allow_lds(zf_tile_kernel, tl);
-    hipLaunchKernelGGL(zf_tile_kernel, dim3((B + kZfSeg - 1) / kZfSeg), dim3(kWG), tl, st, obs,
-                       obs_next, B, T, S, D, use_zf, zs, zq, zc, eps, out, ldo);
-    return;
+  // SMI_ZF_TILE4=0: the float2 tile (A/B)
+  static const bool t4_on = [] { const char* e = getenv("SMI_ZF_TILE4"); return !(e && e[0] == '0'); }();
+  if (form == 0) {
+    // (from 4096 segments: at C3's 1024 the 128 tile workgroups took 14.5 us
+    // against 9.7 for the row kernel; at 65536, 146 against 169 us)
+    form = 1;
+    if (tile_on && (B >= 4096 || force)) {
+      if (t4_on && pad_ok && pipe_on && pipe_ok) form = 4;
+      else if (t4_on && pad_ok && pad4_ok) form = 5;
+      else if (tile_ok) form = 2;
+      else if (tile4_ok) form = 3;
+    }
   }
+  const int nb = (B + kZfSeg - 1) / kZfSeg;
+  if (form == 4) {
+    if (!pipe_ok) return set_error(SMI_E_ARG, "zf_tmajor: pipelined padded rows do not fit");
+    allow_lds(zf_pipe_kernel, tlp);
+    static int cap = 0;
+    if (!cap) cap = std::max(1, resident_grid(zf_pipe_kernel, kWG, tlp));
+    hipLaunchKernelGGL(zf_pipe_kernel, dim3(std::min(nb, cap)), dim3(kWG), tlp, st, obs, obs_next,
+                       B, T, S, D, use_zf, zs, zq, zc, eps, out, ldo);
+    return check_launch("zf_pipe_kernel");
+  }
+  if (form == 3 || form == 5) {
+    if (!tile4_ok) return set_error(SMI_E_ARG, "zf_tmajor: float4 tile needs 16-byte alignment");
+    if (form == 5 && !pad4_ok) return set_error(SMI_E_ARG, "zf_tmajor: padded rows need ldo == round4(D)");
+    allow_lds(zf_tile4_kernel, tl4);
+    hipLaunchKernelGGL(zf_tile4_kernel, dim3(nb), dim3(kWG), tl4, st, obs, obs_next, B, T, S, D,
+                       use_zf, zs, zq, zc, eps, out, ldo, form == 5 ? 1 : 0);
+    return check_launch("zf_tile4_kernel");
+  }
+  if (form == 2) {
+    if (!tile_ok) return set_error(SMI_E_ARG, "zf_tmajor: float2 tile needs even D, 8-byte alignment");
+    allow_lds(zf_tile_kernel, tl);
+    hipLaunchKernelGGL(zf_tile_kernel, dim3(nb), dim3(kWG), tl, st, obs, obs_next, B, T, S, D,
+                       use_zf, zs, zq, zc, eps, out, ldo);
+    return check_launch("zf_tile_kernel");
+  }
+  if (D > 128) return set_error(SMI_E_ARG, "zf_tmajor: D > 128");
   const size_t zlds = (size_t)2 * round4(D) * 4;
   hipLaunchKernelGGL(zf_tmajor_kernel, dim3(zf_grid((int64_t)S * B)), dim3(kWG), zlds, st, obs,
                      obs_next, B, T, S, D, use_zf, zs, zq, zc, eps, out, ldo);
+  return check_launch("zf_tmajor_kernel");
+}
+
+int launch_zfilter_tmajor(const float* obs, const float* obs_next, int B, int T, int S, int D,
+                          int use_zf, const float* zs, const float* zq, const float* zc, float eps,
+                          float* out, int ldo, int form, hipStream_t st) {
+  return launch_zf_tmajor(obs, obs_next, B, T, S, D, use_zf, zs, zq, zc, eps, out, ldo, st, form,
+                          form >= 4);
 }
 
 struct Head {   // one MLP head over rows of an activation matrix
@@ -1361,10 +1655,11 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
   switch (phase) {
     case SMI_RNN_PH_GAE: {
       int kt = ktime_begin(st);
-      launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum, a.zf_sumsq,
-                       a.zf_count, a.zf_eps, s.Xz, d.ldx, st);
+      const int zrc = launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.S1, d.D, a.use_zf, a.zf_sum,
+                                       a.zf_sumsq, a.zf_count, a.zf_eps, s.Xz, d.ldx, st, 0,
+                                       d.F == 0);
       ktime_end(kt, KT_ZF_TMAJOR, 8.0 * (double)d.NG * d.D, st);      // read x, write z(x)
-      RC(check_launch("zf_tmajor_kernel"));
+      RC(zrc);
       RC(cnn_features(a, d, cnn, d.S1, s.Xz, nullptr, s, st, nullptr));
       // the critic's LSTM pass over T + 1 steps (ppo.py:385) with the cell
       // states and gates of its first E steps kept: the first policy forward
@@ -1375,9 +1670,9 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
         // PREP's input (the reference z-filter over obs_iter), then both
         // recurrences in one launch: the critic's over T + 1 steps keeping E
         // steps' cells / gates, the reference policy's over E steps
-        launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
-                         a.rzf_count, a.zf_eps, s.Xr, d.ldx, st);
-        RC(check_launch("zf_tmajor_kernel"));
+        RC(launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum,
+                            a.rzf_sumsq, a.rzf_count, a.zf_eps, s.Xr, d.ldx, st, 0,
+                            d.F == 0));
         const LstmP lc = lstm_layer(d, a.lstm, 0), lr = lstm_layer(d, a.ref_lstm, 0);
         LstmFwdArgs g0{nullptr, lc.Whh, lc.bhh, a.h0, a.c0, d.S1, d.B, d.H, hbuf_of(d, s, 0),
                        cbuf_of(d, s, 0), gates_of(d, s, 0), nullptr, s.Xz, d.ldx, d.Din, lc.Wih,
@@ -1411,9 +1706,9 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       sp.xproj = s.xprojR; sp.hbuf = s.hbufR; sp.HA1 = s.HA1R; sp.HA2 = s.HA2R; sp.A2 = s.A2R;
       const float* X = s.Xr;
       if (!gae_prep_dual(d)) {      // (else the GAE phase ran this input and recurrence)
-        launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum, a.rzf_sumsq,
-                         a.rzf_count, a.zf_eps, s.Xr, d.ldx, st);
-        RC(check_launch("zf_tmajor_kernel"));
+        RC(launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum,
+                            a.rzf_sumsq, a.rzf_count, a.zf_eps, s.Xr, d.ldx, st, 0,
+                            d.F == 0));
         RC(cnn_features(a, d, a.ref_lstm + d.nL, d.E, s.Xr, nullptr, sp, st, nullptr));
         if (d.H > 0) RC(lstm_forward(d, a.ref_lstm, X, d.E, a.h0, a.c0, sp, false, st, nullptr));
       }

@@ -112,6 +112,55 @@ def test_zfilter_update_large_partials():
     assert float(zf.count.item()) == pytest.approx(rows + 1e-5)
 
 
+@pytest.mark.parametrize('B,T,S,D,ldo', [
+    (4099, 25, 26, 42, 44),     # C3 widths, ragged last tile, the obs_next row
+    (64, 25, 25, 42, 44),       # no obs_next row
+    (19, 5, 6, 17, 20),         # odd D: the float2 tile does not apply
+    (33, 8, 9, 64, 64),
+    (1, 1, 2, 3, 4),
+])
+def test_zfilter_tmajor_forms(B, T, S, D, ldo):
+    # the learner's time-major z-filtered input (z_filter.py:59-79 per row,
+    # obs_next appended as ppo.py:385-386): every kernel form against the
+    # oracle's ZFilter, and bit-identical to each other
+    g = torch.Generator().manual_seed(B + D)
+    obs = torch.randn(B, T, D, generator=g) * 3 + 0.5
+    nxt = torch.randn(B, 1, D, generator=g) * 3 + 0.5
+    zf = R.ZFilterRef(D)
+    zf.z_update(torch.randn(200, D, generator=g) * 2 + 0.25)
+    full = torch.cat([obs, nxt], 1)[:, :S]                       # [B][S][D]
+    ref = zf(full).transpose(0, 1).reshape(S * B, D)
+    od, nd = obs.to(DEV), nxt.to(DEV)
+    zs, zq, zc = (zf.running_sum.to(DEV), zf.running_sumsq.to(DEV), zf.count.to(DEV))
+    outs = {}
+    for form in (0, 1, 2, 3, 4, 5):
+        if (form == 2 and D % 2) or (form >= 4 and ldo != (D + 3) // 4 * 4):
+            continue
+        out = torch.full((S * B, ldo), -7.0, device=DEV)
+        L.call('smi_zfilter_tmajor', L.ptr(od), L.ptr(nd), B, T, S, D, 1, L.ptr(zs), L.ptr(zq),
+               L.ptr(zc), 1e-5, L.ptr(out), ldo, form, st())
+        o = out.cpu()
+        # the row padding: untouched, or zeros with the whole-row form
+        assert torch.all(o[:, D:] == (0.0 if form >= 4 else -7.0)), form
+        assert max_rel_err(o[:, :D], ref) < RTOL, form
+        outs[form] = o
+    for form, o in outs.items():
+        assert torch.equal(o[:, :D], outs[1][:, :D]), form
+    # use_zf == 0: a plain time-major copy
+    out = torch.empty(S * B, ldo, device=DEV)
+    L.call('smi_zfilter_tmajor', L.ptr(od), L.ptr(nd), B, T, S, D, 0, None, None, None, 1e-5,
+           L.ptr(out), ldo, 3, st())
+    assert torch.equal(out.cpu()[:, :D], full.transpose(0, 1).reshape(S * B, D))
+
+
+def test_zfilter_tmajor_rejects_misaligned_tile():
+    od = torch.zeros(8 * 5 * 6 + 1, device=DEV)
+    out = torch.zeros(8 * 6 * 8 + 1, device=DEV)
+    with pytest.raises(RuntimeError):
+        L.call('smi_zfilter_tmajor', L.ptr(od[1:]), L.ptr(od[1:]), 8, 5, 6, 6, 0, None, None, None,
+               1e-5, L.ptr(out[1:]), 8, 3, st())
+
+
 def test_diag_gauss_vs_oracle_and_kats():
     A, N = 6, 257
     g = torch.Generator().manual_seed(2)
