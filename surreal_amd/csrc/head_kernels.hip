@@ -462,7 +462,7 @@ head_fwd_kernel(HeadFwdArgs a) {
     // layer 3
     constexpr int R_ = HC_R * RT, PA = 8;
     __shared__ float smu[PS ? R_ * PA : 1];
-    float prm[PS ? PA : 1], pac[PS ? PA : 1], pbm[PS ? PA : 1], pbs[PS ? PA : 1], padv = 0.f, pret = 0.f;
+    float prm[PS ? PA : 1], pac[PS ? PA : 1], pbl = 1.f, prbd = 0.f, padv = 0.f, pret = 0.f;
     const int64_t prow = r0 + threadIdx.x;
     const bool pown = PS && (int)threadIdx.x < R_ && prow < a.rows;
     if constexpr (PS) {
@@ -470,9 +470,9 @@ head_fwd_kernel(HeadFwdArgs a) {
         const int64_t N = (int64_t)a.ps.E * a.ps.B;
         ld_row<PA>(prm, a.ps.refmu + prow * PA, PA);
         ld_fields<PA>(pac, a.ps.rowin, N, prow, 0, PA);
-        ld_fields<PA>(pbm, a.ps.rowin, N, prow, PA, PA);
-        ld_fields<PA>(pbs, a.ps.rowin, N, prow, 2 * PA, PA);
-        padv = a.ps.rowin[rin_idx(row_w(PA), prow, 3 * PA)];
+        padv = a.ps.rowin[rin_idx(row_w(PA), prow, rin_adv(PA))];
+        pbl = a.ps.rowin[rin_idx(row_w(PA), prow, rin_bl(PA))];
+        prbd = a.ps.rowin[rin_idx(row_w(PA), prow, rin_rbd(PA))];
         pret = a.ps.ret_tm[prow];
       }
     }
@@ -535,7 +535,7 @@ head_fwd_kernel(HeadFwdArgs a) {
         }
         const PolStatsCols<PA> cols(sg, lsg, rsg, PA);
         const AdvNorm nadv(a.ps);
-        pol_stats_row_adapt<PA>(a.ps, cols, nadv, mu, prm, pac, pbm, pbs, padv, pret, acc);
+        pol_stats_row_adapt<PA>(a.ps, cols, nadv, mu, prm, pac, pbl, prbd, padv, pret, acc);
       }
       if (wave == 0) {
 #pragma unroll

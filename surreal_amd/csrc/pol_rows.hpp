@@ -24,8 +24,15 @@ enum {
 enum { CI_STOP = 0, CI_RUNS, CI_NG, CI_NP, CI_COUNT = 8 };
 enum { CF_KLCOEF = 0, CF_SURRW, CF_COUNT = 8 };
 
-// fields of a packed row: A actions, 2A behaviour parameters, the advantage
-__host__ __device__ inline int row_w(int A) { return 3 * A + 1; }
+// fields of a packed row: A actions, 2A behaviour parameters, the advantage,
+// then the row's behaviour-policy terms, fixed for the whole learn() (the
+// behaviour parameters and the reference policy do not change across epochs):
+// the clamped behaviour likelihood and the row's KL(ref || behaviour) term,
+// computed once by row_pack_kernel instead of in every epoch's row passes
+__host__ __device__ inline int row_w(int A) { return 3 * A + 3; }
+__host__ __device__ inline int rin_adv(int A) { return 3 * A; }
+__host__ __device__ inline int rin_bl(int A) { return 3 * A + 1; }
+__host__ __device__ inline int rin_rbd(int A) { return 3 * A + 2; }
 // rowin is blocked by 64 rows: block b holds field f of rows 64b .. 64b + 63
 // as 64 consecutive floats, the block's fields back to back, so one wave's
 // row loads read one contiguous ~5 KB run (a field-major [W][NE] layout made
@@ -50,7 +57,7 @@ struct PolRowArgs {
   const float* behave;    // [B][T][2A]
   const float* adv;       // [B][E] raw
   const float* ret;       // [B][E]
-  const float* rowin;     // {actions | behave | raw adv} blocked by 64 rows (rin_idx)
+  const float* rowin;     // {actions | behave | raw adv | bl | rbd} blocked by 64 rows (rin_idx)
   const float* ret_tm;    // [NE] time-major returns
   const double* moments;  // [3] global (sum, sumsq, n) of adv, or null (no norm)
   int norm_adv;
@@ -208,6 +215,25 @@ __device__ __forceinline__ void ld_fields(float* dst, const float* __restrict__ 
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) dst[j] = rowin[rin_idx(W, n, f0 + j)];
 }
 
+// a row's behaviour-policy terms (row_pack_kernel, once per learn): the
+// clamped behaviour likelihood max(exp(loglik(ac; bmu, bsd)), 1e-5) and the
+// KL(ref || behaviour) row term (ppo.py:203-224's prob_behave, 569's
+// ref_behave_diff), the ops of the row passes that computed them per epoch
+template <int AT>
+__device__ __forceinline__ void behave_terms(const float* ac, const float* bmu, const float* bsd,
+                                             const float* rm, const float* lrsig, const float* s02,
+                                             int A, float c_ll, float& bl, float& rbd) {
+  constexpr int AM = AT > 0 ? AT : 32;
+  float blsd[AM], ibsd[AM];
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    blsd[j] = logf(bsd[j]);
+    ibsd[j] = 1.f / bsd[j];
+  }
+  bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, c_ll)), 1e-5f);
+  rbd = row_kl_rb<AT>(rm, lrsig, s02, bmu, blsd, ibsd, A);
+}
+
 // After the (all-reduced) policy sums of POLICY_FWD(e): early stop, adapt
 // coefficient and statistics (ppo.py:265-284, 541-557, 568-575).  ps = the
 // sums; write = store the decision (stats, stop flag, coefficients), else only
@@ -358,15 +384,14 @@ struct PolGradCols {
 template <int AT>
 struct PolGradRow {
   static constexpr int AM = AT > 0 ? AT : 32;
-  float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], adv;
+  float m[AM], rm[AM], ac[AM], adv, bl;
   __device__ void load(const PolRowArgs& a, int64_t n, int A) {
     const int64_t N = (int64_t)a.E * a.B;
     ld_row<AT>(m, a.mu + n * A, A);
     ld_row<AT>(rm, a.refmu + n * A, A);
     ld_fields<AT>(ac, a.rowin, N, n, 0, A);
-    ld_fields<AT>(bmu, a.rowin, N, n, A, A);
-    ld_fields<AT>(bsd, a.rowin, N, n, 2 * A, A);
-    adv = a.rowin[rin_idx(row_w(A), n, 3 * A)];
+    adv = a.rowin[rin_idx(row_w(A), n, rin_adv(A))];
+    bl = a.rowin[rin_idx(row_w(A), n, rin_bl(A))];
   }
 };
 
@@ -381,20 +406,11 @@ __device__ __forceinline__ void pol_grad_compute(const PolRowArgs& a, const PolG
   const float* m = x.m;
   const float* rm = x.rm;
   const float* ac = x.ac;
-  const float* bmu = x.bmu;
-  const float* bsd = x.bsd;
-  float blsd[AM];
   const float av = nadv(x.adv);
   const float ll = row_loglik_r<AT>(ac, m, c.inv1, c.lsig, A, a.c_ll);
   const float ex = expf(ll);
   const float lp = fmaxf(ex, 1e-5f);
-  float ibsd[AM];
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    blsd[j] = logf(bsd[j]);
-    ibsd[j] = 1.f / bsd[j];
-  }
-  const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
+  const float bl = x.bl;
   float g_lp;
   if (a.mode == 0) {
     const float ratio = lp / bl;
@@ -483,26 +499,18 @@ template <int AT, class Cols>
 __device__ __forceinline__ void pol_stats_row_adapt(const PolRowArgs& a, const Cols& c,
                                                     const AdvNorm& nadv, const float* m,
                                                     const float* rm, const float* ac,
-                                                    const float* bmu, const float* bsd, float adv,
+                                                    float bl, float rbd, float adv,
                                                     float ret, double* acc) {
-  constexpr int AM = AT > 0 ? AT : 32;
   const int A = c.A;
-  float blsd[AM], ibsd[AM];
   const float av = nadv(adv);
   const float ex = expf(row_loglik_r<AT>(ac, m, c.isig, c.lsig, A, a.c_ll));
   const float lp = fmaxf(ex, 1e-5f);
-#pragma unroll
-  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-    blsd[j] = logf(bsd[j]);
-    ibsd[j] = 1.f / bsd[j];
-  }
-  const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
   acc[PS_KL] += (double)row_kl_cc<AT>(rm, m, c.lkl, c.s02, c.iden2, A);
   acc[PS_SURR] += (double)(av * (lp / fmaxf(bl, 1e-2f)));
   acc[PS_CLIP] += 0.0;
   acc[PS_ISW] += (double)(lp / (bl + 1e-4f));
   acc[PS_BL] += (double)bl;
-  acc[PS_RBD] += (double)row_kl_rb<AT>(rm, c.lrsig, c.s02, bmu, blsd, ibsd, A);
+  acc[PS_RBD] += (double)rbd;
   acc[PS_RET] += (double)ret;
 }
 

@@ -81,7 +81,8 @@ struct RnnScratch {
   float *values, *adv, *ret, *refmu, *lvpart;
   // time-major per-row inputs of the row kernels, packed once per learn,
   // field-major within blocks of 64 rows: rowin[rin_idx(W, n, f)], f =
-  // {actions (A) | behave mu, sigma (2A) | raw advantage}, n = t*B + b;
+  // {actions (A) | behave mu, sigma (2A) | raw advantage | behaviour
+  // likelihood | KL(ref || behaviour) row term}, n = t*B + b;
   // ret_tm[n] the window return
   float *rowin, *ret_tm;
   float *A1, *A2, *dA2, *dF, *cpart;        // pixel stem (empty without one)
@@ -616,20 +617,58 @@ adv_export_kernel(PolRowArgs a, float* __restrict__ adv_out, float* __restrict__
 // consecutive floats
 // (a row-major 100-byte row per lane made every load instruction touch ~56
 // cache lines: the row kernels waited on the texture addresser, PMC TA_BUSY)
+// + each row's behaviour-policy terms (behave_terms: the reference means
+// refmu of PREP and the reference std are fixed for the learn)
+template <int AT>
 __global__ void __launch_bounds__(kWG)
 row_pack_kernel(PolRowArgs a, float* __restrict__ rowin, float* __restrict__ ret_tm) {
-  const int A = a.A;
+  constexpr int AM = AT > 0 ? AT : 32;
+  const int A = AT > 0 ? AT : a.A;
+  float lrsig[AM], s02[AM];                        // PolStatsCols' reference-std terms
+#pragma unroll
+  for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+    const float rsig = expf(a.ref_lv[j]);
+    s02[j] = rsig * rsig;
+    lrsig[j] = logf(rsig);
+  }
   const int64_t N = (int64_t)a.E * a.B;
+  const int W = row_w(A);
   for (int64_t n = (int64_t)blockIdx.x * kWG + threadIdx.x; n < N; n += (int64_t)gridDim.x * kWG) {
     const int t = (int)(n / a.B), b = (int)(n - (int64_t)t * a.B);
     const int64_t src = (int64_t)b * a.T + t;
-    const float* ac = a.actions + src * A;
+    const float* acp = a.actions + src * A;
     const float* bh = a.behave + src * 2 * A;
-    const int W = row_w(A);
-    for (int j = 0; j < A; ++j) rowin[rin_idx(W, n, j)] = ac[j];
-    for (int j = 0; j < 2 * A; ++j) rowin[rin_idx(W, n, A + j)] = bh[j];
-    rowin[rin_idx(W, n, 3 * A)] = a.adv[(int64_t)b * a.E + t];
+    float ac[AM], bmu[AM], bsd[AM], rm[AM];
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+      ac[j] = acp[j];
+      bmu[j] = bh[j];
+      bsd[j] = bh[A + j];
+      rm[j] = a.refmu[n * A + j];
+    }
+#pragma unroll
+    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
+      rowin[rin_idx(W, n, j)] = ac[j];
+      rowin[rin_idx(W, n, A + j)] = bmu[j];
+      rowin[rin_idx(W, n, 2 * A + j)] = bsd[j];
+    }
+    rowin[rin_idx(W, n, rin_adv(A))] = a.adv[(int64_t)b * a.E + t];
+    float bl, rbd;
+    behave_terms<AT>(ac, bmu, bsd, rm, lrsig, s02, A, a.c_ll, bl, rbd);
+    rowin[rin_idx(W, n, rin_bl(A))] = bl;
+    rowin[rin_idx(W, n, rin_rbd(A))] = rbd;
     ret_tm[n] = a.ret[(int64_t)b * a.E + t];
+  }
+}
+
+static void launch_row_pack(int A, int64_t rows, const PolRowArgs& p, float* rowin, float* ret_tm,
+                            hipStream_t st) {
+  const int g = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (rows + kWG - 1) / kWG));
+  switch (A) {
+#define RP(K) case K: hipLaunchKernelGGL(row_pack_kernel<K>, dim3(g), dim3(kWG), 0, st, p, rowin, ret_tm); break;
+    RP(1) RP(2) RP(3) RP(4) RP(5) RP(6) RP(7) RP(8)
+#undef RP
+    default: hipLaunchKernelGGL(row_pack_kernel<0>, dim3(g), dim3(kWG), 0, st, p, rowin, ret_tm); break;
   }
 }
 
@@ -684,33 +723,25 @@ policy_rows_stats_kernel(PolRowArgs a) {
   // alternating register sets, the next row's loads in flight behind this
   // row's arithmetic (clamped row index: always issued, so the waitcnt pass
   // waits for exactly the set it consumes)
-  struct RowIn { float m[AM], rm[AM], ac[AM], bmu[AM], bsd[AM], adv, ret; };
+  // (bl / rbd: the row's behaviour-policy terms, packed once per learn)
+  struct RowIn { float m[AM], rm[AM], ac[AM], adv, ret, bl, rbd; };
   auto load_row = [&](RowIn& x, int64_t n) {
     ld_row<AT>(x.m, a.mu + n * A, A);
     ld_row<AT>(x.rm, a.refmu + n * A, A);
     ld_fields<AT>(x.ac, a.rowin, N, n, 0, A);
-    ld_fields<AT>(x.bmu, a.rowin, N, n, A, A);
-    ld_fields<AT>(x.bsd, a.rowin, N, n, 2 * A, A);
-    x.adv = a.rowin[rin_idx(row_w(A), n, 3 * A)];
+    x.adv = a.rowin[rin_idx(row_w(A), n, rin_adv(A))];
+    x.bl = a.rowin[rin_idx(row_w(A), n, rin_bl(A))];
+    x.rbd = a.rowin[rin_idx(row_w(A), n, rin_rbd(A))];
     x.ret = a.ret_tm[n];
   };
   auto row = [&](const RowIn& x, int64_t n) {
     const float* m = x.m;
     const float* rm = x.rm;
     const float* ac = x.ac;
-    const float* bmu = x.bmu;
-    const float* bsd = x.bsd;
-    float blsd[AM];
     const float av = nadv(x.adv);
     const float ex = expf(row_loglik_r<AT>(ac, m, isig, lsig, A, a.c_ll));
     const float lp = fmaxf(ex, 1e-5f);
-    float ibsd[AM];
-#pragma unroll
-    for (int j = 0; j < (AT > 0 ? AT : A); ++j) {
-      blsd[j] = logf(bsd[j]);
-      ibsd[j] = 1.f / bsd[j];
-    }
-    const float bl = fmaxf(expf(row_loglik_r<AT>(ac, bmu, ibsd, blsd, A, a.c_ll)), 1e-5f);
+    const float bl = x.bl;
     acc[PS_KL] += (double)row_kl_cc<AT>(rm, m, lkl, s02, iden2, A);
     // both modes add into fixed accumulators (adapt adds an exact 0 to the
     // clip sum): merged branches had indexed acc[] by mode, i.e. from scratch
@@ -729,7 +760,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
     acc[PS_CLIP] += (double)t_clip;
     acc[PS_ISW] += (double)(lp / (bl + 1e-4f));
     acc[PS_BL] += (double)bl;
-    acc[PS_RBD] += (double)row_kl_rb<AT>(rm, lrsig, s02, bmu, blsd, ibsd, A);
+    acc[PS_RBD] += (double)x.rbd;
     acc[PS_RET] += (double)x.ret;
     if constexpr (FUSE) {          // policy_rows_grad_kernel's clip branch, weight a.invN
       const float ratio = lp / bl;
@@ -1092,14 +1123,14 @@ policy_rows_stats_lean_kernel(PolRowArgs a) {
   const int64_t N = (int64_t)a.E * a.B;
   const AdvNorm nadv(a);
   for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
-    float m[AT], rm[AT], ac[AT], bmu[AT], bsd[AT];
+    float m[AT], rm[AT], ac[AT];
     ld_row<AT>(m, a.mu + n * AT, AT);
     ld_row<AT>(rm, a.refmu + n * AT, AT);
     ld_fields<AT>(ac, a.rowin, N, n, 0, AT);
-    ld_fields<AT>(bmu, a.rowin, N, n, AT, AT);
-    ld_fields<AT>(bsd, a.rowin, N, n, 2 * AT, AT);
-    const float adv = a.rowin[rin_idx(row_w(AT), n, 3 * AT)];
-    pol_stats_row_adapt<AT>(a, sc, nadv, m, rm, ac, bmu, bsd, adv, a.ret_tm[n], acc);
+    const float adv = a.rowin[rin_idx(row_w(AT), n, rin_adv(AT))];
+    const float bl = a.rowin[rin_idx(row_w(AT), n, rin_bl(AT))];
+    const float rbd = a.rowin[rin_idx(row_w(AT), n, rin_rbd(AT))];
+    pol_stats_row_adapt<AT>(a, sc, nadv, m, rm, ac, bl, rbd, adv, a.ret_tm[n], acc);
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -1718,8 +1749,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     }
     case SMI_RNN_PH_POLICY_FWD: {
       if (e == 0) {
-        hipLaunchKernelGGL(row_pack_kernel, dim3(grid_of(d.NE)), dim3(kWG), 0, st, pol_rows(a, d, s),
-                           s.rowin, s.ret_tm);
+        launch_row_pack(d.A, d.NE, pol_rows(a, d, s), s.rowin, s.ret_tm, st);
         RC(check_launch("row_pack_kernel"));
       }
       if (e == 0 && (a.adv_out || a.ret_out)) {
@@ -1739,8 +1769,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
         const int kt = ktime_begin(st);
         if (a.mode == 0) launch_pol_stats<true>(d.A, nb, p, st);     // + the clip gradient
         else launch_pol_stats<false>(d.A, nb, p, st);
-        // per row: mu, refmu, actions (3A) + behave (2A) + adv, ret (2) floats read
-        ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (5 * d.A + 2), st);
+        // per row: mu, refmu, actions (3A) + adv, ret, bl, rbd (4) floats read
+        ktime_end(kt, KT_POLICY_STATS, 4.0 * (double)d.NE * (3 * d.A + 4), st);
         RC(check_launch("policy_rows_stats_kernel"));
       }
       if (fused_decide(a, d, s, actor, e)) return SMI_OK;     // decided by POLICY_BWD's gradient pass
@@ -1792,8 +1822,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
           case 8: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 8>), dim3(nb), dim3(kRowNT), 0, st, p); break;
           default: hipLaunchKernelGGL((policy_rows_grad_kernel<kRowNT, 0>), dim3(nb), dim3(kRowNT), 0, st, p); break;
         }
-        // per row: mu, refmu, actions, behave (5A) + adv read, dz (A) written
-        ktime_end(kt, KT_POLICY_GRAD, 4.0 * (double)d.NE * (6 * d.A + 1), st);
+        // per row: mu, refmu, actions (3A) + adv, bl (2) read, dz (A) written
+        ktime_end(kt, KT_POLICY_GRAD, 4.0 * (double)d.NE * (4 * d.A + 2), st);
         RC(check_launch("policy_rows_grad_kernel"));
       }
       // the log_var gradient (and, fused, the clip-norm partials and the step
