@@ -23,8 +23,11 @@ def load(d, counter):
 
 
 def main(root, cfg):
-    fe = load(os.path.join(root, f'pmc_{cfg}_fetch'), 'FETCH_SIZE')
-    wr = load(os.path.join(root, f'pmc_{cfg}_write'), 'WRITE_SIZE')
+    def pdir(short, counter):     # tools/pmc_bench.sh / tools/gpu.sh pmc directory names
+        d = os.path.join(root, f'pmc_{cfg}_{short}')
+        return d if os.path.isdir(d) else os.path.join(root, f'pmc_{cfg}_{counter}')
+    fe = load(pdir('fetch', 'FETCH_SIZE'), 'FETCH_SIZE')
+    wr = load(pdir('write', 'WRITE_SIZE'), 'WRITE_SIZE')
     out = {}
     for k in sorted(set(fe) | set(wr)):
         f, nf = fe.get(k, (0.0, 0))
