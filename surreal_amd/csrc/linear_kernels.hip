@@ -984,7 +984,6 @@ struct DwGroup {
   int vec[kDwGroupMax];          // 2*VA + VB
   int narrow[kDwGroupMax];       // last m-tile is a 16-wide tail (M % 64 in 1..16)
   int n;
-  int rel;                       // elements per reducer block: 64, or 4 kWG (red_layout)
 };
 
 // output tile width of the grouped launch in 16-column sub-tiles, and its
@@ -1136,27 +1135,6 @@ __device__ void dw_epilogue_block(const DwEpilogue& x, int nsq) {
   }
 }
 
-// four consecutive elements' sums over S slabs in the 64-element form's order
-// (slab classes z mod 4, each (z) + (z + 4), then (c0 + c1) + (c2 + c3))
-template <int S>
-__device__ __forceinline__ float4 red4_sum(const float* __restrict__ part, int64_t MN, int64_t e0) {
-  float4 p[S];
-#pragma unroll
-  for (int z = 0; z < S; ++z) p[z] = *reinterpret_cast<const float4*>(part + (int64_t)z * MN + e0);
-  float4 c[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    c[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (k < S) c[k] = p[k < S ? k : 0];
-    if (k + 4 < S) {
-      const float4 q = p[k + 4 < S ? k + 4 : 0];
-      c[k] = float4{c[k].x + q.x, c[k].y + q.y, c[k].z + q.z, c[k].w + q.w};
-    }
-  }
-  return float4{(c[0].x + c[1].x) + (c[2].x + c[3].x), (c[0].y + c[1].y) + (c[2].y + c[3].y),
-                (c[0].z + c[1].z) + (c[2].z + c[3].z), (c[0].w + c[1].w) + (c[2].w + c[3].w)};
-}
-
 __global__ void __launch_bounds__(kWG)
 gemm_group_reduce_kernel(DwGroup G) {
   __shared__ float red[4][64];
@@ -1174,38 +1152,6 @@ gemm_group_reduce_kernel(DwGroup G) {
   const int S = G.S[gi];
   const float* __restrict__ part = g.part;
   const int64_t MN = (int64_t)g.M * g.N;
-  if (G.rel == 4 * kWG) {
-    // four consecutive elements per thread (every S <= 8, M N % 4 == 0,
-    // 16-byte aligned partials: red_layout): all S float4 partials in flight
-    // at once, summed in the 64-element form's order — slab classes z mod 4,
-    // each (z) + (z + 4), then (c0 + c1) + (c2 + c3)
-    const int64_t e0 = (int64_t)(b - G.rb0[gi]) * (4 * kWG) + 4 * threadIdx.x;
-    double qd = 0.0;
-    if (e0 < MN) {
-      float4 v4;
-      switch (S) {   // compile-time slab counts: every load unconditional
-        case 1: v4 = red4_sum<1>(part, MN, e0); break;
-        case 2: v4 = red4_sum<2>(part, MN, e0); break;
-        case 3: v4 = red4_sum<3>(part, MN, e0); break;
-        case 4: v4 = red4_sum<4>(part, MN, e0); break;
-        case 5: v4 = red4_sum<5>(part, MN, e0); break;
-        case 6: v4 = red4_sum<6>(part, MN, e0); break;
-        case 7: v4 = red4_sum<7>(part, MN, e0); break;
-        default: v4 = red4_sum<8>(part, MN, e0); break;
-      }
-      const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t e = e0 + j;
-        const int m = (int)(e / g.N), n = (int)(e - (int64_t)m * g.N);
-        qd += (double)dw_put(g, m, n, v[j]);
-      }
-    }
-    if (!G.x.sq) return;
-    const double t = block_sum_d(qd, sqr);
-    if (threadIdx.x == 0) G.x.sq[b] = t;
-    return;
-  }
   const int el = threadIdx.x & 63, zl = threadIdx.x >> 6;
   const int64_t e = (int64_t)(b - G.rb0[gi]) * 64 + el;
   const int64_t ec = e < MN ? e : MN - 1;
@@ -1698,23 +1644,6 @@ static int dw_prepare(DwGroup& G, int wv, int slots, int64_t ws_off, int64_t& ne
   return SMI_OK;
 }
 
-// the reducer's block layout: 4 kWG elements per block (four per thread,
-// every slab's float4 in flight) where every entry allows it, else 64 (one
-// element per thread and wave-interleaved slabs).  Off unless SMI_RED4=1 (A/B)
-static void red_layout(DwGroup& R) {
-  static const bool on = [] { const char* e = getenv("SMI_RED4"); return e && e[0] == '1'; }();
-  bool v = on;
-  for (int i = 0; i < R.n; ++i) {
-    const GemmArgs& g = R.g[i];
-    v = v && R.S[i] <= 8 && ((int64_t)g.M * g.N) % 4 == 0 &&
-        (reinterpret_cast<uintptr_t>(g.part) & 15) == 0;
-  }
-  R.rel = v ? 4 * kWG : 64;
-  R.rb0[0] = 0;
-  for (int i = 0; i < R.n; ++i)
-    R.rb0[i + 1] = R.rb0[i] + (int)(((int64_t)R.g[i].M * R.g[i].N + R.rel - 1) / R.rel);
-}
-
 // short-batch 16 x 16-tile kernels (gemm_t16_kernel, gemm_dwt16_kernel): 16-k
 // chunks per wave, K <= 4 * 16 * 8 = 512
 constexpr int T16_MAXC = 8;
@@ -1833,7 +1762,6 @@ int dw_group_flush(hipStream_t st) {
     if (!G.x.on) return SMI_OK;
     if (G.x.sq) return set_error(SMI_E_ARG, "dw group: fused sum of squares over an empty group");
     G.rb0[0] = 0;                                   // the epilogue task alone
-    G.rel = 64;
     hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(1), dim3(kWG), 0, st, G);
     return check_launch("gemm_group_reduce_kernel");
   }
@@ -1877,7 +1805,6 @@ int dw_group_flush(hipStream_t st) {
     R.n += G.n;
     need += g_pre_need;
   }
-  red_layout(R);
   const int rslot = ktime_begin(st);
   hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(R.rb0[R.n] + (R.x.on ? 1 : 0)), dim3(kWG), 0,
                      st, R);
