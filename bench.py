@@ -199,6 +199,183 @@ def roofline_hbm(kt, n_inst):
             'note': f'in-workload ({where}); > 256 MB sweeps: tools/bench_hbm.py, profiles/'}
 
 
+def calibrate(dev, mfma_iters=20000, stream_mb=1024, reps=5):
+    """Fixed-work calibration launches right before the timed region
+    (calib_kernels.hip): what this box delivers today, so a slow box reads as a
+    slow box and not as a code regression.  MFMA: 512 workgroups (2 per CU) x 4
+    waves x iters x 4 v_mfma_f32_32x32x2_f32 on random register operands; HBM:
+    a float4 read + write stream over 2 x stream_mb MB (> the 256 MB MALL).
+    Best of `reps` launches each (HIP events on the current stream)."""
+    from surreal_amd import _lib as L
+    st = L.stream(dev)
+    n_wg = 512
+    out = torch.empty(n_wg * 256, device=dev)
+    stamps = torch.zeros(2 * n_wg, dtype=torch.int64, device=dev)
+    n = stream_mb * (1 << 20) // 4
+    x = torch.rand(n, device=dev)
+    y = torch.empty_like(x)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed(fn):
+        best = None
+        fn()                                     # warm (code object, first touch)
+        for _ in range(reps):
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        return best
+    ms_m = timed(lambda: L.call('smi_calib_mfma', n_wg, mfma_iters, L.ptr(out), L.ptr(stamps), st))
+    ms_s = timed(lambda: L.call('smi_calib_stream', L.ptr(x), L.ptr(y), n, st))
+    s = stamps.view(n_wg, 2).cpu().numpy().astype(np.float64)
+    clk = np.median(s[:, 0] / np.maximum(s[:, 1], 1)) * 100.0
+    flops = n_wg * 4 * mfma_iters * 4 * 4096.0
+    tf = flops / (ms_m * 1e-3) / 1e12
+    tbps = 8.0 * n / (ms_s * 1e-3) / 1e12
+    del x, y
+    return {'calib_mfma_tflops': round(tf, 2), 'calib_mfma_frac': round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+            'calib_mfma_clock_mhz': round(float(clk), 1),
+            'calib_hbm_tbps': round(tbps, 3), 'calib_hbm_frac': round(tbps * 1e3 / HBM_PEAK_GBS, 4),
+            'note': f'fixed-work launches right before the timed region (best of {reps}): '
+                    f'{n_wg} x 4 waves x {mfma_iters} x 4 v_mfma_f32_32x32x2_f32 on random register '
+                    f'operands; float4 read+write stream over 2 x {stream_mb} MB'}
+
+
+class ClockProbe(object):
+    """The shader clock over the timed region: one sleeping wave on a side
+    stream stamps s_memtime / s_memrealtime from before the first timed launch
+    until a stop kernel enqueued on the learner's stream after the last one
+    (bounded by max_s of wall time, so it always exits)."""
+
+    def __init__(self, dev, max_s=30.0):
+        from surreal_amd import _lib as L
+        self.L, self.dev = L, dev
+        self.flag = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.out = torch.zeros(3, dtype=torch.int64, device=dev)
+        self.side = torch.cuda.Stream(device=dev)
+        self.max_ticks = int(max_s * 1e8)
+        torch.cuda.synchronize(dev)
+
+    def start(self):
+        L = self.L
+        L.call('smi_clock_probe', L.ptr(self.flag), self.max_ticks, L.ptr(self.out),
+               ctypes_stream(self.side))
+
+    def stop(self):
+        """enqueue the stop kernel on the learner's stream after the last timed
+        launch, BEFORE the closing barrier (a device-wide synchronize waits for
+        the probe's stream too)"""
+        L = self.L
+        L.call('smi_clock_probe_stop', L.ptr(self.flag), 1, L.stream(self.dev))
+
+    def read(self):
+        self.side.synchronize()
+        m, r, to = (int(v) for v in self.out.cpu().tolist())
+        if to or r <= 0:
+            return None
+        return {'clock_mhz': round(m / r * 100.0, 1), 'window_ms': round(r / 1e5, 3),
+                'source': 'one sleeping wave on a side stream: d s_memtime / d s_memrealtime x '
+                          '100 MHz from before the first timed step to a stop kernel enqueued '
+                          'after the last (inside the timed region: one ~2 us launch)'}
+
+
+class SmiClockSampler(object):
+    """The GPU's current gfx clock over the timed region, sampled by a host
+    thread from the SMU through amdsmi (gpu_metrics current_gfxclk, MHz) every
+    `period_s`; reported as the mean and range of the samples.  No kernel runs
+    beside the timed launches."""
+
+    def __init__(self, dev, period_s=0.002):
+        import threading
+        import amdsmi
+        self.amdsmi = amdsmi
+        amdsmi.amdsmi_init()
+        hs = amdsmi.amdsmi_get_processor_handles()
+        idx = torch.device(dev).index or 0
+        vis = os.environ.get('HIP_VISIBLE_DEVICES') or os.environ.get('ROCR_VISIBLE_DEVICES')
+        if vis:
+            idx = int(vis.split(',')[idx])
+        self.h = hs[idx] if idx < len(hs) else hs[0]
+        self.period = period_s
+        self.samples = []
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, daemon=True)
+        self.read_one()                                  # fail here, not in the thread
+
+    def read_one(self):
+        m = self.amdsmi.amdsmi_get_gpu_metrics_info(self.h)
+        v = m.get('current_gfxclk')
+        if isinstance(v, (list, tuple)):
+            v = [x for x in v if isinstance(x, (int, float)) and 0 < x < 10000]
+            v = sum(v) / len(v) if v else None
+        return v if isinstance(v, (int, float)) and 0 < v < 10000 else None
+
+    def _run(self):
+        while not self._stop.wait(self.period):
+            self._sample()
+
+    def _sample(self):
+        v = self.read_one()
+        if v is not None:
+            self.samples.append(float(v))
+
+    def start(self):
+        self._sample()                  # at the start of the timed region
+        self._th.start()
+
+    def stop(self):
+        self._stop.set()
+        self._sample()                  # after the last timed step was issued
+
+    def read(self):
+        self._th.join(timeout=5)
+        try:
+            self.amdsmi.amdsmi_shut_down()
+        except Exception:
+            pass
+        if not self.samples:
+            return None
+        return {'clock_mhz': round(float(np.mean(self.samples)), 1),
+                'min_mhz': round(min(self.samples), 1), 'max_mhz': round(max(self.samples), 1),
+                'samples': len(self.samples),
+                'source': f'amdsmi gpu_metrics current_gfxclk at the start and end of the timed '
+                          f'region and every {self.period * 1e3:.0f} ms between (host thread; '
+                          'SMU-reported, reads up to ~5 % below the in-kernel s_memtime clock of '
+                          'calib.calib_mfma_clock_mhz); an in-kernel probe wave beside the timed '
+                          'launches cost 15 % of the C3 step (profiles/r06/clock_ab), so none runs'}
+
+
+def make_clock(mode, dev):
+    """--clock probe | smi | none"""
+    if mode == 'probe':
+        return ClockProbe(dev)
+    if mode == 'smi':
+        try:
+            return SmiClockSampler(dev)
+        except Exception as e:          # amdsmi not usable here: report, do not fail the bench
+            print(f'clock sampler unavailable: {e!r}', file=sys.stderr)
+    return None
+
+
+def ctypes_stream(s):
+    import ctypes
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def attach_calib(out, calib, clock):
+    """clock_mhz (shader clock over the timed region) and the calibration
+    rates next to the headline, which stays unnormalised"""
+    if clock is not None:
+        out['clock_mhz'] = clock['clock_mhz']
+        out['clock'] = clock
+    if calib is not None:
+        out['calib_mfma_tflops'] = calib['calib_mfma_tflops']
+        out['calib_hbm_tbps'] = calib['calib_hbm_tbps']
+        out['calib'] = calib
+
+
 def mlp_flops_per_row(d, h1, h2, o):
     fwd = 2 * (d * h1 + h1 * h2 + h2 * o)
     bwd = fwd + 2 * (h1 * h2 + h2 * o)        # dW of all layers + dX of layers 2, 3
@@ -340,14 +517,21 @@ def run_ddpg(args):
             dist.barrier()
             torch.cuda.synchronize()
 
+    calib = None if args.no_calib else calibrate(dev)
     for _ in range(args.warmup):
         step()
     barrier()
+    probe = None if args.no_calib else make_clock(args.clock, dev)
+    if probe is not None:
+        probe.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if probe is not None:
+        probe.stop()
     barrier()
     elapsed = time.perf_counter() - t0
+    clock = probe.read() if probe is not None else None
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -392,6 +576,7 @@ def run_ddpg(args):
         'kernels': kernels,
         'kernels_sum': kernels_sum_note(kernels, elapsed / args.steps * 1e3),
     }
+    attach_calib(out, calib, clock)
     if dist is not None:
         barrier()
         dist.destroy_process_group()
@@ -469,6 +654,12 @@ def main():
     ap.add_argument('--ppo-mode', choices=['adapt', 'clip'], default=None,
                     help='override the workload\'s PPO surrogate (A/B only; C2-C5 are adapt)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-calib', action='store_true',
+                    help='skip the fixed-work calibration launches and the clock measurement')
+    ap.add_argument('--clock', choices=['smi', 'probe', 'none'], default='smi',
+                    help='GPU clock over the timed region: amdsmi samples from a host thread '
+                         '(smi), an in-kernel s_memtime probe wave on a side stream (probe; '
+                         'A/B only), or none')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
     ap.add_argument('--local-segments', type=int, default=None,
                     help='segments per rank (overrides --scaling): e.g. 128 runs on one GPU '
@@ -523,15 +714,22 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
+    calib = None if args.no_calib else calibrate(dev)
     for i in range(args.warmup):
         learner.learn(pool[i % len(pool)])
     barrier()
+    probe = None if args.no_calib else make_clock(args.clock, dev)
+    if probe is not None:
+        probe.start()
     # timed region: the learner exactly as a caller runs it (no instrumentation)
     t0 = time.perf_counter()
     for k in range(args.steps):
         learner.learn(pool[k % len(pool)])
+    if probe is not None:
+        probe.stop()
     barrier()
     elapsed = time.perf_counter() - t0
+    clock = probe.read() if probe is not None else None
     if dist is not None:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -664,6 +862,7 @@ def main():
         'kernels_sum': kernels_sum_note(kernels, ms),
         'phase_ms_per_step': phases,
     }
+    attach_calib(out, calib, clock)
     if rhbm is not None:
         out['roofline_hbm'] = rhbm
     if allreduce is not None:

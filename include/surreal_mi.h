@@ -87,6 +87,21 @@ int          smi_context_destroy(smi_context* ctx);
 int smi_kernel_timing(int on);
 int smi_kernel_timing_report(int cls, double* out4);
 
+/* Measurement only: what the box delivers, beside bench.py's timed region
+ * (calib_kernels.hip).  smi_calib_mfma: n_wg workgroups of 4 waves, each
+ * wave `iters` x 4 v_mfma_f32_32x32x2_f32 on random register operands
+ * (16384 flops per wave and iteration); out[n_wg * 256] keeps the sums live,
+ * stamps[2 n_wg] = per workgroup (d s_memtime, d s_memrealtime), i.e. the
+ * in-kernel clock d_memtime / d_realtime x 100 MHz.  smi_calib_stream:
+ * y[i] = x[i] * (1 + 1e-7), n floats (8 bytes moved per float), float4
+ * nontemporal.  smi_clock_probe: one wave sleeping in a loop until *flag != 0
+ * (smi_clock_probe_stop, on another stream) or max_ticks of the 100 MHz
+ * counter pass; out3 = {d s_memtime, d s_memrealtime, timed_out}. */
+int smi_calib_mfma(int n_wg, int iters, float* out, long long* stamps, void* stream);
+int smi_calib_stream(const float* x, float* y, int64_t n, void* stream);
+int smi_clock_probe(const int* flag, long long max_ticks, long long* out3, void* stream);
+int smi_clock_probe_stop(int* flag, int value, void* stream);
+
 /* --------------------------------------------------------------- layouts */
 /* Number of floats in a flat MLP buffer (in -> h1 -> h2 -> out [+ log_var]). */
 int64_t smi_mlp_param_count(int in_dim, int h1, int h2, int out_dim, int with_log_var);
@@ -378,10 +393,12 @@ int smi_ppo_epoch_apply(const smi_ppo_args* args, int epoch, void* stream);
  * in the same order on every rank; between some phases a data-parallel caller
  * all-reduces (SUM) the buffer named in the phase table (include order):
  *   GAE              -> all-reduce moments (double[3], smi_ppo_rnn_args.moments)
- *   PREP             (reference-policy forward; after GAE on the same stream —
- *                    at one segment per workgroup GAE runs PREP's recurrence
- *                    in its own launch and PREP only the reference head, unless
- *                    SMI_PREP_SIDE=1 puts PREP on a second stream)
+ *   PREP             (reference-policy forward; with prep_independent == 0
+ *                    after GAE on the same stream — at one segment per
+ *                    workgroup GAE then runs PREP's recurrence in its own
+ *                    launch and PREP only the reference head; with
+ *                    prep_independent != 0 GAE leaves PREP's work alone and
+ *                    the caller may issue PREP on a second stream)
  *   POLICY_FWD(e)    e = 0..epoch_policy: forward + loss sums -> all-reduce pstat
  *   POLICY_DECIDE(e) KL early stop / adapt coefficient / statistics from pstat
  *                    (with B_global == B, one rank, POLICY_FWD already decides
@@ -477,6 +494,10 @@ typedef struct smi_ppo_rnn_args {
      and `lstm` / `ref_lstm` hold the layers one after another, each in
      nn.LSTM's order [W_ih | W_hh | b_ih | b_hh] (layer k >= 1: W_ih is 4H x H) */
   int rnn_layer;
+  /* 0: PREP is issued after GAE on the same stream (GAE may run PREP's
+     recurrence, see the phase table); != 0: PREP is independent of GAE (the
+     caller runs it on another stream, before or beside GAE) */
+  int prep_independent;
 } smi_ppo_rnn_args;
 
 #define SMI_RNN_PSTAT 16

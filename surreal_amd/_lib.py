@@ -4,7 +4,9 @@ The product path has no CPU fallback: if the library is missing or no GPU is
 visible, calls raise.  torch is imported first so the process holds torch's
 HIP runtime before the library binds to it (same SONAME, one runtime).
 """
+import contextlib
 import ctypes
+import gc
 import os
 
 import torch
@@ -86,7 +88,7 @@ class RNNArgs(ctypes.Structure):
         ('pix_c', c_int), ('pix_h', c_int), ('pix_w', c_int), ('cnn_feat', c_int),
         ('pixels', P), ('pixels_next', P),
         ('adv_out', P), ('ret_out', P),
-        ('rnn_layer', c_int),
+        ('rnn_layer', c_int), ('prep_independent', c_int),
     ]
 
 
@@ -181,6 +183,10 @@ _SIGS = {
     'smi_lstm_param_count': (c_i64, [c_int, c_int]),
     'smi_kernel_timing': (c_int, [c_int]),
     'smi_kernel_timing_report': (c_int, [c_int, P]),
+    'smi_calib_mfma': (c_int, [c_int, c_int, P, P, P]),
+    'smi_calib_stream': (c_int, [P, P, c_i64, P]),
+    'smi_clock_probe': (c_int, [P, ctypes.c_longlong, P, P]),
+    'smi_clock_probe_stop': (c_int, [P, c_int, P]),
     'smi_ppo_rnn_scratch_bytes': (c_i64, [c_int] * 15),
     'smi_ppo_rnn_xbuf_floats': (c_i64, [c_int] * 12),
     'smi_cnn_param_count': (c_i64, [c_int] * 4),
@@ -285,6 +291,23 @@ class Context(object):
         h, self.handle = getattr(self, 'handle', None), None
         if h and _lib is not None:
             _lib.smi_context_destroy(ctypes.c_void_p(h))
+
+
+@contextlib.contextmanager
+def gc_paused():
+    """Python's cyclic collector off while a hipGraph is captured: a
+    collection inside the capture runs __del__ of unreachable objects that hold
+    HIP resources from earlier work (events, graph execs), whose destroy calls
+    are not allowed during stream capture and abort the process (seen once in
+    the pixel graph-replay test).  torch.cuda.graph collects on entry; this
+    keeps the collector from running again until the capture has ended."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def require_gpu():

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(HERE)
 BUILD = os.path.join(ROOT, 'build', 'obj')
 LIB = os.path.join(HERE, 'libsurreal_mi.so')
 SOURCES = ['ppo_gae.hip', 'ppo_epochs.hip', 'ops_kernels.hip', 'sampler_kernels.hip',
-           'linear_kernels.hip', 'ddpg_kernels.hip', 'lstm_kernels.hip', 'cnn_kernels.hip', 'head_kernels.hip', 'ppo_rnn.hip', 'capi.hip']
+           'linear_kernels.hip', 'ddpg_kernels.hip', 'lstm_kernels.hip', 'cnn_kernels.hip', 'head_kernels.hip', 'ppo_rnn.hip', 'calib_kernels.hip', 'capi.hip']
 HEADERS = ['smi_device.hpp', 'smi_internal.hpp']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'

@@ -72,14 +72,19 @@ static smi_context* cur_ctx() {
   smi_context* c = t_ctx;
   return c && c->alive.load(std::memory_order_acquire) ? c : &g_default_ctx;
 }
+// floats at the start of the current workspace that hold partials a later
+// launch of this thread still reads (the BPTT + heads' dW launch's split-K
+// partials until its group's reducer): every request is served above them
+static thread_local int64_t t_ws_reserved = 0;
+void workspace_reserve(int64_t nfloats) { t_ws_reserved = nfloats > 0 ? nfloats : 0; }
 int64_t smi_workspace_floats() {
   const smi_context* c = cur_ctx();
-  return c->ws ? c->bytes / 4 : 0;
+  return c->ws ? c->bytes / 4 - t_ws_reserved : 0;
 }
 float* workspace_f32(int64_t nfloats) {
   const smi_context* c = cur_ctx();
-  if (!c->ws || nfloats > c->bytes / 4) return nullptr;
-  return static_cast<float*>(c->ws);
+  if (!c->ws || nfloats + t_ws_reserved > c->bytes / 4) return nullptr;
+  return static_cast<float*>(c->ws) + t_ws_reserved;
 }
 
 // declared in the other translation units

@@ -1413,13 +1413,23 @@ static int dwd_launch(GemmArgs g, hipStream_t st) {
 }
 
 // ---- grouped weight gradients (gemm_dwd_group_kernel) ----------------------
+// whether an M x N weight gradient over row-major operands joins an open group
+// (gemm_launch's rule; the dW2 / bias column included in N by the caller)
+bool dw_group_takes(int M, int N) { return use_dwd() && M >= 1 && N >= 1 && M <= 512 && N <= 512; }
+
 // the queue of the calling thread (begin ... flush bracket one call sequence)
 static thread_local DwGroup g_grp;
 static thread_local bool g_grp_on = false;
 static thread_local double g_grp_flops = 0.0;
+// set when a weight gradient issued inside an open bracket did not join the
+// group (group full, or a shape / layout the grouped kernel does not take):
+// with a fused sum of squares (x.sq) its gradient would be missing from the
+// clip_grad_norm_ partials, so the flush fails instead of clipping wrongly
+static thread_local bool g_grp_missed = false;
 
 int dw_group_begin() {
   g_grp_on = true;
+  g_grp_missed = false;
   g_grp.n = 0;
   g_grp.x = DwEpilogue{};
   g_grp_flops = 0.0;
@@ -1436,11 +1446,10 @@ int dw_group_epilogue(const DwEpilogue& x) {
   return SMI_OK;
 }
 
-static thread_local bool g_grp_overflow = false;
 static bool dw_group_add(const GemmArgs& g) {
   if (!g_grp_on) return false;
   if (g_grp.n >= kDwGroupMax) {
-    g_grp_overflow = true;
+    g_grp_missed = true;
     return false;
   }
   auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -1752,12 +1761,16 @@ constexpr size_t kDwdLds = (size_t)2 * 4 * DWG_NT * 64 * sizeof(float4);
 int dw_group_flush(hipStream_t st) {
   g_grp_on = false;
   DwGroup& G = g_grp;
-  const bool overflow = g_grp_overflow;
-  g_grp_overflow = false;
+  const bool missed = g_grp_missed;
+  g_grp_missed = false;
   const bool pre = g_pre_on;
   g_pre_on = false;
-  if (G.x.on && G.x.sq && overflow)
-    return set_error(SMI_E_ARG, "dw group: a fused sum of squares needs every dW GEMM in the group");
+  // the pre partials stay reserved through this flush's own requests (its
+  // partials land above them), released on every return
+  struct Release { ~Release() { workspace_reserve(0); } } release_;
+  if (G.x.on && G.x.sq && missed)
+    return set_error(SMI_E_ARG, "dw group: a fused sum of squares needs every dW GEMM of the "
+                                "bracket in the group (one ran outside it)");
   if (G.n == 0 && !pre) {
     if (!G.x.on) return SMI_OK;
     if (G.x.sq) return set_error(SMI_E_ARG, "dw group: fused sum of squares over an empty group");
@@ -1780,7 +1793,7 @@ int dw_group_flush(hipStream_t st) {
   }
   int64_t need = 0;
   if (G.n > 0) {
-    RC_CHECK(dw_prepare(G, dwd_waves(), dwd_group_slots(kDwdLds), pre ? g_pre_need : 0, need));
+    RC_CHECK(dw_prepare(G, dwd_waves(), dwd_group_slots(kDwdLds), 0, need));
     const int kslot = ktime_begin(st);
     if (dwd_waves() == 8)
       hipLaunchKernelGGL(gemm_dwd_group_kernel<8>, dim3(G.wg0[G.n]), dim3(512), kDwdLds, st, G);
@@ -1855,6 +1868,7 @@ int launch_lstm_bwd_dw(const float* dh, const float* gates, const float* cbuf, c
   g_pre = Ga;
   g_pre_on = true;
   g_pre_need = need;
+  workspace_reserve(need);     // no launch before the flush may reuse these partials
   g_grp.n = 0;                                      // the group queues the rest
   g_grp_flops = 0.0;                                // (its launch times the rest only)
   return SMI_OK;
@@ -2120,9 +2134,13 @@ static int gemm_launch(int epi, GemmArgs g, hipStream_t st) {
   if (epi == EPI_DX && use_dx_smallk() && g.K >= 1 && g.K <= 8 && g.a_cs == 1 && g.b_cs == 1)
     return dx_smallk_launch(g, st);
   if (epi != EPI_DW && !g.xsrc && panel_ok(epi, g)) return panel_launch(epi, g, st);
-  if (epi == EPI_DW && use_dwd() && g.a_rs == 1 && g.b_cs == 1 && g.K >= 1 &&
-      (g.ones_col >= 0 ? g.ones_col : g.N) >= 1 && g.M <= 512 && g.N <= 512)
-    return dw_group_add(g) ? SMI_OK : dwd_launch(g, st);
+  if (epi == EPI_DW) {
+    const bool grp_ok = use_dwd() && g.a_rs == 1 && g.b_cs == 1 && g.K >= 1 &&
+                        (g.ones_col >= 0 ? g.ones_col : g.N) >= 1 && g.M <= 512 && g.N <= 512;
+    if (grp_ok && dw_group_add(g)) return SMI_OK;
+    if (g_grp_on) g_grp_missed = true;     // runs outside the open group
+    if (grp_ok) return dwd_launch(g, st);
+  }
   const bool ak = g.a_cs == 1;         // A contiguous along k
   const bool bk = g.b_rs == 1;         // B contiguous along k (rows n)
   auto al16 = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -2289,7 +2307,9 @@ int launch_linear_bwd_dw2(const float* dY, int64_t ldg, int M, int N, const floa
   g.ones_col = K1p + K2; g.bias_out = db1; g.bias_out2 = db2; g.skip = skip;
   if (!(g.a_rs == 1 && g.b_cs == 1 && use_dwd() && g.M <= 512 && g.N <= 512))
     return set_error(SMI_E_ARG, "bwd_dw2: shape not supported");
-  return dw_group_add(g) ? SMI_OK : dwd_launch(g, st);
+  if (dw_group_add(g)) return SMI_OK;
+  if (g_grp_on) g_grp_missed = true;
+  return dwd_launch(g, st);
 }
 
 int launch_linear_bwd_dw(const float* dY, int64_t ldg, int M, int N, const float* X, int64_t ldx,

@@ -1469,8 +1469,10 @@ static int lstm_backward(const RnnDims& d, const float* P, float* G, const RnnSc
     float* dg = dgates_of(d, s, l);
     float* hb = hbuf_of(d, s, l);
     // one layer, no pixel stem: the BPTT shares its launch with the heads'
-    // weight gradients queued so far (nothing between here and the group's
-    // flush uses the workspace that holds their partials)
+    // weight gradients queued so far (their partials stay reserved in the
+    // workspace until the group's flush: workspace_reserve; one layer, so the
+    // pre entries (<= 6 after tail splits) and this layer's (<= 2) fit the
+    // reducer's 8)
     int rb = SMI_E_NOFIT;
     if (d.L == 1 && d.F == 0)
       rb = launch_lstm_bwd_dw(s.dh, gates_of(d, s, l), cbuf_of(d, s, l), lp.Whh, d.E, d.B, d.H, dg,
@@ -1602,24 +1604,30 @@ static PolRowArgs pol_rows(const smi_ppo_rnn_args& a, const RnnDims& d, const Rn
 // run Adam alone.  Data parallel: the norm is of the all-reduced gradient, so
 // the sums of squares stay in APPLY (sumsq_part_kernel); with the pixel stem
 // the CNN gradient is not a reducer output.
+// Every weight gradient of both optimizers must join the group for that
+// (dw_group_takes: heads wider than 511 or 4H > 512 run outside it); the flush
+// also fails loudly if one ran outside an open bracket with the fused norm.
 static bool fused_clip_norm(const smi_ppo_rnn_args& a, const RnnDims& d) {
   static const bool off = [] { const char* e = getenv("SMI_FUSED_NORM"); return e && e[0] == '0'; }();
-  return !off && a.B_global == a.B && d.F == 0 && d.L <= 3 && fault() == 0;
+  if (off || a.B_global != a.B || d.F != 0 || d.L > 3 || fault() != 0) return false;
+  const bool heads = dw_group_takes(d.h1, d.Hin + 1) && dw_group_takes(d.h2, d.h1 + 1) &&
+                     dw_group_takes(d.A, d.h2 + 1) && dw_group_takes(d.c1, d.Hin + 1) &&
+                     dw_group_takes(d.c2, d.c1 + 1) && dw_group_takes(1, d.c2 + 1);
+  const bool stem = d.H == 0 || (dw_group_takes(d.G4, d.ldx + d.H + 1) &&
+                                 (d.L == 1 || dw_group_takes(d.G4, d.H + d.H + 1)));
+  return heads && stem;
 }
 
 // the GAE critic pass (T + 1 steps) and PREP's reference-policy forward (E
 // steps) as ONE recurrence launch (two weight sets over two inputs, B
 // workgroups each): one LSTM layer, no pixel stem, the one-segment form for 2B
-// segments, PREP on the learner's stream (SMI_PREP_SIDE unset); GAE then also
+// segments, PREP issued after GAE on the same stream (a.prep_independent == 0:
+// the caller's explicit statement, no environment read here); GAE then also
 // forms PREP's z-filtered input and PREP runs the reference head only.
 // SMI_GAE_DUAL=0: two launches (A/B knob)
-static bool gae_prep_dual(const RnnDims& d) {
-  static const bool off = [] {
-    const char* e = getenv("SMI_GAE_DUAL");
-    const char* p = getenv("SMI_PREP_SIDE");
-    return (e && e[0] == '0') || (p && p[0] == '1');
-  }();
-  return !off && d.H > 0 && d.L == 1 && d.F == 0 &&
+static bool gae_prep_dual(const smi_ppo_rnn_args& a, const RnnDims& d) {
+  static const bool off = [] { const char* e = getenv("SMI_GAE_DUAL"); return e && e[0] == '0'; }();
+  return !off && a.prep_independent == 0 && d.H > 0 && d.L == 1 && d.F == 0 &&
          lstm_fwd_x_dual_fits(d.B, d.B, d.S1 > d.E ? d.S1 : d.E, d.H, d.Din);
 }
 
@@ -1697,7 +1705,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       // (ppo.py:253-262 at epoch 0) is the same recurrence over the same
       // inputs from the same (h0, c0) with the same parameters, so
       // POLICY_FWD(0) reads these instead of recomputing them
-      if (gae_prep_dual(d)) {
+      if (gae_prep_dual(a, d)) {
         // PREP's input (the reference z-filter over obs_iter), then both
         // recurrences in one launch: the critic's over T + 1 steps keeping E
         // steps' cells / gates, the reference policy's over E steps
@@ -1730,13 +1738,15 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
     }
     case SMI_RNN_PH_PREP: {
       // ref_pol (ppo.py:539): the reference model's forward over obs_iter.
-      // Independent of GAE: it reads only the batch and the reference
+      // With a.prep_independent != 0 it reads only the batch and the reference
       // parameters and writes only its own buffers (sp) and refmu, so the host
       // may run it on a second stream beside GAE (with its own smi_context).
+      // With a.prep_independent == 0 it must follow GAE on the same stream: GAE
+      // may have run its input transpose and recurrence (gae_prep_dual).
       RnnScratch sp = s;
       sp.xproj = s.xprojR; sp.hbuf = s.hbufR; sp.HA1 = s.HA1R; sp.HA2 = s.HA2R; sp.A2 = s.A2R;
       const float* X = s.Xr;
-      if (!gae_prep_dual(d)) {      // (else the GAE phase ran this input and recurrence)
+      if (!gae_prep_dual(a, d)) {   // (else the GAE phase ran this input and recurrence)
         RC(launch_zf_tmajor(a.obs, a.obs_next, d.B, d.T, d.E, d.D, a.use_zf, a.rzf_sum,
                             a.rzf_sumsq, a.rzf_count, a.zf_eps, s.Xr, d.ldx, st, 0,
                             d.F == 0));

@@ -26,6 +26,9 @@ void ktime_end(int slot, int cls, double flops, hipStream_t st);
 // nfloats (nullptr when it does not fit)
 int64_t smi_workspace_floats();
 float* workspace_f32(int64_t nfloats);
+// keep the first nfloats of this thread's workspace out of later requests
+// (0: release); workspace_f32 / smi_workspace_floats serve what lies above
+void workspace_reserve(int64_t nfloats);
 int launch_linear_fwd(const float* X, int64_t ldx, int M, int K, const float* W, int64_t ldw,
                       const float* b, int N, int act, float* Y, int64_t ldy, hipStream_t st,
                       const int* skip = nullptr);
@@ -60,6 +63,8 @@ struct DwEpilogue {
   const int* skip;
 };
 int dw_group_epilogue(const DwEpilogue& x);
+// an M x N weight gradient (bias column included in N) joins an open group
+bool dw_group_takes(int M, int N);
 // BR of the one-segment-per-workgroup BPTT form for (B, H), 0 when another form runs
 int lstm_bwd_q_form(int B, int H);
 // the LSTM BPTT (lstm_bwd_q form) and the weight gradients queued so far in the

@@ -740,7 +740,7 @@ class DDPGLearner(LearnerHooks):
             self._gin = [torch.zeros(tuple(t.shape), dtype=torch.float32, device=self.device)
                          for t in ins]
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode='thread_local'):
+            with L.gc_paused(), torch.cuda.graph(g, capture_error_mode='thread_local'):
                 self._optimize(*self._gin, target_update=False)
             self._graph = g
             return

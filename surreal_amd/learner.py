@@ -610,6 +610,8 @@ class PPOLearner(LearnerHooks):
         a.actions = actions.data_ptr()
         a.pix_c, a.pix_h, a.pix_w, a.cnn_feat = pc, ph, pw, F
         a.rnn_layer = self.rnn_layer
+        # PREP on a second stream (below) must not depend on GAE: say so explicitly
+        a.prep_independent = 1 if self.prep_side_stream else 0
         a.pixels = pix.data_ptr() if pix is not None else None
         a.pixels_next = pixn.data_ptr() if pixn is not None else None
         a.rewards, a.dones, a.behave = rewards.data_ptr(), dones.data_ptr(), pds.data_ptr()
@@ -811,7 +813,7 @@ class PPOLearner(LearnerHooks):
             g = torch.cuda.CUDAGraph()
             err = None
             try:
-                with torch.cuda.graph(g, capture_error_mode='thread_local'):
+                with L.gc_paused(), torch.cuda.graph(g, capture_error_mode='thread_local'):
                     self._ctx.make_current()
                     for buf in self._device_phases(static):
                         if dp is not None:            # RCCL all-reduce, captured

@@ -389,8 +389,10 @@ def report_json(report):
         if k == '_fail':
             continue
         d = {'gpu': float(v[0]), 'bar': float(v[1])}
-        if len(v) > 3:
+        if len(v) > 3 and v[3] is not None:
             d['env'] = float(v[3])
+        if len(v) > 4:
+            d.update(v[4])
         d['gpu_over_bar'] = float(v[0]) / float(v[1]) if v[1] > 0 else float('inf')
         d['ok'] = bool(v[2])
         out[k] = d
@@ -416,7 +418,9 @@ def print_report(report, case=None):
     print('\n(GPU err, applied bar[, envelope width]) vs the fp64 oracle (per scale):')
     for k, v in report.items():
         if k != '_fail':
-            env = f'  env {v[3]:.3e}' if len(v) > 3 else ''
+            env = f'  env {v[3]:.3e}' if len(v) > 3 and v[3] is not None else ''
+            if len(v) > 4:
+                env += f"  (set by {v[4]['bar_set_by']}; wide bar {v[4]['bar_wide']:.3e})"
             print(f'  {k:30s} gpu {v[0]:.3e}  bar {v[1]:.3e}{env}  {"" if v[2] else "FAIL"}')
     if case is not None:
         save_report(case, report)
@@ -551,40 +555,62 @@ def recompute_stats(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run):
     value)}: the same computation in fp32 (the reference's precision) says
     how far fp32 arithmetic itself lands from fp64 at this very state."""
     s64 = _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, torch.float64)
-    # several fp32 executions: two segment orders (given, reversed: the row
-    # sums behind a gradient norm round differently) and four with a few ulp
-    # of relative noise on the observations, cells and parameters (the
-    # rounding of the products a GEMM's summation order changes):
-    # pre-activations within fp32 noise of 0 then take the other side of a
-    # ReLU, as they do between any two fp32 implementations --
-    # tools/exp/critic_grad_check.py found the C3 critic gradient's hidden
-    # blocks 1e-3 apart between valid fp32 executions (one HA2 mask flip),
-    # 1.2e-5 in its norm.  The farthest execution sets the bar
-    s32s = [_stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, torch.float32, perm=pm)
-            for pm in (None, 'reversed', ('ulp', 1), ('ulp', 2), ('ulp', 3), ('ulp', 4))]
-    return {k: (v, sc, max((x[k][0] for x in s32s), key=lambda u: abs(u - v)))
-            for k, (v, sc) in s64.items()}
+    # Two sets of fp32 executions, each the same statistics up to fp32
+    # rounding (ADVICE r5: the narrow set stays the bar that decides).
+    #  STRICT (the round-4 set): two segment orders (given, reversed: the row
+    #   sums behind a gradient norm round differently) and two with one ulp of
+    #   relative noise on the observations and cells.
+    #  WIDE (round 5, reported beside it): four more with a few ulp of noise on
+    #   the observations, cells AND parameters (the rounding of the products a
+    #   GEMM's summation order changes): pre-activations within fp32 noise of 0
+    #   take the other side of a ReLU, as they do between any two fp32
+    #   implementations -- tools/exp/critic_grad_check.py found the C3 critic
+    #   gradient's hidden blocks 1e-3 apart between valid fp32 executions (one
+    #   HA2 mask flip), 1.2e-5 in its norm.
+    # Returns {key: (fp64, scale, fp32 farthest in STRICT, fp32 farthest in
+    # STRICT + WIDE, the variant that set each)}; check_stats applies STRICT.
+    runs = {_variant_name(pm): _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run,
+                                         torch.float32, perm=pm)
+            for pm in STAT_VARIANTS_STRICT + STAT_VARIANTS_WIDE}
+    strict = [_variant_name(pm) for pm in STAT_VARIANTS_STRICT]
+    out = {}
+    for k, (v, sc) in s64.items():
+        ns = max(strict, key=lambda n: abs(runs[n][k][0] - v))
+        nw = max(runs, key=lambda n: abs(runs[n][k][0] - v))
+        out[k] = (v, sc, runs[ns][k][0], runs[nw][k][0], ns, nw)
+    return out
+
+
+STAT_VARIANTS_STRICT = (None, 'reversed', ('ulp1', 1), ('ulp1', 2))
+STAT_VARIANTS_WIDE = (('ulp', 1), ('ulp', 2), ('ulp', 3), ('ulp', 4))
+
+
+def _variant_name(pm):
+    return 'given' if pm is None else pm if isinstance(pm, str) else f'{pm[0]}{pm[1]}' if pm[0] == 'ulp' \
+        else f'ulp1x{pm[1]}'
 
 
 def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype, perm=None):
     """perm: None, 'reversed' (the segment order the rows are summed in; every
-    per-segment input permuted alike) or ('ulp', k) (observations and cells
-    with one ulp of seeded relative noise): the same statistics up to fp32
-    rounding"""
+    per-segment input permuted alike), ('ulp1', k) (observations and cells with
+    one ulp of seeded relative noise) or ('ulp', k) (observations, cells and
+    parameters with ~4 ulp): the same statistics up to fp32 rounding"""
     B0 = np.asarray(ob['rewards']).shape[0]
     order = np.arange(B0)[::-1].copy() if perm == 'reversed' else None
     noise = np.random.RandomState(977 * perm[1]) if isinstance(perm, tuple) else None
+    rel = 2.0 ** -24 if isinstance(perm, tuple) and perm[0] == 'ulp1' else 2.0 ** -22
+    noisy_params = isinstance(perm, tuple) and perm[0] == 'ulp'
 
     def f64(a, axis=0, noisy=False):
         a = np.asarray(a)
         if order is not None and a.ndim > axis and a.shape[axis] == B0:
             a = np.take(a, order, axis=axis)
-        if noisy and noise is not None:     # 4 ulp of relative noise, rounded to fp32
-            a = (a.astype(np.float64) * (1.0 + 2.0 ** -22 * noise.standard_normal(a.shape))).astype(np.float32)
+        if noisy and noise is not None:     # relative noise, rounded to fp32
+            a = (a.astype(np.float64) * (1.0 + rel * noise.standard_normal(a.shape))).astype(np.float32)
         return torch.as_tensor(a, dtype=torch.float32).to(dtype)
 
     def model(st, zf_):
-        if noise is not None:
+        if noisy_params:
             def pn(v):
                 v = np.asarray(v, dtype=np.float64)
                 return torch.from_numpy((v * (1.0 + 2.0 ** -22 * noise.standard_normal(v.shape))).astype(np.float32))
@@ -691,16 +717,22 @@ def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype, p
 
 
 def check_stats(stats, recomputed, report, rtol=RTOL_STAT, tag=''):
-    """|GPU - fp64| <= max(rtol * scale, 2 |fp32 - fp64|): the north_star's
-    1e-5, or twice what fp32 arithmetic itself costs this statistic at this
-    state (a gradient norm over 21504 rows whose ReLU masks near 0 decide
-    differently in any two fp32 executions)"""
-    for k, (v, scale, v32) in recomputed.items():
+    """|GPU - fp64| <= max(rtol * scale, 2 |fp32 - fp64|) over the STRICT
+    fp32 executions (recompute_stats): the north_star's 1e-5, or twice what
+    fp32 arithmetic itself costs this statistic at this state (a gradient norm
+    over 21504 rows whose ReLU masks near 0 decide differently in any two fp32
+    executions).  The WIDE set's bar is reported beside it, not applied; the
+    report names the variant that set each bar."""
+    for k, (v, scale, v32, v32w, ns, nw) in recomputed.items():
         assert k in stats, (k, sorted(stats))
         scale = max(scale, 1e-30)
         e = abs(stats[k] - v) / scale
         bar = max(rtol, 2.0 * abs(v32 - v) / scale)
+        bar_w = max(rtol, 2.0 * abs(v32w - v) / scale)
         ok = e <= bar
-        report[f'stat{tag}:{k}'] = (e, bar, ok)
+        report[f'stat{tag}:{k}'] = (e, bar, ok, None,
+                                    {'bar_applied': 'strict', 'bar_set_by': ns if bar > rtol else 'rtol',
+                                     'bar_wide': bar_w, 'bar_wide_set_by': nw if bar_w > rtol else 'rtol',
+                                     'over_north_star': bar > rtol})
         if not ok:
             report.setdefault('_fail', []).append(f'stat{tag}:{k}')

@@ -233,3 +233,12 @@ def test_rnn_gradients_match_autograd(B):
         print(name, 'max abs err / scale', float(err.max()) / scale,
               'frac > 1e-4 scale', float((err > 1e-4 * scale).double().mean()))
         assert float(err.max()) <= 1e-4 * scale, name
+
+
+def test_rnn_learn_wide_head_clip_norm():
+    # a head layer wider than 511 puts its weight gradient outside the grouped
+    # dW launch (dw_group_takes): the clip_grad_norm_ sum of squares must still
+    # cover it (the reducer-fused norm is off for such shapes; a GEMM that runs
+    # outside a bracket with the fused norm fails the flush) — grad_norm_actor /
+    # grad_norm_critic are checked against the oracle in _run_rnn
+    _run_rnn('adapt', B=9, T=6, H=2, D=11, A=4, Hd=24, hidden=(520, 32), epochs=(3, 3))
