@@ -641,6 +641,17 @@ int smi_layernorm_backward(const float* dy, int64_t ldg, const float* x, int64_t
                            int n, int relu_input, float* dx, int64_t lddx, float* dgamma,
                            float* dbeta, void* stream);
 
+/* Batched parameter-noise acting (ddpg_agent.py:134-151,172-173; param_noise.py:
+ * 17-24, 63-70): n agents, each with its own perturbed actor.  Row i of x
+ * ([n][ldx], in_dim used) goes through the parameter set at params + i *
+ * pstride: Linear(in, h1)-ReLU-Linear(h1, h2)-ReLU-Linear(h2, out)-out_act
+ * (0 none, 1 ReLU, 2 tanh: ActorNetworkX, builders.py:35-56, without
+ * LayerNorm); offsets6 (host) = the float offsets of W1 b1 W2 b2 W3 b3 inside
+ * one set.  One launch for all n agents; widths <= 1024 (else SMI_E_NOFIT). */
+int smi_mlp3_forward_stacked(const float* params, int64_t pstride, const int64_t* offsets6,
+                             int in_dim, int h1, int h2, int out_dim, int out_act, const float* x,
+                             int64_t ldx, int n, float* y, int64_t ldy, void* stream);
+
 /* Parameter publish (module_dict.py:22-35, parameter_server.py:40-55: the
  * state_dict D2H of ModuleDict.dumps): copy nbytes (multiple of 16, 16-byte
  * aligned) from device memory into PINNED host memory with a kernel on

@@ -167,6 +167,8 @@ _SIGS = {
     'smi_neg_mean_grad': (c_int, [P, c_i64, c_i64, P, P, P]),
     'smi_tanh_backward': (c_int, [P, c_i64, P, c_i64, c_i64, c_int, P, c_i64, P]),
     'smi_copy_cols': (c_int, [P, c_i64, c_i64, c_int, P, c_i64, P]),
+    'smi_mlp3_forward_stacked': (c_int, [P, c_i64, P, c_int, c_int, c_int, c_int, c_int, P, c_i64,
+                                         c_int, P, c_i64, P]),
     'smi_copy_to_host': (c_int, [P, P, c_i64, P]),
     'smi_copy_gather': (c_int, [P, P, P, P, c_int, P]),
     'smi_head_forward': (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_i64, c_i64, P, P, P, P,

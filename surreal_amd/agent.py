@@ -15,6 +15,9 @@ format: onetime [h, c] (rnn_layer, hidden) cells before the step, persistent
 Parameters come from the learner's modules (load_module_dict) or from a
 published numpy dict (load_numpy: ModuleDict.load, distributed/module_dict.py:47-63).
 """
+import ctypes
+import os
+
 import numpy as np
 import torch
 
@@ -161,6 +164,10 @@ class DDPGAgentBatch(object):
             self.pn_dist = [0.0] * self.n                      # total_action_distance
             self._pn_flats = None      # per agent: perturbed [perception | actor] device images
             self._pn_orig = None       # the fetched (unperturbed) images
+            self._pn_stack = None      # [N][P] perturbed actors (batched acting)
+            # SMI_PN_BATCHED=0: one forward per agent (A/B, and the pixel /
+            # LayerNorm forms always)
+            self._batched_pn = os.environ.get('SMI_PN_BATCHED', '1') != '0'
         if exp.noise_type not in ('normal', 'ou_noise'):
             raise ValueError('Noise type {} undefined.'.format(exp.noise_type))
         self.noise_type = exp.noise_type
@@ -209,6 +216,12 @@ class DDPGAgentBatch(object):
             self.model.load_state_dict(_np_state_to_torch(noisy))
             self._pn_flats.append([f.detach().clone() for f in self._acting_flats()])
         self._set_flats(self._pn_orig)
+        # the N perturbed actors stacked [N][P] for one batched forward
+        # (smi_mlp3_forward_stacked): low-dim observations, no LayerNorm
+        m = self.model
+        self._pn_stack = None
+        if not m.is_pixel_input and not m.actor.use_layernorm and self._batched_pn:
+            self._pn_stack = torch.stack([fl[-1] for fl in self._pn_flats]).contiguous()
 
     def _set_flats(self, imgs):
         for f, img in zip(self._acting_flats(), imgs):
@@ -235,13 +248,16 @@ class DDPGAgentBatch(object):
         unperturbed model's actions give total_action_distance
         (param_noise.py:41-46: assigned, not accumulated, as the reference does)"""
         m = self.model
-        rows = []
-        for i in range(self.n):
-            self._set_flats(self._pn_flats[i])
-            xi = self._perceive_row(obs, i) if m.is_pixel_input else x[i:i + 1]
-            rows.append(m.forward_actor(xi))
-        a = torch.cat(rows, 0)
-        self._set_flats(self._pn_orig)
+        if self._pn_stack is not None:
+            a = self._act_stacked(x)
+        else:      # pixel perception or LayerNorm actors: one forward per agent
+            rows = []
+            for i in range(self.n):
+                self._set_flats(self._pn_flats[i])
+                xi = self._perceive_row(obs, i) if m.is_pixel_input else x[i:i + 1]
+                rows.append(m.forward_actor(xi))
+            a = torch.cat(rows, 0)
+            self._set_flats(self._pn_orig)
         if self.param_noise_type == 'adaptive_normal':
             due = [i for i in range(self.n) if self.pn_i[i] % self.PN_DIST_INTERVAL == 0]
             if due:
@@ -250,6 +266,20 @@ class DDPGAgentBatch(object):
                     self.pn_dist[i] = float(((a0[i] - a[i]) ** 2).sum() ** 0.5)
             self.pn_i += 1
         return a
+
+    def _act_stacked(self, x):
+        """the N agents' perturbed actors as ONE launch: row i of x through
+        parameter set i of the [N][P] stack"""
+        act = self.model.actor
+        D, h1, h2, A = act.dims
+        offs = (ctypes.c_int64 * 6)(*[act.off(p) for wb in (act.wb(0), act.wb(1), act.wb(2))
+                                      for p in wb])
+        x = x.contiguous()
+        y = torch.empty(self.n, A, dtype=torch.float32, device=self.device)
+        st = self._pn_stack
+        L.call('smi_mlp3_forward_stacked', L.ptr(st), st.stride(0), offs, D, h1, h2, A, 2,
+               L.ptr(x), x.stride(0), self.n, L.ptr(y), A, L.stream(self.device))
+        return y
 
     def _perceive_row(self, obs, i):
         o = {'pixel': {'camera0': self._camera(obs['pixel']['camera0'])[i:i + 1]}}

@@ -123,13 +123,16 @@ int launch_copy_gather(void*, const void* const*, const int64_t*, const int64_t*
 bool head_fused_ok(int in, int64_t ldx, int h1, int h2, int out, const float* X,
                    const float* W1, const float* W2, const float* W3);
 struct PolRowArgs;
+int launch_mlp3_stacked(const float* P, int64_t pstride, const int64_t* o6, int in, int h1, int h2,
+                        int out, int act_out, const float* x, int64_t ldx, int n, float* y,
+                        int64_t ldy, hipStream_t st);
 int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, const float* W1,
                           const float* b1, int h1, const float* W2, const float* b2, int h2,
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
                           hipStream_t st, const int* skip, const float* vret = nullptr,
                           float* vgrad = nullptr, float vscale = 0.f,
-                          const PolRowArgs* ps = nullptr);
+                          const PolRowArgs* ps = nullptr, double* vpart = nullptr);
 bool head_fwd_ps_ok(int h1, int h2, int out);
 int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
@@ -538,6 +541,18 @@ int smi_copy_cols(const float* src, int64_t lds, int64_t rows, int cols, float* 
   REQUIRE(src && dst && rows >= 0 && cols > 0, "copy_cols: bad args");
   if (rows == 0) return SMI_OK;
   return launch_copy_cols(src, lds, rows, cols, dst, ldd, SMI_STREAM(stream));
+}
+
+int smi_mlp3_forward_stacked(const float* params, int64_t pstride, const int64_t* offsets6,
+                             int in_dim, int h1, int h2, int out_dim, int out_act, const float* x,
+                             int64_t ldx, int n, float* y, int64_t ldy, void* stream) {
+  REQUIRE(params && offsets6 && x && y && n >= 0 && pstride >= 0 && ldx >= in_dim && ldy >= out_dim &&
+              (out_act == 0 || out_act == 1 || out_act == 2),
+          "mlp3_forward_stacked: bad args");
+  for (int i = 0; i < 6; ++i) REQUIRE(offsets6[i] >= 0, "mlp3_forward_stacked: negative offset");
+  if (n == 0) return SMI_OK;
+  return launch_mlp3_stacked(params, pstride, offsets6, in_dim, h1, h2, out_dim, out_act, x, ldx, n, y,
+                             ldy, SMI_STREAM(stream));
 }
 
 int smi_copy_to_host(void* host_dst, const void* src, int64_t nbytes, void* stream) {

@@ -344,3 +344,67 @@ int launch_layernorm_bwd(const float* dy, int64_t ldg, const float* x, int64_t l
 }
 
 }  // namespace smi
+
+namespace smi {
+// ---- batched parameter-noise acting (ddpg_agent.py:134-151,172-173) --------
+// N agents, each with ITS OWN perturbed actor (param_noise.py:17-24 / 63-70):
+// row i of x goes through the parameter set at params + i * pstride (the
+// actor's flat layout, layer offsets o[0..5] = W1 b1 W2 b2 W3 b3), one
+// workgroup per agent, every layer's input in LDS; output unit j of a layer
+// is a wave's dot product (lanes over k, a fixed-order butterfly sum) plus
+// its bias, then ReLU (hidden) or the output activation.  One launch for all
+// N agents instead of N forwards.
+struct Mlp3StackedArgs {
+  const float* P; int64_t pstride;
+  int64_t o[6];
+  int in, h1, h2, out, act_out;
+  const float* x; int64_t ldx;
+  float* y; int64_t ldy;
+};
+constexpr int kMlp3MaxW = 1024;          // widest layer input / output
+
+__device__ __forceinline__ void mlp3_layer(const float* __restrict__ W, const float* __restrict__ b,
+                                           int K, int N, const float* __restrict__ a,
+                                           float* __restrict__ o, int act) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int j = wave; j < N; j += kWG / 64) {
+    const float* w = W + (int64_t)j * K;
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s = fmaf(w[k], a[k], s);
+    s = wave_sum(s);
+    if (lane == 0) {
+      float v = s + b[j];
+      if (act == ACT_RELU) v = v > 0.f ? v : 0.f;
+      else if (act == ACT_TANH) v = tanhf(v);
+      o[j] = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kWG) mlp3_stacked_kernel(Mlp3StackedArgs a) {
+  __shared__ float s0[kMlp3MaxW], s1[kMlp3MaxW], s2[kMlp3MaxW];
+  const int i = blockIdx.x;
+  const float* P = a.P + (int64_t)i * a.pstride;
+  for (int k = threadIdx.x; k < a.in; k += kWG) s0[k] = a.x[(int64_t)i * a.ldx + k];
+  __syncthreads();
+  mlp3_layer(P + a.o[0], P + a.o[1], a.in, a.h1, s0, s1, ACT_RELU);
+  __syncthreads();
+  mlp3_layer(P + a.o[2], P + a.o[3], a.h1, a.h2, s1, s2, ACT_RELU);
+  __syncthreads();
+  mlp3_layer(P + a.o[4], P + a.o[5], a.h2, a.out, s2, s0, a.act_out);
+  __syncthreads();
+  for (int k = threadIdx.x; k < a.out; k += kWG) a.y[(int64_t)i * a.ldy + k] = s0[k];
+}
+
+int launch_mlp3_stacked(const float* P, int64_t pstride, const int64_t* o6, int in, int h1, int h2,
+                        int out, int act_out, const float* x, int64_t ldx, int n, float* y,
+                        int64_t ldy, hipStream_t st) {
+  if (in < 1 || h1 < 1 || h2 < 1 || out < 1 || in > kMlp3MaxW || h1 > kMlp3MaxW ||
+      h2 > kMlp3MaxW || out > kMlp3MaxW)
+    return set_error(SMI_E_NOFIT, "mlp3_forward_stacked: layer widths must be in [1, 1024]");
+  Mlp3StackedArgs a{P, pstride, {o6[0], o6[1], o6[2], o6[3], o6[4], o6[5]}, in, h1, h2, out,
+                    act_out, x, ldx, y, ldy};
+  hipLaunchKernelGGL(mlp3_stacked_kernel, dim3(n), dim3(kWG), 0, st, a);
+  return check_launch("mlp3_stacked_kernel");
+}
+}  // namespace smi

@@ -63,6 +63,10 @@ struct HeadFwdArgs {
   // 8): the rows' sums of policy_rows_stats_kernel's pass from the means the
   // forward just formed, one PS_N partial per workgroup at ps.part
   PolRowArgs ps;
+  // with vgrad: the value statistics of the last value epoch (ppo.py:324-331,
+  // value_rows_kernel's sums {sum (V-R)^2, sum (R-V), sum (R-V)^2, sum R,
+  // sum R^2}), five fp64 per workgroup at vpart[blockIdx.x * 5 ..] (nullable)
+  double* vpart;
 };
 
 struct HeadBwdArgs {
@@ -495,6 +499,9 @@ head_fwd_kernel(HeadFwdArgs a) {
         *reinterpret_cast<float4*>(sR + ((wave * RT + rt) * 64 + lane) * 4) =
             float4{acc[rt][0][0], acc[rt][0][1], acc[rt][0][2], acc[rt][0][3]};
       hc_sync();
+      // value statistics of the rows (vpart; value_rows_kernel's per-row
+      // terms, ppo.py:324-331), summed below in a fixed order
+      double vs[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
       if (wave == 0 && li < a.out) {
         // one wait for the bias / target loads (and the HA2 copy-out stores
         // issued before them): without it the waitcnt pass, unsure of the bias
@@ -511,9 +518,26 @@ head_fwd_kernel(HeadFwdArgs a) {
                              (sR[((2 * RT + rt) * 64 + lane) * 4 + i] + sR[((3 * RT + rt) * 64 + lane) * 4 + i])) + bn;
             const float y = a.tanh_out ? tanhf(v) : v;
             a.Y[(r0 + r) * a.ldy + li] = y;
-            if (a.vgrad) a.vgrad[r0 + r] = a.vscale * (y - vr[rt][i]);
+            if (a.vgrad) {
+              const float rv = vr[rt][i];
+              a.vgrad[r0 + r] = a.vscale * (y - rv);
+              if (a.vpart) {
+                const float e = y - rv;
+                const double dd = (double)rv - (double)y;
+                vs[0] += (double)(e * e);
+                vs[1] += dd; vs[2] += dd * dd;
+                vs[3] += (double)rv; vs[4] += (double)rv * (double)rv;
+              }
+            }
             if constexpr (PS) smu[r * PA + li] = y;
           }
+      }
+      if (a.vpart && wave == 0) {        // lanes li >= out hold zeros
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const double t = wave_sum_d(vs[k]);
+          if (lane == 0) a.vpart[(int64_t)blockIdx.x * 5 + k] = t;
+        }
       }
     }
     if constexpr (PS) {
@@ -803,13 +827,15 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
                           const float* W3, const float* b3, int out, int tanh_out, float* HA1,
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
                           hipStream_t st, const int* skip, const float* vret, float* vgrad,
-                          float vscale, const PolRowArgs* ps) {
+                          float vscale, const PolRowArgs* ps, double* vpart) {
   if (rows <= 0) return SMI_OK;
   if (vgrad && (out != 1 || !vret)) return set_error(SMI_E_ARG, "head_forward: value epilogue needs out == 1");
+  if (vpart && !vgrad) return set_error(SMI_E_ARG, "head_forward: value statistics need the value epilogue");
   if (ps && !head_fwd_ps_ok(h1, h2, out)) return set_error(SMI_E_ARG, "head_forward: statistics epilogue shape");
   HeadFwdArgs a{X, ldx, in, W1, b1, W2, b2, W3, b3, h1, h2, out, tanh_out, HA1, HA2, Y, ldy,
                 W1T, W2T, rows, skip, hc_ld(in), hc_ld(h1), hc_ld(h2), vret, vgrad, vscale};
   if (ps) a.ps = *ps;
+  a.vpart = vpart;
   const int rt = hc_rt(rows);
   const int R = HC_R * rt;
   const size_t lds = (size_t)(R * ((a.ld0 > a.ld2 ? a.ld0 : a.ld2) + a.ld1) + hc_sr(rt)) * 4;

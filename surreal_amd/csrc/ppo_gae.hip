@@ -646,6 +646,11 @@ int launch_gae_windows(const float* values, float* values_masked, const float* r
   if (!faulted) {
     int rc = 0;
     // the reference defaults: RNN n_step 25 / horizon 5; non-RNN n_step 50
+    // 64-segment workgroups (19.5 KB of LDS, one wave: several resident per
+    // CU, so one block's stores overlap another's loads; 16 blocks at C3
+    // instead of 4); SMI_GAE_SEG=256: the round-5 256-segment blocks (A/B)
+    static const int seg = [] { const char* e = getenv("SMI_GAE_SEG"); return e && atoi(e) == 256 ? 256 : 64; }();
+    if (seg == 64 && try_gae_seg<25, 5, 64>(a, n_partials, stream, &rc)) return rc;
     if (try_gae_seg<25, 5, 256>(a, n_partials, stream, &rc)) return rc;
     if (try_gae_seg<50, 50, 128>(a, n_partials, stream, &rc)) return rc;
   }

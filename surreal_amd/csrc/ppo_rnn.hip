@@ -103,6 +103,19 @@ __host__ __device__ inline int rnn_nblk(int64_t rows, int nt = kWG) {
 // 336 CUs' worth of blocks instead of 84 four-wave blocks
 constexpr int kRowNT = 64;
 
+int head_bwd_blocks(int64_t rows);
+// doubles of s.part: 65536, or the value statistics' five per head workgroup
+static int64_t part_doubles(const RnnDims& d) {
+  const int64_t v = 5 * (int64_t)head_bwd_blocks(d.NE);
+  return v > 65536 ? v : 65536;
+}
+// the last value epoch's statistics from the critic head forward's epilogue
+// (SMI_VALUE_STATS_HEAD=0: value_rows_kernel; A/B knob)
+static bool use_value_stats_head() {
+  static const bool on = [] { const char* e = getenv("SMI_VALUE_STATS_HEAD"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   RnnScratch s{};
   float* p = static_cast<float*>(base);
@@ -146,7 +159,7 @@ static RnnScratch rnn_scratch(const RnnDims& d, void* base) {
   s.dA2 = take(px ? d.NE * d.G.flat : 0);
   s.dF = take(px ? d.NE * d.F : 0);
   s.cpart = take(px ? (int64_t)cnn_bwd_grid(d.NE) * d.G.nconv : 0);
-  s.part = reinterpret_cast<double*>(take(2 * 4096 * 16));   // 65536 doubles
+  s.part = reinterpret_cast<double*>(take(2 * part_doubles(d)));   // >= 65536 doubles
   s.gaepart = reinterpret_cast<double*>(take(2 * 2 * 2048));
   s.ci = reinterpret_cast<int*>(take(CI_COUNT));
   s.cf = take(CF_COUNT);
@@ -1306,7 +1319,7 @@ int launch_head_fwd_fused(const float* X, int64_t ldx, int64_t rows, int in, con
                           float* HA2, float* Y, int64_t ldy, float* W1T, float* W2T,
                           hipStream_t st, const int* skip, const float* vret = nullptr,
                           float* vgrad = nullptr, float vscale = 0.f,
-                          const PolRowArgs* ps = nullptr);
+                          const PolRowArgs* ps = nullptr, double* vpart = nullptr);
 bool head_fwd_ps_ok(int h1, int h2, int out);
 int launch_head_bwd_fused(const float* dZ, int out, int64_t rows, const float* W3,
                           const float* W2T, const float* W1T, int h1, int h2, int dx0, int dxn,
@@ -1329,7 +1342,8 @@ static bool head_fused(const Head& h, const float* X, int64_t ldx) {
 static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, float* HA1,
                     float* HA2, float* Y, hipStream_t st, const int* skip, float* wT = nullptr,
                     const float* vret = nullptr, float* vgrad = nullptr, float vscale = 0.f,
-                    bool* vdone = nullptr, const PolRowArgs* ps = nullptr) {
+                    bool* vdone = nullptr, const PolRowArgs* ps = nullptr,
+                    double* vpart = nullptr) {
   const MlpLayout& L = h.L;
   if (vdone) *vdone = false;
   if (head_fused(h, X, ldx)) {
@@ -1338,7 +1352,8 @@ static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, fl
     return launch_head_fwd_fused(X, ldx, rows, h.in, h.P + L.fW1, h.P + L.fb1, h.h1, h.P + L.fW2,
                                  h.P + L.fb2, h.h2, h.P + L.fW3, h.P + L.fb3, h.out, h.tanh_out,
                                  HA1, HA2, Y, h.out, wT, wT ? wT + (int64_t)h.in * h.h1 : nullptr,
-                                 st, skip, ve ? vret : nullptr, ve ? vgrad : nullptr, vscale, ps);
+                                 st, skip, ve ? vret : nullptr, ve ? vgrad : nullptr, vscale, ps,
+                                 ve ? vpart : nullptr);
   }
   if (ps) return set_error(SMI_E_ARG, "head_forward: the statistics epilogue needs the fused head");
   const int M = (int)rows;
@@ -1883,12 +1898,18 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       // dV = 2 (V - R) / N: written by the head forward's epilogue, except in
       // the last epoch, whose value_rows pass also sums the statistics of
       // ppo.py:324-331 (and on the layer-GEMM path)
+      // (round 6: the last epoch's statistics too, one 5-double partial per
+      // head workgroup, when the fused head runs and the partials fit s.part)
       const bool last = e == a.epoch_baseline - 1;
       const float vscale = (float)(2.0 / (double)NEg);
       bool vdone = false;
+      const bool vstats = last && use_value_stats_head() &&
+                          5 * (int64_t)head_bwd_blocks(d.NE) <= part_doubles(d);
       RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, nullptr,
-                  s.wT, last ? nullptr : s.ret_tm, last ? nullptr : s.dOUT, vscale, &vdone));
-      const int nb = rnn_nblk((d.NE + 3) / 4, kRowNT);     // 4 rows per thread
+                  s.wT, last && !vstats ? nullptr : s.ret_tm, last && !vstats ? nullptr : s.dOUT,
+                  vscale, &vdone, nullptr, vstats ? s.part : nullptr));
+      int nb = rnn_nblk((d.NE + 3) / 4, kRowNT);           // 4 rows per thread
+      if (vdone && vstats) nb = head_bwd_blocks(d.NE);     // the head forward's partials
       if (!vdone) {
         const int kt = ktime_begin(st);
         hipLaunchKernelGGL(value_rows_kernel<kRowNT>, dim3(nb), dim3(kRowNT), 0, st, s.OUT, s.ret_tm, d.B,

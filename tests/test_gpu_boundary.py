@@ -499,3 +499,51 @@ def test_ppo_graph_replay_bit_exact(kind):
             assert torch.equal(v, graph.optimizer_state()[k]), (it, k)
         assert eager.last_stats() == graph.last_stats(), it
     assert graph._graph is not None
+
+
+@pytest.mark.parametrize('pn', ['normal', 'adaptive_normal'])
+def test_ddpg_param_noise_acting_is_one_batched_forward(pn, monkeypatch):
+    """With parameter noise, N = 16 agents' perturbed actors run as ONE launch
+    (smi_mlp3_forward_stacked over the [N][P] stack of perturbed actors), with
+    the actions of the per-agent loop (one forward per agent, SMI_PN_BATCHED=0
+    form) up to fp32 summation order; ddpg_agent.py:134-151,172-173."""
+    from surreal_amd import _lib as L
+    lc = copy.deepcopy(DDPG_DEFAULT_LEARNER_CONFIG)
+    ex = lc.algo.exploration
+    ex.noise_type = 'normal'
+    ex.param_noise_type = pn
+    ex.param_noise_sigma, ex.param_noise_alpha, ex.param_noise_target_stddev = 0.05, 1.15, 0.02
+    D, A, N = 17, 6, 16
+    ec = gym_env_config(D, A)
+    bat = DDPGAgentBatch(lc, ec, N, seed=4)
+    loop = DDPGAgentBatch(lc, ec, N, seed=4)
+    loop._batched_pn = False
+    base = {k: v.detach().cpu().numpy() for k, v in bat.model.state_dict().items()}
+    rs = np.random.RandomState(3)
+    for fetch in range(2):
+        params = {'ddpg': {k: v + 0.01 * fetch for k, v in base.items()}}
+        for ag in (bat, loop):
+            np.random.seed(21 + fetch)
+            ag.load_numpy(copy.deepcopy(params))
+        assert bat._pn_stack is not None and bat._pn_stack.shape[0] == N and loop._pn_stack is None
+        for step in range(11):
+            obs = rs.randn(N, D)
+            calls = []
+            orig = L.call
+
+            def spy(name, *a):
+                calls.append(name)
+                return orig(name, *a)
+            np.random.seed(100 + step)
+            monkeypatch.setattr(L, 'call', spy)
+            a_b = bat.act(obs)
+            monkeypatch.setattr(L, 'call', orig)
+            np.random.seed(100 + step)
+            a_l = loop.act(obs)
+            assert max_rel_err(a_b, a_l, floor=1e-2) < 1e-5, (fetch, step)
+            # one batched forward (+ the unperturbed forward of the adaptive
+            # distance measurement on its due steps): never one per agent
+            assert calls.count('smi_mlp3_forward_stacked') == 1, calls
+            assert calls.count('smi_linear_forward') <= 3, calls
+        if pn == 'adaptive_normal':
+            np.testing.assert_allclose(bat.pn_dist, loop.pn_dist, rtol=1e-4, atol=1e-7)
