@@ -352,6 +352,28 @@ gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, GemmArgs g, con
   const int64_t ec = e < MN ? e : MN - 1;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int z = zl;
+  if (S <= 64) {
+    // every slab of the thread (z = zl + 4k) in flight at once, then the same
+    // additions in the same order as the loop below (bit-identical): one
+    // memory round trip instead of one per four slabs
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int zk = zl + 4 * k;
+      v[k] = zk < S ? part[(int64_t)zk * MN + ec] : 0.f;
+    }
+    const int nfull = S > zl + 12 ? (S - zl - 12 + 15) / 16 : 0;   // z + 12 < S trips
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < nfull) {
+        s0 += v[4 * j]; s1 += v[4 * j + 1]; s2 += v[4 * j + 2]; s3 += v[4 * j + 3];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k >= 4 * nfull && zl + 4 * k < S) s0 += v[k];
+    z = S;
+  }
   for (; z + 12 < S; z += 16) {
     s0 += part[(int64_t)z * MN + ec];
     s1 += part[(int64_t)(z + 4) * MN + ec];
@@ -1112,7 +1134,26 @@ __device__ void dw_epilogue_block(const DwEpilogue& x, int nsq) {
     // d log_var[j] = std_j * sum_blocks lvpart[.][j] (logvar_grad_kernel's order)
     for (int j = wave; j < x.lv_A; j += kWG / 64) {
       float t = 0.f;
-      for (int i = lane; i < x.lv_nb; i += 64) t += x.lvpart[(int64_t)i * x.lv_A + j];
+      int i = lane;
+      // 16 of the lane's partials in flight per trip (same additions, same order)
+      for (; i + 15 * 64 < x.lv_nb; i += 16 * 64) {
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = x.lvpart[(int64_t)(i + 64 * k) * x.lv_A + j];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t += v[k];
+      }
+      {
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int ik = i + 64 * k;
+          v[k] = ik < x.lv_nb ? x.lvpart[(int64_t)ik * x.lv_A + j] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (i + 64 * k < x.lv_nb) t += v[k];
+      }
       t = wave_sum(t);
       const float gv = t * expf(x.lv[j]);
       if (lane == 0) {
@@ -1157,6 +1198,28 @@ gemm_group_reduce_kernel(DwGroup G) {
   const int64_t ec = e < MN ? e : MN - 1;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int z = zl;
+  if (S <= 64) {
+    // every slab of the thread (z = zl + 4k) in flight at once, then the same
+    // additions in the same order as the loop below (bit-identical): one
+    // memory round trip instead of one per four slabs
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int zk = zl + 4 * k;
+      v[k] = zk < S ? part[(int64_t)zk * MN + ec] : 0.f;
+    }
+    const int nfull = S > zl + 12 ? (S - zl - 12 + 15) / 16 : 0;   // z + 12 < S trips
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < nfull) {
+        s0 += v[4 * j]; s1 += v[4 * j + 1]; s2 += v[4 * j + 2]; s3 += v[4 * j + 3];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k >= 4 * nfull && zl + 4 * k < S) s0 += v[k];
+    z = S;
+  }
   for (; z + 12 < S; z += 16) {
     s0 += part[(int64_t)z * MN + ec];
     s1 += part[(int64_t)(z + 4) * MN + ec];

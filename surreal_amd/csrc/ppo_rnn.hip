@@ -1021,14 +1021,22 @@ adam_split_kernel(AdamSplitArgs a) {
     vf = a.v[i_first];
   }
   const int np = a.np_dev ? a.np_dev[0] : a.np;
-  double s4[4] = {0.0, 0.0, 0.0, 0.0};       // four partials in flight per thread
-  int i0 = threadIdx.x;
-  for (; i0 + 3 * kWG < np; i0 += 4 * kWG) {
+  // every partial of the thread in flight at once: one memory round trip for
+  // np <= 16 * kWG (the dW reducer's ~2300 at C3 widths; four in flight per
+  // trip took three), summed in a fixed order
+  constexpr int U = 16;
+  double s = 0.0;
+  for (int i0 = threadIdx.x; i0 < np; i0 += U * kWG) {
+    double v[U];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) s4[k] += a.part[i0 + k * kWG];
+    for (int k = 0; k < U; ++k) {
+      const int i = i0 + k * kWG;
+      v[k] = i < np ? a.part[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) s += v[k];
   }
-  for (; i0 < np; i0 += kWG) s4[0] += a.part[i0];
-  double s = block_sum_d((s4[0] + s4[1]) + (s4[2] + s4[3]), red);
+  s = block_sum_d(s, red);
   const int t = a.step[0];      // already bumped (sumsq_part_kernel or the dW reducer's epilogue)
   if (threadIdx.x == 0) {
     const float norm = (float)sqrt(s);

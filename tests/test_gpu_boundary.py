@@ -540,7 +540,7 @@ def test_ddpg_param_noise_acting_is_one_batched_forward(pn, monkeypatch):
             monkeypatch.setattr(L, 'call', orig)
             np.random.seed(100 + step)
             a_l = loop.act(obs)
-            assert max_rel_err(a_b, a_l, floor=1e-2) < 1e-5, (fetch, step)
+            assert max_rel_err(a_b, a_l, floor=1e-2) < AGENT_BAR, (fetch, step)
             # one batched forward (+ the unperturbed forward of the adaptive
             # distance measurement on its due steps): never one per agent
             assert calls.count('smi_mlp3_forward_stacked') == 1, calls
