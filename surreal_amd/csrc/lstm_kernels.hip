@@ -1228,9 +1228,15 @@ lstm_bwd_v_kernel(LstmBwdArgs a) {
 // a1: a second, independent sequence set in the same launch (workgroups >=
 // a0.B: the GAE critic pass and the reference policy's forward, two weight
 // sets over two inputs); single launches pass a0 twice over a0.B workgroups
-template <int KQ, int XQ, bool XM, int WI>
+// A4 (x staged, XQ > 0): every lane finishes all four gates of its unit (after
+// the two quad DPP adds each lane holds all four sums, and xP keeps unit u's
+// four x parts at 4u .. 4u + 3): four independent activations instead of one
+// followed by four quad broadcasts on the step's dependent chain (same ops on
+// the same values: bit-identical)
+template <int KQ, int XQ, bool XM, int WI, bool A4 = false>
 __global__ void __launch_bounds__(kVT)
 lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
+  static_assert(!A4 || XQ > 0, "A4 reads the staged x parts");
   static_assert(WI != 2 || KQ % 4 == 0, "float4 k runs");
   const bool second = (int)blockIdx.x >= a0.B;
   const LstmFwdArgs& a = second ? a1 : a0;
@@ -1426,8 +1432,11 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
   for (int t = 0; t < a.S; ++t) {
     const float* hp = hS[t & 1] + (WI == 2 ? 4 * q : WI ? 2 * q : q * KQ);
     float* hn = hS[(t + 1) & 1];
-    float xacc;
-    if constexpr (XQ > 0) {
+    float xacc = 0.f;
+    float4 x4 = float4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (A4) {
+      x4 = *reinterpret_cast<const float4*>(xP + (int64_t)t * NT + 4 * uc);
+    } else if constexpr (XQ > 0) {
       xacc = xP[(int64_t)t * NT + tid];
     } else {
       xacc = xnext + bh;
@@ -1474,11 +1483,20 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
       pj[j] += dpp_x1(pj[j]);
       pj[j] += dpp_x2(pj[j]);
     }
-    const float mine = q == 0 ? pj[0] : q == 1 ? pj[1] : q == 2 ? pj[2] : pj[3];
-    const float pre = xacc + mine;
-    const float av = q == 2 ? ftanh(pre) : sigm(pre);
-    const float ig = quad_bcast<0>(av), fg = quad_bcast<1>(av);
-    const float cg = quad_bcast<2>(av), og = quad_bcast<3>(av);
+    float ig, fg, cg, og, av;
+    if constexpr (A4) {
+      ig = sigm(x4.x + pj[0]);
+      fg = sigm(x4.y + pj[1]);
+      cg = ftanh(x4.z + pj[2]);
+      og = sigm(x4.w + pj[3]);
+      av = q == 0 ? ig : q == 1 ? fg : q == 2 ? cg : og;
+    } else {
+      const float mine = q == 0 ? pj[0] : q == 1 ? pj[1] : q == 2 ? pj[2] : pj[3];
+      const float pre = xacc + mine;
+      av = q == 2 ? ftanh(pre) : sigm(pre);
+      ig = quad_bcast<0>(av); fg = quad_bcast<1>(av);
+      cg = quad_bcast<2>(av); og = quad_bcast<3>(av);
+    }
     const float c = fg * creg + ig * cg;
     const float h = og * ftanh(c);
     creg = c;
@@ -1608,10 +1626,16 @@ static void fwd_q_dispatch(const LstmFwdArgs& a, hipStream_t st, const LstmFwdAr
   // W_hh register layout (SMI_LSTM_WI; A/B knob): 0 a contiguous quarter row
   // per lane, 1 k pairs interleaved over the quad, 2 float4 runs interleaved
   static const int wi = [] { const char* e = getenv("SMI_LSTM_WI"); return e && e[0] ? atoi(e) : 2; }();
+  // all four gates finished in every lane (SMI_LSTM_A4=0: one gate per lane +
+  // quad broadcasts; A/B knob)
+  static const bool a4 = [] { const char* e = getenv("SMI_LSTM_A4"); return !(e && e[0] == '0'); }();
   const size_t lds = XQ > 0 ? lstm_fwd_v_lds(smax, 1, 4 * XQ, blk.x) : 0;
 #define SMI_FQ(KQ, W)                                                              \
   do {                                                                             \
-    if (xm) {                                                                      \
+    if (xm && a4) {                                                                \
+      allow_lds(lstm_fwd_q_kernel<KQ, XQ, true, W, XQ != 0>, lds);                 \
+      hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ, true, W, XQ != 0>), grid, blk, lds, st, a, a2); \
+    } else if (xm) {                                                               \
       allow_lds(lstm_fwd_q_kernel<KQ, XQ, true, W>, lds);                          \
       hipLaunchKernelGGL((lstm_fwd_q_kernel<KQ, XQ, true, W>), grid, blk, lds, st, a, a2);  \
     } else {                                                                       \
