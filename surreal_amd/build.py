@@ -16,7 +16,7 @@ BUILD = os.path.join(ROOT, 'build', 'obj')
 LIB = os.path.join(HERE, 'libsurreal_mi.so')
 SOURCES = ['ppo_gae.hip', 'ppo_epochs.hip', 'ops_kernels.hip', 'sampler_kernels.hip',
            'linear_kernels.hip', 'ddpg_kernels.hip', 'lstm_kernels.hip', 'cnn_kernels.hip', 'head_kernels.hip', 'ppo_rnn.hip', 'calib_kernels.hip', 'capi.hip']
-HEADERS = ['smi_device.hpp', 'smi_internal.hpp']
+HEADERS = ['smi_device.hpp', 'smi_internal.hpp', 'lstm_cell.hpp', 'pol_rows.hpp']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 CXXFLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-mcode-object-version=5',
@@ -67,7 +67,9 @@ VARIANTS = {None: [], 'prof': ['-DSMI_PROF'], 'noinl': ['-DSMI_DENSE_NOINLINE'],
             'dwtrace': ['-DSMI_DWD_DIAG=3'], 'dwtrace_mfma': ['-DSMI_DWD_DIAG=1', '-DSMI_DWD_TRACE=1'],
             # test-only fault injection (tests/negative_controls.py): the parity
             # checks must FAIL on this build's deliberate departures
-            'fault': ['-DSMI_FAULT_INJECTION']}
+            'fault': ['-DSMI_FAULT_INJECTION'],
+            # round 6 A/B: the BPTT's recurrent dot product in four FMA chains
+            'ch4': ['-DSMI_BPTT_CH4=1']}
 
 
 def lib_path(variant=None):

@@ -1110,7 +1110,7 @@ template <int BR>
 __global__ void __launch_bounds__(kVT, 1)
 lstm_bwd_dw_kernel(LstmBwdArgs la, DwGroup G) {
   if ((int)blockIdx.x < la.B) {
-    lstm_bwd_q_body<BR>(la, blockIdx.x);
+    lstm_bwd_q_body<BR, SMI_BPTT_CH4 != 0>(la, blockIdx.x);
     return;
   }
   extern __shared__ float4 dwd_red[];

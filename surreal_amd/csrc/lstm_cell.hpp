@@ -92,7 +92,12 @@ __device__ __forceinline__ float dpp_ror8(float v) {          // row_ror:8
 // BPTT of one segment (b) at one segment per workgroup (the K-split form,
 // lstm_kernels.hip): BR rows of W_hh per lane of a 16-lane row (16 BR >= 4H),
 // BRP their padding to whole b128 reads
-template <int BR>
+// CH4: the recurrent dot product in four FMA chains instead of two (build
+// knob SMI_BPTT_CH4, variant 'ch4' of surreal_amd/build.py)
+#ifndef SMI_BPTT_CH4
+#define SMI_BPTT_CH4 0
+#endif
+template <int BR, bool CH4 = false>
 __device__ __forceinline__ void lstm_bwd_q_body(const LstmBwdArgs& a, int b) {
   if (a.skip && a.skip[0] != 0) return;
   constexpr int BRP = (BR + 3) & ~3;
@@ -167,12 +172,31 @@ __device__ __forceinline__ void lstm_bwd_q_body(const LstmBwdArgs& a, int b) {
 #pragma unroll
     for (int i = 0; i < BRP / 4; ++i) dv[i] = dp[i];
     vf2 p01 = {0.f, 0.f}, p23 = {0.f, 0.f};
+    if constexpr (CH4) {
+      // four FMA chains (even / odd rows), half as long, summed at the end
+      vf2 q01 = {0.f, 0.f}, q23 = {0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const float d = (i & 3) == 0 ? dv[i >> 2].x : (i & 3) == 1 ? dv[i >> 2].y
-                    : (i & 3) == 2 ? dv[i >> 2].z : dv[i >> 2].w;
-      p01 = __builtin_elementwise_fma(vf2{d, d}, w01[i], p01);
-      p23 = __builtin_elementwise_fma(vf2{d, d}, w23[i], p23);
+      for (int i = 0; i < BR; ++i) {
+        const float d = (i & 3) == 0 ? dv[i >> 2].x : (i & 3) == 1 ? dv[i >> 2].y
+                      : (i & 3) == 2 ? dv[i >> 2].z : dv[i >> 2].w;
+        if (i & 1) {
+          q01 = __builtin_elementwise_fma(vf2{d, d}, w01[i], q01);
+          q23 = __builtin_elementwise_fma(vf2{d, d}, w23[i], q23);
+        } else {
+          p01 = __builtin_elementwise_fma(vf2{d, d}, w01[i], p01);
+          p23 = __builtin_elementwise_fma(vf2{d, d}, w23[i], p23);
+        }
+      }
+      p01 = p01 + q01;
+      p23 = p23 + q23;
+    } else {
+#pragma unroll
+      for (int i = 0; i < BR; ++i) {
+        const float d = (i & 3) == 0 ? dv[i >> 2].x : (i & 3) == 1 ? dv[i >> 2].y
+                      : (i & 3) == 2 ? dv[i >> 2].z : dv[i >> 2].w;
+        p01 = __builtin_elementwise_fma(vf2{d, d}, w01[i], p01);
+        p23 = __builtin_elementwise_fma(vf2{d, d}, w23[i], p23);
+      }
     }
     float pu[4] = {p01.x, p01.y, p23.x, p23.y};
 #pragma unroll

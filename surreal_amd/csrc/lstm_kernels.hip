@@ -1519,7 +1519,7 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
 template <int BR>
 __global__ void __launch_bounds__(kVT)
 lstm_bwd_q_kernel(LstmBwdArgs a) {
-  lstm_bwd_q_body<BR>(a, blockIdx.x);
+  lstm_bwd_q_body<BR, SMI_BPTT_CH4 != 0>(a, blockIdx.x);
 }
 #endif  // SMI_LSTM_VALU_HALF
 
