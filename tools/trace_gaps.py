@@ -5,8 +5,8 @@
 
 Prints, per kernel name (template arguments cut), launches, mean duration and
 mean gap from the previous kernel's end to this kernel's start (same queue),
-over the dispatches of the last N learn() calls (a learn() starts at each
-zf_tmajor / zf_pipe launch)."""
+over the dispatches of the last N learn() calls (a learn() ends with its
+rnn_final_kernel launch)."""
 import csv
 import glob
 import os
@@ -33,9 +33,9 @@ def main():
             for r in csv.DictReader(fh):
                 rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']))
     rows.sort()
-    starts = [i for i, r in enumerate(rows) if 'zf_tmajor' in r[2] or 'zf_pipe' in r[2]]
-    if len(starts) > last:
-        rows = rows[starts[-last - 1]:starts[-1]] if len(starts) > last else rows
+    ends = [i for i, r in enumerate(rows) if 'rnn_final_kernel' in r[2]]
+    if len(ends) > last:
+        rows = rows[ends[-last - 1] + 1:ends[-1] + 1]
     dur, gap, cnt = defaultdict(float), defaultdict(float), defaultdict(int)
     prev_end = None
     for s, e, n in rows:
