@@ -1242,6 +1242,7 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
   const LstmFwdArgs& a = second ? a1 : a0;
   const int b = second ? (int)blockIdx.x - a0.B : (int)blockIdx.x;
   if (a.skip && a.skip[0] != 0) return;
+  LSTM_T0();
   const int keepS = a.keep > 0 ? a.keep : a.S;
   static_assert(KQ % 2 == 0 && XQ % 4 == 0, "K split: pairs of h, float4 runs of x");
   constexpr int KX = 4 * XQ, KXS = XQ > 0 ? KX : 4;
@@ -1303,6 +1304,7 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
     }
   }
   __syncthreads();
+  LSTM_TICK(0);                                  // x staged, c0 / h0, W_ih issued
   // W_hh rows j*H + u over the k pairs (8i + 2q, 8i + 2q + 1), i < KQ / 2: the
   // quad's four lanes read 32 contiguous bytes of a row per load (a lane-
   // contiguous quarter row put every lane of a load on its own cache line: the
@@ -1384,6 +1386,7 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
       }
     }
     __syncthreads();
+    LSTM_TICK(1);                                // x parts on the matrix cores
   } else if constexpr (XQ > 0) {
     // x parts of every step: W_ih rows j*H + u over x columns [q*XQ, q*XQ + XQ)
     float wx[4][XQ];
@@ -1420,6 +1423,7 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
     }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): W_hh (and xproj of step 0) landed
+  LSTM_TICK(2);                                  // W_hh wait
   float* hb = a.hbuf + BH + (int64_t)b * H + uc;
   float* cb = a.cbuf ? a.cbuf + BH + (int64_t)b * H + uc : nullptr;
   float* gp = a.gates ? a.gates + (int64_t)b * G4 + g : nullptr;
@@ -1504,6 +1508,7 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
     ph = h; pc = c; pav = av;
     __syncthreads();
   }
+  LSTM_TICK(3);                                  // the step loop
   if (a.S > 0 && act) {
     if (q == 0) {
       hb[0] = ph;
@@ -1519,7 +1524,9 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
 template <int BR>
 __global__ void __launch_bounds__(kVT)
 lstm_bwd_q_kernel(LstmBwdArgs a) {
+  LSTM_T0();
   lstm_bwd_q_body<BR, SMI_BPTT_CH4 != 0>(a, blockIdx.x);
+  LSTM_TICK(4);                                  // the whole BPTT (its own launch)
 }
 #endif  // SMI_LSTM_VALU_HALF
 
