@@ -1897,7 +1897,7 @@ static bool use_bwd_dw() {
 
 int launch_lstm_bwd_dw(const float* dh, const float* gates, const float* cbuf, const float* w_hh,
                        int S, int B, int H, float* dgates, hipStream_t st, const int* skip) {
-  const int br = lstm_bwd_q_form(B, H);
+  const int br = lstm_bwd_q_form(B, H, w_hh);
   if (!use_bwd_dw() || !g_grp_on || g_pre_on || g_grp.n == 0 || br == 0 || S <= 0 || B <= 0)
     return SMI_E_NOFIT;
   int cus = 0, dev = 0;

@@ -111,26 +111,22 @@ __device__ __forceinline__ void lstm_bwd_q_body(const LstmBwdArgs& a, int b) {
   const int64_t BH = (int64_t)B * H;
   const int ug = tid >> 4, rr = tid & 15;
   for (int e = tid; e < 2 * 16 * BRP; e += blockDim.x) (&dG[0][0])[e] = 0.f;
-  // W_hh[r][4ug + i], r in [rr*BR, rr*BR + BR) (rows past 4H and units past H read as 0)
+  // W_hh[r][4ug + i], r in [rr*BR, rr*BR + BR)
   vf2 w01[BR], w23[BR];
   {
-    const bool vec = (H & 3) == 0 && (reinterpret_cast<uintptr_t>(a.w_hh) & 15) == 0 && 4 * ug + 3 < H;
+    // float4 loads (lstm_bwd_q_ok: H % 4 == 0 and a 16-byte aligned W_hh),
+    // unconditional from clamped addresses with nothing selected on them: a
+    // per-lane condition (or a run-time vector / scalar branch) turned the loads
+    // into single dwords behind branches with a vmcnt(0) wait at each merge
+    // (round 6).  Rows past 4H meet the zero padding of the dgates image; units
+    // past H feed only lanes whose results are dropped.
+    const int c0 = min(4 * ug, H - 4);
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      const int r = rr * BR + i;
-      const bool rok = r < G4;
-      const float* row = a.w_hh + (int64_t)(rok ? r : 0) * H;
-      if (vec) {
-        const float4 v = rok ? *reinterpret_cast<const float4*>(row + 4 * ug) : float4{0.f, 0.f, 0.f, 0.f};
-        w01[i] = vf2{v.x, v.y};
-        w23[i] = vf2{v.z, v.w};
-      } else {
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = rok && 4 * ug + k < H ? row[4 * ug + k] : 0.f;
-        w01[i] = vf2{v[0], v[1]};
-        w23[i] = vf2{v[2], v[3]};
-      }
+      const int r = min(rr * BR + i, G4 - 1);
+      const float4 v = *reinterpret_cast<const float4*>(a.w_hh + (int64_t)r * H + c0);
+      w01[i] = vf2{v.x, v.y};
+      w23[i] = vf2{v.z, v.w};
     }
   }
   const int dgi = (g / BR) * BRP + g % BR;        // this lane's dgate in the padded image

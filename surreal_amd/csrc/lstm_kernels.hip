@@ -1241,7 +1241,9 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
   const bool second = (int)blockIdx.x >= a0.B;
   const LstmFwdArgs& a = second ? a1 : a0;
   const int b = second ? (int)blockIdx.x - a0.B : (int)blockIdx.x;
-  if (a.skip && a.skip[0] != 0) return;
+  // the skip flag is read with the prologue's loads and tested before the
+  // first global store (its own round trip in front of them cost ~1 us)
+  const int skipv = a.skip ? a.skip[0] : 0;
   LSTM_T0();
   const int keepS = a.keep > 0 ? a.keep : a.S;
   static_assert(KQ % 2 == 0 && XQ % 4 == 0, "K split: pairs of h, float4 runs of x");
@@ -1255,101 +1257,143 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
   const int uc = act ? u : H - 1;
   const int g = q * H + uc;
   const int64_t BH = (int64_t)B * H;
-  float bh = a.b_hh[g];
-  // x staging, c0 / h0 (every load issued before W_hh's)
+  // Round 6: the prologue issues all of its loads (biases, c0 / h0, the
+  // matrix-core W_ih operands, the x sequence) before waiting on any, each
+  // unconditionally from a clamped address with nothing selected on it
+  // afterwards.  A load whose value was used under a per-lane condition was
+  // sunk into its own exec-masked branch with a vmcnt(0) wait at the merge,
+  // and loads behind a dependent store waited for it: one memory round trip
+  // per load group.  Padding needs no select: a weight loaded for k past the
+  // row (or for a gate row / unit past the shape) only ever multiplies a zero
+  // of the LDS-staged x / h images (or feeds a result that is dropped), and
+  // x * 0 = +-0 leaves every sum bit-identical; the staged x / h0 images get
+  // their zeros by a multiply.
+  // the x sequence's first XB * NT elements (all of it up to S * KX = 7168
+  // at KX 48 on 448 threads), issued first; stored to LDS after the rest
+  constexpr int XB = 4;                           // x loads in flight per thread
+  float xv[XB];
   if constexpr (XQ > 0) {
-    bh += a.b_ih[g];
-    for (int e = tid; e < a.S * KX; e += NT) {
+#pragma unroll
+    for (int j = 0; j < XB; ++j) {
+      const int e = min(tid + j * NT, a.S * KX - 1);
       const int t = e / KX, k = e - t * KX;
-      xS[e] = k < a.din ? a.x[((int64_t)t * B + b) * a.ldx + k] : 0.f;
+      xv[j] = a.x[((int64_t)t * B + b) * a.ldx + min(k, a.din - 1)];
     }
   }
-  float creg = a.c0[(int64_t)b * H + uc];
-  if (act && q == 0 && a.cbuf) a.cbuf[(int64_t)b * H + u] = creg;
-  for (int e = tid; e < 4 * KQ; e += NT) {
-    const float v = e < H ? a.h0[(int64_t)b * H + e] : 0.f;
-    hS[0][e] = v;
-    hS[1][e] = 0.f;
-    if (e < H) a.hbuf[(int64_t)b * H + e] = v;
-  }
-  // the matrix-core x parts' B operands (W_ih^T, below), issued before W_hh's
-  // so that the x parts wait on them alone: wave w's gate tiles w + ti*NW
-  // (ti < 4 covers ceil(H/4) tiles over ceil(H/16) waves).  The k order is
-  // permuted so a lane's operands are contiguous: MFMA step s of lane l takes
-  // k = 16 (s >> 2) + 4 (l >> 4) + (s & 3) (A from the staged x rows alike), so
-  // the four lane groups of a row read 64 contiguous bytes per k chunk
+  const float bhh = a.b_hh[g];
+  const float bih = XQ > 0 ? a.b_ih[g] : 0.f;
+  const float creg0 = a.c0[(int64_t)b * H + uc];
+  const float h0v = a.h0[(int64_t)b * H + min(tid, H - 1)];   // (NT >= 4 KQ: one h0 slot per thread)
+  // the matrix-core x parts' B operands (W_ih^T, below) and bias sums, issued
+  // before W_hh's so that the x parts wait on them alone: wave w's gate tiles
+  // w + ti*NW (ti < 4 covers ceil(H/4) tiles over ceil(H/16) waves).  The k
+  // order is permuted so a lane's operands are contiguous: MFMA step s of lane
+  // l takes k = 16 (s >> 2) + 4 (l >> 4) + (s & 3) (A from the staged x rows
+  // alike), so the four lane groups of a row read 64 contiguous bytes per k
+  // chunk
   constexpr int XT = 4, KS = KX / 4;
   constexpr bool XMF = XQ > 0 && XM;
   float bw[XMF ? XT : 1][XMF ? KS : 1];
+  float bbi[XMF ? XT : 1], bbh[XMF ? XT : 1];
   if constexpr (XMF) {
     const int lane = tid & 63, wave = tid >> 6, NW = NT >> 6;
-    const bool v2 = (a.din & 1) == 0 && (reinterpret_cast<uintptr_t>(a.w_ih) & 7) == 0;
+    // float2 runs (the dispatcher takes this form only for an even din and an
+    // 8-byte aligned W_ih); k >= din and gate rows >= G4 load clamped (finite)
+    // weights: they meet the zero x columns / are dropped with their output rows
 #pragma unroll
     for (int ti = 0; ti < XT; ++ti) {
-      const int gg = (wave + ti * NW) * 16 + (lane & 15);
-      const float* wr = a.w_ih + (int64_t)(gg < G4 ? gg : 0) * a.din;
+      const int gg = min((wave + ti * NW) * 16 + (lane & 15), G4 - 1);
+      const float* wr = a.w_ih + (int64_t)gg * a.din;
 #pragma unroll
       for (int m = 0; m < KS / 4; ++m) {
         const int k0 = 16 * m + 4 * (lane >> 4);
-        if (gg < G4 && v2 && k0 + 3 < a.din) {
-          const float2 p0 = *reinterpret_cast<const float2*>(wr + k0);
-          const float2 p1 = *reinterpret_cast<const float2*>(wr + k0 + 2);
-          bw[ti][4 * m] = p0.x; bw[ti][4 * m + 1] = p0.y;
-          bw[ti][4 * m + 2] = p1.x; bw[ti][4 * m + 3] = p1.y;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) bw[ti][4 * m + i] = (gg < G4 && k0 + i < a.din) ? wr[k0 + i] : 0.f;
-        }
+        const float2 p0 = *reinterpret_cast<const float2*>(wr + min(k0, a.din - 2));
+        const float2 p1 = *reinterpret_cast<const float2*>(wr + min(k0 + 2, a.din - 2));
+        bw[ti][4 * m] = p0.x; bw[ti][4 * m + 1] = p0.y;
+        bw[ti][4 * m + 2] = p1.x; bw[ti][4 * m + 3] = p1.y;
       }
+      bbi[ti] = a.b_ih[gg];
+      bbh[ti] = a.b_hh[gg];
     }
   }
-  __syncthreads();
-  LSTM_TICK(0);                                  // x staged, c0 / h0, W_ih issued
   // W_hh rows j*H + u over the k pairs (8i + 2q, 8i + 2q + 1), i < KQ / 2: the
   // quad's four lanes read 32 contiguous bytes of a row per load (a lane-
   // contiguous quarter row put every lane of a load on its own cache line: the
-  // prologue re-fetched W_hh from L2 many times over); in flight during the x
-  // parts
+  // prologue re-fetched W_hh from L2 many times over); issued last of the
+  // prologue's loads, in flight through the x staging and the x parts
   vf2 wv[4][KQ / 2];
+  // The vector width is the dispatcher's (fwd_q_dispatch: WI 2 needs H % 4 ==
+  // 0 and a 16-byte aligned W_hh, WI 1 H even and 8 bytes).  A run-time
+  // vec / scalar branch here was merged by the compiler into one path of
+  // single-dword loads with selected addresses: 112 load instructions per lane
+  // instead of 28, each touching 16 rows (13 us of the prologue, round 6).
   if constexpr (WI == 2) {
-    // k runs (16 i + 4q .. + 3): 64 contiguous bytes of a row per quad and load
-    const bool vec = (H & 3) == 0 && (reinterpret_cast<uintptr_t>(a.w_hh) & 15) == 0;
+    // k runs (16 i + 4q .. + 3): 64 contiguous bytes of a row per quad and load;
+    // k past H: a clamped (finite) weight times the zero h padding
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float* r = a.w_hh + (int64_t)(j * H + uc) * H;
 #pragma unroll
       for (int i = 0; i < KQ / 4; ++i) {
-        const int k = 16 * i + 4 * q;
-        float4 v;
-        if (vec) {
-          v = k + 3 < H ? *reinterpret_cast<const float4*>(r + k) : float4{0.f, 0.f, 0.f, 0.f};
-        } else {
-          v = float4{k < H ? r[k] : 0.f, k + 1 < H ? r[k + 1] : 0.f, k + 2 < H ? r[k + 2] : 0.f,
-                     k + 3 < H ? r[k + 3] : 0.f};
-        }
+        const float4 v = *reinterpret_cast<const float4*>(r + min(16 * i + 4 * q, H - 4));
         wv[j][2 * i] = vf2{v.x, v.y};
         wv[j][2 * i + 1] = vf2{v.z, v.w};
       }
     }
   } else {
-    const bool vec = (H & 1) == 0 && (reinterpret_cast<uintptr_t>(a.w_hh) & 7) == 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float* r = a.w_hh + (int64_t)(j * H + uc) * H;
 #pragma unroll
       for (int i = 0; i < KQ / 2; ++i) {
         const int k = WI ? 8 * i + 2 * q : q * KQ + 2 * i;
-        vf2 v;
-        if (vec) {
-          const float2 t2 = k + 1 < H ? *reinterpret_cast<const float2*>(r + k) : float2{0.f, 0.f};
-          v = vf2{t2.x, t2.y};
+        if constexpr (WI == 1) {
+          const float2 t2 = *reinterpret_cast<const float2*>(r + min(k, H - 2));
+          wv[j][i] = vf2{t2.x, t2.y};
         } else {
-          v = vf2{k < H ? r[k] : 0.f, k + 1 < H ? r[k + 1] : 0.f};
+          wv[j][i] = vf2{r[min(k, H - 1)], r[min(k + 1, H - 1)]};
         }
-        wv[j][i] = v;
       }
     }
   }
+  if constexpr (XQ > 0) {
+    // stored unconditionally at the clamped index (a thread past the end
+    // writes the owner's own value; a store under a per-lane condition let the
+    // compiler sink its load into the branch, with a vmcnt(0) at the merge)
+#pragma unroll
+    for (int j = 0; j < XB; ++j) {
+      const int e = min(tid + j * NT, a.S * KX - 1);
+      xS[e] = xv[j] * (float)(e % KX < a.din);
+    }
+    for (int e0 = tid + XB * NT; e0 < a.S * KX; e0 += XB * NT) {     // longer sequences
+      float v[XB];
+#pragma unroll
+      for (int j = 0; j < XB; ++j) {
+        const int e = min(e0 + j * NT, a.S * KX - 1);
+        const int t = e / KX, k = e - t * KX;
+        v[j] = a.x[((int64_t)t * B + b) * a.ldx + min(k, a.din - 1)];
+      }
+#pragma unroll
+      for (int j = 0; j < XB; ++j) {
+        const int e = e0 + j * NT;
+        if (e < a.S * KX) xS[e] = v[j] * (float)(e % KX < a.din);
+      }
+    }
+  }
+  if (skipv != 0) return;                        // (uniform)
+  const float bh = bhh + bih;
+  float creg = creg0;
+  if (act && q == 0 && a.cbuf) a.cbuf[(int64_t)b * H + u] = creg;
+  {
+    // (clamped like the x stores: 4 KQ >= H, so a thread past 4 KQ writes the
+    // value slot 4 KQ - 1 holds)
+    const int e = min(tid, 4 * KQ - 1);
+    hS[0][e] = h0v * (float)(e < H);
+    hS[1][e] = 0.f;
+    if (tid < H) a.hbuf[(int64_t)b * H + tid] = h0v;
+  }
+  __syncthreads();
+  LSTM_TICK(0);                                  // x staged, c0 / h0, W_ih issued
   if constexpr (XMF) {
     // x parts of every step on the matrix cores: xP[t][tid(g)] = sum_k x_t[k]
     // W_ih[g][k] + b_ih[g] + b_hh[g] as v_mfma_f32_16x16x4_f32 tiles of 16 steps
@@ -1363,7 +1407,7 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
       const int nt = wave + ti * NW;
       if (nt * 16 >= G4) break;
       const int gs = nt * 16 + (lane & 15);                 // the D column's gate
-      const float bsum = gs < G4 ? a.b_ih[gs] + a.b_hh[gs] : 0.f;
+      const float bsum = bbi[ti] + bbh[ti];                  // (gs >= G4 dropped)
       const int dst = gs < G4 ? 4 * (gs % H) + gs / H : 0;
       for (int mt = 0; mt < nmt; ++mt) {
         const int r = min(mt * 16 + (lane & 15), a.S - 1);
@@ -1629,10 +1673,19 @@ static void fwd_q_dispatch(const LstmFwdArgs& a, hipStream_t st, const LstmFwdAr
   const dim3 grid(a.B + (a1 ? a1->B : 0)), blk((4 * a.H + 63) & ~63);
   const LstmFwdArgs& a2 = a1 ? *a1 : a;
   const int smax = a1 && a1->S > a.S ? a1->S : a.S;
-  const bool xm = XQ > 0 && use_xm();
+  auto aligned = [&](const float* LstmFwdArgs::*p, uintptr_t m) {
+    return (reinterpret_cast<uintptr_t>(a.*p) & m) == 0 && (reinterpret_cast<uintptr_t>(a2.*p) & m) == 0;
+  };
+  // the matrix-core x parts load W_ih rows as float2 runs
+  const bool xm = XQ > 0 && use_xm() && a.din % 2 == 0 && aligned(&LstmFwdArgs::w_ih, 7);
   // W_hh register layout (SMI_LSTM_WI; A/B knob): 0 a contiguous quarter row
-  // per lane, 1 k pairs interleaved over the quad, 2 float4 runs interleaved
-  static const int wi = [] { const char* e = getenv("SMI_LSTM_WI"); return e && e[0] ? atoi(e) : 2; }();
+  // per lane, 1 k pairs interleaved over the quad (float2 loads), 2 float4 runs
+  // interleaved (float4 loads); a shape / alignment the vector loads cannot
+  // take steps down (the kernel has no run-time vector / scalar branch)
+  static const int wi_knob = [] { const char* e = getenv("SMI_LSTM_WI"); return e && e[0] ? atoi(e) : 2; }();
+  int wi = wi_knob;
+  if (wi == 2 && !(a.H % 4 == 0 && aligned(&LstmFwdArgs::w_hh, 15))) wi = 1;
+  if (wi == 1 && !(a.H % 2 == 0 && aligned(&LstmFwdArgs::w_hh, 7))) wi = 0;
   // all four gates finished in every lane (SMI_LSTM_A4=0: one gate per lane +
   // quad broadcasts; A/B knob)
   static const bool a4 = [] { const char* e = getenv("SMI_LSTM_A4"); return !(e && e[0] == '0'); }();
@@ -1682,8 +1735,12 @@ void lstm_v_fwd(const LstmFwdArgs& a, int R, int kx, hipStream_t st) {
   else if (kx <= 48) fwd_v_dispatch_kp<1, 48>(a, st);
   else fwd_v_dispatch_kp<1, 64>(a, st);
 }
+// the BPTT's K-split form loads W_hh as float4 runs (lstm_bwd_q_body)
+bool lstm_bwd_q_ok(int H, const float* w_hh) {
+  return use_q() && H % 4 == 0 && (reinterpret_cast<uintptr_t>(w_hh) & 15) == 0;
+}
 void lstm_v_bwd(const LstmBwdArgs& a, int R, hipStream_t st) {
-  if (R == 1 && use_q()) {
+  if (R == 1 && lstm_bwd_q_ok(a.H, a.w_hh)) {
     const dim3 grid(a.B), blk((4 * a.H + 63) & ~63);
     if (a.H <= 64) hipLaunchKernelGGL(lstm_bwd_q_kernel<16>, grid, blk, 0, st, a);
     else if (a.H <= 100) hipLaunchKernelGGL(lstm_bwd_q_kernel<25>, grid, blk, 0, st, a);
@@ -1822,8 +1879,9 @@ bool lstm_use_q();
 // BR of the BPTT's one-segment-per-workgroup K-split form (lstm_bwd_q_kernel)
 // when launch_lstm_bwd would run it for (B, H), else 0: the form that the
 // BPTT + weight-gradient launch (linear_kernels.hip) embeds
-int lstm_bwd_q_form(int B, int H) {
-  if (lstm_valu_r(B, H) != 1 || !lstm_use_q()) return 0;
+bool lstm_bwd_q_ok(int H, const float* w_hh);
+int lstm_bwd_q_form(int B, int H, const float* w_hh) {
+  if (lstm_valu_r(B, H) != 1 || !lstm_bwd_q_ok(H, w_hh)) return 0;
   return H <= 64 ? 16 : H <= 100 ? 25 : 32;
 }
 

@@ -66,7 +66,7 @@ int dw_group_epilogue(const DwEpilogue& x);
 // an M x N weight gradient (bias column included in N) joins an open group
 bool dw_group_takes(int M, int N);
 // BR of the one-segment-per-workgroup BPTT form for (B, H), 0 when another form runs
-int lstm_bwd_q_form(int B, int H);
+int lstm_bwd_q_form(int B, int H, const float* w_hh);
 // the LSTM BPTT (lstm_bwd_q form) and the weight gradients queued so far in the
 // open dW group in one launch (linear_kernels.hip); SMI_E_NOFIT: run
 // launch_lstm_bwd instead (nothing launched)

@@ -44,6 +44,34 @@ def main():
            'us_per_fwd_launch': {nm: round(buf[i] * 0.01 / n_fwd, 3) for i, nm in enumerate(names[:4])},
            'bwd_total_us_all_launches': round(buf[4] * 0.01, 1)}
     print(json.dumps(out), flush=True)
+    # the same kernel alone, back to back (hot instruction cache / L2), and with
+    # a 1 GiB write between launches (cold): does the prologue cost come from
+    # the launch's context in the learner?
+    S, H = T + 1, 100
+    g = torch.Generator(device='cpu').manual_seed(0)
+    x = torch.randn(S, B, D, generator=g).cuda()
+    w_ih, w_hh = (torch.randn(4 * H, D, generator=g) * 0.1).cuda(), (torch.randn(4 * H, H, generator=g) * 0.1).cuda()
+    b_ih, b_hh = torch.zeros(4 * H, device='cuda'), torch.zeros(4 * H, device='cuda')
+    h0, c0 = torch.zeros(B, H, device='cuda'), torch.zeros(B, H, device='cuda')
+    hb, cb = torch.empty(S + 1, B, H, device='cuda'), torch.empty(S + 1, B, H, device='cuda')
+    ga, xs = torch.empty(S, B, 4 * H, device='cuda'), torch.empty(S, B, 4 * H, device='cuda')
+    junk = torch.empty(1 << 28, device='cuda')
+    st = torch.cuda.current_stream().cuda_stream
+    for mode in ('hot', 'cold'):
+        n = 50
+        for it in range(n + 1):
+            if it == 1:
+                torch.cuda.synchronize()
+                lib.smi_lstm_v_phase_ticks(ctypes.cast(buf, ctypes.c_void_p))
+            if mode == 'cold':
+                junk.fill_(float(it))
+            L.call('smi_lstm_forward_x', L.ptr(x), D, D, L.ptr(w_ih), L.ptr(b_ih), L.ptr(w_hh), L.ptr(b_hh),
+                   L.ptr(h0), L.ptr(c0), S, B, H, L.ptr(hb), L.ptr(cb), L.ptr(ga), L.ptr(xs), st)
+        torch.cuda.synchronize()
+        lib.smi_lstm_v_phase_ticks(ctypes.cast(buf, ctypes.c_void_p))
+        print(json.dumps({'standalone': mode, 'B': B, 'S': S,
+                          'us_per_fwd_launch': {nm: round(buf[i] * 0.01 / n, 3) for i, nm in enumerate(names[:4])}}),
+              flush=True)
 
 
 if __name__ == '__main__':
