@@ -285,9 +285,11 @@ class SmiClockSampler(object):
     """The GPU's current gfx clock over the timed region, sampled by a host
     thread from the SMU through amdsmi (gpu_metrics current_gfxclk, MHz) every
     `period_s`; reported as the mean and range of the samples.  No kernel runs
-    beside the timed launches."""
+    beside the timed launches.  The period is 50 ms: each sample is a gpu_metrics
+    read plus Python work under the GIL, and at 2 ms the thread slowed the C4
+    step (host-side replay sampling every 0.25 ms)."""
 
-    def __init__(self, dev, period_s=0.002):
+    def __init__(self, dev, period_s=0.05):
         import threading
         import amdsmi
         self.amdsmi = amdsmi
@@ -326,8 +328,10 @@ class SmiClockSampler(object):
         self._th.start()
 
     def stop(self):
+        # no sample here: a gpu_metrics read between the last issue and the
+        # closing barrier is host time inside the timed region (C4: 0.267 ->
+        # 0.31-0.37 ms per step, profiles/r06/clock_ab)
         self._stop.set()
-        self._sample()                  # after the last timed step was issued
 
     def read(self):
         self._th.join(timeout=5)
@@ -340,8 +344,8 @@ class SmiClockSampler(object):
         return {'clock_mhz': round(float(np.mean(self.samples)), 1),
                 'min_mhz': round(min(self.samples), 1), 'max_mhz': round(max(self.samples), 1),
                 'samples': len(self.samples),
-                'source': f'amdsmi gpu_metrics current_gfxclk at the start and end of the timed '
-                          f'region and every {self.period * 1e3:.0f} ms between (host thread; '
+                'source': f'amdsmi gpu_metrics current_gfxclk at the start of the timed region and '
+                          f'every {self.period * 1e3:.0f} ms through it (host thread; '
                           'SMU-reported, reads up to ~5 % below the in-kernel s_memtime clock of '
                           'calib.calib_mfma_clock_mhz); an in-kernel probe wave beside the timed '
                           'launches cost 15 % of the C3 step (profiles/r06/clock_ab), so none runs'}
