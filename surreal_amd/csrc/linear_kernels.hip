@@ -335,6 +335,11 @@ gemm_kernel(GemmArgs g) {
   }
 }
 
+// zero row / ones vector selected by address (dwd_load, the reducers)
+constexpr int DWD_ZMAX = 8192;
+__device__ __attribute__((aligned(16))) float g_dwd_zero[DWD_ZMAX];
+__device__ __attribute__((aligned(16))) float g_dwd_one[4] = {1.f, 0.f, 0.f, 0.f};
+
 // split-K reducer: C[m][n] (+)= sum_z part[z][m][n]; the ones column goes to
 // bias_out[m].  A workgroup owns 64 consecutive elements x 4 slab lanes: lane
 // zl sums slabs zl, zl+4, ... with 4 independent accumulators (loads in
@@ -356,12 +361,19 @@ gemm_splitk_reduce_kernel(const float* __restrict__ part, int S, GemmArgs g, con
     // every slab of the thread (z = zl + 4k) in flight at once, then the same
     // additions in the same order as the loop below (bit-identical): one
     // memory round trip instead of one per four slabs
+    // (loads unconditional, slabs past S read a zero by address, and pinned
+    // before the conditional adds below: with `zk < S ? load : 0` the compiler
+    // sank each load into its own branch and waited on it there -- up to 16
+    // round trips per block, round 6)
+    // (addresses advanced by 4 slabs per k: the 64-bit index products per
+    // load made the allocator reuse address registers and wait between loads)
+    const float* pz = part + (int64_t)zl * MN + ec;
+    const int64_t st4 = 4 * MN;
     float v[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int zk = zl + 4 * k;
-      v[k] = zk < S ? part[(int64_t)zk * MN + ec] : 0.f;
-    }
+    for (int k = 0; k < 16; ++k) v[k] = *(zl + 4 * k < S ? pz + k * st4 : g_dwd_zero);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[k]));
     const int nfull = S > zl + 12 ? (S - zl - 12 + 15) / 16 : 0;   // z + 12 < S trips
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -685,9 +697,6 @@ constexpr int DWD_P = SMI_DWD_P;   // steps in flight per wave
 // loaded value: the loads then feed the MFMAs untouched and the compiler keeps
 // all P steps in flight.  Columns past M / N read clamped addresses; they only
 // reach outputs the epilogue drops.
-constexpr int DWD_ZMAX = 8192;
-__device__ __attribute__((aligned(16))) float g_dwd_zero[DWD_ZMAX];
-__device__ __attribute__((aligned(16))) float g_dwd_one[4] = {1.f, 0.f, 0.f, 0.f};
 
 template <int MT, int NT, bool VA, bool VB, int NB = NT>
 __device__ __forceinline__ void dwd_load(const GemmArgs& g, int r, int ke, int m0, int n0, int bdata,
@@ -1144,12 +1153,17 @@ __device__ void dw_epilogue_block(const DwEpilogue& x, int nsq) {
         for (int k = 0; k < 16; ++k) t += v[k];
       }
       {
+        // the tail's loads unconditional (past the end: a zero by address) and
+        // pinned before the conditional adds: a load whose only use sat under
+        // its lane condition was sunk into that branch, one round trip each
         float v[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           const int ik = i + 64 * k;
-          v[k] = ik < x.lv_nb ? x.lvpart[(int64_t)ik * x.lv_A + j] : 0.f;
+          v[k] = *(ik < x.lv_nb ? x.lvpart + (int64_t)ik * x.lv_A + j : g_dwd_zero);
         }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[k]));
 #pragma unroll
         for (int k = 0; k < 16; ++k)
           if (i + 64 * k < x.lv_nb) t += v[k];
@@ -1176,9 +1190,74 @@ __device__ void dw_epilogue_block(const DwEpilogue& x, int nsq) {
   }
 }
 
+// one element's sum over its S slabs as lane zl of the reducer sees it: slabs
+// z = zl, zl + 4, ... into four accumulators (z, z + 4, z + 8, z + 12 of each
+// 16-slab trip), the rest into the first; p = the element's slab-0 address.
+// For S <= 64 every slab is loaded before the first add (one memory round trip):
+// the loads are unconditional (slabs past S read a zero by address) and pinned
+// before the conditional adds -- with `zk < S ? load : 0` the compiler sank
+// each load into its own branch and waited on it there, and 64-bit index
+// products per load made it reuse address registers between loads (round 6)
+template <int U>
+__device__ __forceinline__ void red_slabs(const float* const (&p)[U], int64_t MN, int S, int zl,
+                                          float (&r)[U]) {
+  float s0[U], s1[U], s2[U], s3[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) s0[u] = s1[u] = s2[u] = s3[u] = 0.f;
+  int z = zl;
+  if (S <= 64) {
+    const int64_t st4 = 4 * MN;
+    float v[U][16];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float* pz = p[u] + (int64_t)zl * MN;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[u][k] = *(zl + 4 * k < S ? pz + k * st4 : g_dwd_zero);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[u][k]));
+    const int nfull = S > zl + 12 ? (S - zl - 12 + 15) / 16 : 0;   // z + 12 < S trips
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < nfull) {
+          s0[u] += v[u][4 * j]; s1[u] += v[u][4 * j + 1]; s2[u] += v[u][4 * j + 2]; s3[u] += v[u][4 * j + 3];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k >= 4 * nfull && zl + 4 * k < S) s0[u] += v[u][k];
+    }
+    z = S;
+  }
+  for (; z + 12 < S; z += 16) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s0[u] += p[u][(int64_t)z * MN];
+      s1[u] += p[u][(int64_t)(z + 4) * MN];
+      s2[u] += p[u][(int64_t)(z + 8) * MN];
+      s3[u] += p[u][(int64_t)(z + 12) * MN];
+    }
+  }
+  for (; z < S; z += 4)
+#pragma unroll
+    for (int u = 0; u < U; ++u) s0[u] += p[u][(int64_t)z * MN];
+#pragma unroll
+  for (int u = 0; u < U; ++u) r[u] = (s0[u] + s1[u]) + (s2[u] + s3[u]);
+}
+
+// U: 64-element groups per block (block = 64 U consecutive elements; lane el
+// of wave zl sums slabs zl, zl + 4, ... of elements el + 64 u).  Every element
+// gets the additions of gemm_splitk_reduce_kernel in the same order whatever
+// U is; U = 4 dispatches a quarter of the workgroups with 4x the loads in
+// flight per thread (SMI_RED_U, host side)
+template <int U>
 __global__ void __launch_bounds__(kWG)
 gemm_group_reduce_kernel(DwGroup G) {
-  __shared__ float red[4][64];
+  __shared__ float red[4][64 * U];
   __shared__ double sqr[kWG / 64];
   const int b = blockIdx.x;
   if (b >= G.rb0[G.n]) {                          // the epilogue task's block
@@ -1191,49 +1270,25 @@ gemm_group_reduce_kernel(DwGroup G) {
   const GemmArgs& g = G.g[gi];
   if (g.skip && g.skip[0] != 0) return;
   const int S = G.S[gi];
-  const float* __restrict__ part = g.part;
   const int64_t MN = (int64_t)g.M * g.N;
   const int el = threadIdx.x & 63, zl = threadIdx.x >> 6;
-  const int64_t e = (int64_t)(b - G.rb0[gi]) * 64 + el;
-  const int64_t ec = e < MN ? e : MN - 1;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int z = zl;
-  if (S <= 64) {
-    // every slab of the thread (z = zl + 4k) in flight at once, then the same
-    // additions in the same order as the loop below (bit-identical): one
-    // memory round trip instead of one per four slabs
-    float v[16];
+  const int64_t eb = (int64_t)(b - G.rb0[gi]) * 64 * U;
+  const float* p[U];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int zk = zl + 4 * k;
-      v[k] = zk < S ? part[(int64_t)zk * MN + ec] : 0.f;
-    }
-    const int nfull = S > zl + 12 ? (S - zl - 12 + 15) / 16 : 0;   // z + 12 < S trips
+  for (int u = 0; u < U; ++u) p[u] = g.part + min(eb + el + 64 * u, MN - 1);
+  float r[U];
+  red_slabs<U>(p, MN, S, zl, r);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j < nfull) {
-        s0 += v[4 * j]; s1 += v[4 * j + 1]; s2 += v[4 * j + 2]; s3 += v[4 * j + 3];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (k >= 4 * nfull && zl + 4 * k < S) s0 += v[k];
-    z = S;
-  }
-  for (; z + 12 < S; z += 16) {
-    s0 += part[(int64_t)z * MN + ec];
-    s1 += part[(int64_t)(z + 4) * MN + ec];
-    s2 += part[(int64_t)(z + 8) * MN + ec];
-    s3 += part[(int64_t)(z + 12) * MN + ec];
-  }
-  for (; z < S; z += 4) s0 += part[(int64_t)z * MN + ec];
-  red[zl][el] = (s0 + s1) + (s2 + s3);
+  for (int u = 0; u < U; ++u) red[zl][el + 64 * u] = r[u];
   __syncthreads();
   float q = 0.f;
-  if (zl == 0 && e < MN) {
-    const float v = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
-    const int m = (int)(e / g.N), n = (int)(e - (int64_t)m * g.N);
-    q = dw_put(g, m, n, v);
+  for (int i = threadIdx.x; i < 64 * U; i += kWG) {
+    const int64_t e = eb + i;
+    if (e < MN) {
+      const float v = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+      const int m = (int)(e / g.N), n = (int)(e - (int64_t)m * g.N);
+      q += dw_put(g, m, n, v);
+    }
   }
   if (!G.x.sq) return;
   const double t = block_sum_d((double)q, sqr);
@@ -1590,6 +1645,13 @@ static int dwd_group_slots(size_t lds) {
 // ws_off floats into the workspace; wv: waves per workgroup of the launch that
 // runs them, slots: its resident workgroups.  Sets G.wg0 / rb0 / S / part and
 // need (floats used from ws_off).
+// 64-element groups per block of the grouped reducer (SMI_RED_U=1: one, the
+// round-5 form; A/B knob)
+static int red_u() {
+  static const int u = [] { const char* e = getenv("SMI_RED_U"); return e && e[0] == '1' ? 1 : 4; }();
+  return u;
+}
+
 static int dw_prepare(DwGroup& G, int wv, int slots, int64_t ws_off, int64_t& need,
                       int target_fixed = 0) {
   constexpr int MT = 4, NT = DWG_NT;
@@ -1711,7 +1773,7 @@ static int dw_prepare(DwGroup& G, int wv, int slots, int64_t ws_off, int64_t& ne
     g.part = base + off;
     off += (int64_t)G.S[i] * g.M * g.N;
     G.wg0[i + 1] = G.wg0[i] + (int)(tiles[i] * G.S[i]);
-    G.rb0[i + 1] = G.rb0[i] + (int)(((int64_t)g.M * g.N + 63) / 64);
+    G.rb0[i + 1] = G.rb0[i] + (int)(((int64_t)g.M * g.N + 64 * red_u() - 1) / (64 * red_u()));
   }
   return SMI_OK;
 }
@@ -1838,7 +1900,7 @@ int dw_group_flush(hipStream_t st) {
     if (!G.x.on) return SMI_OK;
     if (G.x.sq) return set_error(SMI_E_ARG, "dw group: fused sum of squares over an empty group");
     G.rb0[0] = 0;                                   // the epilogue task alone
-    hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(1), dim3(kWG), 0, st, G);
+    hipLaunchKernelGGL(gemm_group_reduce_kernel<1>, dim3(1), dim3(kWG), 0, st, G);
     return check_launch("gemm_group_reduce_kernel");
   }
   // short batches (every entry <= 512 rows, one group, no epilogue task):
@@ -1876,14 +1938,18 @@ int dw_group_flush(hipStream_t st) {
       const int j = R.n + i;
       R.g[j] = G.g[i];
       R.S[j] = G.S[i];
-      R.rb0[j + 1] = R.rb0[j] + (int)(((int64_t)G.g[i].M * G.g[i].N + 63) / 64);
+      R.rb0[j + 1] = R.rb0[j] + (int)(((int64_t)G.g[i].M * G.g[i].N + 64 * red_u() - 1) / (64 * red_u()));
     }
     R.n += G.n;
     need += g_pre_need;
   }
   const int rslot = ktime_begin(st);
-  hipLaunchKernelGGL(gemm_group_reduce_kernel, dim3(R.rb0[R.n] + (R.x.on ? 1 : 0)), dim3(kWG), 0,
-                     st, R);
+  if (red_u() == 4)
+    hipLaunchKernelGGL(gemm_group_reduce_kernel<4>, dim3(R.rb0[R.n] + (R.x.on ? 1 : 0)), dim3(kWG), 0,
+                       st, R);
+  else
+    hipLaunchKernelGGL(gemm_group_reduce_kernel<1>, dim3(R.rb0[R.n] + (R.x.on ? 1 : 0)), dim3(kWG), 0,
+                       st, R);
   ktime_end(rslot, KT_GEMM_REDUCE, (double)need, st);
   return check_launch("gemm_group_reduce_kernel");
 }
