@@ -106,7 +106,7 @@ CLASS_KERNELS = {
     'lstm_fwd': ('lstm_fwd',), 'lstm_bwd': ('lstm_bwd',),
     'cnn_fwd': ('cnn_fwd_kernel',), 'cnn_bwd': ('cnn_bwd_kernel',),
 }
-PMC_TRAFFIC = {'c3': 'profiles/r05/pmc_traffic_c3_r5.json',
+PMC_TRAFFIC = {'c3': 'profiles/r06/pmc_traffic_c3_r6.json',
                'c5': 'profiles/r02/pmc_traffic_c5_r2.json'}
 
 
