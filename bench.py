@@ -324,8 +324,8 @@ class SmiClockSampler(object):
             self.samples.append(float(v))
 
     def start(self):
+        self._th.start()                # (thread start-up before the timed region)
         self._sample()                  # at the start of the timed region
-        self._th.start()
 
     def stop(self):
         # no sample here: a gpu_metrics read between the last issue and the
