@@ -249,6 +249,8 @@ class ClockProbe(object):
     until a stop kernel enqueued on the learner's stream after the last one
     (bounded by max_s of wall time, so it always exits)."""
 
+    stop_in_region = True      # its stop kernel must precede the closing barrier
+
     def __init__(self, dev, max_s=30.0):
         from surreal_amd import _lib as L
         self.L, self.dev = L, dev
@@ -289,6 +291,8 @@ class SmiClockSampler(object):
     read plus Python work under the GIL, and at 2 ms the thread slowed the C4
     step (host-side replay sampling every 0.25 ms)."""
 
+    stop_in_region = False     # stopped after the closing barrier and the clock read
+
     def __init__(self, dev, period_s=0.05):
         import threading
         import amdsmi
@@ -328,9 +332,10 @@ class SmiClockSampler(object):
         self._sample()                  # at the start of the timed region
 
     def stop(self):
-        # no sample here: a gpu_metrics read between the last issue and the
-        # closing barrier is host time inside the timed region (C4: 0.267 ->
-        # 0.31-0.37 ms per step, profiles/r06/clock_ab)
+        # called after the closing barrier, with no sample: a gpu_metrics read
+        # (or the thread's wake-up) between the last issue and the barrier is
+        # host time inside the timed region (C4: 0.267 -> 0.31-0.37 ms per
+        # step with a read there, profiles/r06/clock_ab)
         self._stop.set()
 
     def read(self):
@@ -531,10 +536,12 @@ def run_ddpg(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    if probe is not None:
+    if probe is not None and probe.stop_in_region:
         probe.stop()
     barrier()
     elapsed = time.perf_counter() - t0
+    if probe is not None and not probe.stop_in_region:
+        probe.stop()
     clock = probe.read() if probe is not None else None
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -729,10 +736,12 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         learner.learn(pool[k % len(pool)])
-    if probe is not None:
+    if probe is not None and probe.stop_in_region:
         probe.stop()
     barrier()
     elapsed = time.perf_counter() - t0
+    if probe is not None and not probe.stop_in_region:
+        probe.stop()
     clock = probe.read() if probe is not None else None
     if dist is not None:
         t = torch.tensor([elapsed], device=dev)
