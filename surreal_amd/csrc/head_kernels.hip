@@ -340,6 +340,7 @@ __device__ __forceinline__ void hc_store(const f32x4 (&acc)[RT][NT], const float
 template <int RT>
 __device__ __forceinline__ void hc_copy_out(const float* sO, int ld, int N, float* __restrict__ G,
                                            int64_t r0, int64_t rows) {
+  if (G == nullptr) return;                      // (no backward reads them: not stored)
   constexpr int J = HC_MAXK / 4 / 16;
   const int nq = N >> 2, q0 = threadIdx.x & 15;
 #pragma unroll

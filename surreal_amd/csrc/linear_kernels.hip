@@ -1131,7 +1131,7 @@ lstm_bwd_dw_kernel(LstmBwdArgs la, DwGroup G) {
 // the fixed order of gemm_splitk_reduce_kernel.  With an epilogue task
 // (G.x.on): every block also writes the fp64 sum of squares of the values it
 // stored to x.sq[block] (fixed order: lane values, wave butterfly, waves in
-// order), and one more block (the last) runs the task itself: the log_var
+// order), and one more block (block 0) runs the task itself: the log_var
 // gradient from its row partials, that block's sum of squares, the partial
 // count and the optimizer step bump (what sumsq_part_kernel and
 // logvar_grad_kernel did as launches of their own)
@@ -1140,39 +1140,58 @@ __device__ void dw_epilogue_block(const DwEpilogue& x, int nsq) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float q = 0.f;
   if (x.lvpart) {
-    // d log_var[j] = std_j * sum_blocks lvpart[.][j] (logvar_grad_kernel's order)
-    for (int j = wave; j < x.lv_A; j += kWG / 64) {
-      float t = 0.f;
+    // d log_var[j] = std_j * sum_blocks lvpart[.][j] (logvar_grad_kernel's order);
+    // a wave takes its columns j = wave + 4 i two at a time (both columns'
+    // partials in flight together: 16 of the lane's partials per column per
+    // trip, the same additions in the same order per column)
+    constexpr int NW = kWG / 64;
+    for (int j0 = wave; j0 < x.lv_A; j0 += 2 * NW) {
+      const int jj[2] = {j0, min(j0 + NW, x.lv_A - 1)};      // (a clamped second column is dropped)
+      float t[2] = {0.f, 0.f};
       int i = lane;
-      // 16 of the lane's partials in flight per trip (same additions, same order)
       for (; i + 15 * 64 < x.lv_nb; i += 16 * 64) {
-        float v[16];
+        float v[2][16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = x.lvpart[(int64_t)(i + 64 * k) * x.lv_A + j];
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) t += v[k];
+          for (int k = 0; k < 16; ++k) v[c][k] = x.lvpart[(int64_t)(i + 64 * k) * x.lv_A + jj[c]];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) t[c] += v[c][k];
       }
       {
         // the tail's loads unconditional (past the end: a zero by address) and
         // pinned before the conditional adds: a load whose only use sat under
         // its lane condition was sunk into that branch, one round trip each
-        float v[16];
+        float v[2][16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const int ik = i + 64 * k;
-          v[k] = *(ik < x.lv_nb ? x.lvpart + (int64_t)ik * x.lv_A + j : g_dwd_zero);
-        }
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[k]));
+          for (int k = 0; k < 16; ++k) {
+            const int ik = i + 64 * k;
+            v[c][k] = *(ik < x.lv_nb ? x.lvpart + (int64_t)ik * x.lv_A + jj[c] : g_dwd_zero);
+          }
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-          if (i + 64 * k < x.lv_nb) t += v[k];
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[c][k]));
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if (i + 64 * k < x.lv_nb) t[c] += v[c][k];
       }
-      t = wave_sum(t);
-      const float gv = t * expf(x.lv[j]);
+      const float e0 = expf(x.lv[jj[0]]), e1 = expf(x.lv[jj[1]]);
+      const float g0 = wave_sum(t[0]) * e0;
+      const float g1 = wave_sum(t[1]) * e1;
       if (lane == 0) {
-        x.lv_out[j] = gv;
-        q += gv * gv;
+        x.lv_out[jj[0]] = g0;
+        q += g0 * g0;
+        if (j0 + NW < x.lv_A) {
+          x.lv_out[jj[1]] = g1;
+          q += g1 * g1;
+        }
       }
     }
   }
@@ -1259,12 +1278,15 @@ __global__ void __launch_bounds__(kWG)
 gemm_group_reduce_kernel(DwGroup G) {
   __shared__ float red[4][64 * U];
   __shared__ double sqr[kWG / 64];
-  const int b = blockIdx.x;
-  if (b >= G.rb0[G.n]) {                          // the epilogue task's block
+  // the epilogue task (when on) is block 0: dispatched first, its chain of
+  // dependent steps overlaps the reduction blocks instead of trailing them
+  const int ep = G.x.on ? 1 : 0;
+  if (ep && blockIdx.x == 0) {
     if (G.x.skip && G.x.skip[0] != 0) return;
     dw_epilogue_block(G.x, G.rb0[G.n]);
     return;
   }
+  const int b = (int)blockIdx.x - ep;
   int gi = 0;
   while (gi + 1 < G.n && b >= G.rb0[gi + 1]) ++gi;
   const GemmArgs& g = G.g[gi];

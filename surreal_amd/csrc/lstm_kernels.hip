@@ -614,10 +614,14 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
   // step (a select right after the load made the compiler wait vmcnt(0) on it
   // in every step, the x fetch latency on the recurrence's critical path)
   auto xload = [&](int t) -> float { return a.x[(int64_t)t * B * a.ldx + xoff0]; };
-  float xnext = 0.f;
+  // Round 6: x_0, x_1, c0 and h0 are loaded unconditionally (clamped
+  // addresses, the selects after the loads) together with the weights above
+  // and stored after; a load used only under a per-lane condition (xown, ok)
+  // was sunk into that branch and waited on there, one round trip each
+  float xnext = 0.f, x0 = 0.f;
   if constexpr (KX > 0) {
-    if (xown && a.S > 0) xS[0][xr * KXS + xk] = xval ? xload(0) : 0.f;
-    if (xown && a.S > 1) xnext = xload(1);
+    x0 = xload(0);
+    xnext = xload(a.S > 1 ? 1 : 0);
   }
   // cell owned by this thread: (crow, cunit)
   const bool cell = tid < LR4 * H;
@@ -625,15 +629,25 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
   const int cunit = cell ? tid - crow * H : 0;
   const int cgr = r0 + crow;
   const bool cok = cell && cgr < B;
-  float creg = cok ? a.c0[(int64_t)cgr * H + cunit] : 0.f;
+  const float c0v = a.c0[(int64_t)min(cgr, B - 1) * H + cunit];
+  static_assert(LR4 * KP <= kWG8, "one h0 slot per thread");
+  const int he = min(tid, LR4 * KP - 1);
+  const int hr = he / KP, hk = he - hr * KP;
+  float h0v = a.h0[(int64_t)min(r0 + hr, B - 1) * H + min(hk, H - 1)];
+  // (pinned: their only uses sit under per-lane conditions)
+  asm volatile("" : "+v"(h0v));
+  if constexpr (KX > 0) asm volatile("" : "+v"(x0));
+  if constexpr (KX > 0) {
+    if (xown && a.S > 0) xS[0][xr * KXS + xk] = xval ? x0 : 0.f;
+  }
+  float creg = cok ? c0v : 0.f;
   if (cok && a.cbuf) a.cbuf[(int64_t)cgr * H + cunit] = creg;
-  for (int e = tid; e < LR4 * KP; e += kWG8) {
-    const int r = e / KP, k = e - r * KP;
-    const bool ok = k < H && r0 + r < B;
-    const float v = ok ? a.h0[(int64_t)(r0 + r) * H + k] : 0.f;
-    hS[0][e] = v;
-    hS[1][e] = 0.f;
-    if (ok) a.hbuf[(int64_t)(r0 + r) * H + k] = v;        // hbuf[0] = h0
+  if (tid < LR4 * KP) {
+    const bool ok = hk < H && r0 + hr < B;
+    const float v = ok ? h0v : 0.f;
+    hS[0][he] = v;
+    hS[1][he] = 0.f;
+    if (ok) a.hbuf[(int64_t)(r0 + hr) * H + hk] = v;       // hbuf[0] = h0
   }
   int64_t xoff[4];
 #pragma unroll

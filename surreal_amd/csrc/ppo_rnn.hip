@@ -1351,10 +1351,15 @@ static int head_fwd(const Head& h, const float* X, int64_t ldx, int64_t rows, fl
                     float* HA2, float* Y, hipStream_t st, const int* skip, float* wT = nullptr,
                     const float* vret = nullptr, float* vgrad = nullptr, float vscale = 0.f,
                     bool* vdone = nullptr, const PolRowArgs* ps = nullptr,
-                    double* vpart = nullptr) {
+                    double* vpart = nullptr, bool keep_act = true) {
   const MlpLayout& L = h.L;
   if (vdone) *vdone = false;
   if (head_fused(h, X, ldx)) {
+    // keep_act false: no backward follows (the GAE critic pass, PREP's
+    // reference forward, the KL check after the last policy update), so the
+    // fused chain skips the HA1 / HA2 copy-outs (the layer-GEMM path below
+    // needs them as its intermediates)
+    if (!keep_act) HA1 = HA2 = nullptr;
     const bool ve = vgrad && h.out == 1;
     if (vdone) *vdone = ve;
     return launch_head_fwd_fused(X, ldx, rows, h.in, h.P + L.fW1, h.P + L.fb1, h.h1, h.P + L.fW2,
@@ -1745,7 +1750,8 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       } else if (d.H > 0) {
         RC(lstm_forward(d, a.lstm, s.Xz, d.S1, a.h0, a.c0, s, true, st, nullptr, d.E));
       }
-      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr));
+      RC(head_fwd(critic, head_in(d, s, s.Xz), d.Hld, d.NG, s.HA1, s.HA2, s.OUT, st, nullptr,
+                  nullptr, nullptr, nullptr, 0.f, nullptr, nullptr, nullptr, false));
       hipLaunchKernelGGL(tmajor_to_bmajor_kernel, dim3(grid_of(d.NG)), dim3(kWG), 0, st, s.OUT,
                          d.S1, d.B, s.values, s.ci, s.cf);
       RC(check_launch("tmajor_to_bmajor_kernel"));
@@ -1778,7 +1784,7 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       }
       const Head ref{a.ref_actor, d.LA, d.Hin, d.h1, d.h2, d.A, 1};
       return head_fwd(ref, head_in(d, sp, X), d.Hld, d.NE, sp.HA1, sp.HA2, s.refmu, st,
-                      nullptr);
+                      nullptr, nullptr, nullptr, nullptr, 0.f, nullptr, nullptr, nullptr, false);
     }
     case SMI_RNN_PH_POLICY_FWD: {
       if (e == 0) {
@@ -1795,8 +1801,12 @@ int ppo_rnn_phase(const smi_ppo_rnn_args& a, int phase, int e, hipStream_t st) {
       PolRowArgs p = pol_rows(a, d, s);
       p.invN = (float)(1.0 / (double)NEg);
       const bool hs = pol_head_stats(a, d, s, actor);
-      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop, s.wT,
-                  nullptr, nullptr, 0.f, nullptr, hs ? &p : nullptr));
+      // (the KL check after the last update, e == epoch_policy, has no backward:
+      // neither the activations nor the weight transposes are kept)
+      const bool bwd_next = e < a.epoch_policy;
+      RC(head_fwd(actor, head_in(d, s, s.Xz), d.Hld, d.NE, s.HA1, s.HA2, s.OUT, st, stop,
+                  bwd_next ? s.wT : nullptr, nullptr, nullptr, 0.f, nullptr, hs ? &p : nullptr,
+                  nullptr, bwd_next));
       const int nb = pol_stats_nb(a, d, s, actor);
       if (!hs) {
         const int kt = ktime_begin(st);
