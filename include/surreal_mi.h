@@ -61,8 +61,9 @@ int          smi_context_make_current(smi_context* ctx);            /* this thre
  * launches; making a dead context current is an error.  A launch that another
  * thread is issuing on ctx concurrently with the destroy may still use its
  * workspace: free the workspace only after every thread that had ctx current
- * has finished issuing launches with it (the Python owner keeps it alive for
- * as long as any thread holds the context). */
+ * has finished issuing launches with it (the Python owner, _lib.Context, is
+ * referenced from each thread's current-context slot, so the workspace lives
+ * while any thread has the context current). */
 int          smi_context_destroy(smi_context* ctx);
 
 /* Measurement only (not part of the reference API): per-launch HIP-event

@@ -5,6 +5,7 @@ visible, calls raise.  torch is imported first so the process holds torch's
 HIP runtime before the library binds to it (same SONAME, one runtime).
 """
 import contextlib
+import threading
 import ctypes
 import gc
 import os
@@ -267,6 +268,9 @@ def ensure_workspace(device):
     return _workspaces[key]
 
 
+_ctx_tls = threading.local()
+
+
 class Context(object):
     """An smi_context (include/surreal_mi.h, re-entrancy): its own device
     workspace for the split-K / reduction partials of the launches its owner
@@ -284,6 +288,10 @@ class Context(object):
 
     def make_current(self):
         check(lib().smi_context_make_current(ctypes.c_void_p(self.handle)), 'smi_context_make_current')
+        # the thread keeps the context (and so its workspace) alive for as long
+        # as it is this thread's current one: a launch the thread issues after
+        # the owner dropped its reference still has live partial buffers
+        _ctx_tls.current = self
 
     def __del__(self):
         # no make_current(None) here: the collector may run this on any thread
