@@ -1625,7 +1625,11 @@ static int lstm_valu_r(int B, int H) {
   if (R < 1) R = 1;
   if (R == 3) R = 4;
   if (R > 4) return 0;
-  if (m < 0 && R > 2) return 0;
+  // auto: the row forms only at one segment per CU (the K-split q form); at
+  // two or more the r4 MFMA form (384 / 512 segments: 4.32 / 4.98 ms per
+  // learn against 4.76 / 5.44 with R = 2 and 4.42 / 5.12 with the q form at
+  // two workgroups per CU, round 6, profiles/r06/ab/lstm_form_*)
+  if (m < 0 && R > 1) return 0;
   return R;
 }
 
