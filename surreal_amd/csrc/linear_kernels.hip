@@ -1115,14 +1115,14 @@ gemm_dwd_group_kernel(DwGroup G) {
 // others) in ONE launch: the heads' gradients need nothing from the BPTT, so
 // they run on the CUs the recurrence leaves idle (la.B segments on one CU
 // each) instead of after it
-template <int BR>
+template <int BR, bool STG>
 __global__ void __launch_bounds__(kVT, 1)
 lstm_bwd_dw_kernel(LstmBwdArgs la, DwGroup G) {
+  extern __shared__ float4 dwd_red[];             // (the BPTT workgroups: their staged step inputs)
   if ((int)blockIdx.x < la.B) {
-    lstm_bwd_q_body<BR, SMI_BPTT_CH4 != 0>(la, blockIdx.x);
+    lstm_bwd_q_body<BR, SMI_BPTT_CH4 != 0, STG>(la, blockIdx.x, reinterpret_cast<float*>(dwd_red));
     return;
   }
-  extern __shared__ float4 dwd_red[];
   int gi = 0, rows = 0;
   dwd_group_run<8>(G, blockIdx.x - la.B, gridDim.x - la.B, dwd_red, gi, rows);
 }
@@ -2001,14 +2001,23 @@ int launch_lstm_bwd_dw(const float* dh, const float* gates, const float* cbuf, c
   // one workgroup per CU (the LDS request): the recurrence's workgroups keep
   // their CUs to themselves, the weight gradients take the others
   static const bool excl = [] { const char* e = getenv("SMI_BWD_DW_EXCL"); return !(e && e[0] == '0'); }();
-  const size_t lds = excl ? std::max(kDwdLds, (size_t)84 * 1024) : kDwdLds;
+  size_t lds = excl ? std::max(kDwdLds, (size_t)84 * 1024) : kDwdLds;
+  // the BPTT workgroups stage their step inputs in the same dynamic LDS
+  const size_t stg = (size_t)lstm_bwd_stage_floats(S, H) * 4;
+  const bool stage = use_bwd_stage() && stg <= kBwdStageMax;
+  if (stage) lds = std::max(lds, stg);
   LstmBwdArgs la{dh, gates, cbuf, w_hh, S, B, H, dgates, skip};
   const dim3 grid((unsigned)(B + Ga.wg0[Ga.n]));
   const int kslot = ktime_begin(st);
-#define SMI_BD(BR_)                                                                  \
-  do {                                                                               \
-    allow_lds(lstm_bwd_dw_kernel<BR_>, lds);                                         \
-    hipLaunchKernelGGL(lstm_bwd_dw_kernel<BR_>, grid, dim3(kVT), lds, st, la, Ga);   \
+#define SMI_BD(BR_)                                                                          \
+  do {                                                                                       \
+    if (stage) {                                                                             \
+      allow_lds(lstm_bwd_dw_kernel<BR_, true>, lds);                                         \
+      hipLaunchKernelGGL((lstm_bwd_dw_kernel<BR_, true>), grid, dim3(kVT), lds, st, la, Ga); \
+    } else {                                                                                 \
+      allow_lds(lstm_bwd_dw_kernel<BR_, false>, lds);                                        \
+      hipLaunchKernelGGL((lstm_bwd_dw_kernel<BR_, false>), grid, dim3(kVT), lds, st, la, Ga);\
+    }                                                                                        \
   } while (0)
   if (br == 16) SMI_BD(16);
   else if (br == 25) SMI_BD(25);

@@ -98,8 +98,23 @@ __device__ __forceinline__ float dpp_ror8(float v) {          // row_ror:8
 #ifndef SMI_BPTT_CH4
 #define SMI_BPTT_CH4 1
 #endif
-template <int BR, bool CH4 = false>
-__device__ __forceinline__ void lstm_bwd_q_body(const LstmBwdArgs& a, int b) {
+// Floats of the BPTT's staged per-step inputs (lstm_bwd_q_body with a
+// stage): gates [S][4H], cell states [S+1][H], dh [S][H] of one segment
+__host__ __device__ inline int64_t lstm_bwd_stage_floats(int S, int H) {
+  return (int64_t)S * 4 * H + (int64_t)(S + 1) * H + (int64_t)S * H;
+}
+
+// STG: stage = LDS of lstm_bwd_stage_floats(S, H) floats, 16-byte aligned
+// (a compile-time choice: a run-time one leaves the global-load path's waits
+// in the loop).  With it every step input (activated gates, c_t, c_{t-1}, dh_t) is
+// copied to LDS in the prologue and the step loop issues no global load
+// (without it the loop header waits vmcnt(0) every step: the inputs fetched
+// two steps ahead, and the previous step's dgates store, stores counting in
+// vmcnt on gfx950).  Measured neutral-to-worse (the staging prologue costs
+// what the waits did): an A/B knob, SMI_BWD_STAGE=1 (round 6)
+template <int BR, bool CH4 = false, bool STG = false>
+__device__ __forceinline__ void lstm_bwd_q_body(const LstmBwdArgs& a, int b,
+                                                float* __restrict__ stage = nullptr) {
   if (a.skip && a.skip[0] != 0) return;
   constexpr int BRP = (BR + 3) & ~3;
   __shared__ __attribute__((aligned(16))) float dG[2][16 * BRP];
@@ -131,13 +146,53 @@ __device__ __forceinline__ void lstm_bwd_q_body(const LstmBwdArgs& a, int b) {
   }
   const int dgi = (g / BR) * BRP + g % BR;        // this lane's dgate in the padded image
   float gq, ct, ctm, dho, gqn, ctn, ctmn, dhon;
-  auto fetch = [&](int t, float& G, float& C, float& CM, float& DH) {
-    G = a.gates[((int64_t)t * B + b) * G4 + g];
-    C = a.cbuf[(int64_t)(t + 1) * BH + (int64_t)b * H + uc];
-    CM = a.cbuf[(int64_t)t * BH + (int64_t)b * H + uc];
-    DH = a.dh[(int64_t)t * BH + (int64_t)b * H + uc];
-  };
   if (a.S <= 0) return;
+  float* sG = stage;                                // [S][4H]
+  float* sC = STG ? sG + (int64_t)a.S * G4 : nullptr;       // [S+1][H]
+  float* sD = STG ? sC + (int64_t)(a.S + 1) * H : nullptr;  // [S][H]
+  if constexpr (STG) {
+    // rows of 4H / H floats, float4 runs (H % 4 == 0: lstm_bwd_q_ok), eight
+    // float4 loads per thread in flight per trip, then their LDS stores
+    const int q4 = H >> 2, g4 = 4 * q4;
+    const int ng = a.S * g4, nc = (a.S + 1) * q4, nd = a.S * q4;
+    const int n4 = ng + nc + nd, NT = blockDim.x;
+    auto src = [&](int e) -> const float4* {
+      if (e < ng) {
+        const int t = e / g4, j = e - t * g4;
+        return reinterpret_cast<const float4*>(a.gates + ((int64_t)t * B + b) * G4) + j;
+      }
+      e -= ng;
+      if (e < nc) {
+        const int t = e / q4, j = e - t * q4;
+        return reinterpret_cast<const float4*>(a.cbuf + (int64_t)t * BH + (int64_t)b * H) + j;
+      }
+      e -= nc;
+      const int t = e / q4, j = e - t * q4;
+      return reinterpret_cast<const float4*>(a.dh + (int64_t)t * BH + (int64_t)b * H) + j;
+    };
+    float4* s4 = reinterpret_cast<float4*>(stage);
+    for (int e0 = tid; e0 < n4; e0 += 8 * NT) {
+      float4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *src(min(e0 + j * NT, n4 - 1));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s4[min(e0 + j * NT, n4 - 1)] = v[j];   // (a clamped index writes its owner's value)
+    }
+    __syncthreads();
+  }
+  auto fetch = [&](int t, float& G, float& C, float& CM, float& DH) {
+    if constexpr (STG) {
+      G = sG[t * G4 + g];
+      C = sC[(t + 1) * H + uc];
+      CM = sC[t * H + uc];
+      DH = sD[t * H + uc];
+    } else {
+      G = a.gates[((int64_t)t * B + b) * G4 + g];
+      C = a.cbuf[(int64_t)(t + 1) * BH + (int64_t)b * H + uc];
+      CM = a.cbuf[(int64_t)t * BH + (int64_t)b * H + uc];
+      DH = a.dh[(int64_t)t * BH + (int64_t)b * H + uc];
+    }
+  };
   fetch(a.S - 1, gq, ct, ctm, dho);
   fetch(a.S >= 2 ? a.S - 2 : 0, gqn, ctn, ctmn, dhon);
   float dcreg = 0.f, dhr = 0.f;

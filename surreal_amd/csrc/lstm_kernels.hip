@@ -1579,11 +1579,12 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
 // BR: rows of W_hh per lane of a 16-lane row (16 BR >= 4H); the body is
 // lstm_bwd_q_body (lstm_cell.hpp), shared with the BPTT + weight-gradient
 // launch of linear_kernels.hip
-template <int BR>
+template <int BR, bool STG>
 __global__ void __launch_bounds__(kVT)
 lstm_bwd_q_kernel(LstmBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float bstage[];
   LSTM_T0();
-  lstm_bwd_q_body<BR, SMI_BPTT_CH4 != 0>(a, blockIdx.x);
+  lstm_bwd_q_body<BR, SMI_BPTT_CH4 != 0, STG>(a, blockIdx.x, bstage);
   LSTM_TICK(4);                                  // the whole BPTT (its own launch)
 }
 #endif  // SMI_LSTM_VALU_HALF
@@ -1753,6 +1754,14 @@ void lstm_v_fwd(const LstmFwdArgs& a, int R, int kx, hipStream_t st) {
   else if (kx <= 48) fwd_v_dispatch_kp<1, 48>(a, st);
   else fwd_v_dispatch_kp<1, 64>(a, st);
 }
+// the BPTT's step inputs staged in LDS (SMI_BWD_STAGE=1; A/B knob, off: the
+// staging prologue cost what the loop's per-step vmcnt(0) did -- 128 segments
+// 2.771-2.777 vs 2.764-2.765 ms per learn, BPTT 27.7 vs 26.7-27.0 us at 256,
+// profiles/r06/ab/bwd_stage_*; the inputs are read two steps ahead instead)
+bool use_bwd_stage() {
+  static const bool on = [] { const char* e = getenv("SMI_BWD_STAGE"); return e && e[0] == '1'; }();
+  return on;
+}
 // the BPTT's K-split form loads W_hh as float4 runs (lstm_bwd_q_body)
 bool lstm_bwd_q_ok(int H, const float* w_hh) {
   return use_q() && H % 4 == 0 && (reinterpret_cast<uintptr_t>(w_hh) & 15) == 0;
@@ -1760,9 +1769,22 @@ bool lstm_bwd_q_ok(int H, const float* w_hh) {
 void lstm_v_bwd(const LstmBwdArgs& a, int R, hipStream_t st) {
   if (R == 1 && lstm_bwd_q_ok(a.H, a.w_hh)) {
     const dim3 grid(a.B), blk((4 * a.H + 63) & ~63);
-    if (a.H <= 64) hipLaunchKernelGGL(lstm_bwd_q_kernel<16>, grid, blk, 0, st, a);
-    else if (a.H <= 100) hipLaunchKernelGGL(lstm_bwd_q_kernel<25>, grid, blk, 0, st, a);
-    else hipLaunchKernelGGL(lstm_bwd_q_kernel<32>, grid, blk, 0, st, a);
+    // the step inputs staged in LDS when they fit (lstm_bwd_q_body)
+    const size_t stg = (size_t)lstm_bwd_stage_floats(a.S, a.H) * 4;
+    const bool s = use_bwd_stage() && stg <= kBwdStageMax;
+#define SMI_BQ(BR_)                                                                       \
+    do {                                                                                  \
+      if (s) {                                                                            \
+        allow_lds(lstm_bwd_q_kernel<BR_, true>, stg);                                     \
+        hipLaunchKernelGGL((lstm_bwd_q_kernel<BR_, true>), grid, blk, stg, st, a);        \
+      } else {                                                                            \
+        hipLaunchKernelGGL((lstm_bwd_q_kernel<BR_, false>), grid, blk, 0, st, a);         \
+      }                                                                                   \
+    } while (0)
+    if (a.H <= 64) SMI_BQ(16);
+    else if (a.H <= 100) SMI_BQ(25);
+    else SMI_BQ(32);
+#undef SMI_BQ
     return;
   }
   if (R == 1) bwd_v_dispatch_kp<1>(a, st);

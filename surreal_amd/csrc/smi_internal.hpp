@@ -67,6 +67,9 @@ int dw_group_epilogue(const DwEpilogue& x);
 bool dw_group_takes(int M, int N);
 // BR of the one-segment-per-workgroup BPTT form for (B, H), 0 when another form runs
 int lstm_bwd_q_form(int B, int H, const float* w_hh);
+// the BPTT's step inputs staged in LDS (lstm_bwd_q_body) when they fit kBwdStageMax
+bool use_bwd_stage();
+constexpr size_t kBwdStageMax = 120 * 1024;
 // the LSTM BPTT (lstm_bwd_q form) and the weight gradients queued so far in the
 // open dW group in one launch (linear_kernels.hip); SMI_E_NOFIT: run
 // launch_lstm_bwd instead (nothing launched)
