@@ -1423,13 +1423,15 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
       const int gs = nt * 16 + (lane & 15);                 // the D column's gate
       const float bsum = bbi[ti] + bbh[ti];                  // (gs >= G4 dropped)
       const int dst = gs < G4 ? 4 * (gs % H) + gs / H : 0;
-      for (int mt = 0; mt < nmt; ++mt) {
+      auto x_tile = [&](int mt) {
         const int r = min(mt * 16 + (lane & 15), a.S - 1);
         const float4* xr = reinterpret_cast<const float4*>(xS + r * KX + 4 * (lane >> 4));
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        // every k chunk (no early exit at din: columns past din are the zero
+        // padding of the staged x, exact zeros in the sums), so a tile's LDS
+        // reads issue together instead of one wait per chunk
 #pragma unroll
         for (int m = 0; m < KS / 4; ++m) {
-          if (16 * m >= a.din) break;
           const float4 xv = xr[4 * m];
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, bw[ti][4 * m], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, bw[ti][4 * m + 1], acc, 0, 0, 0);
@@ -1441,7 +1443,14 @@ lstm_fwd_q_kernel(LstmFwdArgs a0, LstmFwdArgs a1) {
           const int t = mt * 16 + 4 * (lane >> 4) + i;
           if (t < a.S && gs < G4) xP[(int64_t)t * NT + dst] = acc[i] + bsum;
         }
-      }
+      };
+      // the step tiles unrolled (S <= 61 in this form: kVxMax), no loop back
+      // edge for the waitcnt pass to merge over (the first tile had waited
+      // vmcnt(0), i.e. on W_hh's loads as well as its own W_ih operands)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        if (mt < nmt) x_tile(mt);
+      for (int mt = 4; mt < nmt; ++mt) x_tile(mt);
     }
     __syncthreads();
     LSTM_TICK(1);                                // x parts on the matrix cores

@@ -551,6 +551,11 @@ static bool try_gae_seg(const GaeWinArgs& a, int* n_partials, hipStream_t stream
   if (!cap) {
     cap = resident_grid(k, SEG, G::LDS);
     if (cap > 1024) cap = 1024;
+    // SMI_GAE_GRID: workgroups of the grid-stride loop (each block's loads
+    // prefetched behind the previous block's rows; A/B knob)
+    const char* e = getenv("SMI_GAE_GRID");
+    const int g = e && e[0] ? atoi(e) : 0;
+    if (g > 0 && g < cap) cap = g;
   }
   const int grid = (int)(nblk < cap ? nblk : cap);
   hipLaunchKernelGGL(k, dim3(grid), dim3(SEG), G::LDS, stream, a, nblk);
