@@ -57,6 +57,10 @@ struct LstmFwdArgs {
   // over more steps than a backward needs (the GAE critic pass over T + 1
   // steps serves as the first policy forward over its first E steps)
   int keep;
+  // r4 MFMA forward (round 6): W_ih and W_hh reach the lanes' row registers
+  // through LDS (coalesced global reads) instead of a row per lane from global
+  // memory; set by the launcher with the dynamic LDS it sized for it
+  int wstage;
 };
 
 struct LstmBwdArgs {

@@ -577,10 +577,33 @@ __device__ __forceinline__ f32x4 mfma4x64(float a, float b, f32x4 c) {
 // joins W_hh's in registers, x_t of the 4 segments is staged in LDS one step
 // ahead, and the k loop runs over [x_t | h_{t-1}] — no xproj GEMM and no
 // [S][B][4H] round trip through HBM.
+// r4 forward weight staging (round 6).  A lane's W_hh / W_ih row loaded
+// straight from global memory puts 64 rows -- 64 cache lines -- behind every
+// load instruction of the wave (the prologue: 11 us of a 54 us launch at C3,
+// tools/lstm_ticks.py, tick 6).  Staged (A/B knob SMI_R4_WSTAGE=1, measured
+// slower: 18.8 us), each pass
+// is a contiguous block of rows read as float4 runs by the whole workgroup
+// (R4_PT per thread, one trip), stored to LDS, and each lane then reads its
+// own row from LDS; the next pass's global loads are in flight meanwhile.
+constexpr int R4_PT = 11;
+template <int N>
+__device__ __forceinline__ void r4_row_from_lds(const float* lds, int rb, int rc, int len, int myrow,
+                                                float (&dst)[N]) {
+  if (myrow >= rb && myrow < rb + rc) {
+    const float* r = lds + (myrow - rb) * len;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const float t = r[min(k, len - 1)];
+      dst[k] = k < len ? t : 0.f;
+    }
+  }
+}
+
 template <int KP, int KX>
 __global__ void __launch_bounds__(kWG8)
 lstm_fwd_r4_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  LSTM_T0();
   const int keepS = a.keep > 0 ? a.keep : a.S;     // steps whose c / gates are stored
   constexpr int KXS = KX > 0 ? KX : 8;
   __shared__ __attribute__((aligned(16))) float hS[2][LR4 * KP];
@@ -593,16 +616,48 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
   const int col = wave * 64 + lane;
   const bool cact = wave * 64 < G4;              // wave-uniform
   const int colc = col < G4 ? col : G4 - 1;
-  // the lane's W_hh (and W_ih) row in registers, loaded in 16- (8-) byte runs
-  // where the rows allow (a load per k put 64 rows' lines behind every
-  // instruction, 32 instructions per line)
   float w[KP];
-  load_row<KP>(a.w_hh + (int64_t)colc * H, H, w);
-  float bh = a.b_hh[colc];
   float wx[KXS];
-  if constexpr (KX > 0) {
-    load_row<KX>(a.w_ih + (int64_t)colc * a.din, a.din, wx);
-    bh += a.b_ih[colc];
+  float bh = a.b_hh[colc];
+  if constexpr (KX > 0) bh += a.b_ih[colc];
+  if (a.wstage) {                                  // (uniform; the launcher sized the LDS)
+    extern __shared__ __attribute__((aligned(16))) float4 wst4[];
+    const float* wst = reinterpret_cast<const float*>(wst4);
+    float4 v[R4_PT];
+    auto gload = [&](const float* M, int n4) {
+#pragma unroll
+      for (int j = 0; j < R4_PT; ++j)
+        v[j] = reinterpret_cast<const float4*>(M)[min(tid + j * kWG8, n4 - 1)];
+    };
+    auto lstore = [&](int n4) {
+#pragma unroll
+      for (int j = 0; j < R4_PT; ++j) wst4[min(tid + j * kWG8, n4 - 1)] = v[j];
+    };
+    const int nh4 = (2 * H * H) >> 2;              // half of W_hh: rows [0, 2H) / [2H, 4H)
+    if constexpr (KX > 0) {
+      gload(a.w_ih, (G4 * a.din) >> 2);
+      lstore((G4 * a.din) >> 2);
+      __syncthreads();
+      gload(a.w_hh, nh4);
+      r4_row_from_lds<KX>(wst, 0, G4, a.din, colc, wx);
+      __syncthreads();
+    } else {
+      gload(a.w_hh, nh4);
+    }
+    lstore(nh4);
+    __syncthreads();
+    gload(a.w_hh + (int64_t)2 * H * H, nh4);
+    r4_row_from_lds<KP>(wst, 0, 2 * H, H, colc, w);
+    __syncthreads();
+    lstore(nh4);
+    __syncthreads();
+    r4_row_from_lds<KP>(wst, 2 * H, 2 * H, H, colc, w);
+  } else {
+    // the lane's W_hh (and W_ih) row in registers, loaded in 16- (8-) byte runs
+    // where the rows allow (a load per k put 64 rows' lines behind every
+    // instruction, 32 instructions per line)
+    load_row<KP>(a.w_hh + (int64_t)colc * H, H, w);
+    if constexpr (KX > 0) load_row<KX>(a.w_ih + (int64_t)colc * a.din, a.din, wx);
   }
   // x staging: thread tid < 4*KX owns (row tid / KX, k tid % KX) of x_t
   const int xr = tid / KXS, xk = tid - (tid / KXS) * KXS;
@@ -661,7 +716,7 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
     for (int i = 0; i < 4; ++i) xp[i] = a.xproj[xoff[i]];
   }
   __syncthreads();
-  LSTM_T0();
+  LSTM_TICK(6);                                  // prologue (weights, x_0, c0 / h0)
   // x_t W_ih^T does not depend on h_{t-1}: its MFMAs for step t+1 are issued
   // right after step t's pre-activations are published, so the matrix pipe
   // works through them while the same waves run the cell update (VALU /
@@ -779,6 +834,7 @@ template <int KW>
 __global__ void __launch_bounds__(kWG8)
 lstm_bwd_r4_kernel(LstmBwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
+  LSTM_T0();
   constexpr int G4P = 4 * 128 + KW;               // dG row stride (reads run up to KW past 4H)
   __shared__ __attribute__((aligned(16))) float dG[LR4 * G4P];
   __shared__ float red[8][LR4][64];
@@ -820,7 +876,7 @@ lstm_bwd_r4_kernel(LstmBwdArgs a) {
   if (cell && a.S > 0) fetch(a.S - 1);
   float dcreg = 0.f;
   __syncthreads();
-  LSTM_T0();
+  LSTM_TICK(7);                                  // prologue (W_hh, first step inputs)
   for (int t = a.S - 1; t >= 0; --t) {
     if (cell) {
       float dhr = 0.f;
@@ -1840,6 +1896,28 @@ extern "C" int smi_lstm_phase_ticks(unsigned long long* out /* [8] */) {
 int64_t lstm_fwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * lstm_q(H)) * 4; }
 int64_t lstm_bwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * H) * 4; }
 
+// the r4 forward's weight staging (lstm_fwd_r4_kernel): dynamic LDS bytes, 0
+// when it does not apply (off unless SMI_R4_WSTAGE=1: measured slower, the
+// prologue 11.1 -> 18.8 us and C3 6.92-6.93 -> 7.15-7.19 ms per learn -- three
+// staged passes with their barriers and 4-way conflicted row reads cost more
+// than the row-per-lane loads; also: more than one resident round of
+// workgroups, rows not in float4 runs, a pass beyond one trip)
+static size_t r4_wstage_bytes(const LstmFwdArgs& a, bool fused_x) {
+  static const bool on = [] { const char* e = getenv("SMI_R4_WSTAGE"); return e && e[0] == '1'; }();
+  if (!on) return 0;
+  const int H = a.H, G4 = 4 * H;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if ((a.B + LR4 - 1) / LR4 > device_cus() || H % 4 != 0 || !al16(a.w_hh)) return 0;
+  const int64_t cap4 = (int64_t)R4_PT * kWG8;
+  int64_t floats = 2LL * H * H;                    // half of W_hh per pass
+  if (floats / 4 > cap4) return 0;
+  if (fused_x) {
+    if (!al16(a.w_ih) || ((int64_t)G4 * a.din) % 4 != 0 || (int64_t)G4 * a.din / 4 > cap4) return 0;
+    floats = std::max<int64_t>(floats, (int64_t)G4 * a.din);
+  }
+  return (size_t)floats * 4;
+}
+
 int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, const float* h0,
                     const float* c0, int S, int B, int H, float* hbuf, float* cbuf, float* gates,
                     hipStream_t st, const int* skip, int keep) {
@@ -1857,10 +1935,18 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
   }
   if (H <= 128 && use_r4()) {
     const dim3 g4((B + LR4 - 1) / LR4);
-    if (H <= 32) hipLaunchKernelGGL((lstm_fwd_r4_kernel<32, 0>), g4, dim3(kWG8), 0, st, a);
-    else if (H <= 64) hipLaunchKernelGGL((lstm_fwd_r4_kernel<64, 0>), g4, dim3(kWG8), 0, st, a);
-    else if (H <= 104) hipLaunchKernelGGL((lstm_fwd_r4_kernel<104, 0>), g4, dim3(kWG8), 0, st, a);
-    else hipLaunchKernelGGL((lstm_fwd_r4_kernel<128, 0>), g4, dim3(kWG8), 0, st, a);
+    const size_t wl = r4_wstage_bytes(a, false);
+    a.wstage = wl > 0;
+#define SMI_R4F(KP_)                                                                 \
+    do {                                                                             \
+      if (wl) allow_lds(lstm_fwd_r4_kernel<KP_, 0>, wl);                             \
+      hipLaunchKernelGGL((lstm_fwd_r4_kernel<KP_, 0>), g4, dim3(kWG8), wl, st, a);   \
+    } while (0)
+    if (H <= 32) SMI_R4F(32);
+    else if (H <= 64) SMI_R4F(64);
+    else if (H <= 104) SMI_R4F(104);
+    else SMI_R4F(128);
+#undef SMI_R4F
     return check_launch("lstm_fwd_r4_kernel");
   }
   const size_t lds = (size_t)lstm_fwd_lds(H);
@@ -1914,13 +2000,21 @@ int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, c
     return check_launch("lstm_fwd_v_kernel");
   }
   const dim3 g4((B + LR4 - 1) / LR4);
+  const size_t wl = r4_wstage_bytes(a, true);
+  a.wstage = wl > 0;
+#define SMI_R4X(KP_, KX_)                                                              \
+  do {                                                                                 \
+    if (wl) allow_lds(lstm_fwd_r4_kernel<KP_, KX_>, wl);                               \
+    hipLaunchKernelGGL((lstm_fwd_r4_kernel<KP_, KX_>), g4, dim3(kWG8), wl, st, a);     \
+  } while (0)
   if (din <= 48) {
-    if (H <= 64) hipLaunchKernelGGL((lstm_fwd_r4_kernel<64, 48>), g4, dim3(kWG8), 0, st, a);
-    else hipLaunchKernelGGL((lstm_fwd_r4_kernel<104, 48>), g4, dim3(kWG8), 0, st, a);
+    if (H <= 64) SMI_R4X(64, 48);
+    else SMI_R4X(104, 48);
   } else {
-    if (H <= 64) hipLaunchKernelGGL((lstm_fwd_r4_kernel<64, 64>), g4, dim3(kWG8), 0, st, a);
-    else hipLaunchKernelGGL((lstm_fwd_r4_kernel<104, 64>), g4, dim3(kWG8), 0, st, a);
+    if (H <= 64) SMI_R4X(64, 64);
+    else SMI_R4X(104, 64);
   }
+#undef SMI_R4X
   return check_launch("lstm_fwd_r4_kernel");
 }
 

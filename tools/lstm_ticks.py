@@ -5,6 +5,7 @@ wave 0 accumulates wall-clock ticks (100 MHz) per phase of every step:
   fwd [0] recurrent MFMAs + pre-activation store  [1] barrier + x-part issue +
       cell update  [2] second barrier
   bwd [3] cell backward + stores  [4] barrier  [5] dh_rec MFMAs + barrier
+  r4 prologues (round 6): [6] forward, [7] BPTT, kernel start to first barrier
 Prints one JSON line: microseconds per step per phase."""
 import ctypes
 import json
@@ -52,7 +53,13 @@ def main():
                       'fwd_us_per_step': {'mfma': us(buf[0], fwd_steps), 'cell': us(buf[1], fwd_steps),
                                           'barrier2': us(buf[2], fwd_steps)},
                       'bwd_us_per_step': {'cell': us(buf[3], bwd_steps), 'barrier': us(buf[4], bwd_steps),
-                                          'mfma': us(buf[5], bwd_steps)}}), flush=True)
+                                          'mfma': us(buf[5], bwd_steps)},
+                      # round 6: the r4 forms' prologues (kernel start to the first barrier),
+                      # per launch (launches per learn: GAE + PREP + the policy forwards +
+                      # 10 value, and one BPTT per update)
+                      'r4_prologue_us_per_launch': {'fwd': us(bufs[0][6], K * (2 + runs + 1 + 10)),
+                                                    'bwd': us(bufs[0][7], K * (runs + 10))}}),
+          flush=True)
 
 
 if __name__ == '__main__':
