@@ -599,7 +599,32 @@ __device__ __forceinline__ void r4_row_from_lds(const float* lds, int rb, int rc
   }
 }
 
-template <int KP, int KX>
+// VF (round 6): the launcher checked that W_hh rows are float4 runs (H % 4 == 0,
+// 16-byte aligned) and W_ih rows float2 runs (din even, 8-byte aligned), so the
+// row loads take ONE vector width without a run-time branch -- load_row's
+// uniform alignment branch made the waitcnt pass wait vmcnt(0) at its merge,
+// serializing the W_hh and W_ih loads into separate memory round trips
+// (n % V == 0: a run is wholly inside the row or wholly past it; runs past it
+// read a zero vector by address -- a select on the loaded value would make
+// the waitcnt pass wait for the load right there)
+__device__ __attribute__((aligned(16))) float g_lstm_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+template <int N, int V>
+__device__ __forceinline__ void load_row_v(const float* r, int n, float* dst) {
+  static_assert(N % 4 == 0 && (V == 4 || V == 2), "vector rows");
+#pragma unroll
+  for (int k = 0; k < N; k += V) {
+    const float* src = k < n ? r + k : g_lstm_zero4;
+    if constexpr (V == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(src);
+      dst[k] = v.x; dst[k + 1] = v.y; dst[k + 2] = v.z; dst[k + 3] = v.w;
+    } else {
+      const float2 v = *reinterpret_cast<const float2*>(src);
+      dst[k] = v.x; dst[k + 1] = v.y;
+    }
+  }
+}
+
+template <int KP, int KX, bool VF = false>
 __global__ void __launch_bounds__(kWG8)
 lstm_fwd_r4_kernel(LstmFwdArgs a) {
   if (a.skip && a.skip[0] != 0) return;
@@ -656,8 +681,13 @@ lstm_fwd_r4_kernel(LstmFwdArgs a) {
     // the lane's W_hh (and W_ih) row in registers, loaded in 16- (8-) byte runs
     // where the rows allow (a load per k put 64 rows' lines behind every
     // instruction, 32 instructions per line)
-    load_row<KP>(a.w_hh + (int64_t)colc * H, H, w);
-    if constexpr (KX > 0) load_row<KX>(a.w_ih + (int64_t)colc * a.din, a.din, wx);
+    if constexpr (VF) {
+      load_row_v<KP, 4>(a.w_hh + (int64_t)colc * H, H, w);
+      if constexpr (KX > 0) load_row_v<KX, 2>(a.w_ih + (int64_t)colc * a.din, a.din, wx);
+    } else {
+      load_row<KP>(a.w_hh + (int64_t)colc * H, H, w);
+      if constexpr (KX > 0) load_row<KX>(a.w_ih + (int64_t)colc * a.din, a.din, wx);
+    }
   }
   // x staging: thread tid < 4*KX owns (row tid / KX, k tid % KX) of x_t
   const int xr = tid / KXS, xk = tid - (tid / KXS) * KXS;
@@ -1896,6 +1926,15 @@ extern "C" int smi_lstm_phase_ticks(unsigned long long* out /* [8] */) {
 int64_t lstm_fwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * lstm_q(H)) * 4; }
 int64_t lstm_bwd_lds(int H) { return (int64_t)2 * LR * lstm_ld(4 * H) * 4; }
 
+// the r4 forward's fixed-width row loads (VF): W_hh float4 runs, W_ih float2
+// runs (SMI_R4_VF=0: the alignment-branching loads; A/B knob)
+static bool r4_vf(const LstmFwdArgs& a, bool fused_x) {
+  static const bool on = [] { const char* e = getenv("SMI_R4_VF"); return !(e && e[0] == '0'); }();
+  auto al = [](const void* p, uintptr_t m) { return (reinterpret_cast<uintptr_t>(p) & m) == 0; };
+  if (!on || a.H % 4 != 0 || !al(a.w_hh, 15)) return false;
+  return !fused_x || (a.din % 2 == 0 && a.din >= 2 && al(a.w_ih, 7));
+}
+
 // the r4 forward's weight staging (lstm_fwd_r4_kernel): dynamic LDS bytes, 0
 // when it does not apply (off unless SMI_R4_WSTAGE=1: measured slower, the
 // prologue 11.1 -> 18.8 us and C3 6.92-6.93 -> 7.15-7.19 ms per learn -- three
@@ -1937,10 +1976,15 @@ int launch_lstm_fwd(const float* xproj, const float* w_hh, const float* b_hh, co
     const dim3 g4((B + LR4 - 1) / LR4);
     const size_t wl = r4_wstage_bytes(a, false);
     a.wstage = wl > 0;
-#define SMI_R4F(KP_)                                                                 \
-    do {                                                                             \
-      if (wl) allow_lds(lstm_fwd_r4_kernel<KP_, 0>, wl);                             \
-      hipLaunchKernelGGL((lstm_fwd_r4_kernel<KP_, 0>), g4, dim3(kWG8), wl, st, a);   \
+    const bool vf = !a.wstage && r4_vf(a, false);
+#define SMI_R4F(KP_)                                                                        \
+    do {                                                                                    \
+      if (vf) {                                                                             \
+        hipLaunchKernelGGL((lstm_fwd_r4_kernel<KP_, 0, true>), g4, dim3(kWG8), 0, st, a);   \
+      } else {                                                                              \
+        if (wl) allow_lds(lstm_fwd_r4_kernel<KP_, 0>, wl);                                  \
+        hipLaunchKernelGGL((lstm_fwd_r4_kernel<KP_, 0>), g4, dim3(kWG8), wl, st, a);        \
+      }                                                                                     \
     } while (0)
     if (H <= 32) SMI_R4F(32);
     else if (H <= 64) SMI_R4F(64);
@@ -2002,10 +2046,15 @@ int launch_lstm_fwd_x(const float* x, int64_t ldx, int din, const float* w_ih, c
   const dim3 g4((B + LR4 - 1) / LR4);
   const size_t wl = r4_wstage_bytes(a, true);
   a.wstage = wl > 0;
-#define SMI_R4X(KP_, KX_)                                                              \
-  do {                                                                                 \
-    if (wl) allow_lds(lstm_fwd_r4_kernel<KP_, KX_>, wl);                               \
-    hipLaunchKernelGGL((lstm_fwd_r4_kernel<KP_, KX_>), g4, dim3(kWG8), wl, st, a);     \
+  const bool vf = !a.wstage && r4_vf(a, true);
+#define SMI_R4X(KP_, KX_)                                                                     \
+  do {                                                                                        \
+    if (vf) {                                                                                 \
+      hipLaunchKernelGGL((lstm_fwd_r4_kernel<KP_, KX_, true>), g4, dim3(kWG8), 0, st, a);     \
+    } else {                                                                                  \
+      if (wl) allow_lds(lstm_fwd_r4_kernel<KP_, KX_>, wl);                                    \
+      hipLaunchKernelGGL((lstm_fwd_r4_kernel<KP_, KX_>), g4, dim3(kWG8), wl, st, a);          \
+    }                                                                                         \
   } while (0)
   if (din <= 48) {
     if (H <= 64) SMI_R4X(64, 48);
