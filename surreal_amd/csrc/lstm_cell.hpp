@@ -201,6 +201,14 @@ __device__ __forceinline__ void lstm_bwd_q_body(const LstmBwdArgs& a, int b,
   fetch(a.S >= 2 ? a.S - 2 : 0, gqn, ctn, ctmn, dhon);
   float dcreg = 0.f, dhr = 0.f;
   __syncthreads();
+  // waves past ceil(4H / 64) (the BPTT + dW launch's 512-thread workgroups:
+  // an eighth wave at H = 100) hold only units past H and rows past 4H, whose
+  // results are dropped: they take the step loop's barriers and nothing else
+  // (one barrier per step, as below)
+  if ((tid & ~63) >= ((G4 + 63) & ~63)) {
+    for (int t = a.S - 1; t >= 0; --t) __syncthreads();
+    return;
+  }
   for (int t = a.S - 1; t >= 0; --t) {
     float* dgw = dG[t & 1];
     const float ig = quad_bcast<0>(gq), fg = quad_bcast<1>(gq);
