@@ -964,14 +964,23 @@ obs_iter_colsum_kernel(const float* __restrict__ obs, int B, int T, int E, int D
     const bool ok = c < D;
     double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
     for (int64_t n = n0 + wave; n < n1; n += 16) {
+      // the four rows' loads unconditional (clamped row / column) and pinned
+      // before the conditional adds (same additions): under `if (ok && m < n1)`
+      // each load was its own branch with a wait, four round trips per trip
+      float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int64_t m = n + 4 * j;
-        if (ok && m < n1) {
-          const int b = (int)(m / E), t = (int)(m - (int64_t)b * E);
-          const float v = obs[((int64_t)b * T + t) * D + c];
-          s1[j] += (double)v;
-          s2[j] += (double)(v * v);
+        const int64_t m = min(n + 4 * j, n1 - 1);
+        const int b = (int)(m / E), t = (int)(m - (int64_t)b * E);
+        v[j] = obs[((int64_t)b * T + t) * D + min(c, D - 1)];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(v[j]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (ok && n + 4 * j < n1) {
+          s1[j] += (double)v[j];
+          s2[j] += (double)(v[j] * v[j]);
         }
       }
     }
