@@ -368,9 +368,23 @@ __device__ __forceinline__ void hc_transpose_tile(const float* __restrict__ W, i
   const int tk = (K + 31) >> 5;
   const int m0 = (tix / tk) * 32, k0 = (tix % tk) * 32;
   __syncthreads();
-  for (int e = threadIdx.x; e < 32 * 32; e += kWG) {
-    const int r = e >> 5, c = e & 31;
-    if (m0 + r < M && k0 + c < K) sT[r * 33 + c] = W[(int64_t)(m0 + r) * K + k0 + c];
+  // the tile's loads unconditional (clamped), pinned, then the conditional
+  // LDS stores: a load under the bounds test was its own branch with a wait,
+  // four round trips per tile (round 6)
+  static_assert(32 * 32 % kWG == 0, "whole tile passes");
+  constexpr int TP = 32 * 32 / kWG;
+  float v[TP];
+#pragma unroll
+  for (int i = 0; i < TP; ++i) {
+    const int e = threadIdx.x + i * kWG, r = e >> 5, c = e & 31;
+    v[i] = W[(int64_t)min(m0 + r, M - 1) * K + min(k0 + c, K - 1)];
+  }
+#pragma unroll
+  for (int i = 0; i < TP; ++i) asm volatile("" : "+v"(v[i]));
+#pragma unroll
+  for (int i = 0; i < TP; ++i) {
+    const int e = threadIdx.x + i * kWG, r = e >> 5, c = e & 31;
+    if (m0 + r < M && k0 + c < K) sT[r * 33 + c] = v[i];
   }
   __syncthreads();
   for (int e = threadIdx.x; e < 32 * 32; e += kWG) {
