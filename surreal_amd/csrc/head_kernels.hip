@@ -634,9 +634,10 @@ head_bwd_kernel(HeadBwdArgs a) {
     if (own) x.load(a.pg, n, AT);
     SA.init(a.W2T, a.h2, a.h2, a.h1, wave, 4, 0, 1);
     float wsurr, wkl;
-    if (pol_grad_weights(a.pg, psh, wsurr, wkl)) return;
-    const PolGradCols<AT> cols(a.pg, psh, AT);
-    const AdvNorm nadv(a.pg);
+    PolGradPre pre;
+    if (pol_grad_weights(a.pg, psh, wsurr, wkl, pre)) return;
+    const PolGradCols<AT> cols(pre, psh, AT);
+    const AdvNorm nadv(a.pg, pre.mom);
     float glv[AT];
 #pragma unroll
     for (int j = 0; j < AT; ++j) glv[j] = 0.f;

@@ -84,10 +84,15 @@ struct PolRowArgs {
 struct AdvNorm {
   bool on; float mean, den;
   __device__ explicit AdvNorm(const PolRowArgs& a) : on(a.norm_adv && a.moments), mean(0.f), den(1.f) {
-    if (!on) return;
-    const double n = a.moments[2];
-    const double m = a.moments[0] / n;
-    const double var = (a.moments[1] - n * m * m) / (n - 1.0);
+    if (on) init(a.moments[0], a.moments[1], a.moments[2]);
+  }
+  // from moments already in registers (PolGradPre)
+  __device__ AdvNorm(const PolRowArgs& a, const double* mom) : on(a.norm_adv && a.moments), mean(0.f), den(1.f) {
+    if (on) init(mom[0], mom[1], mom[2]);
+  }
+  __device__ void init(double s, double ss, double n) {
+    const double m = s / n;
+    const double var = (ss - n * m * m) / (n - 1.0);
     mean = (float)m;
     den = fmaxf((float)sqrt(var > 0.0 ? var : 0.0), 1e-4f);
   }
@@ -239,9 +244,13 @@ __device__ __forceinline__ void behave_terms(const float* ac, const float* bmu, 
 // sums; write = store the decision (stats, stop flag, coefficients), else only
 // return it (the blocks of a fused gradient pass other than block 0)
 struct Decision { int stop; float surrw, klcoef; };
-__device__ inline Decision policy_decide_body(const DecideArgs& a, const double* ps, bool write) {
+// pre (the gradient pass): the stop flag and beta loaded at the pass's start,
+// and log(exp(lv)) per column from its LDS (the same ops as the entropy's)
+struct DecidePre { int stop; float beta; const float* lsig; };
+__device__ inline Decision policy_decide_body(const DecideArgs& a, const double* ps, bool write,
+                                              const DecidePre* pre = nullptr) {
   Decision r{1, 0.f, 0.f};
-  if (a.ci[CI_STOP]) return r;
+  if (pre ? pre->stop : a.ci[CI_STOP]) return r;
   const double n = (double)a.N;
   const float kl = (float)(ps[PS_KL] / n);
   // statistics of the forward with the current parameters (curr_pol after the
@@ -268,7 +277,7 @@ __device__ inline Decision policy_decide_body(const DecideArgs& a, const double*
   r.surrw = (float)(1.0 / n);
   if (write) {
     float ent = 0.f;
-    for (int j = 0; j < a.A; ++j) ent += logf(expf(a.lv[j]));
+    for (int j = 0; j < a.A; ++j) ent += pre ? pre->lsig[j] : logf(expf(a.lv[j]));
     ent = 0.5f * ent + a.c_ent;
     a.stats[SMI_ST_ENTROPY] = ent;
     a.cf[CF_SURRW] = r.surrw;
@@ -280,7 +289,7 @@ __device__ inline Decision policy_decide_body(const DecideArgs& a, const double*
       a.cf[CF_KLCOEF] = 0.f;
     }
   } else {
-    const float beta = a.hyper[SMI_HYP_BETA];
+    const float beta = pre ? pre->beta : a.hyper[SMI_HYP_BETA];
     const float surr = -(float)(ps[PS_SURR] / n);
     float loss = surr + beta * kl;
     float coef = beta;
@@ -313,26 +322,100 @@ struct PolGradShared { float sig[32], lsig[32], rsig[32]; double sps[PS_N]; };
 // (reduced in reduce_decide_kernel's order: lane i sums blocks i, i + 64, ...
 // then the wave butterfly, so every workgroup reaches the same decision; block
 // 0 writes it).  Also stages the stds in sh.  Returns true when the epoch does
-// not train (early stop / loop done): the caller returns, uniformly.  Every
+// not train (early stop / loop done) or skip[0] != 0 (the caller's skip
+// flag, optional): the caller returns, uniformly.  Every
 // thread of the workgroup must call it (it has barriers).
+//
+// Every global value the pass reads before its rows — the stds' log_vars, the
+// decision's flag and beta, the clip range, the advantage moments, the
+// coefficients and the partials — is loaded up front, together (PolGradPre;
+// the partials CH 64-block slabs per round trip): read where used, each was a
+// dependent memory round trip of its own (a load the compiler cannot move
+// above the decision's global stores, or a per-lane-conditional load sunk into
+// its branch), ~12 of them at C3's 336 partials.  The sums are the same adds
+// in the same order (lane i: blocks i, i + 64, ...).
+// (a global, never written: a constant-space zero made the pointer selects
+// below flat loads, whose lgkmcnt waits held back the partials' loads)
+static __device__ double g_pol_zero[4];
+struct PolGradPre {
+  int stop; float beta, clip_lo, clip_hi, cf_surrw, cf_klcoef; double mom[3];
+};
+template <int CH = 4>
 __device__ inline bool pol_grad_weights(const PolRowArgs& a, PolGradShared& sh, float& wsurr,
-                                        float& wkl) {
+                                        float& wkl, PolGradPre& pre, const int* skip = nullptr) {
   const int A = a.A;
-  for (int j = threadIdx.x; j < A; j += blockDim.x) {
-    sh.sig[j] = expf(a.lv[j]);
-    sh.lsig[j] = logf(sh.sig[j]);
-    sh.rsig[j] = expf(a.ref_lv[j]);
+  const bool dec = a.dec_part != nullptr;
+  const int lane = threadIdx.x & 63;
+  const bool dw = dec && threadIdx.x < 64;      // wave 0 reduces the partials
+  const int nb = a.dec_nb;
+  const double2* P = reinterpret_cast<const double2*>(a.dec_part);
+  // vector loads first: the stds' inputs (column threadIdx.x, A <= 32 <
+  // blockDim.x, clamped) and the first CH slabs of partials (clamped) ...
+  const int jc = min((int)threadIdx.x, A - 1);
+  float lvj = a.lv[jc], rlvj = a.ref_lv[jc];
+  double2 v[CH][PS_N / 2];
+  auto load_slabs = [&](int i0) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int64_t ic = min(i0 + 64 * c + lane, nb - 1);
+#pragma unroll
+      for (int q = 0; q < PS_N / 2; ++q) v[c][q] = P[ic * (PS_N / 2) + q];
+    }
+  };
+  if (dw) load_slabs(0);
+  // ... then the scalars (their lgkmcnt wait ahead of the slab loads was a
+  // round trip of its own), the caller's skip flag among them
+  const float* fz = reinterpret_cast<const float*>(g_pol_zero);
+  const int* zi = reinterpret_cast<const int*>(g_pol_zero);
+  int sk;
+  {
+    const int* cip = dec ? a.dec.ci + CI_STOP : zi;
+    const float* bp = dec ? a.dec.hyper + SMI_HYP_BETA : fz;
+    const float* cfp = dec ? fz : a.cf;
+    const double* mp = (a.norm_adv && a.moments) ? a.moments : g_pol_zero;
+    sk = *(skip ? skip : zi);
+    pre.stop = *cip;
+    pre.beta = *bp;
+    pre.clip_lo = a.hyper[SMI_HYPX_CLIP_LO];
+    pre.clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
+    pre.cf_surrw = cfp[CF_SURRW];
+    pre.cf_klcoef = cfp[CF_KLCOEF];
+    pre.mom[0] = mp[0]; pre.mom[1] = mp[1]; pre.mom[2] = mp[2];
   }
-  if (a.dec_part) {
-    const int lane = threadIdx.x & 63;
-    if (threadIdx.x < 64) {
-      double t[PS_N];
+  double t[PS_N];
 #pragma unroll
-      for (int j = 0; j < PS_N; ++j) t[j] = 0.0;
-      for (int i = lane; i < a.dec_nb; i += 64) {
+  for (int j = 0; j < PS_N; ++j) t[j] = 0.0;
+  if (dw) {
+    // the slabs pinned (else the last one's loads sank into its per-lane
+    // branch), then the guarded adds; further slab groups (> 64 CH partials)
+    // one round trip each
+    auto add_slabs = [&](int i0) {
 #pragma unroll
-        for (int j = 0; j < PS_N; ++j) t[j] += a.dec_part[(int64_t)i * PS_N + j];
+      for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int q = 0; q < PS_N / 2; ++q) asm volatile("" : "+v"(v[c][q].x), "+v"(v[c][q].y));
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        if (i0 + 64 * c + lane < nb) {
+#pragma unroll
+          for (int q = 0; q < PS_N / 2; ++q) { t[2 * q] += v[c][q].x; t[2 * q + 1] += v[c][q].y; }
+        }
       }
+    };
+    add_slabs(0);
+    for (int i0 = 64 * CH; i0 < nb; i0 += 64 * CH) { load_slabs(i0); add_slabs(i0); }
+  }
+  if (sk != 0) return true;      // uniform: before the first barrier
+  asm volatile("" : "+v"(lvj));
+  asm volatile("" : "+v"(rlvj));
+  if ((int)threadIdx.x < A) {
+    const int j = threadIdx.x;
+    sh.sig[j] = expf(lvj);
+    sh.lsig[j] = logf(sh.sig[j]);
+    sh.rsig[j] = expf(rlvj);
+  }
+  if (dec) {
+    if (threadIdx.x < 64) {
 #pragma unroll
       for (int j = 0; j < PS_N; ++j) {
         const double u = wave_sum_d(t[j]);
@@ -345,14 +428,15 @@ __device__ inline bool pol_grad_weights(const PolRowArgs& a, PolGradShared& sh, 
       double* out = const_cast<double*>(a.dec.ps);
       for (int j = 0; j < PS_N; ++j) out[j] = sh.sps[j];
     }
-    const Decision dd = policy_decide_body(a.dec, sh.sps, wr);
+    const DecidePre dp{pre.stop, pre.beta, sh.lsig};
+    const Decision dd = policy_decide_body(a.dec, sh.sps, wr, &dp);
     wsurr = dd.surrw;
     wkl = dd.klcoef;
     return dd.stop != 0;
   }
   __syncthreads();
-  wsurr = a.cf[CF_SURRW];
-  wkl = a.cf[CF_KLCOEF];
+  wsurr = pre.cf_surrw;
+  wkl = pre.cf_klcoef;
   return false;
 }
 
@@ -364,7 +448,7 @@ struct PolGradCols {
   float lsig[AM], inv1[AM], is1sq[AM], is1cu[AM], rs2[AM];
   float clip_lo, clip_hi;
   int A;
-  __device__ PolGradCols(const PolRowArgs& a, const PolGradShared& sh, int A_) : A(A_) {
+  __device__ PolGradCols(const PolGradPre& pre, const PolGradShared& sh, int A_) : A(A_) {
 #pragma unroll
     for (int j = 0; j < (AT > 0 ? AT : A_); ++j) {
       const float sg = sh.sig[j], rsig = sh.rsig[j];
@@ -374,8 +458,8 @@ struct PolGradCols {
       is1cu[j] = 1.f / (sg * sg * sg);
       rs2[j] = rsig * rsig;
     }
-    clip_lo = a.hyper[SMI_HYPX_CLIP_LO];
-    clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
+    clip_lo = pre.clip_lo;
+    clip_hi = pre.clip_hi;
   }
 };
 

@@ -849,22 +849,28 @@ policy_rows_stats_kernel(PolRowArgs a) {
 template <int NT, int AT>
 __global__ void __launch_bounds__(NT)
 policy_rows_grad_kernel(PolRowArgs a) {
-  if (a.skip && a.skip[0] != 0) return;
   constexpr int AM = AT > 0 ? AT : 32;
   __shared__ PolGradShared sh;
   __shared__ float gls[NT / 64][32];
   const int A = AT > 0 ? AT : a.A;
+  const int64_t N = (int64_t)a.E * a.B;
+  // the thread's first row (clamped) in flight through the epoch's weights
+  // and decision (the skip flag is read with the decision's scalars)
+  const int64_t n0 = (int64_t)blockIdx.x * NT + threadIdx.x;
+  PolGradRow<AT> x;
+  x.load(a, n0 < N ? n0 : N - 1, A);
   float wsurr, wkl;
-  if (pol_grad_weights(a, sh, wsurr, wkl)) return;
-  const PolGradCols<AT> cols(a, sh, A);
+  PolGradPre pre;
+  if (pol_grad_weights<8>(a, sh, wsurr, wkl, pre, a.skip)) return;
+  const PolGradCols<AT> cols(pre, sh, A);
   float glv[AM];
 #pragma unroll
   for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
-  const int64_t N = (int64_t)a.E * a.B;
-  const AdvNorm nadv(a);
-  for (int64_t n = (int64_t)blockIdx.x * NT + threadIdx.x; n < N; n += (int64_t)gridDim.x * NT) {
+  const AdvNorm nadv(a, pre.mom);
+  for (int64_t n = n0; n < N; n += (int64_t)gridDim.x * NT) {
     float dz[AM];
-    pol_grad_row<AT>(a, cols, nadv, n, wsurr, wkl, dz, glv);
+    if (n != n0) x.load(a, n, A);
+    pol_grad_compute<AT>(a, cols, nadv, x, wsurr, wkl, dz, glv);
     st_row<AT>(a.dz + n * A, dz, A);
   }
   // block partials of sum_rows d/dstd (times std at the reduction: d/dlog_var)
