@@ -635,7 +635,10 @@ head_bwd_kernel(HeadBwdArgs a) {
     SA.init(a.W2T, a.h2, a.h2, a.h1, wave, 4, 0, 1);
     float wsurr, wkl;
     PolGradPre pre;
-    if (pol_grad_weights(a.pg, psh, wsurr, wkl, pre)) return;
+    // one 64-partial slab per round trip: a deeper group of slabs in flight
+    // pushed the one-row-tile forms into scratch spills (<5, 2, 1>: 143 -> 168
+    // VGPRs + 80 B); a rank's 128 segments have 42 partials
+    if (pol_grad_weights<1>(a.pg, psh, wsurr, wkl, pre)) return;
     const PolGradCols<AT> cols(pre, psh, AT);
     const AdvNorm nadv(a.pg, pre.mom);
     float glv[AT];

@@ -694,16 +694,54 @@ static void launch_row_pack(int A, int64_t rows, const PolRowArgs& p, float* row
 template <int NT, int AT, bool FUSE>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, AT > 0 ? 3 : 8)))
 policy_rows_stats_kernel(PolRowArgs a) {
-  if (a.skip && a.skip[0] != 0) return;
   constexpr int AM = AT > 0 ? AT : 32;
   __shared__ float ssig[32], slsig[32], srsig[32];
   __shared__ double scr[NT / 64][PS_N];
   __shared__ float gls[FUSE ? NT / 64 : 1][32];
   const int A = AT > 0 ? AT : a.A;
-  for (int j = threadIdx.x; j < A; j += NT) {
-    ssig[j] = expf(a.lv[j]);                 // builders.py:127 std = exp(log_var)
+  const int64_t N = (int64_t)a.E * a.B;
+  const int64_t n0 = (int64_t)blockIdx.x * NT + threadIdx.x, ns = (int64_t)gridDim.x * NT;
+  // one row's inputs; with a compile-time action width the row loop runs two
+  // alternating register sets, the next row's loads in flight behind this
+  // row's arithmetic (clamped row index: always issued, so the waitcnt pass
+  // waits for exactly the set it consumes)
+  // (bl / rbd: the row's behaviour-policy terms, packed once per learn)
+  struct RowIn { float m[AM], rm[AM], ac[AM], adv, ret, bl, rbd; };
+  auto load_row = [&](RowIn& x, int64_t n) {
+    ld_row<AT>(x.m, a.mu + n * A, A);
+    ld_row<AT>(x.rm, a.refmu + n * A, A);
+    ld_fields<AT>(x.ac, a.rowin, N, n, 0, A);
+    x.adv = a.rowin[rin_idx(row_w(A), n, rin_adv(A))];
+    x.bl = a.rowin[rin_idx(row_w(A), n, rin_bl(A))];
+    x.rbd = a.rowin[rin_idx(row_w(A), n, rin_rbd(A))];
+    x.ret = a.ret_tm[n];
+  };
+  // every load ahead of the first wait (as in pol_grad_weights): the stds'
+  // log_vars (column threadIdx.x, A <= 32 < NT, clamped), the first row
+  // (clamped), then the scalars with the skip flag — one round trip for all
+  // (the flag, the log_vars, the clip range, the moments and the row had
+  // waited one after the other)
+  const int jc = min((int)threadIdx.x, A - 1);
+  float lvj = a.lv[jc], rlvj = a.ref_lv[jc];
+  [[maybe_unused]] RowIn X0, X1;
+  if constexpr (AT > 0) load_row(X0, n0 < N ? n0 : N - 1);
+  const int* zi = reinterpret_cast<const int*>(g_pol_zero);
+  const double* mp = (a.norm_adv && a.moments) ? a.moments : g_pol_zero;
+  int sk = *(a.skip ? a.skip : zi);
+  float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
+  double mom[3] = {mp[0], mp[1], mp[2]};
+  // (pinned together: left to their uses, the moments' loads sank into
+  // AdvNorm's branch and the clip range's past it, a scalar round trip each)
+  asm volatile("" : "+s"(sk), "+s"(clip_lo), "+s"(clip_hi));
+  asm volatile("" : "+s"(mom[0]), "+s"(mom[1]), "+s"(mom[2]));
+  asm volatile("" : "+v"(lvj));
+  asm volatile("" : "+v"(rlvj));
+  if (sk != 0) return;
+  if ((int)threadIdx.x < A) {
+    const int j = threadIdx.x;
+    ssig[j] = expf(lvj);                     // builders.py:127 std = exp(log_var)
     slsig[j] = logf(ssig[j]);                // std0.log() of ppo_net.py:40
-    srsig[j] = expf(a.ref_lv[j]);
+    srsig[j] = expf(rlvj);
   }
   __syncthreads();
   // per-column terms of the learner std (log-likelihood, KL(ref || learner))
@@ -721,7 +759,6 @@ policy_rows_stats_kernel(PolRowArgs a) {
     iden2[j] = 1.f / (2.f * (sig[j] * sig[j]));
     lrsig[j] = logf(rsig);
   }
-  const float clip_lo = a.hyper[SMI_HYPX_CLIP_LO], clip_hi = a.hyper[SMI_HYPX_CLIP_HI];
   double acc[PS_N];
 #pragma unroll
   for (int k = 0; k < PS_N; ++k) acc[k] = 0.0;
@@ -730,23 +767,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
 #pragma unroll
     for (int j = 0; j < (AT > 0 ? AT : A); ++j) glv[j] = 0.f;
   }
-  const int64_t N = (int64_t)a.E * a.B;
-  const AdvNorm nadv(a);
-  // one row's inputs; with a compile-time action width the row loop runs two
-  // alternating register sets, the next row's loads in flight behind this
-  // row's arithmetic (clamped row index: always issued, so the waitcnt pass
-  // waits for exactly the set it consumes)
-  // (bl / rbd: the row's behaviour-policy terms, packed once per learn)
-  struct RowIn { float m[AM], rm[AM], ac[AM], adv, ret, bl, rbd; };
-  auto load_row = [&](RowIn& x, int64_t n) {
-    ld_row<AT>(x.m, a.mu + n * A, A);
-    ld_row<AT>(x.rm, a.refmu + n * A, A);
-    ld_fields<AT>(x.ac, a.rowin, N, n, 0, A);
-    x.adv = a.rowin[rin_idx(row_w(A), n, rin_adv(A))];
-    x.bl = a.rowin[rin_idx(row_w(A), n, rin_bl(A))];
-    x.rbd = a.rowin[rin_idx(row_w(A), n, rin_rbd(A))];
-    x.ret = a.ret_tm[n];
-  };
+  const AdvNorm nadv(a, mom);
   auto row = [&](const RowIn& x, int64_t n) {
     const float* m = x.m;
     const float* rm = x.rm;
@@ -794,10 +815,7 @@ policy_rows_stats_kernel(PolRowArgs a) {
       st_row<AT>(a.dz + n * A, dz, A);
     }
   };
-  const int64_t n0 = (int64_t)blockIdx.x * NT + threadIdx.x, ns = (int64_t)gridDim.x * NT;
   if constexpr (AT > 0) {
-    RowIn X0, X1;
-    if (n0 < N) load_row(X0, n0);
     for (int64_t n = n0; n < N; n += 2 * ns) {
       load_row(X1, min(n + ns, N - 1));
       row(X0, n);
