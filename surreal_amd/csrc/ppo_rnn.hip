@@ -601,6 +601,19 @@ reduce_partials_kernel(const double* __restrict__ part, int nb, int w, double* o
     // four partials in flight per lane (independent sums, combined in order)
     double s4[4] = {0.0, 0.0, 0.0, 0.0};
     int i = l;
+    // four of those steps' loads (16 partials) per round trip, added in the
+    // steps' order (a column summed by few lanes had one trip per 4 partials)
+    for (; i + 15 * L < nb; i += 16 * L) {
+      double v[4][4];
+#pragma unroll
+      for (int it = 0; it < 4; ++it)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[it][k] = part[(int64_t)(i + (4 * it + k) * L) * w + jj];
+#pragma unroll
+      for (int it = 0; it < 4; ++it)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s4[k] += v[it][k];
+    }
     for (; i + 3 * L < nb; i += 4 * L) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) s4[k] += part[(int64_t)(i + k * L) * w + jj];
